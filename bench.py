@@ -1,0 +1,192 @@
+"""bench.py — particle-steps/sec of Gen's particle-filter hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): 10-dim linear-Gaussian SSM (Static
+DSL + Unfold), bootstrap particle filter with 2^20 particles per GPU,
+systematic resampling at ESS < N/2, synthetic observations simulated from the
+model.  One "step" = one pass of the hot path over the particle set: the
+reference's caller loop body {maybe_resample!; particle_filter_step!}
+(test/inference/particle_filter.jl:157-162) for one time step.
+
+value = whole-job particle-steps/s = N_global * K / (max over ranks of the
+timed region).  Multi-GPU (torchrun): particles shard across ranks (weak
+scaling, 2^20 per GPU) and the ranks form ONE filter: RCCL all-gathers the
+(max, sum, sum^2) weight triple every step and the integer CDF totals plus
+the ancestor states on resample steps.
+
+Also reported:
+  roofline     achieved HBM GB/s of the dominant kernel (k_step) from its
+               algorithmic bytes (16d+16 per particle-step, +4 on resample
+               steps) / its hipEvent-timed average duration on its stream;
+               traffic = PMC HBM bytes per launch from profiles/ when present.
+  cpu_baseline the CPU oracle (C restatement of Gen's PF, 1 core) on a bounded
+               sample of the same workload, timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--particles", type=int, default=1 << 20, help="particles per GPU")
+    p.add_argument("--d", type=int, default=10)
+    p.add_argument("--resampler", default="systematic")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-history", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(model, ys, budget_s):
+    """The oracle (scalar C, 1 core) on N = 2^14 particles, as many steps of
+    the same workload as fit in ~budget_s seconds."""
+    from oracle import oracle as O
+
+    n = 1 << 14
+    pf = O.OraclePF(model, n, 42, record_history=False)
+    t0 = time.perf_counter()
+    pf.init(ys[0])
+    steps = 0
+    i = 1
+    while time.perf_counter() - t0 < budget_s:
+        pf.maybe_resample()
+        pf.step(ys[i % len(ys)])
+        i += 1
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {
+        "value": n * (steps + 1) / dt,
+        "unit": "particle-steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"oracle/gh_oracle.c (C restatement of Gen's PF, not Gen.jl: no Julia on the box), "
+                  f"LG-SSM d={model.d}, N={n}, {steps + 1} steps incl. init, {dt:.1f} s",
+    }
+
+
+def main():
+    a = parse()
+    import gen_amd as gen
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+        uid = [gen.Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx = gen.Context(device=local, rank=rank, world=world, unique_id=uid[0])
+    else:
+        ctx = gen.Context(device=0)
+    gen.set_default_context(ctx)
+
+    model = gen.LinearGaussianSSM.benchmark(a.d)
+    T = a.warmup + a.steps + 1
+    _, ys = model.simulate(T, np.random.default_rng(2))
+    n_global = a.particles * world
+    st = gen.initialize_particle_filter(
+        model, (1,), {("chain", 1, "y"): ys[0]}, n_global, seed=42, resampler=a.resampler,
+        record_history=not a.no_history, history_capacity=T + 2, time_kernels=True,
+    )
+    gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]))
+    ctx.synchronize()
+    st.kernel_time_ms(reset=True)
+    ess0, did0 = st.ess_history()
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    gen.run_particle_filter(st, list(ys[1 + a.warmup : 1 + a.warmup + a.steps]))
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kms, kcount = st.kernel_time_ms()
+    ess, did = st.ess_history()
+    n_res = int(did[a.warmup : a.warmup + a.steps].sum())  # resamples ahead of the timed steps
+    lml = gen.log_ml_estimate(st)
+
+    bytes_pp = 16 * a.d + 16 + 4.0 * n_res / max(1, a.steps)
+    achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    value = n_global * a.steps / dt
+    out = {
+        "metric": "particle-steps/sec (whole node) + log-ML error vs CPU ref, 1M-particle SSM",
+        "value": value,
+        "unit": "particle-steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (observations simulated from the model, numpy seed 2)",
+        "config": {
+            "workload": f"C2: {a.d}-dim linear-Gaussian SSM bootstrap PF, {a.particles} particles/GPU, "
+                        f"systematic resampling at ESS<N/2, record_history={not a.no_history}",
+            "particles_global": n_global,
+            "d": a.d,
+            "resampler": a.resampler,
+            "parallelism": f"particle-dp{world}",
+            "resample_steps_timed": n_res,
+            "log_ml": lml,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "k_step<LGModel<10>,false>",
+            "kernel_avg_ms": kms,
+            "kernel_launches": kcount,
+            "bytes_per_particle_step": bytes_pp,
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(model, ys, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    st.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

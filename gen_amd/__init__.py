@@ -1,0 +1,39 @@
+"""gen_amd — MI355X-native particle-inference engine for Gen's SMC hot path.
+
+The product is libgen_hip.so (hand-written HIP kernels for gfx950 behind the
+C ABI in include/gen_hip.h).  This package is its Python host mirror of Gen's
+inference API (src/inference/particle_filter.jl, importance.jl); see
+DESIGN.md.  Importing it does not touch the GPU; the first call does.
+"""
+from .choicemap import ChoiceMap, EmptyChoiceMap, choicemap
+from .models import DiscreteHMM, KitagawaSSM, LinearGaussianSSM, Model
+from .pf import (
+    Context,
+    NoChange,
+    OptimalProposal,
+    ParticleFilterState,
+    UnknownChange,
+    default_context,
+    get_log_weights,
+    get_traces,
+    importance_resampling,
+    importance_sampling,
+    initialize_particle_filter,
+    log_ml_estimate,
+    maybe_resample,
+    maybe_resample_async,
+    particle_filter_step,
+    run_particle_filter,
+    sample_unweighted_traces,
+    set_default_context,
+)
+from ._lib import GenHipError
+
+__all__ = [
+    "ChoiceMap", "EmptyChoiceMap", "choicemap", "DiscreteHMM", "KitagawaSSM", "LinearGaussianSSM", "Model",
+    "Context", "NoChange", "OptimalProposal", "ParticleFilterState", "UnknownChange", "default_context",
+    "get_log_weights", "get_traces", "importance_resampling", "importance_sampling",
+    "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",
+    "particle_filter_step", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
+    "GenHipError",
+]

@@ -1,0 +1,981 @@
+// gh_api.hip — host side of libgen_hip.so: the C ABI declared in
+// include/gen_hip.h, implemented over the kernels in gh_kernels.h.
+//
+// Mirrors the reference's ParticleFilterState machine
+// (src/inference/particle_filter.jl:18-216): init -> {maybe_resample!, step!}*
+// -> log_ml_estimate, with every per-particle loop moved to the device and
+// every decision (ESS test, resample) kept device-resident so that a whole
+// filter can be enqueued without a host round trip.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gen_hip.h"
+#include "gh_kernels.h"
+
+using namespace gh;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+static int set_err(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(x)                                                                       \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) return set_err(GH_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCL_TRY(x)                                                                           \
+  do {                                                                                        \
+    ncclResult_t r_ = (x);                                                                    \
+    if (r_ != ncclSuccess) return set_err(GH_E_RCCL, "%s: %s", #x, ncclGetErrorString(r_));   \
+  } while (0)
+
+#define CHECK(x)            \
+  do {                      \
+    int rc_ = (x);          \
+    if (rc_ != GH_OK) return rc_; \
+  } while (0)
+
+extern "C" const char* gh_last_error(void) { return g_err.c_str(); }
+extern "C" const char* gh_version(void) { return "gen_hip 0.1.0 (gfx950)"; }
+
+// --------------------------------------------------------------- context
+struct gh_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+};
+
+static int ctx_setup(int device, void* stream, gh_ctx* c) {
+  c->device = device;
+  HIP_TRY(hipSetDevice(device));
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_create(int device, void* hip_stream, gh_ctx** out) {
+  if (!out) return set_err(GH_E_INVAL, "gh_ctx_create: out is NULL");
+  gh_ctx* c = new gh_ctx();
+  int rc = ctx_setup(device, hip_stream, c);
+  if (rc) { delete c; return rc; }
+  *out = c;
+  return GH_OK;
+}
+
+extern "C" int gh_comm_unique_id(uint8_t id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  memcpy(id, &u, 128);
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_create_dist(int device, int rank, int world, const uint8_t id[128],
+                                  void* hip_stream, gh_ctx** out) {
+  if (!out || world < 1 || rank < 0 || rank >= world)
+    return set_err(GH_E_INVAL, "gh_ctx_create_dist: bad rank/world %d/%d", rank, world);
+  gh_ctx* c = new gh_ctx();
+  int rc = ctx_setup(device, hip_stream, c);
+  if (rc) { delete c; return rc; }
+  c->rank = rank;
+  c->world = world;
+  if (world > 1) {
+    ncclUniqueId u;
+    memcpy(&u, id, 128);
+    ncclResult_t r = ncclCommInitRank(&c->comm, world, u, rank);
+    if (r != ncclSuccess) {
+      delete c;
+      return set_err(GH_E_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+  }
+  *out = c;
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_destroy(gh_ctx* c) {
+  if (!c) return GH_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  delete c;
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_rank(const gh_ctx* c, int* rank, int* world) {
+  if (!c) return set_err(GH_E_INVAL, "null ctx");
+  if (rank) *rank = c->rank;
+  if (world) *world = c->world;
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_stream(const gh_ctx* c, void** s) {
+  if (!c || !s) return set_err(GH_E_INVAL, "null ctx");
+  *s = (void*)c->stream;
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_synchronize(gh_ctx* c) {
+  if (!c) return set_err(GH_E_INVAL, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return GH_OK;
+}
+
+// ------------------------------------------------ host linear algebra (§5.1)
+// Same operation order as oracle/gh_oracle.c so derived parameters agree bit
+// for bit (Cholesky–Banachiewicz, forward substitution, log-det).
+static int chol(int d, const double* S, double* L) {
+  for (int i = 0; i < d * d; ++i) L[i] = 0.0;
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = S[i * d + j];
+      for (int k = 0; k < j; ++k) s = fma(-L[i * d + k], L[j * d + k], s);
+      if (i == j) {
+        if (!(s > 0.0)) return -1;
+        L[i * d + i] = sqrt(s);
+      } else {
+        L[i * d + j] = s / L[j * d + j];
+      }
+    }
+  return 0;
+}
+static void fwdsub(int d, int m, const double* L, const double* B, double* Y) {
+  for (int c = 0; c < m; ++c)
+    for (int i = 0; i < d; ++i) {
+      double s = B[i * m + c];
+      for (int k = 0; k < i; ++k) s = fma(-L[i * d + k], Y[k * m + c], s);
+      Y[i * m + c] = s / L[i * d + i];
+    }
+}
+static double gauss_cst(int d, const double* L) {
+  double acc = 0.0;
+  for (int i = 0; i < d; ++i) acc += gh_log(L[i * d + i]);
+  const double logdet = 2.0 * acc;
+  return -0.5 * ((double)d * LOG_2PI + logdet);
+}
+
+// ------------------------------------------------------------------ models
+struct gh_model {
+  gh_ctx* ctx = nullptr;
+  int family = 0, d = 0, dy = 0, k = 0, v = 0;
+  double* dparams = nullptr;  // device copy of the derived parameters
+  // host copies needed per step
+  std::vector<double> LR, c;  // LGSSM: chol(R), offset c
+  LGParams lg{};
+  HMMParams hmm{};
+  KitParams kit{};
+};
+
+static bool lg_supported(int d) { return (d >= 1 && d <= 8) || d == 10 || d == 12 || d == 16; }
+
+extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model** out) {
+  if (!ctx || !desc || !out) return set_err(GH_E_INVAL, "gh_model_create: null argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  gh_model* m = new gh_model();
+  m->ctx = ctx;
+  m->family = desc->family;
+  m->d = desc->d;
+  m->dy = desc->dy;
+  m->k = desc->k;
+  m->v = desc->v;
+  std::vector<double> h;  // packed derived parameters
+  const double* p = desc->params;
+  auto fail = [&](int code, const char* msg) {
+    delete m;
+    return set_err(code, "gh_model_create: %s", msg);
+  };
+  if (!p) return fail(GH_E_INVAL, "params is NULL");
+  if (desc->family == GH_FAMILY_LGSSM) {
+    const int d = desc->d, dy = desc->dy;
+    if (!lg_supported(d)) return fail(GH_E_INVAL, "LGSSM: unsupported d (1..8, 10, 12, 16)");
+    if (dy < 1 || dy > kMaxObs) return fail(GH_E_INVAL, "LGSSM: dy must be in 1..32");
+    const int64_t need = (int64_t)d * d + d + (int64_t)d * d + (int64_t)dy * d + dy +
+                         (int64_t)dy * dy + d + (int64_t)d * d;
+    if (desc->n_params < need) return fail(GH_E_INVAL, "LGSSM: too few parameters");
+    const double *A = p, *b = A + d * d, *Q = b + d, *H = Q + d * d, *c = H + dy * d, *R = c + dy,
+                 *mu0 = R + dy * dy, *P0 = mu0 + d;
+    std::vector<double> LQ(d * d), L0(d * d), M(dy * d);
+    m->LR.assign(dy * dy, 0.0);
+    if (chol(d, Q, LQ.data())) return fail(GH_E_INVAL, "LGSSM: Q not positive definite");
+    if (chol(dy, R, m->LR.data())) return fail(GH_E_INVAL, "LGSSM: R not positive definite");
+    if (chol(d, P0, L0.data())) return fail(GH_E_INVAL, "LGSSM: P0 not positive definite");
+    fwdsub(dy, d, m->LR.data(), H, M.data());
+    m->c.assign(c, c + dy);
+    // layout: A | b | LQ | M | mu0 | L0
+    h.insert(h.end(), A, A + d * d);
+    h.insert(h.end(), b, b + d);
+    h.insert(h.end(), LQ.begin(), LQ.end());
+    h.insert(h.end(), M.begin(), M.end());
+    h.insert(h.end(), mu0, mu0 + d);
+    h.insert(h.end(), L0.begin(), L0.end());
+    m->lg.dy = dy;
+    m->lg.cstR = gauss_cst(dy, m->LR.data());
+  } else if (desc->family == GH_FAMILY_HMM) {
+    const int K = desc->k, V = desc->v;
+    if (K < 1 || K > 64 || V < 1) return fail(GH_E_INVAL, "HMM: need 1 <= k <= 64, v >= 1");
+    if (desc->n_params < (int64_t)K + K * K + (int64_t)V * K) return fail(GH_E_INVAL, "HMM: too few parameters");
+    m->d = 1;
+    h.insert(h.end(), p, p + K + K * K + V * K);  // prior | T | E
+    for (int i = 0; i < V * K; ++i) h.push_back(gh_log(p[K + K * K + i]));  // logE
+    m->hmm.k = K;
+    m->hmm.v = V;
+  } else if (desc->family == GH_FAMILY_KITAGAWA) {
+    if (desc->n_params < 4) return fail(GH_E_INVAL, "Kitagawa: need mu1 s1 var_x var_y");
+    if (!(p[2] > 0.0) || !(p[3] > 0.0)) return fail(GH_E_INVAL, "Kitagawa: variances must be > 0");
+    m->d = 1;
+    m->kit.mu1 = p[0];
+    m->kit.s1 = p[1];
+    m->kit.sx = sqrt(p[2]);
+    m->kit.inv2vy = 1.0 / (2.0 * p[3]);
+    m->kit.csty = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * p[3]);
+    h.push_back(0.0);
+  } else {
+    return fail(GH_E_INVAL, "unknown family");
+  }
+  if (hipMalloc(&m->dparams, h.size() * sizeof(double)) != hipSuccess) return fail(GH_E_NOMEM, "hipMalloc params");
+  if (hipMemcpy(m->dparams, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    return fail(GH_E_HIP, "hipMemcpy params");
+  if (m->family == GH_FAMILY_LGSSM) {
+    const int d = m->d, dy = m->dy;
+    double* q = m->dparams;
+    m->lg.A = q; q += d * d;
+    m->lg.b = q; q += d;
+    m->lg.LQ = q; q += d * d;
+    m->lg.M = q; q += dy * d;
+    m->lg.mu0 = q; q += d;
+    m->lg.L0 = q;
+  } else if (m->family == GH_FAMILY_HMM) {
+    const int K = m->k, V = m->v;
+    m->hmm.prior = m->dparams;
+    m->hmm.T = m->dparams + K;
+    m->hmm.E = m->dparams + K + K * K;
+    m->hmm.logE = m->dparams + K + K * K + V * K;
+  }
+  *out = m;
+  return GH_OK;
+}
+
+extern "C" int gh_model_destroy(gh_model* m) {
+  if (!m) return GH_OK;
+  hipSetDevice(m->ctx->device);
+  if (m->dparams) hipFree(m->dparams);
+  delete m;
+  return GH_OK;
+}
+
+extern "C" int gh_model_state_dim(const gh_model* m, int* d) {
+  if (!m || !d) return set_err(GH_E_INVAL, "null model");
+  *d = m->d;
+  return GH_OK;
+}
+
+// host preprocessing of one step's observation
+static int make_obs(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
+  memset(o, 0, sizeof(*o));
+  o->present = (in && in->present && in->values) ? 1 : 0;
+  if (m->family == GH_FAMILY_KITAGAWA) o->ct = 8.0 * gh_cos(1.2 * (double)t);
+  if (!o->present) return GH_OK;
+  if (m->family == GH_FAMILY_LGSSM) {
+    if (in->n_values != m->dy) return set_err(GH_E_INVAL, "observation has %d values, dy = %d", in->n_values, m->dy);
+    double r[kMaxObs];
+    for (int i = 0; i < m->dy; ++i) r[i] = in->values[i] - m->c[i];
+    fwdsub(m->dy, 1, m->LR.data(), r, o->v);
+  } else if (m->family == GH_FAMILY_HMM) {
+    const double s = in->values[0];
+    if (!(s >= 0.0) || s >= (double)m->v || s != floor(s))
+      return set_err(GH_E_INVAL, "HMM observation %g is not a symbol in 0..%d", s, m->v - 1);
+    o->v[0] = s;
+    o->sym = (int)s;
+  } else {
+    o->v[0] = in->values[0];
+  }
+  return GH_OK;
+}
+
+// ------------------------------------------------------------ the PF state
+struct gh_pf {
+  gh_model* m = nullptr;
+  gh_ctx* ctx = nullptr;
+  hipStream_t s = nullptr;
+  int D = 0;
+  int64_t n_global = 0, n = 0, lo = 0;
+  uint64_t seed = 0;
+  gh_pf_opts opts{};
+  int t = 0;                      // completed steps
+  int resample_calls = 0;         // maybe_resample calls since the last step
+  // states: history slots (record_history) or 2 ping-pong slots
+  std::vector<double*> xs;        // index t-1 (history) or t&1
+  std::vector<int32_t*> ancs;     // index t-1: ancestors used by step t
+  int32_t* anc_scratch = nullptr;
+  double* logw = nullptr;
+  uint64_t* C = nullptr;
+  uint64_t* bsum = nullptr;
+  int64_t nb_scan = 0;
+  int64_t nb_step = 0;
+  double *pm = nullptr, *ps = nullptr, *ps2 = nullptr;
+  DevScalars* dev = nullptr;
+  double* stats_all = nullptr;    // [3*world]
+  uint64_t* totals_all = nullptr; // [world]
+  int cap = 0;                    // history/ess capacity (steps)
+  double* ess_hist = nullptr;     // [cap+2]
+  int32_t* res_hist = nullptr;    // [cap+2]
+  // multi-rank resample exchange
+  double* recv = nullptr;         // [D][n]
+  double* send = nullptr;         // [D][n]
+  int64_t* xslot = nullptr;       // [n] slots emitted by this rank
+  int32_t* xanc = nullptr;        // [n]
+  std::vector<void*> chunks;      // history allocations (record_history)
+  // kernel timing
+  std::vector<hipEvent_t> ev;
+  size_t ev_used = 0;
+  double ev_ms = 0.0;
+  int64_t ev_count = 0;
+};
+
+static int64_t split_lo(int64_t n, int r, int R) { return (n * r) / R; }
+
+static double* slot_x(gh_pf* pf, int t) {  // states of step t (1-based)
+  return pf->opts.record_history ? pf->xs[t - 1] : pf->xs[t & 1];
+}
+
+static int ensure_capacity(gh_pf* pf, int steps) {
+  // history slots, ancestor slots and per-step records for steps 1..steps
+  if (steps <= pf->cap) return GH_OK;
+  int nc = pf->cap ? pf->cap : 16;
+  while (nc < steps) nc *= 2;
+  const size_t xbytes = sizeof(double) * (size_t)pf->D * (size_t)pf->n;
+  const size_t abytes = sizeof(int32_t) * (size_t)(pf->n ? pf->n : 1);
+  if (pf->opts.record_history) {
+    // allocate the new slots as one chunk (no hipMalloc per step)
+    const int add = nc - pf->cap;
+    char* chunk = nullptr;
+    if (hipMalloc(&chunk, (xbytes + abytes) * (size_t)add) != hipSuccess)
+      return set_err(GH_E_NOMEM, "history: cannot allocate %d more steps", add);
+    pf->chunks.push_back(chunk);
+    for (int i = 0; i < add; ++i) {
+      pf->xs.push_back((double*)(chunk + (xbytes + abytes) * i));
+      pf->ancs.push_back((int32_t*)(chunk + (xbytes + abytes) * i + xbytes));
+    }
+  }
+  double* ne = nullptr;
+  int32_t* nr = nullptr;
+  HIP_TRY(hipMalloc(&ne, sizeof(double) * (nc + 2)));
+  HIP_TRY(hipMalloc(&nr, sizeof(int32_t) * (nc + 2)));
+  HIP_TRY(hipMemsetAsync(nr, 0, sizeof(int32_t) * (nc + 2), pf->s));
+  HIP_TRY(hipMemsetAsync(ne, 0, sizeof(double) * (nc + 2), pf->s));
+  if (pf->ess_hist) {
+    HIP_TRY(hipMemcpyAsync(ne, pf->ess_hist, sizeof(double) * (pf->cap + 2), hipMemcpyDeviceToDevice, pf->s));
+    HIP_TRY(hipMemcpyAsync(nr, pf->res_hist, sizeof(int32_t) * (pf->cap + 2), hipMemcpyDeviceToDevice, pf->s));
+    HIP_TRY(hipStreamSynchronize(pf->s));
+    hipFree(pf->ess_hist);
+    hipFree(pf->res_hist);
+  }
+  pf->ess_hist = ne;
+  pf->res_hist = nr;
+  pf->cap = nc;
+  return GH_OK;
+}
+
+static int32_t* anc_for_step(gh_pf* pf, int t) {  // ancestors consumed by step t
+  return pf->opts.record_history ? pf->ancs[t - 1] : pf->ancs[0];
+}
+
+extern "C" void gh_pf_opts_default(gh_pf_opts* o) {
+  memset(o, 0, sizeof(*o));
+  o->resampler = GH_RESAMPLE_SYSTEMATIC;
+  o->record_history = 1;
+}
+
+static void pf_free(gh_pf* pf) {
+  if (!pf) return;
+  hipSetDevice(pf->ctx->device);
+  hipStreamSynchronize(pf->s);
+  for (auto c : pf->chunks) hipFree(c);
+  for (auto e : pf->ev) hipEventDestroy(e);
+  hipFree(pf->logw); hipFree(pf->C); hipFree(pf->bsum); hipFree(pf->pm); hipFree(pf->ps);
+  hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->stats_all); hipFree(pf->totals_all);
+  hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
+  hipFree(pf->recv); hipFree(pf->send); hipFree(pf->xslot); hipFree(pf->xanc);
+  if (!pf->opts.record_history) {
+    for (auto p : pf->xs) hipFree(p);
+    for (auto p : pf->ancs) hipFree(p);
+  }
+  delete pf;
+}
+
+extern "C" int gh_pf_destroy(gh_pf* pf) {
+  pf_free(pf);
+  return GH_OK;
+}
+
+// ----------------------------------------------------------- kernel launch
+template <class Model>
+static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const StepObs& o,
+                          const StepArgs& a, bool init) {
+  const dim3 grid((unsigned)pf->nb_step), block(kBlock);
+  if (init) hipLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, p, o, a);
+  else hipLaunchKernelGGL((k_step<Model, false>), grid, block, 0, pf->s, p, o, a);
+}
+
+static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
+  gh_model* m = pf->m;
+  switch (m->family) {
+    case GH_FAMILY_LGSSM:
+      switch (m->d) {
+#define GH_LG_CASE(DD) case DD: launch_step_t<LGModel<DD>>(pf, m->lg, o, a, init); break;
+        GH_LG_CASE(1) GH_LG_CASE(2) GH_LG_CASE(3) GH_LG_CASE(4) GH_LG_CASE(5) GH_LG_CASE(6)
+        GH_LG_CASE(7) GH_LG_CASE(8) GH_LG_CASE(10) GH_LG_CASE(12) GH_LG_CASE(16)
+#undef GH_LG_CASE
+        default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", m->d);
+      }
+      break;
+    case GH_FAMILY_HMM: launch_step_t<HMMModel>(pf, m->hmm, o, a, init); break;
+    case GH_FAMILY_KITAGAWA: launch_step_t<KitModel>(pf, m->kit, o, a, init); break;
+    default: return set_err(GH_E_INVAL, "unknown family");
+  }
+  HIP_TRY(hipGetLastError());
+  return GH_OK;
+}
+
+static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
+  if (!pf->opts.time_kernels) return launch_step(pf, o, a, init);
+  if (pf->ev_used + 2 > pf->ev.size()) {
+    for (int i = 0; i < 64; ++i) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      pf->ev.push_back(e);
+    }
+  }
+  hipEvent_t e0 = pf->ev[pf->ev_used], e1 = pf->ev[pf->ev_used + 1];
+  pf->ev_used += 2;
+  HIP_TRY(hipEventRecord(e0, pf->s));
+  CHECK(launch_step(pf, o, a, init));
+  HIP_TRY(hipEventRecord(e1, pf->s));
+  return GH_OK;
+}
+
+// after the step kernel: share the rank's (M, S, S2) with every rank
+static int share_stats(gh_pf* pf) {
+  if (pf->ctx->world == 1) return GH_OK;
+  NCCL_TRY(ncclAllGather(pf->dev->stats, pf->stats_all, 3, ncclDouble, pf->ctx->comm, pf->s));
+  return GH_OK;
+}
+
+extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles,
+                          uint64_t seed, const gh_pf_opts* opts, gh_pf** out) {
+  if (!m || !out) return set_err(GH_E_INVAL, "gh_pf_init: null argument");
+  if (n_particles < 1 || n_particles > 0x7fffffffLL)
+    return set_err(GH_E_INVAL, "gh_pf_init: num_particles must be in 1..2^31-1");
+  if (proposal == GH_PROPOSAL_OPTIMAL && m->family != GH_FAMILY_HMM)
+    return set_err(GH_E_INVAL, "gh_pf_init: the optimal proposal is implemented for HMM only");
+  gh_ctx* ctx = m->ctx;
+  HIP_TRY(hipSetDevice(ctx->device));
+  gh_pf* pf = new gh_pf();
+  pf->m = m;
+  pf->ctx = ctx;
+  pf->s = ctx->stream;
+  pf->D = m->d;
+  if (opts) pf->opts = *opts;
+  else gh_pf_opts_default(&pf->opts);
+  if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC && pf->opts.resampler != GH_RESAMPLE_MULTINOMIAL) {
+    delete pf;
+    return set_err(GH_E_INVAL, "unknown resampler %d", pf->opts.resampler);
+  }
+  pf->n_global = n_particles;
+  pf->lo = split_lo(n_particles, ctx->rank, ctx->world);
+  pf->n = split_lo(n_particles, ctx->rank + 1, ctx->world) - pf->lo;
+  pf->seed = seed;
+  const int64_t n = pf->n > 0 ? pf->n : 1;
+  pf->nb_step = (n + kBlock - 1) / kBlock;
+  pf->nb_scan = (n + kScanTile - 1) / kScanTile;
+  auto fail = [&](int rc) { pf_free(pf); return rc; };
+#define ALLOC(ptr, bytes) \
+  if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return fail(set_err(GH_E_NOMEM, "hipMalloc %s", #ptr));
+  ALLOC(pf->logw, sizeof(double) * n);
+  ALLOC(pf->C, sizeof(uint64_t) * n);
+  ALLOC(pf->bsum, sizeof(uint64_t) * pf->nb_scan);
+  ALLOC(pf->pm, sizeof(double) * pf->nb_step);
+  ALLOC(pf->ps, sizeof(double) * pf->nb_step);
+  ALLOC(pf->ps2, sizeof(double) * pf->nb_step);
+  ALLOC(pf->dev, sizeof(DevScalars));
+  ALLOC(pf->stats_all, sizeof(double) * 3 * ctx->world);
+  ALLOC(pf->totals_all, sizeof(uint64_t) * ctx->world);
+  ALLOC(pf->anc_scratch, sizeof(int32_t) * n);
+  if (ctx->world > 1) {
+    ALLOC(pf->recv, sizeof(double) * pf->D * n);
+    ALLOC(pf->send, sizeof(double) * pf->D * n);
+    ALLOC(pf->xslot, sizeof(int64_t) * n);
+    ALLOC(pf->xanc, sizeof(int32_t) * n);
+  }
+  if (!pf->opts.record_history) {
+    for (int i = 0; i < 2; ++i) {
+      double* x = nullptr;
+      ALLOC(x, sizeof(double) * pf->D * n);
+      pf->xs.push_back(x);
+    }
+    int32_t* a = nullptr;
+    ALLOC(a, sizeof(int32_t) * n);
+    pf->ancs.push_back(a);
+  }
+#undef ALLOC
+  {
+    DevScalars z;
+    memset(&z, 0, sizeof z);
+    z.one = 1;
+    if (hipMemcpyAsync(pf->dev, &z, sizeof z, hipMemcpyHostToDevice, pf->s) != hipSuccess)
+      return fail(set_err(GH_E_HIP, "init scalars"));
+    if (hipStreamSynchronize(pf->s) != hipSuccess) return fail(set_err(GH_E_HIP, "sync"));
+  }
+  const int cap0 = pf->opts.history_capacity > 0 ? pf->opts.history_capacity : 16;
+  {
+    int rc = ensure_capacity(pf, cap0);
+    if (rc) return fail(rc);
+  }
+  StepObs o;
+  int rc = make_obs(m, 1, obs, &o);
+  if (rc) return fail(rc);
+  StepArgs a{};
+  a.xout = slot_x(pf, 1);
+  a.ld_out = pf->n;
+  a.logw = pf->logw;
+  a.n = pf->n;
+  a.lo = pf->lo;
+  a.seed = seed;
+  a.t = 1;
+  a.proposal = proposal;
+  a.dev = pf->dev;
+  a.pm = pf->pm;
+  a.ps = pf->ps;
+  a.ps2 = pf->ps2;
+  a.stats_out = ctx->world == 1 ? pf->stats_all : pf->dev->stats;
+  rc = timed_step(pf, o, a, true);
+  if (rc) return fail(rc);
+  rc = share_stats(pf);
+  if (rc) return fail(rc);
+  pf->t = 1;
+  *out = pf;
+  return GH_OK;
+}
+
+static int grow_for_step(gh_pf* pf, int t) { return ensure_capacity(pf, t + 1); }
+
+extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family != GH_FAMILY_HMM)
+    return set_err(GH_E_INVAL, "the optimal proposal is implemented for HMM only");
+  const int t = pf->t + 1;
+  CHECK(grow_for_step(pf, t));
+  StepObs o;
+  CHECK(make_obs(pf->m, t, obs, &o));
+  StepArgs a{};
+  a.xprev = slot_x(pf, t - 1);
+  a.ld_prev = pf->n;
+  a.anc = anc_for_step(pf, t);
+  a.remote = pf->recv;
+  a.ld_remote = pf->n;
+  a.xout = slot_x(pf, t);
+  a.ld_out = pf->n;
+  a.logw = pf->logw;
+  a.n = pf->n;
+  a.lo = pf->lo;
+  a.seed = pf->seed;
+  a.t = (uint32_t)t;
+  a.proposal = proposal;
+  a.dev = pf->dev;
+  a.pm = pf->pm;
+  a.ps = pf->ps;
+  a.ps2 = pf->ps2;
+  a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
+  CHECK(timed_step(pf, o, a, false));
+  CHECK(share_stats(pf));
+  pf->t = t;
+  pf->resample_calls = 0;
+  return GH_OK;
+}
+
+// multi-rank exchange of ancestor states; defined below
+static int exchange_states(gh_pf* pf, int32_t* anc_out);
+
+static int resample_enqueue(gh_pf* pf, double thr) {
+  const int t = pf->t;
+  CHECK(grow_for_step(pf, t + 1));
+  const int R = pf->ctx->world;
+  hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, R,
+                     pf->n_global, thr, pf->ess_hist, pf->res_hist, t);
+  GateArgs g;
+  g.gate = &pf->dev->fire;
+  g.M = &pf->dev->M;
+  g.zero_w = &pf->dev->pending;
+  g.shift = quant_shift((uint64_t)pf->n_global);
+  const int64_t n = pf->n;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum);
+    hipLaunchKernelGGL(k_qscan, dim3(1), dim3(1024), 0, pf->s, pf->bsum, pf->nb_scan, g, pf->dev);
+  }
+  if (R > 1) {
+    NCCL_TRY(ncclAllGather(&pf->dev->local, pf->totals_all, 1, ncclUint64, pf->ctx->comm, pf->s));
+  }
+  const uint32_t stream = STREAM_RESAMPLE;
+  hipLaunchKernelGGL(k_rs_const, dim3(1), dim3(64), 0, pf->s, g, pf->dev,
+                     R > 1 ? (const uint64_t*)pf->totals_all : (const uint64_t*)nullptr, R,
+                     pf->ctx->rank, pf->n_global, pf->seed, (uint32_t)t, stream);
+  if (n > 0)
+    hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g,
+                       pf->bsum, pf->dev, pf->C);
+  int32_t* anc_target = anc_for_step(pf, t + 1);
+  const bool second = pf->resample_calls > 0;
+  if (R == 1) {
+    SearchArgs sa{};
+    sa.C = pf->C;
+    sa.n_cdf = n;
+    sa.n_slots = n;
+    sa.slot_lo = 0;
+    sa.n_global = pf->n_global;
+    sa.seed = pf->seed;
+    sa.t = (uint32_t)t;
+    sa.mode = pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC ? SEARCH_SYSTEMATIC : SEARCH_MULTINOMIAL;
+    sa.anc_old = second ? anc_target : nullptr;
+    sa.anc_out = second ? pf->anc_scratch : anc_target;
+    hipLaunchKernelGGL(k_search, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, sa, g, pf->dev);
+    if (second)
+      hipLaunchKernelGGL(k_copy_anc, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
+                         pf->anc_scratch, anc_target, n);
+  } else {
+    if (second) return set_err(GH_E_STATE, "multi-rank: maybe_resample twice without a step is not supported");
+    CHECK(exchange_states(pf, anc_target));
+  }
+  HIP_TRY(hipGetLastError());
+  pf->resample_calls++;
+  return GH_OK;
+}
+
+extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  if (pf->t < 1) return set_err(GH_E_STATE, "maybe_resample before init");
+  if (!(thr > 0.0)) thr = (double)pf->n_global / 2.0;
+  CHECK(resample_enqueue(pf, thr));
+  if (did || ess) {
+    DevScalars h;
+    HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
+    HIP_TRY(hipStreamSynchronize(pf->s));
+    if (h.error) return set_err(h.error, "maybe_resample: all log-weights are -Inf or NaN");
+    if (did) *did = h.fire;
+    if (ess) *ess = h.ess;
+  }
+  return GH_OK;
+}
+
+extern "C" int gh_pf_run(gh_pf* pf, int n_steps, const gh_obs* obs, int proposal, double thr) {
+  if (!pf || n_steps < 0) return set_err(GH_E_INVAL, "gh_pf_run: bad argument");
+  for (int i = 0; i < n_steps; ++i) {
+    CHECK(gh_pf_maybe_resample(pf, thr, nullptr, nullptr));
+    CHECK(gh_pf_step(pf, obs ? &obs[i] : nullptr, proposal));
+  }
+  return GH_OK;
+}
+
+static int read_scalars(gh_pf* pf, DevScalars* h, std::vector<double>* stats) {
+  HIP_TRY(hipMemcpyAsync(h, pf->dev, sizeof *h, hipMemcpyDeviceToHost, pf->s));
+  if (stats) {
+    stats->resize(3 * pf->ctx->world);
+    HIP_TRY(hipMemcpyAsync(stats->data(), pf->stats_all, sizeof(double) * stats->size(), hipMemcpyDeviceToHost, pf->s));
+  }
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  return GH_OK;
+}
+
+extern "C" int gh_pf_log_ml_estimate(gh_pf* pf, double* out) {
+  if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
+  DevScalars h;
+  std::vector<double> st;
+  CHECK(read_scalars(pf, &h, &st));
+  if (h.error) return set_err(h.error, "log_ml_estimate: numeric error raised on the device");
+  if (h.pending | h.fire) {  // all weights are 0: logsumexp(w) - log N = 0
+    *out = h.log_ml_est;
+    return GH_OK;
+  }
+  // log_ml_est + logsumexp(log_weights) - log(N)   (particle_filter.jl:52-55)
+  const int R = pf->ctx->world;
+  double M = -INFINITY;
+  for (int r = 0; r < R; ++r) M = fmax(M, st[3 * r]);
+  if (!(M > -INFINITY)) {
+    *out = -INFINITY;
+    return GH_OK;
+  }
+  double S = 0.0;
+  for (int r = 0; r < R; ++r)
+    if (st[3 * r] > -INFINITY) S += st[3 * r + 1] * gh_exp(st[3 * r] - M);
+  *out = h.log_ml_est + (M + gh_log(S)) - gh_log((double)pf->n_global);
+  return GH_OK;
+}
+
+extern "C" int gh_pf_num_particles(const gh_pf* pf, int64_t* ng, int64_t* nl, int64_t* first) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  if (ng) *ng = pf->n_global;
+  if (nl) *nl = pf->n;
+  if (first) *first = pf->lo;
+  return GH_OK;
+}
+
+extern "C" int gh_pf_num_steps(const gh_pf* pf, int* t) {
+  if (!pf || !t) return set_err(GH_E_INVAL, "null argument");
+  *t = pf->t;
+  return GH_OK;
+}
+
+extern "C" int gh_pf_get_log_weights(gh_pf* pf, double* out) {
+  if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
+  DevScalars h;
+  CHECK(read_scalars(pf, &h, nullptr));
+  if (h.pending | h.fire) {
+    for (int64_t i = 0; i < pf->n; ++i) out[i] = 0.0;
+    return GH_OK;
+  }
+  HIP_TRY(hipMemcpy(out, pf->logw, sizeof(double) * pf->n, hipMemcpyDeviceToHost));
+  return GH_OK;
+}
+
+extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
+  if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
+  if (t < 1 || t > pf->t) return set_err(GH_E_INVAL, "step %d outside 1..%d", t, pf->t);
+  if (!pf->opts.record_history && t != pf->t)
+    return set_err(GH_E_STATE, "record_history is off: only the current step is kept");
+  if (pf->ctx->world > 1 && t != pf->t)
+    return set_err(GH_E_STATE, "multi-rank: trajectories before the current step are not materialised");
+  const int64_t n = pf->n;
+  if (n == 0) return GH_OK;
+  double* dout = nullptr;
+  const double** dxs = nullptr;
+  const int32_t** dancs = nullptr;
+  HIP_TRY(hipMalloc(&dout, sizeof(double) * pf->D * n));
+  const int T = pf->t;
+  std::vector<const double*> hx(T);
+  std::vector<const int32_t*> ha(T);
+  for (int s = 1; s <= T; ++s) {
+    hx[s - 1] = slot_x(pf, s);
+    ha[s - 1] = anc_for_step(pf, s);
+  }
+  HIP_TRY(hipMalloc(&dxs, sizeof(double*) * T));
+  HIP_TRY(hipMalloc(&dancs, sizeof(int32_t*) * T));
+  HIP_TRY(hipMemcpyAsync(dxs, hx.data(), sizeof(double*) * T, hipMemcpyHostToDevice, pf->s));
+  HIP_TRY(hipMemcpyAsync(dancs, ha.data(), sizeof(int32_t*) * T, hipMemcpyHostToDevice, pf->s));
+  TrajArgs ta{};
+  ta.xs = dxs;
+  ta.ancs = dancs;
+  ta.res_before = pf->res_hist;
+  ta.anc_pending = (pf->ctx->world == 1 && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
+  ta.n = n;
+  ta.ld = n;
+  ta.t_target = t;
+  ta.t_cur = T;
+  ta.D = pf->D;
+  ta.out = dout;
+  hipLaunchKernelGGL(k_traj, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, ta, pf->dev);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, dout, sizeof(double) * pf->D * n, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  hipFree(dout);
+  hipFree(dxs);
+  hipFree(dancs);
+  return GH_OK;
+}
+
+extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  if (pf->ctx->world > 1) {
+    DevScalars h;
+    CHECK(read_scalars(pf, &h, nullptr));
+    if (h.pending | h.fire)
+      return set_err(GH_E_STATE, "multi-rank: states of a pending resample are materialised by the next step");
+    HIP_TRY(hipMemcpy(out, slot_x(pf, pf->t), sizeof(double) * pf->D * pf->n, hipMemcpyDeviceToHost));
+    return GH_OK;
+  }
+  return gh_pf_get_trajectory(pf, pf->t, out);
+}
+
+extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
+  if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
+  // ParticleFilterState.parents: ancestors chosen by the most recent resample
+  // (identity before the first one), as global 0-based ids.
+  std::vector<int32_t> res(pf->cap + 2);
+  HIP_TRY(hipMemcpy(res.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2), hipMemcpyDeviceToHost));
+  int s_last = -1;
+  for (int s = pf->t + 1; s >= 2 && s < pf->cap + 2; --s)
+    if (res[s]) { s_last = s; break; }
+  if (s_last < 0) {
+    for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->lo + i;
+    return GH_OK;
+  }
+  if (pf->ctx->world > 1) return set_err(GH_E_STATE, "multi-rank: parents are exchanged as (rank, index) pairs; not exported yet");
+  std::vector<int32_t> a(pf->n);
+  HIP_TRY(hipMemcpy(a.data(), anc_for_step(pf, s_last), sizeof(int32_t) * pf->n, hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->lo + a[i];
+  return GH_OK;
+}
+
+extern "C" int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int32_t* did) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  const int T = pf->t < max_steps ? pf->t : max_steps;
+  std::vector<double> e(pf->cap + 2);
+  std::vector<int32_t> r(pf->cap + 2);
+  HIP_TRY(hipMemcpy(e.data(), pf->ess_hist, sizeof(double) * (pf->cap + 2), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(r.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2), hipMemcpyDeviceToHost));
+  // ess[s-1]: ESS measured by maybe_resample after step s; did[s-1]: resampled then
+  for (int s = 1; s <= T; ++s) {
+    if (ess) ess[s - 1] = e[s];
+    if (did) did[s - 1] = r[s + 1];
+  }
+  return GH_OK;
+}
+
+extern "C" int gh_pf_sample_unweighted(gh_pf* pf, int64_t ns, uint64_t seed, int64_t* idx) {
+  if (!pf || !idx || ns < 0) return set_err(GH_E_INVAL, "bad argument");
+  if (pf->ctx->world > 1) return set_err(GH_E_STATE, "sample_unweighted: single rank only");
+  if (ns == 0) return GH_OK;
+  const int64_t n = pf->n;
+  hipLaunchKernelGGL(k_prep_sample, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, 1);
+  GateArgs g;
+  g.gate = &pf->dev->one;
+  g.M = &pf->dev->sM;
+  g.zero_w = &pf->dev->spend;
+  g.shift = quant_shift((uint64_t)n);
+  hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum);
+  hipLaunchKernelGGL(k_qscan, dim3(1), dim3(1024), 0, pf->s, pf->bsum, pf->nb_scan, g, pf->dev);
+  hipLaunchKernelGGL(k_rs_const, dim3(1), dim3(64), 0, pf->s, g, pf->dev, (const uint64_t*)nullptr, 1, 0,
+                     n, seed, (uint32_t)pf->t, (uint32_t)STREAM_SAMPLE);
+  hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum,
+                     pf->dev, pf->C);
+  int32_t* dout = nullptr;
+  HIP_TRY(hipMalloc(&dout, sizeof(int32_t) * ns));
+  SearchArgs sa{};
+  sa.C = pf->C;
+  sa.n_cdf = n;
+  sa.n_slots = ns;
+  sa.slot_lo = 0;
+  sa.n_global = n;
+  sa.seed = seed;
+  sa.t = (uint32_t)pf->t;
+  sa.mode = SEARCH_SAMPLE;
+  sa.anc_old = nullptr;
+  sa.anc_out = dout;
+  hipLaunchKernelGGL(k_search, dim3((unsigned)((ns + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s, sa, g,
+                     pf->dev);
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> h(ns);
+  HIP_TRY(hipMemcpyAsync(h.data(), dout, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  hipFree(dout);
+  for (int64_t i = 0; i < ns; ++i) idx[i] = h[i];
+  return GH_OK;
+}
+
+extern "C" int gh_pf_kernel_time(gh_pf* pf, double* avg_ms, int64_t* nl, int reset) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  for (size_t i = 0; i + 1 < pf->ev_used; i += 2) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, pf->ev[i], pf->ev[i + 1]));
+    pf->ev_ms += ms;
+    pf->ev_count += 1;
+  }
+  pf->ev_used = 0;
+  if (avg_ms) *avg_ms = pf->ev_count ? pf->ev_ms / (double)pf->ev_count : 0.0;
+  if (nl) *nl = pf->ev_count;
+  if (reset) {
+    pf->ev_ms = 0.0;
+    pf->ev_count = 0;
+  }
+  return GH_OK;
+}
+
+// -------------------------------------------------- multi-rank exchange
+// Stub until the RCCL exchange lands: refuse loudly rather than compute wrong
+// ancestors.
+static int exchange_states(gh_pf* pf, int32_t* anc_out) {
+  (void)pf;
+  (void)anc_out;
+  return set_err(GH_E_STATE, "multi-rank resampling exchange not built yet");
+}
+
+// ------------------------------------------------------ importance sampling
+extern "C" int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t seed,
+                         double* lnw, double* states, double* lml) {
+  if (!m || !lml) return set_err(GH_E_INVAL, "gh_is_run: null argument");
+  gh_pf_opts o;
+  gh_pf_opts_default(&o);
+  o.record_history = 0;
+  gh_pf* pf = nullptr;
+  // importance_sampling = N independent generate() calls (importance.jl:20-33),
+  // i.e. the PF's first step; the lml is logsumexp(w) - log N.
+  CHECK(gh_pf_init(m, obs, proposal, n, seed, &o, &pf));
+  int rc = gh_pf_log_ml_estimate(pf, lml);
+  if (!rc && lnw) {
+    rc = gh_pf_get_log_weights(pf, lnw);
+    if (!rc) {
+      // normalise: lnw - logsumexp(lnw) (importance.jl:29-31)
+      const double L = *lml + gh_log((double)pf->n_global);
+      for (int64_t i = 0; i < pf->n; ++i) lnw[i] -= L;
+    }
+  }
+  if (!rc && states) rc = gh_pf_get_states(pf, states);
+  gh_pf_destroy(pf);
+  return rc;
+}
+
+// ------------------------------------------------------------ self tests
+extern "C" int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double* oe, double* ol,
+                                double* os, double* od) {
+  if (!ctx || n <= 0) return set_err(GH_E_INVAL, "bad argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  double* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(double) * n * 5));
+  HIP_TRY(hipMemcpyAsync(d, in, sizeof(double) * n, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_selftest_math, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     ctx->stream, n, d, d + n, d + 2 * n, d + 3 * n, d + 4 * n);
+  HIP_TRY(hipGetLastError());
+  double* outs[4] = {oe, ol, os, od};
+  for (int i = 0; i < 4; ++i)
+    if (outs[i])
+      HIP_TRY(hipMemcpyAsync(outs[i], d + (i + 1) * n, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  hipFree(d);
+  return GH_OK;
+}
+
+extern "C" int gh_selftest_normals(gh_ctx* ctx, uint64_t seed, int64_t n, uint32_t step, uint32_t stream,
+                                   int dim, double* out) {
+  if (!ctx || n <= 0 || dim <= 0) return set_err(GH_E_INVAL, "bad argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  double* d = nullptr;
+  HIP_TRY(hipMalloc(&d, sizeof(double) * n * dim));
+  hipLaunchKernelGGL(k_selftest_normals, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     ctx->stream, seed, n, step, stream, dim, d);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, d, sizeof(double) * n * dim, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  hipFree(d);
+  return GH_OK;
+}

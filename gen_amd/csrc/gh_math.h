@@ -1,0 +1,253 @@
+// gh_math.h — deterministic fp64 math + counter-based RNG shared by the HIP
+// kernels and the host-side preprocessing of libgen_hip.so.
+//
+// Why this exists: the reference draws randomness from Julia's task-global RNG
+// (src/modeling_library/distributions/normal.jl:96 `mu + std * randn()`,
+// src/inference/particle_filter.jl:200 `Distributions.rand!(Categorical(..))`),
+// which is neither reproducible across processes nor partitionable across
+// GPUs.  The engine replaces it with Philox4x32-10 keyed by (seed) and
+// countered by (global particle id, step, stream, draw), so a particle's
+// randomness does not depend on launch geometry or on how many GPUs share the
+// particle set.  Every transcendental on the sampling path (exp/log/sin/cos)
+// is evaluated with the explicit, IEEE-basic-op-only algorithms below so that
+// the GPU path and the CPU oracle produce bit-identical particle states, and
+// therefore bit-identical resampling ancestors.  Only +,-,*,/,sqrt,fma and
+// rint are used (all correctly rounded on gfx950 and x86-64); the build uses
+// -ffp-contract=off so the compiler cannot fuse a*b+c behind our back.
+//
+// The written specification of every function here is DESIGN.md §4.
+#pragma once
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define GH_HD __host__ __device__ __forceinline__
+#else
+#define GH_HD static inline
+#endif
+
+namespace gh {
+
+// ---------------------------------------------------------------- bit casts
+GH_HD double as_f64(uint64_t u) { return __builtin_bit_cast(double, u); }
+GH_HD uint64_t as_u64(double d) { return __builtin_bit_cast(uint64_t, d); }
+
+// ------------------------------------------------------------ Philox4x32-10
+// Salmon et al., "Parallel random numbers: as easy as 1, 2, 3" (SC'11).
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+GH_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+GH_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t hi0 = mulhi32(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = mulhi32(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+  }
+  return c;
+}
+
+// Stream identifiers (counter word w, high 16 bits).  DESIGN.md §4.2.
+enum : uint32_t {
+  STREAM_INIT = 1,       // latent draws of generate() at the first step
+  STREAM_STEP = 2,       // latent draws of update() at steps t >= 2
+  STREAM_RESAMPLE = 3,   // systematic offset / multinomial positions
+  STREAM_SAMPLE = 4,     // sample_unweighted_traces
+  STREAM_IS = 5,         // importance sampling
+  STREAM_MH = 6,         // MH proposals / accept tests
+};
+
+GH_HD u32x4 rng_block(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream,
+                      uint32_t draw) {
+  return philox4x32_10(u32x4{(uint32_t)id, (uint32_t)(id >> 32), step, (stream << 16) | draw},
+                       (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// 53-bit integer from two words, and the uniform in [0,1) it encodes.
+GH_HD uint64_t u53_bits(uint32_t a, uint32_t b) {
+  return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6);
+}
+GH_HD double u53(uint32_t a, uint32_t b) { return (double)u53_bits(a, b) * 0x1p-53; }
+
+// ------------------------------------------------------------------- exp
+// Cody–Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-13 Taylor in r.
+GH_HD double ldexp_exact(double p, int k) {
+  // p in [0.5, 2); multiply by 2^k without relying on libm ldexp.
+  if (k > -1022 && k < 1024) return p * as_f64((uint64_t)(k + 1023) << 52);
+  if (k >= 1024) return (p * 0x1p1023) * 2.0;  // k == 1024 only
+  // k <= -1022: two exact-then-rounding multiplies (deterministic IEEE).
+  return (p * as_f64((uint64_t)(k + 600 + 1023) << 52)) * 0x1p-600;
+}
+
+GH_HD double gh_exp(double x) {
+  if (x != x) return x;
+  if (x < -745.5) return 0.0;
+  if (x > 709.78) return INFINITY;
+  const double k = rint(x * 0x1.71547652b82fep+0);
+  double r = fma(-k, 0x1.62e42fee00000p-1, x);
+  r = fma(-k, 0x1.a39ef35793c76p-33, r);
+  double p = 0x1.6124613a86d09p-33;  // 1/13!
+  p = fma(p, r, 0x1.1eed8eff8d898p-29);
+  p = fma(p, r, 0x1.ae64567f544e4p-26);
+  p = fma(p, r, 0x1.27e4fb7789f5cp-22);
+  p = fma(p, r, 0x1.71de3a556c734p-19);
+  p = fma(p, r, 0x1.a01a01a01a01ap-16);
+  p = fma(p, r, 0x1.a01a01a01a01ap-13);
+  p = fma(p, r, 0x1.6c16c16c16c17p-10);
+  p = fma(p, r, 0x1.1111111111111p-7);
+  p = fma(p, r, 0x1.5555555555555p-5);
+  p = fma(p, r, 0x1.5555555555555p-3);
+  p = fma(p, r, 0x1.0000000000000p-1);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp_exact(p, (int)k);
+}
+
+// ------------------------------------------------------------------- log
+// fdlibm e_log.c structure: x = 2^k m, m in [sqrt2/2, sqrt2), f = m-1,
+// s = f/(2+f), log(1+f) = f - hfsq + s (hfsq + R(s^2)).
+GH_HD double gh_log(double x) {
+  if (x != x || x < 0.0) return NAN;
+  if (x == 0.0) return -INFINITY;
+  if (x == INFINITY) return x;
+  int k = 0;
+  uint64_t bits = as_u64(x);
+  if (bits < 0x0010000000000000ull) {  // subnormal
+    x *= 0x1p54;
+    k = -54;
+    bits = as_u64(x);
+  }
+  k += (int)(bits >> 52) - 1023;
+  double m = as_f64((bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+  if (m > 0x1.6a09e667f3bcdp+0) {
+    m *= 0.5;
+    k += 1;
+  }
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+  const double t2 = z * (6.666666666666735130e-01 +
+                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+
+// --------------------------------------------------------- sin/cos kernels
+// Taylor polynomials on |x| <= pi/4.
+GH_HD double sin_kernel(double x) {
+  const double x2 = x * x;
+  double p = -0x1.ae7f3e733b81fp-41;  // -1/15!
+  p = fma(p, x2, 0x1.6124613a86d09p-33);  //  1/13!
+  p = fma(p, x2, -0x1.ae64567f544e4p-26);  // -1/11!
+  p = fma(p, x2, 0x1.71de3a556c734p-19);   //  1/9!
+  p = fma(p, x2, -0x1.a01a01a01a01ap-13);  // -1/7!
+  p = fma(p, x2, 0x1.1111111111111p-7);    //  1/5!
+  p = fma(p, x2, -0x1.5555555555555p-3);   // -1/3!
+  return fma(x * x2, p, x);
+}
+GH_HD double cos_kernel(double x) {
+  const double x2 = x * x;
+  double p = 0x1.ae7f3e733b81fp-45;        //  1/16!
+  p = fma(p, x2, -0x1.93974a8c07c9dp-37);  // -1/14!
+  p = fma(p, x2, 0x1.1eed8eff8d898p-29);   //  1/12!
+  p = fma(p, x2, -0x1.27e4fb7789f5cp-22);  // -1/10!
+  p = fma(p, x2, 0x1.a01a01a01a01ap-16);   //  1/8!
+  p = fma(p, x2, -0x1.6c16c16c16c17p-10);  // -1/6!
+  p = fma(p, x2, 0x1.5555555555555p-5);    //  1/4!
+  p = fma(p, x2, -0x1.0000000000000p-1);   // -1/2!
+  return fma(x2, p, 1.0);
+}
+
+// sin(2*pi*u), cos(2*pi*u) for u in [0,1) (u a multiple of 2^-53).
+GH_HD void sincos_2pi(double u, double* s, double* c) {
+  const double v = u * 8.0;               // exact
+  const double o = floor(v);              // octant 0..7
+  const double f = v - o;                 // exact, in [0,1)
+  const int oi = (int)o;
+  double ss, cc;
+  if (oi & 1) {
+    const double b = (1.0 - f) * 0x1.921fb54442d18p-1;  // 1-f exact
+    ss = cos_kernel(b);
+    cc = sin_kernel(b);
+  } else {
+    const double a = f * 0x1.921fb54442d18p-1;
+    ss = sin_kernel(a);
+    cc = cos_kernel(a);
+  }
+  switch (oi >> 1) {
+    case 0: *s = ss; *c = cc; break;
+    case 1: *s = cc; *c = -ss; break;
+    case 2: *s = -ss; *c = -cc; break;
+    default: *s = -cc; *c = ss; break;
+  }
+}
+
+// cos(x) for moderate |x| (< 2^19 * pi/2): fdlibm three-part pi/2 reduction.
+GH_HD double gh_cos(double x) {
+  const double k = rint(x * 0x1.45f306dc9c883p-1);  // 2/pi
+  double r = fma(-k, 1.57079632673412561417e+00, x);
+  r = fma(-k, 6.07710050630396597660e-11, r);
+  r = fma(-k, 2.02226624871116645580e-21, r);
+  const int q = ((int)k) & 3;
+  switch (q) {
+    case 0: return cos_kernel(r);
+    case 1: return -sin_kernel(r);
+    case 2: return -cos_kernel(r);
+    default: return sin_kernel(r);
+  }
+}
+
+// ------------------------------------------------------------ normals
+// Box–Muller on one Philox block: two standard normals.
+GH_HD void normal_pair(u32x4 w, double* z0, double* z1) {
+  const double u1 = 1.0 - u53(w.x, w.y);  // (0, 1]
+  const double u2 = u53(w.z, w.w);        // [0, 1)
+  const double r = sqrt(-2.0 * gh_log(u1));
+  double s, c;
+  sincos_2pi(u2, &s, &c);
+  *z0 = r * c;
+  *z1 = r * s;
+}
+
+// (u53 * S) >> 53 without overflow: floor(u * S) for the integer CDF.
+GH_HD uint64_t scale_u53(uint64_t u, uint64_t S) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t lo = u * S;
+  const uint64_t hi = __umul64hi(u, S);
+#else
+  const unsigned __int128 p = (unsigned __int128)u * S;
+  const uint64_t lo = (uint64_t)p, hi = (uint64_t)(p >> 64);
+#endif
+  return (hi << 11) | (lo >> 53);
+}
+
+// Integer weight quantisation shift for N particles: q = floor(e * 2^shift).
+GH_HD int quant_shift(uint64_t n_global) {
+  int lg = 0;
+  while ((1ull << lg) < n_global) ++lg;
+  int s = 62 - lg;
+  return s > 52 ? 52 : s;
+}
+
+GH_HD uint64_t quantize_weight(double lw, double M, int shift) {
+  const double e = gh_exp(lw - M);  // in [0, 1]
+  return (uint64_t)(e * as_f64((uint64_t)(shift + 1023) << 52));
+}
+
+constexpr double LOG_2PI = 0x1.d67f1c864beb4p+0;
+
+}  // namespace gh

@@ -1,0 +1,222 @@
+// gh_models.h — the model families the engine lowers to device code.
+//
+// Each family is the hand-lowered form of one Static-DSL model wrapped in an
+// Unfold combinator.  The per-particle functions are exactly what Gen's
+// generated code computes for one particle:
+//
+//   init(..)  = generate(model, (1, ...), obs_1)       static_ir/generate.jl:24-43
+//               constrained choice  -> weight += logpdf (generate.jl:31-34)
+//               unconstrained choice-> value = random   (generate.jl:35-37)
+//   step(..)  = update(trace, (t, ...), (UnknownChange(),), obs_t) restricted to
+//               the newly appended Unfold application (unfold/update.jl:54-78):
+//               sample the new latent from the prior, weight = logpdf(obs | latent)
+//
+// With the "optimal" proposal the weight is model_weight - proposal_score
+// (particle_filter.jl:79-91,139-154 via trace_translators.jl:775-802), which
+// for a categorical latent collapses to log sum_z p(z|z_prev) p(x|z).
+//
+// The arithmetic (operation order, explicit fma) is the specification in
+// DESIGN.md §5 and is mirrored by oracle/gh_oracle.c.
+#pragma once
+#include "gh_math.h"
+
+namespace gh {
+
+constexpr int kMaxObs = 32;
+
+// per-step observation, passed by value in the kernel arguments
+struct StepObs {
+  double v[kMaxObs];  // LGSSM: L_R^{-1}(y - c); Kitagawa: y; HMM: symbol
+  double ct;          // Kitagawa: 8 cos(1.2 t)
+  int present;
+  int sym;            // HMM symbol (integer copy of v[0])
+};
+
+// ------------------------------------------------------------------ LGSSM
+struct LGParams {
+  const double* A;    // d*d
+  const double* b;    // d
+  const double* LQ;   // d*d lower Cholesky factor of Q
+  const double* M;    // dy*d  L_R^{-1} H
+  const double* mu0;  // d
+  const double* L0;   // d*d lower Cholesky factor of P0
+  int dy;
+  double cstR;        // -0.5 (dy log 2pi + log det R)
+};
+
+template <int D>
+struct LGModel {
+  static constexpr int kD = D;
+  using Params = LGParams;
+
+  __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, uint32_t stream,
+                                 double* z) {
+#pragma unroll
+    for (int j = 0; 2 * j < D; ++j) {
+      double a, b;
+      normal_pair(rng_block(seed, pid, step, stream, (uint32_t)j), &a, &b);
+      z[2 * j] = a;
+      if (2 * j + 1 < D) z[2 * j + 1] = b;
+    }
+  }
+
+  // mvnormal(H x + c, R) logpdf with the Cholesky factor applied on the host
+  __device__ static double obs(const Params& p, const StepObs& o, const double* x) {
+    if (!o.present) return 0.0;
+    double quad = 0.0;
+    for (int r = 0; r < p.dy; ++r) {
+      double acc = o.v[r];
+#pragma unroll
+      for (int j = 0; j < D; ++j) acc = fma(-p.M[r * D + j], x[j], acc);
+      quad = fma(acc, acc, quad);
+    }
+    return p.cstR - 0.5 * quad;
+  }
+
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                int /*proposal*/, double* x) {
+    double z[D + 1];
+    normals(seed, pid, 1, STREAM_INIT, z);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = p.mu0[i];
+#pragma unroll
+      for (int k = 0; k <= i; ++k) acc = fma(p.L0[i * D + k], z[k], acc);
+      x[i] = acc;
+    }
+    return obs(p, o, x);
+  }
+
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                uint32_t t, int /*proposal*/, const double* xp, double* x) {
+    double z[D + 1];
+    normals(seed, pid, t, STREAM_STEP, z);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = p.b[i];
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc = fma(p.A[i * D + k], xp[k], acc);
+#pragma unroll
+      for (int k = 0; k <= i; ++k) acc = fma(p.LQ[i * D + k], z[k], acc);
+      x[i] = acc;
+    }
+    return obs(p, o, x);
+  }
+};
+
+// -------------------------------------------------------------------- HMM
+struct HMMParams {
+  const double* prior;  // k
+  const double* T;      // k*k, T[new*k + prev]
+  const double* E;      // v*k, E[x*k + z]
+  const double* logE;   // v*k
+  int k;
+  int v;
+};
+
+// inverse-CDF categorical draw over p[0], p[stride], ... (sequential sums)
+__device__ __forceinline__ int cat_sample(const double* p, int K, int stride, double u) {
+  double total = 0.0;
+  for (int k = 0; k < K; ++k) total += p[k * stride];
+  const double target = u * total;
+  double cum = 0.0;
+  int last = -1;
+  for (int k = 0; k < K; ++k) {
+    const double pk = p[k * stride];
+    cum += pk;
+    if (pk > 0.0) last = k;
+    if (cum > target && pk > 0.0) return k;
+  }
+  return last;
+}
+
+// draw from p_k = a[k*sa] * e[k] without storing p (locally optimal proposal)
+__device__ __forceinline__ int cat_sample_prod(const double* a, int sa, const double* e, int K,
+                                               double u, double* total_out) {
+  double total = 0.0;
+  for (int k = 0; k < K; ++k) total += a[k * sa] * e[k];
+  *total_out = total;
+  const double target = u * total;
+  double cum = 0.0;
+  int last = -1;
+  for (int k = 0; k < K; ++k) {
+    const double pk = a[k * sa] * e[k];
+    cum += pk;
+    if (pk > 0.0) last = k;
+    if (cum > target && pk > 0.0) return k;
+  }
+  return last;
+}
+
+struct HMMModel {
+  static constexpr int kD = 1;
+  using Params = HMMParams;
+
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                int proposal, double* x) {
+    const u32x4 w = rng_block(seed, pid, 1, STREAM_INIT, 0);
+    const double u = u53(w.x, w.y);
+    if (proposal == 1 && o.present) {
+      double total;
+      const int z = cat_sample_prod(p.prior, 1, p.E + o.sym * p.k, p.k, u, &total);
+      x[0] = (double)z;
+      return gh_log(total);
+    }
+    const int z = cat_sample(p.prior, p.k, 1, u);
+    x[0] = (double)z;
+    return o.present ? p.logE[o.sym * p.k + z] : 0.0;
+  }
+
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                uint32_t t, int proposal, const double* xp, double* x) {
+    const u32x4 w = rng_block(seed, pid, t, STREAM_STEP, 0);
+    const double u = u53(w.x, w.y);
+    const int zp = (int)xp[0];
+    if (proposal == 1 && o.present) {
+      double total;
+      const int z = cat_sample_prod(p.T + zp, p.k, p.E + o.sym * p.k, p.k, u, &total);
+      x[0] = (double)z;
+      return gh_log(total);
+    }
+    const int z = cat_sample(p.T + zp, p.k, p.k, u);
+    x[0] = (double)z;
+    return o.present ? p.logE[o.sym * p.k + z] : 0.0;
+  }
+};
+
+// --------------------------------------------------------------- Kitagawa
+struct KitParams {
+  double mu1, s1;   // x_1 ~ normal(mu1, s1)
+  double sx;        // sqrt(var_x)
+  double inv2vy;    // 1 / (2 var_y)
+  double csty;      // -0.5 log(2 pi var_y)
+};
+
+struct KitModel {
+  static constexpr int kD = 1;
+  using Params = KitParams;
+
+  __device__ static double obs(const Params& p, const StepObs& o, double x) {
+    if (!o.present) return 0.0;
+    const double diff = o.v[0] - x * x / 20.0;
+    return -(diff * diff) * p.inv2vy + p.csty;
+  }
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                int /*proposal*/, double* x) {
+    double z0, z1;
+    normal_pair(rng_block(seed, pid, 1, STREAM_INIT, 0), &z0, &z1);
+    x[0] = p.mu1 + p.s1 * z0;
+    return obs(p, o, x[0]);
+  }
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                uint32_t t, int /*proposal*/, const double* xp, double* x) {
+    double z0, z1;
+    normal_pair(rng_block(seed, pid, t, STREAM_STEP, 0), &z0, &z1);
+    const double v = xp[0];
+    const double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
+    x[0] = mean + p.sx * z0;
+    return obs(p, o, x[0]);
+  }
+};
+
+}  // namespace gh

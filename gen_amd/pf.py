@@ -1,0 +1,404 @@
+"""Gen's particle-filter API over libgen_hip.so.
+
+Same names, argument meaning and error behaviour as
+src/inference/particle_filter.jl (Julia `!` dropped from the names):
+
+    initialize_particle_filter(model, model_args, observations, num_particles)     :99-108
+    initialize_particle_filter(model, model_args, observations, proposal, (), N)   :79-91
+    particle_filter_step(state, new_args, argdiffs, observations[, proposal, args]):139-180
+    maybe_resample(state, ess_threshold=N/2, verbose=False) -> bool               :189-213
+    log_ml_estimate(state)                                                          :52-55
+    get_traces / get_log_weights / sample_unweighted_traces                         :31-70
+    importance_sampling(model, model_args, observations, N)     src/inference/importance.jl:20-52
+    importance_resampling(model, model_args, observations, N)   src/inference/importance.jl:70-85
+
+Every per-particle loop runs on the GPU; this module only translates
+Gen-style arguments (tuples, choice maps, argdiffs) into gh_* calls.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import byref, c_double, c_int, c_int64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from .choicemap import ChoiceMap
+from .models import Model
+
+
+# ------------------------------------------------------------------ argdiffs
+class NoChange:  # src/diff.jl:39
+    def __repr__(self):
+        return "NoChange()"
+
+
+class UnknownChange:  # src/diff.jl:46
+    def __repr__(self):
+        return "UnknownChange()"
+
+
+class OptimalProposal:
+    """The locally optimal proposal (categorical HMM): q(z_t) ∝ p(z_t|z_{t-1}) p(x_t|z_t).
+    Stands for the reference test's `init_proposal` / `step_proposal`
+    (test/inference/particle_filter.jl:104-127)."""
+
+
+# ------------------------------------------------------------------ context
+class Context:
+    """One GPU (and, for multi-GPU, one rank of an RCCL communicator)."""
+
+    def __init__(self, device: int | None = None, rank: int = 0, world: int = 1, unique_id: bytes | None = None):
+        lib = _lib.load()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        self.device = device
+        h = c_void_p()
+        if world > 1:
+            if unique_id is None or len(unique_id) != 128:
+                raise ValueError("multi-rank context needs the 128-byte RCCL unique id")
+            buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+            _lib.check(lib.gh_ctx_create_dist(device, rank, world, buf, None, byref(h)))
+        else:
+            _lib.check(lib.gh_ctx_create(device, None, byref(h)))
+        self.h = h
+        self.rank, self.world = rank, world
+        self._models = {}
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        _lib.check(_lib.load().gh_comm_unique_id(buf))
+        return bytes(buf)
+
+    def model_handle(self, model: Model):
+        key = id(model)
+        if key not in self._models:
+            desc, keep = model.desc()
+            h = c_void_p()
+            _lib.check(_lib.load().gh_model_create(self.h, byref(desc), byref(h)))
+            self._models[key] = (h, model, keep)
+        return self._models[key][0]
+
+    def stream(self) -> int:
+        s = c_void_p()
+        _lib.check(_lib.load().gh_ctx_stream(self.h, byref(s)))
+        return s.value or 0
+
+    def synchronize(self):
+        _lib.check(_lib.load().gh_ctx_synchronize(self.h))
+
+    def close(self):
+        if self.h:
+            lib = _lib.load()
+            for h, _, _ in self._models.values():
+                lib.gh_model_destroy(h)
+            self._models.clear()
+            lib.gh_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_DEFAULT_CTX: Context | None = None
+
+
+def default_context() -> Context:
+    global _DEFAULT_CTX
+    if _DEFAULT_CTX is None:
+        _DEFAULT_CTX = Context()
+    return _DEFAULT_CTX
+
+
+def set_default_context(ctx: Context) -> None:
+    global _DEFAULT_CTX
+    _DEFAULT_CTX = ctx
+
+
+# ------------------------------------------------------------- observations
+def _step_obs(model: Model, t: int, observations) -> tuple[_lib.Obs, np.ndarray | None]:
+    """The gh_obs of step t from a ChoiceMap / dict / array / None."""
+    val = None
+    if observations is None:
+        val = None
+    elif isinstance(observations, (ChoiceMap, dict)):
+        cm = observations if isinstance(observations, ChoiceMap) else ChoiceMap(observations)
+        addr = model.obs_address(t)
+        for a, _ in cm:
+            if a != addr:
+                # Any other constrained address would update or delete an
+                # existing choice, which the PF step forbids
+                # (particle_filter.jl:168-170) or the model does not have.
+                raise _lib.GenHipError(
+                    2, f"constraint at {a}: only {addr} may be constrained in step {t} (discard must be empty)"
+                )
+        val = cm.get(addr)
+    else:
+        val = observations
+    if val is None:
+        return _lib.Obs(None, 0, 0), None
+    arr = model.obs_values(val)
+    return _lib.Obs(_lib.dptr(arr), arr.size, 1), arr
+
+
+def _proposal_code(proposal) -> int:
+    if proposal is None:
+        return _lib.PROPOSAL_DEFAULT
+    if proposal is OptimalProposal or isinstance(proposal, OptimalProposal) or proposal == "optimal":
+        return _lib.PROPOSAL_OPTIMAL
+    raise _lib.GenHipError(1, f"unsupported proposal {proposal!r}: the engine lowers the model's default "
+                              "proposal and the locally optimal proposal")
+
+
+# ------------------------------------------------------------------- state
+class ParticleFilterState:
+    """Mirror of `ParticleFilterState{U}` (particle_filter.jl:18-24) whose
+    traces, weights and parents live in HBM as structure-of-arrays."""
+
+    def __init__(self, ctx: Context, model: Model, handle, num_particles: int):
+        self.ctx, self.model, self.h = ctx, model, handle
+        self.num_particles = num_particles
+        ng, nl, lo = c_int64(), c_int64(), c_int64()
+        _lib.check(_lib.load().gh_pf_num_particles(handle, byref(ng), byref(nl), byref(lo)))
+        self.n_local, self.first = nl.value, lo.value
+
+    @property
+    def t(self) -> int:
+        t = c_int()
+        _lib.check(_lib.load().gh_pf_num_steps(self.h, byref(t)))
+        return t.value
+
+    def close(self):
+        if self.h:
+            _lib.load().gh_pf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # accessors ---------------------------------------------------------
+    @property
+    def log_weights(self) -> np.ndarray:
+        return get_log_weights(self)
+
+    @property
+    def parents(self) -> np.ndarray:
+        out = np.empty(self.n_local, dtype=np.int64)
+        _lib.check(_lib.load().gh_pf_get_parents(self.h, out.ctypes.data_as(ctypes.POINTER(c_int64))))
+        return out
+
+    def states(self, t: int | None = None) -> np.ndarray:
+        """[n_local, d] latent of step t (default: current) along each particle's genealogy."""
+        d = self.model.d
+        out = np.empty((d, self.n_local), dtype=np.float64)
+        lib = _lib.load()
+        if t is None:
+            _lib.check(lib.gh_pf_get_states(self.h, _lib.dptr(out)))
+        else:
+            _lib.check(lib.gh_pf_get_trajectory(self.h, int(t), _lib.dptr(out)))
+        return out.T.copy()
+
+    def ess_history(self):
+        T = self.t
+        ess = np.empty(T)
+        did = np.empty(T, dtype=np.int32)
+        _lib.check(_lib.load().gh_pf_get_ess_history(self.h, T, _lib.dptr(ess),
+                                                     did.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+        return ess, did.astype(bool)
+
+    def kernel_time_ms(self, reset: bool = False) -> tuple[float, int]:
+        ms, n = c_double(), c_int64()
+        _lib.check(_lib.load().gh_pf_kernel_time(self.h, byref(ms), byref(n), int(reset)))
+        return ms.value, n.value
+
+
+class ParticleTraces:
+    """`get_traces(state)`: the particles' traces, materialised lazily from the
+    SoA history.  `traces[i][addr]` reads one choice; `traces.column(addr)`
+    reads an address across all particles."""
+
+    def __init__(self, state: ParticleFilterState):
+        self.state = state
+        self._cache = {}
+
+    def __len__(self):
+        return self.state.n_local
+
+    def _step_of(self, addr):
+        m = self.state.model
+        for t in range(1, self.state.t + 1):
+            if m.latent_address(t) == addr:
+                return t, "latent"
+            if m.obs_address(t) == addr:
+                return t, "obs"
+        raise KeyError(addr)
+
+    def column(self, addr) -> np.ndarray:
+        t, kind = self._step_of(tuple(addr))
+        if kind == "obs":
+            raise KeyError(f"{addr} is an observation; it is constrained to the same value in every trace")
+        if t not in self._cache:
+            self._cache[t] = self.state.states(t)
+        col = self._cache[t]
+        return col[:, 0] if col.shape[1] == 1 else col
+
+    def __getitem__(self, i):
+        return _TraceView(self, int(i))
+
+
+class _TraceView:
+    def __init__(self, traces: ParticleTraces, i: int):
+        self.traces, self.i = traces, i
+
+    def __getitem__(self, addr):
+        return self.traces.column(addr)[self.i]
+
+
+# --------------------------------------------------------------- the API
+def _opts(resampler: str, record_history: bool, history_capacity: int, time_kernels: bool) -> _lib.PFOpts:
+    o = _lib.PFOpts()
+    _lib.load().gh_pf_opts_default(byref(o))
+    o.resampler = {"systematic": _lib.RESAMPLE_SYSTEMATIC, "multinomial": _lib.RESAMPLE_MULTINOMIAL}[resampler]
+    o.record_history = int(record_history)
+    o.history_capacity = int(history_capacity)
+    o.time_kernels = int(time_kernels)
+    return o
+
+
+def initialize_particle_filter(model: Model, model_args: tuple, observations, *args, seed: int = 0,
+                               resampler: str = "systematic", record_history: bool = True,
+                               history_capacity: int = 0, time_kernels: bool = False,
+                               ctx: Context | None = None) -> ParticleFilterState:
+    """initialize_particle_filter(model, model_args, observations, num_particles)
+    initialize_particle_filter(model, model_args, observations, proposal, proposal_args, num_particles)"""
+    if len(args) == 1:
+        proposal, num_particles = None, args[0]
+    elif len(args) == 3:
+        proposal, _, num_particles = args
+    else:
+        raise TypeError("expected (num_particles) or (proposal, proposal_args, num_particles)")
+    if tuple(model_args)[:1] not in ((1,), ()):
+        raise _lib.GenHipError(1, "the particle filter starts at model_args = (1,)")
+    ctx = ctx or default_context()
+    mh = ctx.model_handle(model)
+    obs, keep = _step_obs(model, 1, observations)
+    h = c_void_p()
+    opts = _opts(resampler, record_history, history_capacity, time_kernels)
+    _lib.check(_lib.load().gh_pf_init(mh, byref(obs), _proposal_code(proposal), int(num_particles),
+                                      int(seed) & 0xFFFFFFFFFFFFFFFF, byref(opts), byref(h)))
+    del keep
+    return ParticleFilterState(ctx, model, h, int(num_particles))
+
+
+def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: tuple, observations,
+                         proposal=None, proposal_args: tuple = ()) -> None:
+    t = state.t + 1
+    if tuple(new_args)[:1] != (t,):
+        raise _lib.GenHipError(1, f"new_args must extend the Unfold by one step: expected ({t},), got {new_args}")
+    if argdiffs and not isinstance(argdiffs[0], UnknownChange):
+        raise _lib.GenHipError(1, "the length argument changes: its argdiff must be UnknownChange()")
+    obs, keep = _step_obs(state.model, t, observations)
+    _lib.check(_lib.load().gh_pf_step(state.h, byref(obs), _proposal_code(proposal)))
+    del keep
+
+
+def maybe_resample(state: ParticleFilterState, ess_threshold: float | None = None, verbose: bool = False) -> bool:
+    thr = state.num_particles / 2 if ess_threshold is None else float(ess_threshold)
+    did, ess = c_int(), c_double()
+    _lib.check(_lib.load().gh_pf_maybe_resample(state.h, thr, byref(did), byref(ess)))
+    if verbose:
+        print(f"effective sample size: {ess.value}, doing resample: {bool(did.value)}")
+    return bool(did.value)
+
+
+def maybe_resample_async(state: ParticleFilterState, ess_threshold: float | None = None) -> None:
+    """maybe_resample! whose decision stays on the device (no host round trip)."""
+    thr = state.num_particles / 2 if ess_threshold is None else float(ess_threshold)
+    _lib.check(_lib.load().gh_pf_maybe_resample(state.h, thr, None, None))
+
+
+def run_particle_filter(state: ParticleFilterState, observations_per_step, ess_threshold: float | None = None,
+                        proposal=None) -> None:
+    """The reference caller loop {maybe_resample!; particle_filter_step!} over
+    the given per-step observations (arrays or None), enqueued without host sync."""
+    model = state.model
+    t0 = state.t
+    keep = []
+    arr = (_lib.Obs * max(1, len(observations_per_step)))()
+    for i, v in enumerate(observations_per_step):
+        if v is None:
+            arr[i] = _lib.Obs(None, 0, 0)
+        else:
+            a = model.obs_values(v)
+            keep.append(a)
+            arr[i] = _lib.Obs(_lib.dptr(a), a.size, 1)
+    thr = state.num_particles / 2 if ess_threshold is None else float(ess_threshold)
+    _lib.check(_lib.load().gh_pf_run(state.h, len(observations_per_step), arr, _proposal_code(proposal), thr))
+    del keep, t0
+
+
+def log_ml_estimate(state: ParticleFilterState) -> float:
+    out = c_double()
+    _lib.check(_lib.load().gh_pf_log_ml_estimate(state.h, byref(out)))
+    return out.value
+
+
+def get_log_weights(state: ParticleFilterState) -> np.ndarray:
+    out = np.empty(state.n_local, dtype=np.float64)
+    _lib.check(_lib.load().gh_pf_get_log_weights(state.h, _lib.dptr(out)))
+    return out
+
+
+def get_traces(state: ParticleFilterState) -> ParticleTraces:
+    return ParticleTraces(state)
+
+
+def sample_unweighted_traces(state: ParticleFilterState, num_samples: int, seed: int = 0):
+    """Indices (and views) of num_samples traces drawn ∝ normalised weights."""
+    idx = np.empty(int(num_samples), dtype=np.int64)
+    _lib.check(_lib.load().gh_pf_sample_unweighted(state.h, int(num_samples), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                                   idx.ctypes.data_as(ctypes.POINTER(c_int64))))
+    tr = get_traces(state)
+    return [tr[i] for i in idx], idx
+
+
+def importance_sampling(model: Model, model_args: tuple, observations, *args, seed: int = 0,
+                        ctx: Context | None = None):
+    """(traces, log_normalized_weights, lml_est) (importance.jl:20-52)."""
+    if len(args) == 1:
+        proposal, n = None, args[0]
+    elif len(args) == 3:
+        proposal, _, n = args
+    else:
+        raise TypeError("expected (num_samples) or (proposal, proposal_args, num_samples)")
+    ctx = ctx or default_context()
+    mh = ctx.model_handle(model)
+    obs, keep = _step_obs(model, 1, observations)
+    lnw = np.empty(int(n))
+    states = np.empty((model.d, int(n)))
+    lml = c_double()
+    _lib.check(_lib.load().gh_is_run(mh, byref(obs), _proposal_code(proposal), int(n), int(seed),
+                                     _lib.dptr(lnw), _lib.dptr(states), byref(lml)))
+    del keep
+    return states.T.copy(), lnw, lml.value
+
+
+def importance_resampling(model: Model, model_args: tuple, observations, *args, seed: int = 0,
+                          ctx: Context | None = None):
+    """(trace, lml_est) (importance.jl:70-108).  The reference's streaming SIR
+    keeps one candidate with probability w_i / sum_{j<=i} w_j; the draw here
+    is the distribution-equivalent single categorical draw over all N weights
+    (SURVEY.md Appendix A.8)."""
+    states, lnw, lml = importance_sampling(model, model_args, observations, *args, seed=seed, ctx=ctx)
+    w = np.exp(lnw - lnw.max())
+    rng = np.random.default_rng(seed)
+    i = int(rng.choice(w.size, p=w / w.sum()))
+    return states[i], lml

@@ -1,0 +1,169 @@
+/* gen_hip.h — C ABI of libgen_hip.so, the MI355X particle-inference engine.
+ *
+ * This is the drop-in boundary for Gen's sequential-Monte-Carlo hot path.
+ * The reference has no FFI: its interface is Julia multiple dispatch on
+ * `ParticleFilterState{U}` and the generative-function interface (GFI).  Each
+ * entry point below replaces one reference function; the Julia `ccall`
+ * binding a maintainer adds is spelled out in INTEGRATION.md.
+ *
+ *   gh_pf_init              initialize_particle_filter   src/inference/particle_filter.jl:79-108
+ *   gh_pf_step              particle_filter_step!        src/inference/particle_filter.jl:139-180
+ *   gh_pf_maybe_resample    maybe_resample!              src/inference/particle_filter.jl:189-213
+ *   gh_pf_log_ml_estimate   log_ml_estimate              src/inference/particle_filter.jl:52-55
+ *   gh_pf_get_log_weights   get_log_weights              src/inference/particle_filter.jl:43-45
+ *   gh_pf_get_states /
+ *   gh_pf_get_trajectory    get_traces (SoA columns)     src/inference/particle_filter.jl:31-34
+ *   gh_pf_get_parents       ParticleFilterState.parents  src/inference/particle_filter.jl:23
+ *   gh_pf_sample_unweighted sample_unweighted_traces     src/inference/particle_filter.jl:62-70
+ *   gh_is_run               importance_sampling          src/inference/importance.jl:20-52
+ *   gh_model_create         a Static-DSL model + Unfold  src/static_ir/, src/modeling_library/unfold/
+ *
+ * Conventions
+ *  - Every function returns an int status (GH_OK = 0); the message of the
+ *    last failure on this thread is gh_last_error().  Julia's `error(...)`
+ *    sites map to status codes (see gh_status).
+ *  - Handles are opaque; the library owns all device memory.  Host inputs are
+ *    copied at call time, outputs are written into caller-allocated buffers.
+ *  - Particle indices are 0-based (Julia's are 1-based).
+ *  - A gh_pf is driven by one host thread (as the reference's mutable state is);
+ *    distinct handles may run concurrently on distinct streams.
+ *  - Multi-GPU: one process per GPU.  Create the context with
+ *    gh_ctx_create_dist(); particles [rank*n/world, (rank+1)*n/world) live on
+ *    each rank and every gh_pf_* call is collective over the ranks.
+ */
+#ifndef GEN_HIP_H
+#define GEN_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  GH_OK = 0,
+  GH_E_INVAL = 1,    /* bad argument (cf. unfold.jl:57-61 negative length, vector.jl:110) */
+  GH_E_DISCARD = 2,  /* a constraint hit an existing choice inside a PF step (particle_filter.jl:168-170) */
+  GH_E_NUMERIC = 3,  /* all log-weights -Inf / NaN (Categorical with NaN probabilities) */
+  GH_E_NOMEM = 4,
+  GH_E_HIP = 5,
+  GH_E_RCCL = 6,
+  GH_E_STATE = 7     /* call out of order (e.g. step before init) */
+} gh_status;
+
+typedef enum {
+  /* x_1 ~ mvnormal(mu0, P0); x_t ~ mvnormal(A x_{t-1} + b, Q); y_t ~ mvnormal(H x_t + c, R)
+     params (row-major doubles): A[d*d] b[d] Q[d*d] H[dy*d] c[dy] R[dy*dy] mu0[d] P0[d*d]
+     supported d: 1..8, 10, 12, 16; dy <= 32 */
+  GH_FAMILY_LGSSM = 1,
+  /* categorical HMM (test/inference/particle_filter.jl:50-78):
+     z_1 ~ categorical(prior); z_t ~ categorical(T[:, z_{t-1}]); x_t ~ categorical(E[:, z_t])
+     params: prior[k] T[k*k] (T[new*k + prev]) E[v*k] (E[x*k + z]); k <= 64 */
+  GH_FAMILY_HMM = 2,
+  /* nonlinear "Kitagawa" SSM (examples/pmmh/model.jl:9-13,40-46):
+     x_1 ~ normal(mu1, s1); x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sqrt(var_x));
+     y_t ~ normal(x_t^2/20, sqrt(var_y));  params: mu1 s1 var_x var_y */
+  GH_FAMILY_KITAGAWA = 3
+} gh_family;
+
+typedef enum { GH_RESAMPLE_SYSTEMATIC = 0, GH_RESAMPLE_MULTINOMIAL = 1 } gh_resampler;
+
+typedef enum {
+  GH_PROPOSAL_DEFAULT = 0, /* the model's internal proposal (prior) */
+  GH_PROPOSAL_OPTIMAL = 1  /* locally optimal proposal (HMM only), the custom proposal
+                              of test/inference/particle_filter.jl:104-127 */
+} gh_proposal;
+
+typedef struct gh_ctx gh_ctx;
+typedef struct gh_model gh_model;
+typedef struct gh_pf gh_pf;
+
+typedef struct {
+  int32_t family; /* gh_family */
+  int32_t d;      /* latent dimension (LGSSM) */
+  int32_t dy;     /* observation dimension (LGSSM) */
+  int32_t k;      /* number of hidden states (HMM) */
+  int32_t v;      /* number of observation symbols (HMM) */
+  const double* params;
+  int64_t n_params;
+} gh_model_desc;
+
+/* The observations of one step: the value(s) at address :chain => t => :y.
+   values == NULL or present == 0 means "no observation at this step". */
+typedef struct {
+  const double* values;
+  int32_t n_values;
+  int32_t present;
+} gh_obs;
+
+typedef struct {
+  int32_t resampler;      /* gh_resampler */
+  int32_t record_history; /* 1: keep every step's states + genealogy (Gen trace semantics) */
+  int32_t history_capacity; /* steps to preallocate when record_history (0 = grow) */
+  int32_t block_size;     /* 0 = default (256) */
+  int32_t time_kernels;   /* 1: time every step kernel with hipEvents (gh_pf_kernel_time) */
+  int32_t reserved[3];
+} gh_pf_opts;
+
+/* ---- context ------------------------------------------------------------ */
+int gh_ctx_create(int device, void* hip_stream /* NULL = own stream */, gh_ctx** out);
+int gh_comm_unique_id(uint8_t id[128]);
+int gh_ctx_create_dist(int device, int rank, int world, const uint8_t id[128], void* hip_stream,
+                       gh_ctx** out);
+int gh_ctx_destroy(gh_ctx* ctx);
+int gh_ctx_rank(const gh_ctx* ctx, int* rank, int* world);
+int gh_ctx_stream(const gh_ctx* ctx, void** hip_stream);
+int gh_ctx_synchronize(gh_ctx* ctx);
+
+/* ---- models --------------------------------------------------------------- */
+int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model** out);
+int gh_model_destroy(gh_model* m);
+int gh_model_state_dim(const gh_model* m, int* d);
+
+/* ---- particle filter -------------------------------------------------------- */
+void gh_pf_opts_default(gh_pf_opts* o);
+int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles, uint64_t seed,
+               const gh_pf_opts* opts, gh_pf** out);
+int gh_pf_destroy(gh_pf* pf);
+int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal);
+/* ess_threshold <= 0 (or NaN) means N/2.  If did_resample/ess are non-NULL the
+   call synchronises and reports them; otherwise the decision stays on the
+   device and the call is asynchronous. */
+int gh_pf_maybe_resample(gh_pf* pf, double ess_threshold, int* did_resample, double* ess);
+/* run {maybe_resample!; particle_filter_step!} for n_steps consecutive steps
+   (the reference caller loop, test/inference/particle_filter.jl:157-162),
+   observations obs[0..n_steps-1]; no host synchronisation inside. */
+int gh_pf_run(gh_pf* pf, int n_steps, const gh_obs* obs, int proposal, double ess_threshold);
+int gh_pf_log_ml_estimate(gh_pf* pf, double* out);
+int gh_pf_num_particles(const gh_pf* pf, int64_t* n_global, int64_t* n_local, int64_t* first);
+int gh_pf_num_steps(const gh_pf* pf, int* t);
+int gh_pf_get_log_weights(gh_pf* pf, double* host_out /* n_local */);
+int gh_pf_get_states(gh_pf* pf, double* host_out /* [d][n_local] current latent */);
+int gh_pf_get_parents(gh_pf* pf, int64_t* host_out /* n_local, global ids */);
+/* latent of step t (1-based) of the current particles' traces: follows the
+   genealogy back from the current step (record_history required) */
+int gh_pf_get_trajectory(gh_pf* pf, int t, double* host_out /* [d][n_local] */);
+int gh_pf_sample_unweighted(gh_pf* pf, int64_t n_samples, uint64_t seed, int64_t* host_idx);
+/* per-step resampling record: ess and did_resample for steps 1..t */
+int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int32_t* did);
+/* average duration (ms) of the step kernel over the timed launches (opts.time_kernels) */
+int gh_pf_kernel_time(gh_pf* pf, double* avg_ms, int64_t* n_launches, int reset);
+
+/* ---- importance sampling ---------------------------------------------------- */
+int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t seed,
+              double* host_log_norm_weights /* may be NULL */, double* host_states /* may be NULL */,
+              double* lml);
+
+/* ---- diagnostics ------------------------------------------------------------ */
+const char* gh_last_error(void);
+const char* gh_version(void);
+/* device self-test: evaluates gh_exp/gh_log/sqrt/div/normals on n inputs on the
+   GPU so tests can compare them bit-for-bit with the CPU oracle */
+int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double* out_exp, double* out_log,
+                     double* out_sqrt, double* out_div);
+int gh_selftest_normals(gh_ctx* ctx, uint64_t seed, int64_t n, uint32_t step, uint32_t stream,
+                        int dim, double* out /* [n][dim] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

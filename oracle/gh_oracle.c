@@ -1,0 +1,686 @@
+/* gh_oracle.c — CPU restatement of Gen's particle-filter hot path.
+ * TEST INFRASTRUCTURE ONLY (see gh_oracle.h for the scope statement and the
+ * reference file:line map).  Plain C11, scalar, single thread.
+ *
+ * Build: oracle/Makefile (gcc -O2 -mfma -ffp-contract=off).  -ffp-contract=off
+ * is required: every fused multiply-add in the specification
+ * is written explicitly as fma(), every other product/sum is rounded
+ * separately, exactly as in the HIP kernels.
+ */
+#include "gh_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ bits */
+static double f64_of(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
+static uint64_t u64_of(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
+
+/* ----------------------------------------------------------- Philox4x32 */
+static uint32_t mulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+  uint32_t k0 = key[0], k1 = key[1];
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    uint32_t h0 = mulhi(0xD2511F53u, c0), l0 = 0xD2511F53u * c0;
+    uint32_t h1 = mulhi(0xCD9E8D57u, c2), l1 = 0xCD9E8D57u * c2;
+    uint32_t n0 = h1 ^ c1 ^ k0, n2 = h0 ^ c3 ^ k1;
+    c0 = n0; c1 = l1; c2 = n2; c3 = l0;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+enum { S_INIT = 1, S_STEP = 2, S_RESAMPLE = 3, S_SAMPLE = 4, S_IS = 5, S_MH = 6 };
+
+static void rng(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, uint32_t draw,
+                uint32_t out[4]) {
+  uint32_t c[4] = {(uint32_t)id, (uint32_t)(id >> 32), step, (stream << 16) | draw};
+  uint32_t k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  orc_philox4x32_10(c, k, out);
+}
+static uint64_t bits53(uint32_t a, uint32_t b) { return ((uint64_t)(a >> 5) << 26) | (uint64_t)(b >> 6); }
+static double unif53(uint32_t a, uint32_t b) { return (double)bits53(a, b) * 0x1p-53; }
+
+/* ------------------------------------------------------------------ exp */
+static double scale2k(double p, int k) {
+  if (k > -1022 && k < 1024) return p * f64_of((uint64_t)(k + 1023) << 52);
+  if (k >= 1024) return (p * 0x1p1023) * 2.0;
+  return (p * f64_of((uint64_t)(k + 600 + 1023) << 52)) * 0x1p-600;
+}
+
+double orc_exp(double x) {
+  if (x != x) return x;
+  if (x < -745.5) return 0.0;
+  if (x > 709.78) return INFINITY;
+  double k = rint(x * 0x1.71547652b82fep+0);
+  double r = fma(-k, 0x1.62e42fee00000p-1, x);
+  r = fma(-k, 0x1.a39ef35793c76p-33, r);
+  static const double c[14] = {
+      1.0, 1.0, 0x1.0000000000000p-1, 0x1.5555555555555p-3, 0x1.5555555555555p-5,
+      0x1.1111111111111p-7, 0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-13, 0x1.a01a01a01a01ap-16,
+      0x1.71de3a556c734p-19, 0x1.27e4fb7789f5cp-22, 0x1.ae64567f544e4p-26, 0x1.1eed8eff8d898p-29,
+      0x1.6124613a86d09p-33};
+  double p = c[13];
+  for (int n = 12; n >= 0; --n) p = fma(p, r, c[n]);
+  return scale2k(p, (int)k);
+}
+
+/* ------------------------------------------------------------------ log */
+double orc_log(double x) {
+  if (x != x || x < 0.0) return NAN;
+  if (x == 0.0) return -INFINITY;
+  if (x == INFINITY) return x;
+  int k = 0;
+  uint64_t b = u64_of(x);
+  if (b < 0x0010000000000000ull) { x *= 0x1p54; k = -54; b = u64_of(x); }
+  k += (int)(b >> 52) - 1023;
+  double m = f64_of((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+  if (m > 0x1.6a09e667f3bcdp+0) { m *= 0.5; k += 1; }
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  double f = m - 1.0;
+  double s = f / (2.0 + f);
+  double z = s * s, w = z * z;
+  double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  double R = t2 + t1;
+  double hfsq = 0.5 * f * f;
+  double dk = (double)k;
+  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+
+/* -------------------------------------------------------------- sin/cos */
+static double ksin(double x) {
+  static const double c[7] = {-0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13,
+                              0x1.71de3a556c734p-19, -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33,
+                              -0x1.ae7f3e733b81fp-41};
+  double x2 = x * x, p = c[6];
+  for (int n = 5; n >= 0; --n) p = fma(p, x2, c[n]);
+  return fma(x * x2, p, x);
+}
+static double kcos(double x) {
+  static const double c[8] = {-0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10,
+                              0x1.a01a01a01a01ap-16, -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29,
+                              -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45};
+  double x2 = x * x, p = c[7];
+  for (int n = 6; n >= 0; --n) p = fma(p, x2, c[n]);
+  return fma(x2, p, 1.0);
+}
+
+void orc_sincos_2pi(double u, double* s, double* c) {
+  double v = u * 8.0, o = floor(v), f = v - o;
+  int oi = (int)o;
+  double ss, cc;
+  if (oi & 1) { double b = (1.0 - f) * 0x1.921fb54442d18p-1; ss = kcos(b); cc = ksin(b); }
+  else { double a = f * 0x1.921fb54442d18p-1; ss = ksin(a); cc = kcos(a); }
+  switch (oi >> 1) {
+    case 0: *s = ss; *c = cc; break;
+    case 1: *s = cc; *c = -ss; break;
+    case 2: *s = -ss; *c = -cc; break;
+    default: *s = -cc; *c = ss; break;
+  }
+}
+
+double orc_cos(double x) {
+  double k = rint(x * 0x1.45f306dc9c883p-1);
+  double r = fma(-k, 1.57079632673412561417e+00, x);
+  r = fma(-k, 6.07710050630396597660e-11, r);
+  r = fma(-k, 2.02226624871116645580e-21, r);
+  switch (((int)k) & 3) {
+    case 0: return kcos(r);
+    case 1: return -ksin(r);
+    case 2: return -kcos(r);
+    default: return ksin(r);
+  }
+}
+
+/* n standard normals for (id, step, stream): Box–Muller on Philox blocks */
+void orc_normals(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, int n, double* z) {
+  for (int j = 0; 2 * j < n; ++j) {
+    uint32_t w[4];
+    rng(seed, id, step, stream, (uint32_t)j, w);
+    double u1 = 1.0 - unif53(w[0], w[1]);
+    double u2 = unif53(w[2], w[3]);
+    double r = sqrt(-2.0 * orc_log(u1));
+    double s, c;
+    orc_sincos_2pi(u2, &s, &c);
+    z[2 * j] = r * c;
+    if (2 * j + 1 < n) z[2 * j + 1] = r * s;
+  }
+}
+
+static uint64_t scale_u53(uint64_t u, uint64_t S) {
+  unsigned __int128 p = (unsigned __int128)u * S;
+  return (uint64_t)(p >> 53);
+}
+static int qshift(uint64_t n) {
+  int lg = 0;
+  while ((1ull << lg) < n) ++lg;
+  int s = 62 - lg;
+  return s > 52 ? 52 : s;
+}
+static uint64_t quantize(double lw, double M, int shift) {
+  double e = orc_exp(lw - M);
+  return (uint64_t)(e * f64_of((uint64_t)(shift + 1023) << 52));
+}
+
+double orc_normal_logpdf(double x, double mu, double std) {
+  /* normal.jl:56-60, literally */
+  double var = std * std;
+  double diff = x - mu;
+  return -(diff * diff) / (2.0 * var) - 0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * var);
+}
+
+/* ------------------------------------------------------- linear algebra */
+/* Cholesky–Banachiewicz, row-major, lower factor in L (full d*d storage). */
+static int chol(int d, const double* S, double* L) {
+  memset(L, 0, sizeof(double) * d * d);
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j <= i; ++j) {
+      double s = S[i * d + j];
+      for (int k = 0; k < j; ++k) s = fma(-L[i * d + k], L[j * d + k], s);
+      if (i == j) {
+        if (!(s > 0.0)) return -1;
+        L[i * d + i] = sqrt(s);
+      } else {
+        L[i * d + j] = s / L[j * d + j];
+      }
+    }
+  return 0;
+}
+/* Y = L^{-1} B for B (d x m) row-major */
+static void fwdsub(int d, int m, const double* L, const double* B, double* Y) {
+  for (int c = 0; c < m; ++c)
+    for (int i = 0; i < d; ++i) {
+      double s = B[i * m + c];
+      for (int k = 0; k < i; ++k) s = fma(-L[i * d + k], Y[k * m + c], s);
+      Y[i * m + c] = s / L[i * d + i];
+    }
+}
+static double gauss_cst(int d, const double* L) {
+  double acc = 0.0;
+  for (int i = 0; i < d; ++i) acc += orc_log(L[i * d + i]);
+  double logdet = 2.0 * acc;
+  return -0.5 * ((double)d * 0x1.d67f1c864beb4p+0 + logdet);
+}
+
+/* ----------------------------------------------------------- the models */
+typedef struct {
+  int family, d, dy, k, v;
+  /* LGSSM */
+  double *A, *b, *LQ, *M, *LR, *c, *mu0, *L0, cstR;
+  /* HMM */
+  double *prior, *T, *E, *logE;
+  /* Kitagawa */
+  double mu1, s1, sx, inv2vy, csty;
+} model_t;
+
+static void model_free(model_t* m) {
+  free(m->A); free(m->b); free(m->LQ); free(m->M); free(m->LR); free(m->c); free(m->mu0);
+  free(m->L0); free(m->prior); free(m->T); free(m->E); free(m->logE);
+}
+
+static int model_build(model_t* m, int family, int d, int dy, int k, int v, const double* p,
+                       int64_t np) {
+  memset(m, 0, sizeof(*m));
+  m->family = family; m->d = d; m->dy = dy; m->k = k; m->v = v;
+  if (family == ORC_LGSSM) {
+    int64_t need = (int64_t)d * d + d + (int64_t)d * d + (int64_t)dy * d + dy + (int64_t)dy * dy + d + (int64_t)d * d;
+    if (np < need) return -1;
+    const double *A = p, *b = A + d * d, *Q = b + d, *H = Q + d * d, *c = H + dy * d, *R = c + dy,
+                 *mu0 = R + dy * dy, *P0 = mu0 + d;
+    m->A = malloc(sizeof(double) * d * d); memcpy(m->A, A, sizeof(double) * d * d);
+    m->b = malloc(sizeof(double) * d); memcpy(m->b, b, sizeof(double) * d);
+    m->LQ = malloc(sizeof(double) * d * d);
+    if (chol(d, Q, m->LQ)) return -2;
+    m->LR = malloc(sizeof(double) * dy * dy);
+    if (chol(dy, R, m->LR)) return -2;
+    m->M = malloc(sizeof(double) * dy * d);
+    fwdsub(dy, d, m->LR, H, m->M);
+    m->c = malloc(sizeof(double) * dy); memcpy(m->c, c, sizeof(double) * dy);
+    m->mu0 = malloc(sizeof(double) * d); memcpy(m->mu0, mu0, sizeof(double) * d);
+    m->L0 = malloc(sizeof(double) * d * d);
+    if (chol(d, P0, m->L0)) return -2;
+    m->cstR = gauss_cst(dy, m->LR);
+  } else if (family == ORC_HMM) {
+    if (np < (int64_t)k + (int64_t)k * k + (int64_t)v * k) return -1;
+    m->d = 1;
+    m->prior = malloc(sizeof(double) * k); memcpy(m->prior, p, sizeof(double) * k);
+    m->T = malloc(sizeof(double) * k * k); memcpy(m->T, p + k, sizeof(double) * k * k);
+    m->E = malloc(sizeof(double) * v * k); memcpy(m->E, p + k + k * k, sizeof(double) * v * k);
+    m->logE = malloc(sizeof(double) * v * k);
+    for (int i = 0; i < v * k; ++i) m->logE[i] = orc_log(m->E[i]);
+  } else if (family == ORC_KITAGAWA) {
+    if (np < 4) return -1;
+    m->d = 1;
+    m->mu1 = p[0]; m->s1 = p[1];
+    m->sx = sqrt(p[2]);
+    m->inv2vy = 1.0 / (2.0 * p[3]);
+    m->csty = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * p[3]);
+  } else {
+    return -1;
+  }
+  return 0;
+}
+
+/* per-step host preprocessing of the observation */
+typedef struct {
+  int present;
+  double bt[64];  /* LGSSM: L_R^{-1}(y - c); Kitagawa: y; HMM: symbol */
+  double ct;      /* Kitagawa: 8 cos(1.2 t) */
+} obs_t;
+
+static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* o) {
+  o->present = has;
+  o->ct = 0.0;
+  if (m->family == ORC_KITAGAWA) o->ct = 8.0 * orc_cos(1.2 * (double)t);
+  if (!has) return;
+  if (m->family == ORC_LGSSM) {
+    double r[64];
+    for (int i = 0; i < m->dy; ++i) r[i] = y[i] - m->c[i];
+    fwdsub(m->dy, 1, m->LR, r, o->bt);
+  } else {
+    o->bt[0] = y[0];
+  }
+}
+
+static double lgssm_obs(const model_t* m, const double* x, const obs_t* o) {
+  if (!o->present) return 0.0;
+  double quad = 0.0;
+  for (int r = 0; r < m->dy; ++r) {
+    double acc = o->bt[r];
+    for (int j = 0; j < m->d; ++j) acc = fma(-m->M[r * m->d + j], x[j], acc);
+    quad = fma(acc, acc, quad);
+  }
+  return m->cstR - 0.5 * quad;
+}
+
+static int cat_sample(const double* p, int K, int stride, double u) {
+  double total = 0.0;
+  for (int k = 0; k < K; ++k) total += p[k * stride];
+  double target = u * total;
+  double cum = 0.0;
+  int last = -1;
+  for (int k = 0; k < K; ++k) {
+    double pk = p[k * stride];
+    cum += pk;
+    if (pk > 0.0) last = k;
+    if (cum > target && pk > 0.0) return k;
+  }
+  return last;
+}
+
+/* generate at t = 1: writes x[d], returns the log weight */
+static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
+                            int proposal, double* x) {
+  if (m->family == ORC_LGSSM) {
+    double z[64];
+    orc_normals(seed, pid, 1, S_INIT, m->d, z);
+    for (int i = 0; i < m->d; ++i) {
+      double acc = m->mu0[i];
+      for (int k = 0; k <= i; ++k) acc = fma(m->L0[i * m->d + k], z[k], acc);
+      x[i] = acc;
+    }
+    return lgssm_obs(m, x, o);
+  } else if (m->family == ORC_KITAGAWA) {
+    double z[2];
+    orc_normals(seed, pid, 1, S_INIT, 1, z);
+    x[0] = m->mu1 + m->s1 * z[0];
+    if (!o->present) return 0.0;
+    double diff = o->bt[0] - x[0] * x[0] / 20.0;
+    return -(diff * diff) * m->inv2vy + m->csty;
+  } else {
+    uint32_t w[4];
+    rng(seed, pid, 1, S_INIT, 0, w);
+    double u = unif53(w[0], w[1]);
+    int K = m->k;
+    if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
+      int xs = (int)o->bt[0];
+      double p[64];
+      for (int kk = 0; kk < K; ++kk) p[kk] = m->prior[kk] * m->E[xs * K + kk];
+      double total = 0.0;
+      for (int kk = 0; kk < K; ++kk) total += p[kk];
+      x[0] = (double)cat_sample(p, K, 1, u);
+      return orc_log(total);
+    }
+    int z = cat_sample(m->prior, K, 1, u);
+    x[0] = (double)z;
+    return o->present ? m->logE[(int)o->bt[0] * K + z] : 0.0;
+  }
+}
+
+/* update at step t >= 2 from previous latent xp: writes x, returns increment */
+static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t,
+                            const obs_t* o, int proposal, const double* xp, double* x) {
+  if (m->family == ORC_LGSSM) {
+    double z[64];
+    orc_normals(seed, pid, t, S_STEP, m->d, z);
+    int d = m->d;
+    for (int i = 0; i < d; ++i) {
+      double acc = m->b[i];
+      for (int k = 0; k < d; ++k) acc = fma(m->A[i * d + k], xp[k], acc);
+      for (int k = 0; k <= i; ++k) acc = fma(m->LQ[i * d + k], z[k], acc);
+      x[i] = acc;
+    }
+    return lgssm_obs(m, x, o);
+  } else if (m->family == ORC_KITAGAWA) {
+    double z[2];
+    orc_normals(seed, pid, t, S_STEP, 1, z);
+    double v = xp[0];
+    double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o->ct;
+    x[0] = mean + m->sx * z[0];
+    if (!o->present) return 0.0;
+    double diff = o->bt[0] - x[0] * x[0] / 20.0;
+    return -(diff * diff) * m->inv2vy + m->csty;
+  } else {
+    uint32_t w[4];
+    rng(seed, pid, t, S_STEP, 0, w);
+    double u = unif53(w[0], w[1]);
+    int K = m->k, zp = (int)xp[0];
+    if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
+      int xs = (int)o->bt[0];
+      double p[64];
+      for (int kk = 0; kk < K; ++kk) p[kk] = m->T[kk * K + zp] * m->E[xs * K + kk];
+      double total = 0.0;
+      for (int kk = 0; kk < K; ++kk) total += p[kk];
+      x[0] = (double)cat_sample(p, K, 1, u);
+      return orc_log(total);
+    }
+    int z = cat_sample(m->T + zp, K, K, u);
+    x[0] = (double)z;
+    return o->present ? m->logE[(int)o->bt[0] * K + z] : 0.0;
+  }
+}
+
+/* ---------------------------------------------------------- PF state */
+struct orc_pf {
+  model_t m;
+  int64_t n_global, lo, n;
+  uint64_t seed;
+  int resampler, record_history;
+  int t;                /* number of completed steps (1 after init) */
+  double* x;            /* [d][n] current */
+  double* xprev;        /* [d][n] scratch */
+  double* logw;
+  int64_t* anc;         /* pending ancestors (global ids) */
+  double* anc_state;    /* [d][n] ancestor states after a (distributed) resample */
+  int pending;          /* resampled since the last step */
+  double log_ml_est;
+  /* history */
+  int cap;
+  double** hx;
+  int32_t** hanc;
+  int* hres;
+};
+
+orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* params, int64_t np,
+                      int64_t n_global, int64_t lo, int64_t n_local, uint64_t seed, int resampler,
+                      int record_history) {
+  orc_pf* pf = calloc(1, sizeof(orc_pf));
+  if (model_build(&pf->m, family, d, dy, k, v, params, np)) { model_free(&pf->m); free(pf); return NULL; }
+  pf->n_global = n_global; pf->lo = lo; pf->n = n_local; pf->seed = seed;
+  pf->resampler = resampler; pf->record_history = record_history;
+  int D = pf->m.d;
+  pf->x = calloc((size_t)D * n_local, sizeof(double));
+  pf->xprev = calloc((size_t)D * n_local, sizeof(double));
+  pf->anc_state = calloc((size_t)D * n_local, sizeof(double));
+  pf->logw = calloc((size_t)n_local, sizeof(double));
+  pf->anc = calloc((size_t)n_local, sizeof(int64_t));
+  return pf;
+}
+
+void orc_pf_destroy(orc_pf* pf) {
+  if (!pf) return;
+  for (int i = 0; i < pf->cap; ++i) { free(pf->hx[i]); free(pf->hanc[i]); }
+  free(pf->hx); free(pf->hanc); free(pf->hres);
+  free(pf->x); free(pf->xprev); free(pf->anc_state); free(pf->logw); free(pf->anc);
+  model_free(&pf->m);
+  free(pf);
+}
+
+static void record(orc_pf* pf) {
+  if (!pf->record_history) return;
+  int t = pf->t;  /* 1-based step just completed */
+  if (t > pf->cap) {
+    int nc = pf->cap ? pf->cap * 2 : 16;
+    while (nc < t) nc *= 2;
+    pf->hx = realloc(pf->hx, sizeof(double*) * nc);
+    pf->hanc = realloc(pf->hanc, sizeof(int32_t*) * nc);
+    pf->hres = realloc(pf->hres, sizeof(int) * nc);
+    for (int i = pf->cap; i < nc; ++i) { pf->hx[i] = NULL; pf->hanc[i] = NULL; pf->hres[i] = 0; }
+    pf->cap = nc;
+  }
+  size_t sz = (size_t)pf->m.d * pf->n;
+  pf->hx[t - 1] = malloc(sizeof(double) * sz);
+  memcpy(pf->hx[t - 1], pf->x, sizeof(double) * sz);
+}
+
+int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+  obs_t o;
+  obs_build(&pf->m, 1, obs, has_obs, &o);
+  int D = pf->m.d;
+  double x[64];
+  for (int64_t i = 0; i < pf->n; ++i) {
+    pf->logw[i] = particle_init(&pf->m, pf->seed, (uint64_t)(pf->lo + i), &o, proposal, x);
+    for (int k = 0; k < D; ++k) pf->x[(size_t)k * pf->n + i] = x[k];
+    pf->anc[i] = pf->lo + i;
+  }
+  pf->t = 1;
+  pf->pending = 0;
+  pf->log_ml_est = 0.0;
+  record(pf);
+  return 0;
+}
+
+int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+  uint32_t t = (uint32_t)(pf->t + 1);
+  obs_t o;
+  obs_build(&pf->m, (int)t, obs, has_obs, &o);
+  int D = pf->m.d;
+  int64_t n = pf->n;
+  double* src = pf->pending ? pf->anc_state : pf->x;
+  memcpy(pf->xprev, src, sizeof(double) * D * n);
+  double xp[64], x[64];
+  for (int64_t i = 0; i < n; ++i) {
+    for (int k = 0; k < D; ++k) xp[k] = pf->xprev[(size_t)k * n + i];
+    double inc = particle_step(&pf->m, pf->seed, (uint64_t)(pf->lo + i), t, &o, proposal, xp, x);
+    for (int k = 0; k < D; ++k) pf->x[(size_t)k * n + i] = x[k];
+    pf->logw[i] = (pf->pending ? 0.0 : pf->logw[i]) + inc;
+  }
+  int was = pf->pending;
+  pf->pending = 0;
+  pf->t = (int)t;
+  record(pf);
+  if (pf->record_history) {
+    pf->hres[t - 1] = was;
+    if (was) {
+      pf->hanc[t - 1] = malloc(sizeof(int32_t) * n);
+      for (int64_t i = 0; i < n; ++i) pf->hanc[t - 1][i] = (int32_t)pf->anc[i];
+    }
+  }
+  return 0;
+}
+
+void orc_pf_local_stats(orc_pf* pf, double out[3]) {
+  double M = -INFINITY;
+  for (int64_t i = 0; i < pf->n; ++i) {
+    double w = pf->pending ? 0.0 : pf->logw[i];
+    if (w > M) M = w;
+  }
+  double S = 0.0, S2 = 0.0;
+  if (M > -INFINITY) {
+    for (int64_t i = 0; i < pf->n; ++i) {
+      double w = pf->pending ? 0.0 : pf->logw[i];
+      double e = orc_exp(w - M);
+      S += e;
+      S2 += e * e;
+    }
+  }
+  out[0] = M; out[1] = S; out[2] = S2;
+}
+
+/* combine per-rank (max, S, S2) in rank order; decision ess < thr */
+int orc_combine_stats(const double* st, int R, int64_t n_global, double thr, double* L, double* ess,
+                      double* Mout) {
+  double M = -INFINITY;
+  for (int r = 0; r < R; ++r) if (st[3 * r] > M) M = st[3 * r];
+  if (!(M > -INFINITY) || M != M || M == INFINITY) { *L = M; *ess = NAN; *Mout = M; return -1; }
+  double S = 0.0, S2 = 0.0;
+  for (int r = 0; r < R; ++r) {
+    if (!(st[3 * r] > -INFINITY)) continue;
+    double e = orc_exp(st[3 * r] - M);
+    S += st[3 * r + 1] * e;
+    S2 += st[3 * r + 2] * (e * e);
+  }
+  *L = M + orc_log(S);
+  *ess = (S * S) / S2;
+  *Mout = M;
+  (void)n_global;
+  return *ess < thr;
+}
+
+uint64_t orc_pf_local_qtotal(orc_pf* pf, double M) {
+  int sh = qshift((uint64_t)pf->n_global);
+  uint64_t s = 0;
+  for (int64_t i = 0; i < pf->n; ++i) s += quantize(pf->pending ? 0.0 : pf->logw[i], M, sh);
+  return s;
+}
+
+/* target of global slot j in [0, S) */
+static uint64_t slot_target(const orc_pf* pf, uint64_t S, int64_t j, uint64_t o) {
+  if (pf->resampler == ORC_SYSTEMATIC) {
+    uint64_t N = (uint64_t)pf->n_global;
+    uint64_t Qs = S / N, Rs = S % N;
+    return (uint64_t)j * Qs + ((uint64_t)j * Rs + o) / N;
+  }
+  uint32_t w[4];
+  rng(pf->seed, (uint64_t)j, (uint32_t)pf->t, S_RESAMPLE, 0, w);
+  return scale_u53(bits53(w[0], w[1]), S);
+}
+
+int64_t orc_pf_resample_emit(orc_pf* pf, double M, const uint64_t* totals, int R, int rank,
+                             int64_t* slot_out, int64_t* anc_out, double* state_out) {
+  int sh = qshift((uint64_t)pf->n_global);
+  uint64_t base = 0, S = 0;
+  for (int r = 0; r < R; ++r) { if (r < rank) base += totals[r]; S += totals[r]; }
+  uint64_t mine = totals[rank];
+  /* inclusive local CDF */
+  uint64_t* C = malloc(sizeof(uint64_t) * (pf->n ? pf->n : 1));
+  uint64_t acc = 0;
+  for (int64_t i = 0; i < pf->n; ++i) {
+    acc += quantize(pf->pending ? 0.0 : pf->logw[i], M, sh);
+    C[i] = acc;
+  }
+  const double* xs = pf->pending ? pf->anc_state : pf->x;
+  uint64_t o = 0;
+  if (pf->resampler == ORC_SYSTEMATIC) {
+    uint32_t w[4];
+    rng(pf->seed, ~0ull, (uint32_t)pf->t, S_RESAMPLE, 0, w);
+    o = scale_u53(bits53(w[0], w[1]), S);
+  }
+  int D = pf->m.d;
+  int64_t cnt = 0;
+  for (int64_t j = 0; j < pf->n_global; ++j) {
+    uint64_t tg = slot_target(pf, S, j, o);
+    if (tg < base || tg >= base + mine) continue;
+    uint64_t lt = tg - base;
+    int64_t lo = 0, hi = pf->n - 1;
+    while (lo < hi) {  /* first i with C[i] > lt */
+      int64_t mid = lo + (hi - lo) / 2;
+      if (C[mid] > lt) hi = mid; else lo = mid + 1;
+    }
+    slot_out[cnt] = j;
+    anc_out[cnt] = pf->pending ? pf->anc[lo] : pf->lo + lo;
+    for (int k = 0; k < D; ++k) state_out[cnt * D + k] = xs[(size_t)k * pf->n + lo];
+    ++cnt;
+  }
+  free(C);
+  return cnt;
+}
+
+void orc_pf_resample_apply(orc_pf* pf, double L, int64_t count, const int64_t* slots,
+                           const int64_t* ancs, const double* states) {
+  int D = pf->m.d;
+  for (int64_t e = 0; e < count; ++e) {
+    int64_t i = slots[e] - pf->lo;
+    if (i < 0 || i >= pf->n) continue;
+    pf->anc[i] = ancs[e];
+    for (int k = 0; k < D; ++k) pf->anc_state[(size_t)k * pf->n + i] = states[e * D + k];
+  }
+  pf->log_ml_est += L - orc_log((double)pf->n_global);
+  pf->pending = 1;
+}
+
+int orc_pf_maybe_resample(orc_pf* pf, double thr, double* ess_out) {
+  double st[3], L, ess, M;
+  orc_pf_local_stats(pf, st);
+  int dec = orc_combine_stats(st, 1, pf->n_global, thr, &L, &ess, &M);
+  if (ess_out) *ess_out = ess;
+  if (dec < 0) return -1;
+  if (!dec) return 0;
+  uint64_t tot = orc_pf_local_qtotal(pf, M);
+  int64_t n = pf->n;
+  int D = pf->m.d;
+  int64_t* slots = malloc(sizeof(int64_t) * n);
+  int64_t* ancs = malloc(sizeof(int64_t) * n);
+  double* sts = malloc(sizeof(double) * n * D);
+  int64_t c = orc_pf_resample_emit(pf, M, &tot, 1, 0, slots, ancs, sts);
+  orc_pf_resample_apply(pf, L, c, slots, ancs, sts);
+  free(slots); free(ancs); free(sts);
+  return 1;
+}
+
+double orc_pf_log_ml_estimate(orc_pf* pf) {
+  double st[3], L, ess, M;
+  orc_pf_local_stats(pf, st);
+  orc_combine_stats(st, 1, pf->n_global, 0.0, &L, &ess, &M);
+  return pf->log_ml_est + L - orc_log((double)pf->n_global);
+}
+
+void orc_pf_get_log_weights(orc_pf* pf, double* out) {
+  for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->pending ? 0.0 : pf->logw[i];
+}
+void orc_pf_get_state(orc_pf* pf, double* out) {
+  double* src = pf->pending ? pf->anc_state : pf->x;
+  memcpy(out, src, sizeof(double) * pf->m.d * pf->n);
+}
+void orc_pf_get_parents(orc_pf* pf, int64_t* out) { memcpy(out, pf->anc, sizeof(int64_t) * pf->n); }
+int orc_pf_num_steps(orc_pf* pf) { return pf->t; }
+
+int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* resampled) {
+  if (!pf->record_history || t < 1 || t > pf->t) return -1;
+  memcpy(x_out, pf->hx[t - 1], sizeof(double) * pf->m.d * pf->n);
+  *resampled = (t >= 2) ? pf->hres[t - 1] : 0;
+  if (*resampled && anc_out) memcpy(anc_out, pf->hanc[t - 1], sizeof(int32_t) * pf->n);
+  return 0;
+}
+
+/* importance_sampling (importance.jl:20-52): generate N times at t=1,
+   normalise with logsumexp, lml = L - log N. */
+int orc_importance_sampling(int family, int d, int dy, int k, int v, const double* params,
+                            int64_t np, const double* obs, int has_obs, int proposal, int64_t n,
+                            uint64_t seed, double* lnw, double* states, double* lml) {
+  model_t m;
+  if (model_build(&m, family, d, dy, k, v, params, np)) { model_free(&m); return -1; }
+  obs_t o;
+  obs_build(&m, 1, obs, has_obs, &o);
+  double x[64];
+  double M = -INFINITY;
+  for (int64_t i = 0; i < n; ++i) {
+    lnw[i] = particle_init(&m, seed, (uint64_t)i, &o, proposal, x);
+    for (int kk = 0; kk < m.d; ++kk) states[(size_t)kk * n + i] = x[kk];
+    if (lnw[i] > M) M = lnw[i];
+  }
+  double S = 0.0;
+  for (int64_t i = 0; i < n; ++i) S += orc_exp(lnw[i] - M);
+  double L = M + orc_log(S);
+  for (int64_t i = 0; i < n; ++i) lnw[i] -= L;
+  *lml = L - orc_log((double)n);
+  model_free(&m);
+  return 0;
+}

@@ -1,0 +1,96 @@
+/* gh_oracle.h — CPU restatement of Gen's particle-filter hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is linked into, loaded by
+ * or called from the product (gen_amd/, libgen_hip.so).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg use it, as the
+ * checker / the CPU baseline.
+ *
+ * Parity status: pinned.  The restatement is checked (tests/test_oracle.py)
+ * against (a) the reference's own known-answer tests re-expressed as golden
+ * vectors in tests/golden/ (HMM forward algorithm hand enumeration,
+ * test/inference/particle_filter.jl:29-48; PF log-ML within atol 0.01 of the
+ * exact HMM forward log-ML at N=10000 with resampling every step,
+ * test/inference/particle_filter.jl:96-168; Unfold update/regenerate weight
+ * closed forms, test/modeling_library/unfold.jl:116-481), and (b) analytic
+ * oracles (Kalman-filter log-ML).  Gen.jl itself cannot run here (no Julia).
+ *
+ * Algorithm sources (reference file:line):
+ *   ParticleFilterState            src/inference/particle_filter.jl:18-24
+ *   initialize_particle_filter     src/inference/particle_filter.jl:79-108
+ *   particle_filter_step!          src/inference/particle_filter.jl:139-180
+ *   maybe_resample!                src/inference/particle_filter.jl:189-213
+ *   effective_sample_size          src/inference/particle_filter.jl:3-6
+ *   log_ml_estimate                src/inference/particle_filter.jl:52-55
+ *   logsumexp                      src/inference/inference.jl:3-6
+ *   normal logpdf / random         src/modeling_library/distributions/normal.jl:56-60,96
+ *   mvnormal logpdf / random       src/modeling_library/distributions/mvnormal.jl:12-16,30-33
+ *   categorical logpdf / random    src/modeling_library/distributions/categorical.jl:10-12,20-22
+ *   Unfold step semantics          src/modeling_library/unfold/update.jl:54-78
+ * RNG, transcendental and resampling arithmetic follow DESIGN.md §4 so that
+ * the GPU path can be compared bit-for-bit.
+ */
+#ifndef GH_ORACLE_H
+#define GH_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_LGSSM = 1, ORC_HMM = 2, ORC_KITAGAWA = 3 };
+enum { ORC_SYSTEMATIC = 0, ORC_MULTINOMIAL = 1 };
+enum { ORC_PROPOSAL_DEFAULT = 0, ORC_PROPOSAL_OPTIMAL = 1 };
+
+typedef struct orc_pf orc_pf;
+
+/* math primitives (exported so tests can check them against libm / KATs) */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+double orc_exp(double x);
+double orc_log(double x);
+double orc_cos(double x);
+void orc_sincos_2pi(double u, double* s, double* c);
+void orc_normals(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, int n, double* z);
+
+/* particle filter over particles [lo, lo+n_local) of a global set of n_global */
+orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* params, int64_t n_params,
+                      int64_t n_global, int64_t lo, int64_t n_local, uint64_t seed, int resampler,
+                      int record_history);
+void orc_pf_destroy(orc_pf* pf);
+int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal);
+int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal);
+/* single-rank maybe_resample!: returns 1/0, or -1 on numeric error */
+int orc_pf_maybe_resample(orc_pf* pf, double ess_threshold, double* ess_out);
+double orc_pf_log_ml_estimate(orc_pf* pf);
+void orc_pf_get_log_weights(orc_pf* pf, double* out);     /* n_local */
+void orc_pf_get_state(orc_pf* pf, double* out);           /* [d][n_local] */
+void orc_pf_get_parents(orc_pf* pf, int64_t* out);        /* n_local, global ids */
+int orc_pf_num_steps(orc_pf* pf);
+int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* resampled);
+
+/* distributed building blocks (sharded oracle, exercised with gloo) */
+void orc_pf_local_stats(orc_pf* pf, double out[3]);      /* (max, sum e, sum e^2) local */
+int orc_combine_stats(const double* stats, int R, int64_t n_global, double thr, double* L,
+                      double* ess, double* M);
+uint64_t orc_pf_local_qtotal(orc_pf* pf, double M);
+/* after the collectives: for every global slot j whose target falls in this
+   rank's CDF range, emit (j, ancestor global id, state[d]).  Returns count. */
+int64_t orc_pf_resample_emit(orc_pf* pf, double M, const uint64_t* totals, int R, int rank,
+                             int64_t* slot_out, int64_t* anc_out, double* state_out);
+/* install incoming (slot, anc, state) for this rank's own slots and mark the
+   resample as done; log_ml update is applied from (L) */
+void orc_pf_resample_apply(orc_pf* pf, double L, int64_t count, const int64_t* slots,
+                           const int64_t* ancs, const double* states);
+
+/* importance sampling (importance.jl:20-52) on the first step of a model */
+int orc_importance_sampling(int family, int d, int dy, int k, int v, const double* params,
+                            int64_t n_params, const double* obs, int has_obs, int proposal,
+                            int64_t n, uint64_t seed, double* log_norm_weights, double* states,
+                            double* lml);
+
+/* static weight helpers used by the golden-vector tests */
+double orc_normal_logpdf(double x, double mu, double std);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,237 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker.  Never imported by gen_amd/.
+See gh_oracle.h for what the oracle restates (reference file:line) and how
+it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+LGSSM, HMM, KITAGAWA = 1, 2, 3
+SYSTEMATIC, MULTINOMIAL = 0, 1
+DEFAULT, OPTIMAL = 0, 1
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "gh_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB_PATH)
+        D, I, I64, U64, U32, V = POINTER(c_double), c_int, c_int64, c_uint64, c_uint32, c_void_p
+        sig = {
+            "orc_philox4x32_10": (None, [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
+            "orc_exp": (c_double, [c_double]),
+            "orc_log": (c_double, [c_double]),
+            "orc_cos": (c_double, [c_double]),
+            "orc_sincos_2pi": (None, [c_double, D, D]),
+            "orc_normals": (None, [U64, U64, U32, U32, I, D]),
+            "orc_pf_create": (V, [I, I, I, I, I, D, I64, I64, I64, I64, U64, I, I]),
+            "orc_pf_destroy": (None, [V]),
+            "orc_pf_init": (I, [V, D, I, I]),
+            "orc_pf_step": (I, [V, D, I, I]),
+            "orc_pf_maybe_resample": (I, [V, c_double, D]),
+            "orc_pf_log_ml_estimate": (c_double, [V]),
+            "orc_pf_get_log_weights": (None, [V, D]),
+            "orc_pf_get_state": (None, [V, D]),
+            "orc_pf_get_parents": (None, [V, POINTER(c_int64)]),
+            "orc_pf_num_steps": (I, [V]),
+            "orc_pf_get_history": (I, [V, I, D, POINTER(c_int32), POINTER(c_int)]),
+            "orc_pf_local_stats": (None, [V, D]),
+            "orc_combine_stats": (I, [D, I, I64, c_double, D, D, D]),
+            "orc_pf_local_qtotal": (U64, [V, c_double]),
+            "orc_pf_resample_emit": (I64, [V, c_double, POINTER(c_uint64), I, I, POINTER(c_int64), POINTER(c_int64), D]),
+            "orc_pf_resample_apply": (None, [V, c_double, I64, POINTER(c_int64), POINTER(c_int64), D]),
+            "orc_importance_sampling": (I, [I, I, I, I, I, D, I64, D, I, I, I64, U64, D, D, D]),
+            "orc_normal_logpdf": (c_double, [c_double, c_double, c_double]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return None if a is None else a.ctypes.data_as(POINTER(c_double))
+
+
+def philox(ctr, key):
+    c = (c_uint32 * 4)(*ctr)
+    k = (c_uint32 * 2)(*key)
+    o = (c_uint32 * 4)()
+    lib().orc_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def normals(seed, id_, step, stream, n):
+    z = np.empty(n)
+    lib().orc_normals(seed, id_, step, stream, n, _d(z))
+    return z
+
+
+def model_args(model):
+    """(family, d, dy, k, v, params) from a gen_amd.models.Model (duck-typed)."""
+    p = np.ascontiguousarray(model.params(), dtype=np.float64)
+    return model.family, model.d, model.dy, model.k, model.v, p
+
+
+class OraclePF:
+    """CPU restatement of ParticleFilterState over particles [lo, lo+n_local)."""
+
+    def __init__(self, model, n_global, seed, resampler=SYSTEMATIC, lo=0, n_local=None, record_history=True):
+        fam, d, dy, k, v, p = model_args(model)
+        self._p = p
+        self.d = d if fam == LGSSM else 1
+        self.n_global = n_global
+        self.lo = lo
+        self.n = n_global if n_local is None else n_local
+        self.h = lib().orc_pf_create(fam, d, dy, k, v, _d(p), p.size, n_global, lo, self.n, seed, resampler,
+                                     int(record_history))
+        if not self.h:
+            raise ValueError("oracle: bad model parameters")
+        self.model = model
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_pf_destroy(self.h)
+            self.h = None
+
+    @staticmethod
+    def _obs(y):
+        if y is None:
+            return None, 0
+        a = np.ascontiguousarray(np.atleast_1d(np.asarray(y, dtype=np.float64)))
+        return a, 1
+
+    def init(self, y, proposal=DEFAULT):
+        a, has = self._obs(y)
+        lib().orc_pf_init(self.h, _d(a), has, proposal)
+
+    def step(self, y, proposal=DEFAULT):
+        a, has = self._obs(y)
+        lib().orc_pf_step(self.h, _d(a), has, proposal)
+
+    def maybe_resample(self, thr=None):
+        thr = self.n_global / 2 if thr is None else thr
+        ess = c_double()
+        r = lib().orc_pf_maybe_resample(self.h, thr, ctypes.byref(ess))
+        if r < 0:
+            raise FloatingPointError("oracle: all log-weights are -Inf/NaN")
+        return bool(r), ess.value
+
+    def log_ml_estimate(self):
+        return lib().orc_pf_log_ml_estimate(self.h)
+
+    def log_weights(self):
+        o = np.empty(self.n)
+        lib().orc_pf_get_log_weights(self.h, _d(o))
+        return o
+
+    def state(self):
+        o = np.empty((self.d, self.n))
+        lib().orc_pf_get_state(self.h, _d(o))
+        return o
+
+    def parents(self):
+        o = np.empty(self.n, dtype=np.int64)
+        lib().orc_pf_get_parents(self.h, o.ctypes.data_as(POINTER(c_int64)))
+        return o
+
+    def history(self, t):
+        x = np.empty((self.d, self.n))
+        anc = np.empty(self.n, dtype=np.int32)
+        res = c_int()
+        rc = lib().orc_pf_get_history(self.h, t, _d(x), anc.ctypes.data_as(POINTER(c_int32)), ctypes.byref(res))
+        if rc:
+            raise ValueError("no history")
+        return x, (anc if res.value else None)
+
+    def trajectory(self, t):
+        """latent of step t along the genealogy of the current particles (single rank)."""
+        T = lib().orc_pf_num_steps(self.h)
+        idx = np.arange(self.n)
+        for s in range(T, t, -1):
+            _, anc = self.history(s)
+            if anc is not None:
+                idx = anc[idx]
+        x, _ = self.history(t)
+        return x[:, idx]
+
+    # distributed building blocks
+    def local_stats(self):
+        o = np.empty(3)
+        lib().orc_pf_local_stats(self.h, _d(o))
+        return o
+
+    def qtotal(self, M):
+        return lib().orc_pf_local_qtotal(self.h, M)
+
+    def emit(self, M, totals, rank):
+        tot = np.ascontiguousarray(totals, dtype=np.uint64)
+        n = self.n_global
+        slots = np.empty(n, dtype=np.int64)
+        ancs = np.empty(n, dtype=np.int64)
+        st = np.empty(n * self.d)
+        c = lib().orc_pf_resample_emit(self.h, M, tot.ctypes.data_as(POINTER(c_uint64)), tot.size, rank,
+                                       slots.ctypes.data_as(POINTER(c_int64)), ancs.ctypes.data_as(POINTER(c_int64)),
+                                       _d(st))
+        return slots[:c].copy(), ancs[:c].copy(), st[: c * self.d].reshape(c, self.d).copy()
+
+    def apply(self, L, slots, ancs, states):
+        slots = np.ascontiguousarray(slots, dtype=np.int64)
+        ancs = np.ascontiguousarray(ancs, dtype=np.int64)
+        states = np.ascontiguousarray(states, dtype=np.float64)
+        lib().orc_pf_resample_apply(self.h, L, slots.size, slots.ctypes.data_as(POINTER(c_int64)),
+                                    ancs.ctypes.data_as(POINTER(c_int64)), _d(states))
+
+
+def combine_stats(stats, n_global, thr):
+    st = np.ascontiguousarray(stats, dtype=np.float64).ravel()
+    L, ess, M = c_double(), c_double(), c_double()
+    r = lib().orc_combine_stats(_d(st), st.size // 3, n_global, thr, ctypes.byref(L), ctypes.byref(ess),
+                                ctypes.byref(M))
+    return r, L.value, ess.value, M.value
+
+
+def importance_sampling(model, y, n, seed, proposal=DEFAULT):
+    fam, d, dy, k, v, p = model_args(model)
+    a = None if y is None else np.ascontiguousarray(np.atleast_1d(np.asarray(y, dtype=np.float64)))
+    dd = d if fam == LGSSM else 1
+    lnw = np.empty(n)
+    st = np.empty((dd, n))
+    lml = c_double()
+    rc = lib().orc_importance_sampling(fam, d, dy, k, v, _d(p), p.size, _d(a), int(a is not None), proposal, n, seed,
+                                       _d(lnw), _d(st), ctypes.byref(lml))
+    if rc:
+        raise ValueError("oracle IS failed")
+    return st, lnw, lml.value
+
+
+def run_pf(model, ys, n, seed, thr=None, resampler=SYSTEMATIC, proposal=DEFAULT, record_history=True):
+    """The reference caller loop (test/inference/particle_filter.jl:152-162)."""
+    pf = OraclePF(model, n, seed, resampler, record_history=record_history)
+    pf.init(ys[0], proposal)
+    for y in ys[1:]:
+        pf.maybe_resample(thr)
+        pf.step(y, proposal)
+    return pf

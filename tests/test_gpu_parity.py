@@ -1,0 +1,247 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar: particle states, log-weights and resampling ancestors
+bit-exact; log-ML within 1e-9 relative (north star: 1e-6) — the only
+non-bitwise quantity is the order of the floating-point weight sums.  At the
+full C2 size (N = 2^20, T = 100) the checks are size-independent: agreement
+with the exact Kalman log-ML within Monte-Carlo tolerance, sorted systematic
+ancestors, and oracle parity of the first steps.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import gen_amd as gen
+from gen_amd import _lib
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gold(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+# ---------------------------------------------------------------- math
+def test_device_math_is_bit_identical_to_oracle(gh_ctx):
+    lib = _lib.load()
+    rng = np.random.default_rng(0)
+    n = 200000
+    x = np.concatenate([rng.uniform(-745, 709, n // 4), rng.uniform(-1, 1, n // 4),
+                        np.exp(rng.uniform(-700, 700, n // 4)), rng.standard_normal(n // 4)])
+    x[:4] = [0.0, 1.0, 5e-324, -1e-310]
+    oe, ol, os_, od = (np.empty_like(x) for _ in range(4))
+    _lib.check(lib.gh_selftest_math(gh_ctx.h, x.size, _lib.dptr(x), _lib.dptr(oe), _lib.dptr(ol),
+                                    _lib.dptr(os_), _lib.dptr(od)))
+    L = O.lib()
+    ref_e = np.array([L.orc_exp(v) for v in x])
+    ref_l = np.array([L.orc_log(abs(v)) for v in x])
+    assert np.array_equal(oe.view(np.uint64), ref_e.view(np.uint64))
+    assert np.array_equal(ol.view(np.uint64), ref_l.view(np.uint64))
+    # IEEE sqrt and division: correctly rounded on both sides
+    assert np.array_equal(os_.view(np.uint64), np.sqrt(np.abs(x)).view(np.uint64))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        assert np.array_equal(od.view(np.uint64), (x / np.roll(x, -1)).view(np.uint64))
+
+
+def test_device_normals_are_bit_identical(gh_ctx):
+    lib = _lib.load()
+    n, dim = 4096, 10
+    out = np.empty((n, dim))
+    _lib.check(lib.gh_selftest_normals(gh_ctx.h, 12345, n, 7, 2, dim, _lib.dptr(out)))
+    ref = np.stack([O.normals(12345, i, 7, 2, dim) for i in range(n)])
+    assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
+
+
+# --------------------------------------------------------------- helpers
+def run_both(model, ys, n, seed, thr=None, resampler="systematic", proposal=None, check_every_step=True):
+    """Drive the GPU PF and the oracle through the reference caller loop,
+    comparing after every step."""
+    ores = O.SYSTEMATIC if resampler == "systematic" else O.MULTINOMIAL
+    oprop = O.OPTIMAL if proposal is not None else O.DEFAULT
+    st = gen.initialize_particle_filter(model, (1,), {model.obs_address(1): ys[0]}, *(
+        (proposal, (), n) if proposal is not None else (n,)), seed=seed, resampler=resampler)
+    orc = O.OraclePF(model, n, seed, ores)
+    orc.init(ys[0], oprop)
+    for t in range(2, len(ys) + 1):
+        did = gen.maybe_resample(st, thr)
+        odid, _ = orc.maybe_resample(thr)
+        assert did == odid, f"resample decision differs at t={t}"
+        gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {model.obs_address(t): ys[t - 1]}, proposal)
+        orc.step(ys[t - 1], oprop)
+        if check_every_step or t == len(ys):
+            assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64)), t
+            assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64)), t
+            assert np.array_equal(st.parents, orc.parents()), t
+    return st, orc
+
+
+def assert_lml_close(st, orc, rel=1e-9):
+    a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+    assert abs(a - b) <= rel * max(1.0, abs(b)), (a, b)
+
+
+# ------------------------------------------------------------------ LGSSM
+@pytest.mark.parametrize("d", [1, 2, 4, 10])
+@pytest.mark.parametrize("thr", [None, "always"])
+def test_lgssm_parity(gh_ctx, d, thr):
+    m = gen.LinearGaussianSSM.benchmark(d)
+    _, ys = m.simulate(16, np.random.default_rng(2))
+    n = 20011  # not a multiple of the block size
+    st, orc = run_both(m, ys, n, seed=42, thr=(n if thr == "always" else None))
+    assert_lml_close(st, orc)
+    # trajectories through the genealogy (get_traces of the Unfold history)
+    for t in (1, 5, 16):
+        assert np.array_equal(st.states(t).T, orc.trajectory(t)), t
+
+
+def test_lgssm_multinomial_parity(gh_ctx):
+    m = gen.LinearGaussianSSM.benchmark(3)
+    _, ys = m.simulate(10, np.random.default_rng(3))
+    st, orc = run_both(m, ys, 5000, seed=7, thr=5000, resampler="multinomial")
+    assert_lml_close(st, orc)
+
+
+def test_kitagawa_parity(gh_ctx):
+    m = gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(30, np.random.default_rng(3))
+    st, orc = run_both(m, ys, 65536, seed=1)
+    assert_lml_close(st, orc)
+
+
+def test_missing_observations(gh_ctx):
+    m = gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(8, np.random.default_rng(5))
+    ys = [y if t % 3 else None for t, y in enumerate(ys)]
+    st, orc = run_both(m, ys, 3000, seed=2, thr=2000)
+    assert_lml_close(st, orc)
+
+
+# -------------------------------------------------------------------- HMM
+@pytest.mark.parametrize("proposal", [None, gen.OptimalProposal])
+def test_hmm_reference_pf_test(gh_ctx, proposal):
+    """test/inference/particle_filter.jl:96-168 on the GPU: N=10000,
+    ess_threshold=10000 (resample every step), log-ML within 0.01 of the
+    exact forward algorithm; and bit-parity with the oracle."""
+    g = gold("hmm.json")["pf_test"]
+    m = gen.DiscreteHMM(g["prior"], np.array(g["transition"]), np.array(g["emission"]))
+    st, orc = run_both(m, g["obs"], g["num_particles"], seed=0, thr=g["ess_threshold"], proposal=proposal)
+    assert abs(gen.log_ml_estimate(st) - g["log_ml"]) < g["atol"]
+    assert_lml_close(st, orc)
+
+
+def test_hmm_large_n_converges(gh_ctx):
+    g = gold("hmm.json")["pf_test"]
+    m = gen.DiscreteHMM(g["prior"], np.array(g["transition"]), np.array(g["emission"]))
+    n = 1 << 22
+    st = gen.initialize_particle_filter(m, (1,), {("x_init",): g["obs"][0]}, n, seed=3)
+    for t in range(2, 5):
+        gen.maybe_resample(st, n)
+        gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {("chain", t - 1, "x"): g["obs"][t - 1]})
+    assert abs(gen.log_ml_estimate(st) - g["log_ml"]) < 2e-3
+
+
+# --------------------------------------------------------- full C2 size
+def test_lgssm_full_size_against_kalman(gh_ctx):
+    """C2: d=10, N=2^20, T=100.  The exact Kalman log-ML bounds the PF estimate
+    (PF log-ML is consistent; its bias/variance at this N is O(1e-1))."""
+    k = gold("kalman.json")["lg10"]
+    d = k["d"]
+    m = gen.LinearGaussianSSM(np.array(k["A"]), 0.1 * np.eye(d), np.eye(d), 0.5 * np.eye(d), np.zeros(d), np.eye(d))
+    ys = np.array(k["ys"])
+    n = 1 << 20
+    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=42, history_capacity=128)
+    gen.run_particle_filter(st, list(ys[1:]))
+    est = gen.log_ml_estimate(st)
+    assert abs(est - k["log_ml"]) < 3.0, (est, k["log_ml"])
+    ess, did = st.ess_history()
+    assert did.any()
+    par = st.parents
+    assert np.all(np.diff(par) >= 0) and par[0] >= 0 and par[-1] < n
+
+
+def test_lgssm_full_size_first_steps_bitexact(gh_ctx):
+    m = gen.LinearGaussianSSM.benchmark(10)
+    _, ys = m.simulate(3, np.random.default_rng(2))
+    st, orc = run_both(m, ys, 1 << 20, seed=42, thr=(1 << 20), check_every_step=False)
+    assert_lml_close(st, orc)
+
+
+# ------------------------------------------------------------- edge cases
+def test_single_particle(gh_ctx):
+    m = gen.KitagawaSSM()
+    _, ys = m.simulate(5, np.random.default_rng(1))
+    st, orc = run_both(m, ys, 1, seed=4, thr=2.0)
+    assert_lml_close(st, orc)
+
+
+def test_all_weights_minus_inf_is_numeric_error(gh_ctx):
+    # symbol 1 has probability 0 under every state: every weight is -Inf and
+    # the reference's Categorical would see NaN probabilities
+    m = gen.DiscreteHMM([0.5, 0.5], [[0.5, 0.5], [0.5, 0.5]], [[1.0, 1.0], [0.0, 0.0]])
+    st = gen.initialize_particle_filter(m, (1,), {("x_init",): 1}, 1000, seed=0)
+    with pytest.raises(gen.GenHipError) as e:
+        gen.maybe_resample(st)
+    assert e.value.code == 3
+
+
+def test_double_maybe_resample(gh_ctx):
+    m = gen.LinearGaussianSSM.benchmark(2)
+    _, ys = m.simulate(4, np.random.default_rng(1))
+    n = 777
+    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=5)
+    orc = O.OraclePF(m, n, 5)
+    orc.init(ys[0])
+    for t in range(2, 5):
+        for _ in range(2):  # the second call sees equal weights: resamples only if thr > N
+            assert gen.maybe_resample(st, n + 1) == orc.maybe_resample(n + 1)[0]
+        gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {("chain", t, "y"): ys[t - 1]})
+        orc.step(ys[t - 1])
+        assert np.array_equal(st.states().T, orc.state())
+    assert_lml_close(st, orc)
+
+
+def test_argument_errors(gh_ctx):
+    m = gen.KitagawaSSM()
+    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): 0.3}, 100, seed=0)
+    with pytest.raises(gen.GenHipError):
+        gen.particle_filter_step(st, (3,), (gen.UnknownChange(),), None)  # must extend by one
+    with pytest.raises(gen.GenHipError):
+        gen.initialize_particle_filter(m, (1,), None, 0)
+    with pytest.raises(gen.GenHipError):
+        gen.initialize_particle_filter(m, (1,), None, gen.OptimalProposal, (), 10)  # HMM only
+
+
+def test_importance_sampling(gh_ctx):
+    # test/inference/importance_sampling.jl:19-30 invariants, plus oracle parity
+    m = gen.KitagawaSSM(10.0, 1.0)
+    states, lnw, lml = gen.importance_sampling(m, (1,), {("chain", 1, "y"): 2.0}, 4096, seed=3)
+    mx = lnw.max()
+    assert abs(mx + math.log(np.exp(lnw - mx).sum())) < 1e-13
+    ost, olnw, olml = O.importance_sampling(m, [2.0], 4096, 3)
+    assert np.array_equal(states[:, 0], ost[0])
+    assert np.allclose(lnw, olnw, rtol=0, atol=1e-12)
+    assert abs(lml - olml) < 1e-12
+    tr, lml2 = gen.importance_resampling(m, (1,), {("chain", 1, "y"): 2.0}, 4096, seed=3)
+    assert lml2 == lml and np.isfinite(tr).all()
+
+
+def test_sample_unweighted_traces(gh_ctx):
+    m = gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(3, np.random.default_rng(8))
+    n = 2000
+    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=1)
+    gen.particle_filter_step(st, (2,), (gen.UnknownChange(),), {("chain", 2, "y"): ys[1]})
+    traces, idx = gen.sample_unweighted_traces(st, 200000, seed=9)
+    w = np.exp(gen.get_log_weights(st) - gen.get_log_weights(st).max())
+    w /= w.sum()
+    counts = np.bincount(idx, minlength=n) / idx.size
+    assert np.abs(counts - w).max() < 0.01
+    x2 = gen.get_traces(st).column(("chain", 2, "x"))
+    assert traces[0][("chain", 2, "x")] == x2[idx[0]]

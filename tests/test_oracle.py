@@ -1,0 +1,188 @@
+"""Pin the CPU oracle before trusting it (CPU only).
+
+The oracle (oracle/gh_oracle.c) is checked against the reference's own
+known-answer tests, re-expressed as the golden vectors in tests/golden/, and
+against analytic oracles.  Gen.jl cannot run in this container (no Julia).
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from gen_amd.models import DiscreteHMM, KitagawaSSM, LinearGaussianSSM
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gold(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def test_philox_known_answers():
+    for v in gold("philox_kat.json")["vectors"]:
+        assert O.philox(v["ctr"], v["key"]) == v["out"]
+
+
+def test_exp_log_within_one_ulp_of_libm():
+    L = O.lib()
+    rng = np.random.default_rng(0)
+    xs = np.concatenate([rng.uniform(-745, 709, 20000), rng.uniform(-1, 1, 20000), [0.0, -0.0, 1e-300, -1e-300]])
+    e = np.array([L.orc_exp(x) for x in xs])
+    ref = np.exp(xs)
+    assert np.all(np.abs(e - ref) <= np.spacing(ref))
+    ys = np.concatenate([np.exp(rng.uniform(-700, 700, 20000)), rng.uniform(0.5, 2, 20000), [5e-324, 1e-310, 1.0]])
+    lg = np.array([L.orc_log(y) for y in ys])
+    ref = np.log(ys)
+    assert np.all(np.abs(lg - ref) <= np.spacing(np.abs(ref)) + 0.0)
+    assert L.orc_log(0.0) == -math.inf and math.isnan(L.orc_log(-1.0))
+    assert L.orc_exp(-1000.0) == 0.0 and L.orc_exp(800.0) == math.inf
+
+
+def test_trig():
+    L = O.lib()
+    rng = np.random.default_rng(1)
+    xs = rng.uniform(0, 2000, 5000)
+    assert np.max(np.abs(np.array([L.orc_cos(x) for x in xs]) - np.cos(xs))) < 5e-16
+    import ctypes
+
+    s, c = ctypes.c_double(), ctypes.c_double()
+    for u in rng.uniform(0, 1, 5000):
+        L.orc_sincos_2pi(u, ctypes.byref(s), ctypes.byref(c))
+        assert abs(s.value - math.sin(2 * math.pi * u)) < 2e-15
+        assert abs(c.value - math.cos(2 * math.pi * u)) < 2e-15
+
+
+def test_normals_are_standard():
+    z = np.concatenate([O.normals(7, i, 3, 2, 10) for i in range(20000)])
+    assert abs(z.mean()) < 0.01 and abs(z.var() - 1) < 0.01
+    # the same counter gives the same draws, a different one different draws
+    assert np.array_equal(O.normals(7, 5, 3, 2, 10), O.normals(7, 5, 3, 2, 10))
+    assert not np.array_equal(O.normals(7, 5, 3, 2, 10), O.normals(7, 5, 4, 2, 10))
+
+
+def test_normal_logpdf_golden():
+    L = O.lib()
+    for row in gold("unfold_kats.json")["normal_logpdf"]:
+        got = L.orc_normal_logpdf(row["x"], row["mu"], row["std"])
+        assert got == pytest.approx(row["logpdf"], rel=1e-15, abs=1e-15)
+
+
+def hmm_forward(prior, E, T, obs):
+    ml = 1.0
+    alpha = np.asarray(prior)
+    for i in range(1, len(obs)):
+        pp = alpha * E[obs[i - 1], :]
+        den = pp.sum()
+        alpha = T @ (pp / den)
+        ml *= den
+    return ml * (alpha * E[obs[-1], :]).sum()
+
+
+def test_hmm_forward_kat():
+    # test/inference/particle_filter.jl:29-48
+    k = gold("hmm.json")["forward_kat"]
+    got = hmm_forward(k["prior"], np.array(k["emission"]), np.array(k["transition"]), k["obs"])
+    assert got == pytest.approx(k["marg_lik"])
+
+
+@pytest.mark.parametrize("proposal", [O.DEFAULT, O.OPTIMAL])
+def test_oracle_pf_matches_hmm_forward(proposal):
+    # test/inference/particle_filter.jl:96-168: N=10000, resample every step,
+    # atol 0.01 against the exact forward-algorithm log-ML.
+    g = gold("hmm.json")["pf_test"]
+    m = DiscreteHMM(g["prior"], np.array(g["transition"]), np.array(g["emission"]))
+    pf = O.run_pf(m, [[o] for o in g["obs"]], g["num_particles"], 0, thr=g["ess_threshold"], proposal=proposal)
+    assert abs(pf.log_ml_estimate() - g["log_ml"]) < g["atol"]
+    # the assertion is statistical: over 8 seeds the mean error is well inside it
+    errs = [
+        O.run_pf(m, [[o] for o in g["obs"]], g["num_particles"], s, thr=g["ess_threshold"], proposal=proposal)
+        .log_ml_estimate() - g["log_ml"]
+        for s in range(1, 9)
+    ]
+    assert abs(np.mean(errs)) < g["atol"]
+
+
+def test_oracle_pf_matches_kalman():
+    k = gold("kalman.json")["lg2"]
+    d = k["d"]
+    m = LinearGaussianSSM(np.array(k["A"]), 0.1 * np.eye(d), np.eye(d), 0.5 * np.eye(d), np.zeros(d), np.eye(d))
+    ests = [O.run_pf(m, np.array(k["ys"]), 20000, s).log_ml_estimate() for s in range(4)]
+    assert abs(np.mean(ests) - k["log_ml"]) < 0.05
+
+
+def test_resampling_invariants():
+    m = KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(12, np.random.default_rng(3))
+    for resampler in (O.SYSTEMATIC, O.MULTINOMIAL):
+        pf = O.OraclePF(m, 5000, 11, resampler)
+        pf.init(ys[0])
+        for y in ys[1:]:
+            did, ess = pf.maybe_resample(5000 + 1)  # always resample
+            assert did
+            par = pf.parents()
+            assert par.min() >= 0 and par.max() < 5000
+            if resampler == O.SYSTEMATIC:
+                assert np.all(np.diff(par) >= 0)  # systematic ancestors are sorted
+            assert np.all(pf.log_weights() == 0.0)
+            pf.step(y)
+
+
+def test_systematic_offspring_counts_are_floor_or_ceil():
+    """Systematic resampling gives particle i either floor(N w_i) or ceil(N w_i)
+    children (w_i from the integer-quantised weights)."""
+    m = KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(3, np.random.default_rng(4))
+    n = 4096
+    pf = O.OraclePF(m, n, 5)
+    pf.init(ys[0])
+    lw = pf.log_weights()
+    pf.maybe_resample(n + 1)
+    counts = np.bincount(pf.parents(), minlength=n)
+    w = np.exp(lw - lw.max())
+    w /= w.sum()
+    assert np.all(counts >= np.floor(n * w) - 1) and np.all(counts <= np.ceil(n * w) + 1)
+    assert counts.sum() == n
+
+
+def test_importance_sampling_normalised():
+    # test/inference/importance_sampling.jl:19-30: logsumexp(lnw) == 0 within 1e-14
+    m = KitagawaSSM(10.0, 1.0)
+    _, lnw, lml = O.importance_sampling(m, [2.0], 4, 0)
+    mx = lnw.max()
+    assert abs(mx + math.log(np.exp(lnw - mx).sum())) < 1e-14
+    assert not math.isnan(lml)
+
+
+def test_sharded_oracle_equals_single_rank():
+    """Two ranks run the distributed algorithm (stats all-gather, integer totals
+    all-gather, emit/apply exchange) and reproduce the single-rank run bit for bit."""
+    m = LinearGaussianSSM.benchmark(4)
+    _, ys = m.simulate(8, np.random.default_rng(5))
+    n = 3001
+    ref = O.run_pf(m, ys, n, 9, thr=n)  # resample every step
+    for R in (2, 3):
+        los = [(n * r) // R for r in range(R + 1)]
+        pfs = [O.OraclePF(m, n, 9, lo=los[r], n_local=los[r + 1] - los[r]) for r in range(R)]
+        for p in pfs:
+            p.init(ys[0])
+        for y in ys[1:]:
+            stats = np.concatenate([p.local_stats() for p in pfs])
+            dec, L, ess, M = O.combine_stats(stats, n, n)
+            assert dec == 1
+            totals = [p.qtotal(M) for p in pfs]
+            emitted = [p.emit(M, totals, r) for r, p in enumerate(pfs)]
+            slots = np.concatenate([e[0] for e in emitted])
+            ancs = np.concatenate([e[1] for e in emitted])
+            sts = np.concatenate([e[2] for e in emitted])
+            assert np.array_equal(np.sort(slots), np.arange(n))
+            for p in pfs:
+                p.apply(L, slots, ancs, sts)
+            for p in pfs:
+                p.step(y)
+        got = np.concatenate([p.state() for p in pfs], axis=1)
+        assert np.array_equal(got, ref.state())
+        assert np.array_equal(np.concatenate([p.parents() for p in pfs]), ref.parents())
