@@ -10,7 +10,7 @@ import os
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint8, c_uint32, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgen_hip.so")
+LIB_PATH = os.environ.get("GEN_HIP_LIB") or os.path.join(HERE, "libgen_hip.so")
 
 GH_OK = 0
 STATUS = {

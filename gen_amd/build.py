@@ -69,5 +69,18 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
+def build_variant(name: str, defines: list[str]) -> str:
+    """Timing-only variant (e.g. -DGH_PHILOX_ROUNDS=7) at gen_amd/variants/<name>.so;
+    never the product, never used by the parity tests."""
+    out_dir = os.path.join(HERE, "variants")
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f"{name}.so")
+    subprocess.run(hipcc_cmd(out=out, extra=[f"-D{d}" for d in defines]), check=True)
+    return out
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if len(sys.argv) > 2 and sys.argv[1] == "--variant":
+        build_variant(sys.argv[2], sys.argv[3:])
+    else:
+        build(force="--force" in sys.argv)

@@ -185,6 +185,7 @@ struct gh_model {
   // host copies needed per step
   std::vector<double> LR, c;  // LGSSM: chol(R), offset c
   LGParams lg{};
+  int lg_struct = 0;  // LGModel<D, S> structure bits (gh_models.h)
   HMMParams hmm{};
   KitParams kit{};
 };
@@ -233,6 +234,12 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     h.insert(h.end(), L0.begin(), L0.end());
     m->lg.dy = dy;
     m->lg.cstR = gauss_cst(dy, m->LR.data());
+    bool lq_diag = true, m_diag = dy == d;
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < i; ++j) lq_diag = lq_diag && LQ[i * d + j] == 0.0;
+    for (int r = 0; m_diag && r < dy; ++r)
+      for (int j = 0; j < d; ++j) m_diag = m_diag && (j == r || M[r * d + j] == 0.0);
+    m->lg_struct = (lq_diag ? 1 : 0) | (m_diag ? 2 : 0);
   } else if (desc->family == GH_FAMILY_HMM) {
     const int K = desc->k, V = desc->v;
     if (K < 1 || K > 64 || V < 1) return fail(GH_E_INVAL, "HMM: need 1 <= k <= 64, v >= 1");
@@ -332,6 +339,10 @@ struct gh_pf {
   int32_t* anc_scratch = nullptr;
   double* logw = nullptr;
   uint64_t* C = nullptr;
+  uint64_t* mark = nullptr;       // systematic: tagged range starts per slot
+  uint64_t* cmark = nullptr;      // systematic: tagged carry per step block
+  uint64_t epoch = 0;             // resample counter for the tags
+  bool marks_pending = false;     // last resample's ancestors only exist as marks
   uint64_t* bsum = nullptr;
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
@@ -415,7 +426,7 @@ static void pf_free(gh_pf* pf) {
   hipStreamSynchronize(pf->s);
   for (auto c : pf->chunks) hipFree(c);
   for (auto e : pf->ev) hipEventDestroy(e);
-  hipFree(pf->logw); hipFree(pf->C); hipFree(pf->bsum); hipFree(pf->pm); hipFree(pf->ps);
+  hipFree(pf->logw); hipFree(pf->C); hipFree(pf->mark); hipFree(pf->cmark); hipFree(pf->bsum); hipFree(pf->pm); hipFree(pf->ps);
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->recv); hipFree(pf->send); hipFree(pf->xslot); hipFree(pf->xanc);
@@ -445,7 +456,15 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
   switch (m->family) {
     case GH_FAMILY_LGSSM:
       switch (m->d) {
-#define GH_LG_CASE(DD) case DD: launch_step_t<LGModel<DD>>(pf, m->lg, o, a, init); break;
+#define GH_LG_CASE(DD)                                                                  \
+  case DD:                                                                              \
+    switch (m->lg_struct) {                                                             \
+      case 1: launch_step_t<LGModel<DD, 1>>(pf, m->lg, o, a, init); break;              \
+      case 2: launch_step_t<LGModel<DD, 2>>(pf, m->lg, o, a, init); break;              \
+      case 3: launch_step_t<LGModel<DD, 3>>(pf, m->lg, o, a, init); break;              \
+      default: launch_step_t<LGModel<DD, 0>>(pf, m->lg, o, a, init); break;             \
+    }                                                                                   \
+    break;
         GH_LG_CASE(1) GH_LG_CASE(2) GH_LG_CASE(3) GH_LG_CASE(4) GH_LG_CASE(5) GH_LG_CASE(6)
         GH_LG_CASE(7) GH_LG_CASE(8) GH_LG_CASE(10) GH_LG_CASE(12) GH_LG_CASE(16)
 #undef GH_LG_CASE
@@ -516,6 +535,8 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return fail(set_err(GH_E_NOMEM, "hipMalloc %s", #ptr));
   ALLOC(pf->logw, sizeof(double) * n);
   ALLOC(pf->C, sizeof(uint64_t) * n);
+  ALLOC(pf->mark, sizeof(uint64_t) * n);
+  ALLOC(pf->cmark, sizeof(uint64_t) * pf->nb_step);
   ALLOC(pf->bsum, sizeof(uint64_t) * pf->nb_scan);
   ALLOC(pf->pm, sizeof(double) * pf->nb_step);
   ALLOC(pf->ps, sizeof(double) * pf->nb_step);
@@ -547,6 +568,9 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
     z.one = 1;
     if (hipMemcpyAsync(pf->dev, &z, sizeof z, hipMemcpyHostToDevice, pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init scalars"));
+    if (hipMemsetAsync(pf->mark, 0, sizeof(uint64_t) * n, pf->s) != hipSuccess ||
+        hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * pf->nb_step, pf->s) != hipSuccess)
+      return fail(set_err(GH_E_HIP, "init marks"));
     if (hipStreamSynchronize(pf->s) != hipSuccess) return fail(set_err(GH_E_HIP, "sync"));
   }
   const int cap0 = pf->opts.history_capacity > 0 ? pf->opts.history_capacity : 16;
@@ -594,6 +618,9 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   a.xprev = slot_x(pf, t - 1);
   a.ld_prev = pf->n;
   a.anc = anc_for_step(pf, t);
+  a.mark = pf->mark;
+  a.carry = pf->cmark;
+  a.mark_mode = pf->marks_pending ? 1 : 0;
   a.remote = pf->recv;
   a.ld_remote = pf->n;
   a.xout = slot_x(pf, t);
@@ -613,6 +640,19 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   CHECK(share_stats(pf));
   pf->t = t;
   pf->resample_calls = 0;
+  pf->marks_pending = false;
+  return GH_OK;
+}
+
+// Expand pending systematic marks into the ancestor array of step t+1 (for
+// genealogy reads before the next step, or a second resample).
+static int materialize_marks(gh_pf* pf) {
+  if (!pf->marks_pending) return GH_OK;
+  int32_t* anc_target = anc_for_step(pf, pf->t + 1);
+  hipLaunchKernelGGL(k_sys_ancestors, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
+                     &pf->dev->pending, pf->mark, pf->cmark, pf->n, (const int32_t*)nullptr, anc_target);
+  HIP_TRY(hipGetLastError());
+  pf->marks_pending = false;
   return GH_OK;
 }
 
@@ -623,31 +663,68 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   const int t = pf->t;
   CHECK(grow_for_step(pf, t + 1));
   const int R = pf->ctx->world;
-  hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, R,
-                     pf->n_global, thr, pf->ess_hist, pf->res_hist, t);
+  const int64_t n = pf->n;
+  const bool second = pf->resample_calls > 0;
+  DecideArgs d{};
+  d.stats_all = pf->stats_all;
+  d.R = R;
+  d.n_global = pf->n_global;
+  d.thr = thr;
+  d.ess_hist = pf->ess_hist;
+  d.res_hist = pf->res_hist;
+  d.t = t;
   GateArgs g;
   g.gate = &pf->dev->fire;
   g.M = &pf->dev->M;
   g.zero_w = &pf->dev->pending;
   g.shift = quant_shift((uint64_t)pf->n_global);
-  const int64_t n = pf->n;
-  if (n > 0) {
-    hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum);
-    hipLaunchKernelGGL(k_qscan, dim3(1), dim3(1024), 0, pf->s, pf->bsum, pf->nb_scan, g, pf->dev);
-  }
+  // The common case fuses the decision into the first resample kernel; a
+  // second call without a step (or an empty shard) decides in its own launch.
+  const bool fused = !second && n > 0;
+  if (second && pf->marks_pending) CHECK(materialize_marks(pf));
+  if (!fused) hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, pf->s, d, pf->dev);
+  if (n > 0)
+    hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum,
+                       fused ? 1 : 0, d, pf->dev);
   if (R > 1) {
+    hipLaunchKernelGGL(k_rank_total, dim3(1), dim3(kBlock), 0, pf->s, g.gate, pf->bsum, n > 0 ? pf->nb_scan : 0,
+                       pf->dev);
     NCCL_TRY(ncclAllGather(&pf->dev->local, pf->totals_all, 1, ncclUint64, pf->ctx->comm, pf->s));
   }
-  const uint32_t stream = STREAM_RESAMPLE;
-  hipLaunchKernelGGL(k_rs_const, dim3(1), dim3(64), 0, pf->s, g, pf->dev,
-                     R > 1 ? (const uint64_t*)pf->totals_all : (const uint64_t*)nullptr, R,
-                     pf->ctx->rank, pf->n_global, pf->seed, (uint32_t)t, stream);
-  if (n > 0)
-    hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g,
-                       pf->bsum, pf->dev, pf->C);
   int32_t* anc_target = anc_for_step(pf, t + 1);
-  const bool second = pf->resample_calls > 0;
-  if (R == 1) {
+  const bool sys1 = R == 1 && pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
+  MarkArgs mk{};
+  mk.mark = pf->mark;
+  mk.cmark = pf->cmark;
+  mk.epoch = ++pf->epoch;
+  mk.n_global = pf->n_global;
+  mk.nb_step = pf->nb_step;
+  mk.enabled = sys1 ? 1 : 0;
+  CdfArgs ca{};
+  ca.bsum = pf->bsum;
+  ca.nb = pf->nb_scan;
+  ca.totals = R > 1 ? pf->totals_all : nullptr;
+  ca.R = R;
+  ca.rank = pf->ctx->rank;
+  ca.n_global = pf->n_global;
+  ca.seed = pf->seed;
+  ca.t = (uint32_t)t;
+  ca.stream = STREAM_RESAMPLE;
+  if (n > 0)
+    hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, ca, pf->dev,
+                       pf->C, mk);
+  if (sys1) {
+    // systematic, one rank: the ancestors are the range marks; the next step
+    // kernel expands them (no search, no ancestor array round trip)
+    if (second) {
+      hipLaunchKernelGGL(k_sys_ancestors, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, g.gate, g.zero_w,
+                         pf->mark, pf->cmark, n, (const int32_t*)anc_target, pf->anc_scratch);
+      hipLaunchKernelGGL(k_copy_anc, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
+                         pf->anc_scratch, anc_target, n);
+    } else {
+      pf->marks_pending = true;
+    }
+  } else if (R == 1) {
     SearchArgs sa{};
     sa.C = pf->C;
     sa.n_cdf = n;
@@ -760,6 +837,7 @@ extern "C" int gh_pf_get_log_weights(gh_pf* pf, double* out) {
 
 extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
+  CHECK(materialize_marks(pf));
   if (t < 1 || t > pf->t) return set_err(GH_E_INVAL, "step %d outside 1..%d", t, pf->t);
   if (!pf->opts.record_history && t != pf->t)
     return set_err(GH_E_STATE, "record_history is off: only the current step is kept");
@@ -818,6 +896,7 @@ extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {
 
 extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
   if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
+  CHECK(materialize_marks(pf));
   // ParticleFilterState.parents: ancestors chosen by the most recent resample
   // (identity before the first one), as global 0-based ids.
   std::vector<int32_t> res(pf->cap + 2);
@@ -862,12 +941,21 @@ extern "C" int gh_pf_sample_unweighted(gh_pf* pf, int64_t ns, uint64_t seed, int
   g.M = &pf->dev->sM;
   g.zero_w = &pf->dev->spend;
   g.shift = quant_shift((uint64_t)n);
-  hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum);
-  hipLaunchKernelGGL(k_qscan, dim3(1), dim3(1024), 0, pf->s, pf->bsum, pf->nb_scan, g, pf->dev);
-  hipLaunchKernelGGL(k_rs_const, dim3(1), dim3(64), 0, pf->s, g, pf->dev, (const uint64_t*)nullptr, 1, 0,
-                     n, seed, (uint32_t)pf->t, (uint32_t)STREAM_SAMPLE);
-  hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum,
-                     pf->dev, pf->C);
+  CHECK(materialize_marks(pf));
+  DecideArgs d{};
+  hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum, 0, d,
+                     pf->dev);
+  MarkArgs mk{};
+  CdfArgs ca{};
+  ca.bsum = pf->bsum;
+  ca.nb = pf->nb_scan;
+  ca.R = 1;
+  ca.n_global = n;
+  ca.seed = seed;
+  ca.t = (uint32_t)pf->t;
+  ca.stream = STREAM_SAMPLE;
+  hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, ca, pf->dev, pf->C,
+                     mk);
   int32_t* dout = nullptr;
   HIP_TRY(hipMalloc(&dout, sizeof(int32_t) * ns));
   SearchArgs sa{};

@@ -19,7 +19,7 @@
 namespace gh {
 
 constexpr int kBlock = 256;
-constexpr int kScanItems = 8;                    // items per thread in the CDF kernels
+constexpr int kScanItems = 4;                    // items per thread in the CDF kernels
 constexpr int kScanTile = kBlock * kScanItems;   // particles per CDF block
 
 // Device-resident state of one particle filter (one rank).
@@ -32,19 +32,26 @@ struct DevScalars {
   uint64_t base;       // this rank's offset in the global integer CDF
   uint64_t local;      // this rank's integer total
   uint64_t o, Qs, Rs;  // systematic offset, S / N, S % N
+  double invN;         // 1 / N (division estimate, corrected exactly)
   int pending;         // a resample happened since the last step
   int fire;            // the current maybe_resample decided to resample
   int spend;           // sample_unweighted: weights are all equal
   int one;             // constant 1 (gate for unconditional launches)
   int error;           // gh_status raised on the device
   unsigned ticket;     // last-block-done counter of k_step
-  int pad[2];
+  unsigned ticket_q;   // ... of k_qsum
+  unsigned ticket_c;   // ... of k_cdf
+
 };
 
 struct StepArgs {
   const double* xprev;   // [D][ld_prev] states of the previous step
   int64_t ld_prev;
-  const int32_t* anc;    // ancestors for this step (used when a resample is pending)
+  int32_t* anc;          // ancestors for this step (read when a resample is pending;
+                         // written here when they come from the systematic marks)
+  const uint64_t* mark;  // systematic range marks + per-block carries (mark_mode)
+  const uint64_t* carry;
+  int mark_mode;
   const double* remote;  // multi-rank: states received from other ranks [D][ld_remote]
   int64_t ld_remote;
   double* xout;          // [D][ld_out]
@@ -99,19 +106,20 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
 
 // Combine per-block (m, s, s2) partials into the rank's triple.  Called by
 // the last block of k_step after the agent-scope acquire.
-__device__ void fold_partials(const double* pm, const double* ps, const double* ps2, int nb,
+__device__ void fold_partials(double* pm, double* ps, double* ps2, int nb,
                               double* sm, double* out) {
   double m = -INFINITY;
-  for (int b = threadIdx.x; b < nb; b += kBlock) m = fmax(m, pm[b]);
+  for (int b = threadIdx.x; b < nb; b += kBlock)
+    m = fmax(m, __hip_atomic_load(&pm[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   const double M = block_max(m, sm);
   double s = 0.0, s2 = 0.0;
   if (M > -INFINITY) {
     for (int b = threadIdx.x; b < nb; b += kBlock) {
-      const double mb = pm[b];
+      const double mb = __hip_atomic_load(&pm[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (mb > -INFINITY) {
         const double e = gh_exp(mb - M);
-        s += ps[b] * e;
-        s2 += ps2[b] * (e * e);
+        s += __hip_atomic_load(&ps[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * e;
+        s2 += __hip_atomic_load(&ps2[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * (e * e);
       }
     }
   }
@@ -126,13 +134,38 @@ __device__ void fold_partials(const double* pm, const double* ps, const double* 
 
 // ---------------------------------------------------------------- k_step
 template <class Model, bool INIT>
-__global__ __launch_bounds__(kBlock) void k_step(typename Model::Params p, StepObs o, StepArgs a) {
+// occupancy target per model (waves per SIMD the register budget must allow)
+__global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(typename Model::Params p, StepObs o, StepArgs a) {
   constexpr int D = Model::kD;
   __shared__ double sm[8];
   __shared__ int am_last;
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  int pend = 0;
-  if (!INIT) pend = a.dev->pending | a.dev->fire;
+  int pend = 0, use_marks = 0;
+  if (!INIT) {
+    const int pending = a.dev->pending, fire = a.dev->fire;
+    pend = pending | fire;
+    use_marks = a.mark_mode && fire && !pending;
+  }
+  int64_t src = j;
+  if (use_marks) {
+    // systematic ancestors from the range marks: block-wide prefix max seeded
+    // with the block's carry (the ancestor of its first slot)
+    __shared__ uint64_t smk[4];
+    uint64_t v = j < a.n ? a.mark[j] : 0;
+    const uint64_t c = a.carry[blockIdx.x];
+    v = v > c ? v : c;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t u = __shfl_up(v, off, 64);
+      if (lane >= off && u > v) v = u;
+    }
+    if (lane == 63) smk[w] = v;
+    __syncthreads();
+    for (int k = 0; k < w; ++k) v = smk[k] > v ? smk[k] : v;
+    src = (int64_t)(uint32_t)v;
+    if (j < a.n) a.anc[j] = (int32_t)src;  // genealogy record
+  }
   double lw = -INFINITY;
   if (j < a.n) {
     double x[D];
@@ -142,18 +175,13 @@ __global__ __launch_bounds__(kBlock) void k_step(typename Model::Params p, StepO
       lw = inc;
     } else {
       double xp[D];
-      if (pend) {
-        const int32_t s = a.anc[j];
-        if (s >= 0) {
+      if (pend && !use_marks) src = a.anc[j];
+      if (src >= 0) {
 #pragma unroll
-          for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + s];
-        } else {
-#pragma unroll
-          for (int k = 0; k < D; ++k) xp[k] = a.remote[k * a.ld_remote + (-1 - s)];
-        }
+        for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
       } else {
 #pragma unroll
-        for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + j];
+        for (int k = 0; k < D; ++k) xp[k] = a.remote[k * a.ld_remote + (-1 - src)];
       }
       inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x);
       lw = (pend ? 0.0 : a.logw[j]) + inc;
@@ -169,12 +197,12 @@ __global__ __launch_bounds__(kBlock) void k_step(typename Model::Params p, StepO
   const double sb = block_sum(e, sm);
   const double s2b = block_sum(e * e, sm);
   if (threadIdx.x == 0) {
-    a.pm[blockIdx.x] = mb;
-    a.ps[blockIdx.x] = sb;
-    a.ps2[blockIdx.x] = s2b;
-    // publish: stores drained, agent release, then the ticket (Guideline 16)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // Publish the three partials with 8-byte agent-scope (sc1) stores, drain
+    // them, then take a ticket.  No release fence: a fence would write back
+    // this XCD's whole L2 (the block's freshly written states) per block.
+    __hip_atomic_store(&a.pm[blockIdx.x], mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.ps[blockIdx.x], sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.ps2[blockIdx.x], s2b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev =
         __hip_atomic_fetch_add(&a.dev->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -182,9 +210,8 @@ __global__ __launch_bounds__(kBlock) void k_step(typename Model::Params p, StepO
   }
   __syncthreads();
   if (!am_last) return;
-  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // the last arriver reads every partial with sc1 loads (fold_partials)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   fold_partials(a.pm, a.ps, a.ps2, (int)gridDim.x, sm, a.stats_out);
   if (threadIdx.x == 0) {
     __hip_atomic_store(&a.dev->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -195,50 +222,79 @@ __global__ __launch_bounds__(kBlock) void k_step(typename Model::Params p, StepO
   }
 }
 
-// --------------------------------------------------------------- k_decide
+// --------------------------------------------------------------- decision
 // maybe_resample! (particle_filter.jl:189-201): combine the ranks' triples in
-// rank order, ESS = S^2 / S2 (= exp(-logsumexp(2 lnw))), resample iff ESS < thr.
-__global__ void k_decide(DevScalars* dev, double* stats_all, int R, int64_t n_global, double thr,
-                         double* ess_hist, int32_t* res_hist, int t) {
+// rank order, ESS = S^2 / S2 (= exp(-logsumexp(2 lnw))), resample iff
+// ESS < thr (strict).  `uniform` = every weight is 0 (a resample is pending).
+struct DecideArgs {
+  const double* stats_all;  // [3*R]
+  int R;
+  int64_t n_global;
+  double thr;
+  double* ess_hist;  // indexed by step
+  int32_t* res_hist; // res_hist[t+1]: a resample precedes step t+1
+  int t;
+};
+
+struct Decision {
+  double M, L, ess;
+  int fire, err;
+};
+
+__device__ __forceinline__ Decision decide(const DecideArgs& d, bool uniform) {
+  Decision r{};
+  double M = -INFINITY;
+  if (uniform) M = 0.0;
+  else
+    for (int q = 0; q < d.R; ++q) M = fmax(M, d.stats_all[3 * q]);
+  if (!(M > -INFINITY) || M == INFINITY || M != M) {
+    r.err = 3;  // GH_E_NUMERIC: the reference's Categorical would get NaN probabilities
+    r.ess = NAN;
+    r.M = M;
+    return r;
+  }
+  double S = 0.0, S2 = 0.0;
+  for (int q = 0; q < d.R; ++q) {
+    if (uniform) {
+      const double nq = (double)((d.n_global * (q + 1)) / d.R - (d.n_global * q) / d.R);
+      S += nq * 1.0;
+      S2 += nq * 1.0;
+      continue;
+    }
+    if (!(d.stats_all[3 * q] > -INFINITY)) continue;
+    const double e = gh_exp(d.stats_all[3 * q] - M);
+    S += d.stats_all[3 * q + 1] * e;
+    S2 += d.stats_all[3 * q + 2] * (e * e);
+  }
+  r.M = M;
+  r.L = M + gh_log(S);
+  r.ess = (S * S) / S2;
+  r.fire = r.ess < d.thr;
+  return r;
+}
+
+__device__ __forceinline__ void commit_decision(const DecideArgs& d, const Decision& r, DevScalars* dev,
+                                                int pending) {
+  dev->M = r.M;
+  dev->L = r.L;
+  dev->ess = r.ess;
+  dev->fire = r.fire;
+  if (r.err) dev->error = r.err;
+  if (r.fire) dev->log_ml_est += r.L - gh_log((double)d.n_global);
+  if (d.ess_hist) d.ess_hist[d.t] = r.ess;
+  if (d.res_hist) d.res_hist[d.t + 1] = pending | r.fire;
+}
+
+// Stand-alone decision: used for a second maybe_resample without a step in
+// between (commits the first one; weights are then all 0).
+__global__ void k_decide(DecideArgs d, DevScalars* dev) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (dev->fire) {  // second maybe_resample without a step: commit the first
+  if (dev->fire) {
     dev->pending = 1;
     dev->fire = 0;
   }
-  double M = -INFINITY;
-  for (int r = 0; r < R; ++r) M = fmax(M, stats_all[3 * r]);
-  if (!(M > -INFINITY) || M == INFINITY || M != M) {
-    dev->error = 3;  // GH_E_NUMERIC
-    dev->ess = NAN;
-    if (ess_hist) ess_hist[t] = NAN;
-    return;
-  }
-  double S = 0.0, S2 = 0.0;
-  for (int r = 0; r < R; ++r) {
-    if (!(stats_all[3 * r] > -INFINITY)) continue;
-    const double e = gh_exp(stats_all[3 * r] - M);
-    S += stats_all[3 * r + 1] * e;
-    S2 += stats_all[3 * r + 2] * (e * e);
-  }
-  const double L = M + gh_log(S);
-  const double ess = (S * S) / S2;
-  const int fire = ess < thr;
-  dev->M = M;
-  dev->L = L;
-  dev->ess = ess;
-  dev->fire = fire;
-  if (fire) {
-    dev->log_ml_est += L - gh_log((double)n_global);
-    // after the resample every weight is 0
-    for (int r = 0; r < R; ++r) {
-      const int64_t nr = (n_global * (r + 1)) / R - (n_global * r) / R;
-      stats_all[3 * r] = 0.0;
-      stats_all[3 * r + 1] = (double)nr;
-      stats_all[3 * r + 2] = (double)nr;
-    }
-  }
-  if (ess_hist) ess_hist[t] = ess;
-  if (res_hist) res_hist[t + 1] = dev->pending | fire;
+  const Decision r = decide(d, dev->pending != 0);
+  commit_decision(d, r, dev, dev->pending);
 }
 
 // ------------------------------------------------------ integer CDF kernels
@@ -254,12 +310,94 @@ __device__ __forceinline__ uint64_t qweight(const double* logw, int64_t i, doubl
   return quantize_weight(zero ? 0.0 : logw[i], M, shift);
 }
 
+__device__ __forceinline__ uint64_t block_sum_u64(uint64_t s, uint64_t* sm) {
+  s = wave_sum_u64(s);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
+  __syncthreads();
+  return (sm[0] + sm[1]) + (sm[2] + sm[3]);
+}
+
+
+// Block-wide (256 threads) inclusive scans of one value per thread.
+__device__ __forceinline__ uint64_t block_incl_sum_u64(uint64_t v, uint64_t* sm4) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t u = __shfl_up(v, off, 64);
+    if (lane >= off) v += u;
+  }
+  __syncthreads();
+  if (lane == 63) sm4[w] = v;
+  __syncthreads();
+  for (int k = 0; k < w; ++k) v += sm4[k];
+  return v;
+}
+__device__ __forceinline__ uint64_t block_incl_max_u64(uint64_t v, uint64_t* sm4) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t u = __shfl_up(v, off, 64);
+    if (lane >= off && u > v) v = u;
+  }
+  __syncthreads();
+  if (lane == 63) sm4[w] = v;
+  __syncthreads();
+  for (int k = 0; k < w; ++k) v = sm4[k] > v ? sm4[k] : v;
+  return v;
+}
+
+// Last-block-done ticket (Guideline 16): the block's sc1 stores are drained
+// by every storing wave, then one lane takes a ticket; returns true in the
+// block that arrived last (which then reads the published values with sc1
+// loads).  The last block re-arms the counter.
+__device__ __forceinline__ bool last_block(unsigned* ticket, int* sm_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sm_flag = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  const bool last = *sm_flag != 0;
+  if (last && threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return last;
+}
+
+template <class T>
+__device__ __forceinline__ T ld_sc1(T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Integer block sums of the quantised weights.  With `fused` the launch also
+// takes the maybe_resample! decision: every block evaluates it from the same
+// inputs (identical result), block 0 commits it, blocks exit unless it fires.
 __global__ __launch_bounds__(kBlock) void k_qsum(const double* logw, int64_t n, GateArgs g,
-                                                 uint64_t* bsum) {
-  if (!*g.gate) return;
+                                                 uint64_t* bsum, int fused, DecideArgs d,
+                                                 DevScalars* dev) {
   __shared__ uint64_t sm[4];
-  const double M = *g.M;
-  const int zero = *g.zero_w;
+  __shared__ double sM;
+  __shared__ int sfire;
+  if (fused) {
+    if (threadIdx.x == 0) {
+      const Decision r = decide(d, false);
+      if (blockIdx.x == 0) commit_decision(d, r, dev, 0);
+      sM = r.M;
+      sfire = r.fire;
+    }
+    __syncthreads();
+    if (!sfire) return;
+  } else {
+    if (!*g.gate) return;
+    if (threadIdx.x == 0) sM = *g.M;
+    __syncthreads();
+  }
+  const double M = sM;
+  const int zero = fused ? 0 : *g.zero_w;
   const int64_t base = (int64_t)blockIdx.x * kScanTile;
   uint64_t s = 0;
 #pragma unroll
@@ -267,66 +405,121 @@ __global__ __launch_bounds__(kBlock) void k_qsum(const double* logw, int64_t n, 
     const int64_t i = base + threadIdx.x + (int64_t)k * kBlock;
     if (i < n) s += qweight(logw, i, M, zero, g.shift);
   }
-  s = wave_sum_u64(s);
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) bsum[blockIdx.x] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+  s = block_sum_u64(s, sm);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = s;
 }
 
-// exclusive scan of the block sums in place (one 1024-thread block); writes
-// the rank total into dev->local.
-__global__ __launch_bounds__(1024) void k_qscan(uint64_t* bsum, int64_t nb, GateArgs g,
-                                                DevScalars* dev) {
-  if (!*g.gate) return;
-  __shared__ uint64_t sm[1024];
-  const int64_t per = (nb + 1023) / 1024;
-  const int64_t b0 = (int64_t)threadIdx.x * per;
+// multi-rank: this rank's integer total (input of the all-gather)
+__global__ __launch_bounds__(kBlock) void k_rank_total(const int* gate, const uint64_t* bsum, int64_t nb,
+                                                       DevScalars* dev) {
+  if (!*gate) return;
+  __shared__ uint64_t sm[4];
   uint64_t s = 0;
-  for (int64_t b = b0; b < b0 + per && b < nb; ++b) s += bsum[b];
-  sm[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    uint64_t v = threadIdx.x >= (unsigned)off ? sm[threadIdx.x - off] : 0;
-    __syncthreads();
-    sm[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint64_t run = sm[threadIdx.x] - s;  // exclusive
-  for (int64_t b = b0; b < b0 + per && b < nb; ++b) {
-    const uint64_t v = bsum[b];
-    bsum[b] = run;
-    run += v;
-  }
-  if (threadIdx.x == 1023) dev->local = sm[1023];
+  for (int64_t b = threadIdx.x; b < nb; b += kBlock) s += bsum[b];
+  s = block_sum_u64(s, sm);
+  if (threadIdx.x == 0) dev->local = s;
 }
 
-// global integer constants of the resample: S, base, systematic offset
-__global__ void k_rs_const(GateArgs g, DevScalars* dev, const uint64_t* totals, int R, int rank,
-                           int64_t n_global, uint64_t seed, uint32_t t, uint32_t stream) {
-  if (!*g.gate || threadIdx.x != 0) return;
-  uint64_t S = 0, base = 0;
-  if (totals) {
-    for (int r = 0; r < R; ++r) {
-      if (r < rank) base += totals[r];
-      S += totals[r];
-    }
-  } else {
-    S = dev->local;
-  }
-  dev->S = S;
-  dev->base = base;
-  const u32x4 w = rng_block(seed, ~0ull, t, stream, 0);
-  dev->o = scale_u53(u53_bits(w.x, w.y), S);
-  dev->Qs = S / (uint64_t)n_global;
-  dev->Rs = S % (uint64_t)n_global;
+// ------------------------------------------------ systematic slot ranges
+// floor(num / N) for num < 2^63: double estimate, then exact correction.
+__device__ __forceinline__ uint64_t udiv_n(uint64_t num, uint64_t N, double invN) {
+  uint64_t q = (uint64_t)((double)num * invN);
+  if (q > (1ull << 50)) return num / N;  // estimate too coarse: exact division
+  int64_t r = (int64_t)(num - q * N);
+  while (r < 0) { --q; r += (int64_t)N; }
+  while (r >= (int64_t)N) { ++q; r -= (int64_t)N; }
+  return q;
 }
 
-// inclusive global CDF C[i]
-__global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, GateArgs g,
-                                                const uint64_t* boff, const DevScalars* dev,
-                                                uint64_t* C) {
+// systematic target of global slot j: floor((j S + o) / N)
+__device__ __forceinline__ uint64_t sys_target(const DevScalars* dev, uint64_t N, uint64_t j) {
+  return j * dev->Qs + udiv_n(j * dev->Rs + dev->o, N, dev->invN);
+}
+
+// #{ j in [0, N) : T_j < X }: the first slot whose target reaches X.
+// Particle i owns the slots [count(C_{i-1}), count(C_i)).
+__device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, uint64_t X) {
+  if (X == 0) return 0;
+  if (X >= dev->S) return (int64_t)N;
+  const double est = ((double)X * (double)N - (double)dev->o) / (double)dev->S;
+  int64_t j = est <= 0.0 ? 0 : (est >= (double)N ? (int64_t)N : (int64_t)est);
+  while (j > 0 && sys_target(dev, N, (uint64_t)(j - 1)) >= X) --j;
+  while (j < (int64_t)N && sys_target(dev, N, (uint64_t)j) < X) ++j;
+  return j;
+}
+
+struct MarkArgs {
+  uint64_t* mark;     // [n slots] tagged (epoch << 32 | ancestor) at each range start
+  uint64_t* cmark;    // [step blocks] tagged ancestor of the block's first slot
+  uint64_t epoch;     // resample counter (tags older marks as stale)
+  int64_t n_global;
+  int64_t nb_step;    // step blocks (entries of cmark)
+  int enabled;        // systematic single-rank path
+};
+
+struct CdfArgs {
+  const uint64_t* bsum;    // integer block sums of k_qsum
+  int64_t nb;              // number of them
+  const uint64_t* totals;  // multi-rank: all-gathered rank totals (nullptr: one rank)
+  int R, rank;
+  int64_t n_global;
+  uint64_t seed;
+  uint32_t t;
+  uint32_t stream;
+};
+
+// Every block derives what it needs from the block sums itself (no separate
+// scan launch): its exclusive offset, the rank total, the global total S,
+// this rank's base and the systematic constants (block 0 also stores them).
+// Then it writes either the inclusive CDF C (multinomial / sampling) or, for
+// systematic resampling on one rank, the range marks: particle i owns slots
+// [count(C_{i-1}), count(C_i)); its range start gets a tagged mark, and every
+// step-block start slot the block's particles cover gets its ancestor in cmark.
+__global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, GateArgs g, CdfArgs ca,
+                                                DevScalars* dev, uint64_t* C, MarkArgs mk) {
   if (!*g.gate) return;
-  __shared__ uint64_t sm[kBlock];
+  __shared__ uint64_t sm4[4];
+  __shared__ DevScalars sd;       // block copy of the resample constants
+  __shared__ uint64_t sboff;
+  __shared__ int32_t se[kScanTile];  // slot end of each particle of the block
+  __shared__ int64_t sfirst;
+  // ---- prologue: offsets and constants from the block sums
+  uint64_t before = 0, all = 0;
+  for (int64_t b = threadIdx.x; b < ca.nb; b += kBlock) {
+    const uint64_t v = ca.bsum[b];
+    all += v;
+    if (b < (int64_t)blockIdx.x) before += v;
+  }
+  before = block_sum_u64(before, sm4);
+  all = block_sum_u64(all, sm4);
+  if (threadIdx.x == 0) {
+    uint64_t S = all, base = 0;
+    if (ca.totals) {
+      S = 0;
+      for (int r = 0; r < ca.R; ++r) {
+        if (r < ca.rank) base += ca.totals[r];
+        S += ca.totals[r];
+      }
+    }
+    sd.S = S;
+    sd.base = base;
+    sd.local = all;
+    const u32x4 w = rng_block(ca.seed, ~0ull, ca.t, ca.stream, 0);
+    sd.o = scale_u53(u53_bits(w.x, w.y), S);
+    sd.Qs = S / (uint64_t)ca.n_global;
+    sd.Rs = S % (uint64_t)ca.n_global;
+    sd.invN = 1.0 / (double)ca.n_global;
+    sboff = base + before;
+    if (blockIdx.x == 0) {
+      dev->S = sd.S;
+      dev->base = sd.base;
+      dev->local = sd.local;
+      dev->o = sd.o;
+      dev->Qs = sd.Qs;
+      dev->Rs = sd.Rs;
+      dev->invN = sd.invN;
+    }
+  }
   const double M = *g.M;
   const int zero = *g.zero_w;
   const int64_t i0 = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
@@ -337,20 +530,67 @@ __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, G
     q[k] = (i0 + k < n) ? qweight(logw, i0 + k, M, zero, g.shift) : 0;
     s += q[k];
   }
-  sm[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < kBlock; off <<= 1) {
-    uint64_t v = threadIdx.x >= (unsigned)off ? sm[threadIdx.x - off] : 0;
-    __syncthreads();
-    sm[threadIdx.x] += v;
-    __syncthreads();
+  const uint64_t incl = block_incl_sum_u64(s, sm4);  // (its barriers also publish sd)
+  uint64_t run = sboff + incl - s;
+  if (!mk.enabled) {
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+      run += q[k];
+      if (i0 + k < n) C[i0 + k] = run;
+    }
+    return;
   }
-  uint64_t run = dev->base + boff[blockIdx.x] + sm[threadIdx.x] - s;
+  const uint64_t N = (uint64_t)mk.n_global;
+  int64_t s_i = sys_count(&sd, N, run);
+  if (threadIdx.x == 0) sfirst = s_i;
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     run += q[k];
-    if (i0 + k < n) C[i0 + k] = run;
+    const int64_t e_i = (i0 + k < n && q[k]) ? sys_count(&sd, N, run) : s_i;
+    se[threadIdx.x * kScanItems + k] = (int32_t)e_i;
+    if (e_i > s_i) mk.mark[s_i] = (mk.epoch << 32) | (uint64_t)(i0 + k);
+    s_i = e_i;
   }
+  __syncthreads();
+  // step-block starts inside [first slot, last slot end) of this particle block
+  const int64_t s_lo = sfirst, s_hi = se[kScanTile - 1];
+  const int64_t pbase = (int64_t)blockIdx.x * kScanTile;
+  for (int64_t b = (s_lo + kBlock - 1) / kBlock + threadIdx.x; b * kBlock < s_hi; b += kBlock) {
+    const int32_t slot = (int32_t)(b * kBlock);
+    int lo = 0, hi = kScanTile - 1;  // first particle p with se[p] > slot
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (se[mid] > slot) hi = mid;
+      else lo = mid + 1;
+    }
+    mk.cmark[b] = (mk.epoch << 32) | (uint64_t)(pbase + lo);
+  }
+}
+
+// systematic ancestors: block-wide prefix max of the slot marks seeded with
+// the block's carry (no search at all)
+__global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const int* zero_w,
+                                                          const uint64_t* mark, const uint64_t* carry,
+                                                          int64_t n, const int32_t* anc_old,
+                                                          int32_t* anc_out) {
+  if (!*gate) return;
+  __shared__ uint64_t sm[4];
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t v = j < n ? mark[j] : 0;
+  const uint64_t c = carry[blockIdx.x];
+  v = v > c ? v : c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t u = __shfl_up(v, off, 64);
+    if (lane >= off && u > v) v = u;
+  }
+  if (lane == 63) sm[w] = v;
+  __syncthreads();
+  for (int k = 0; k < w; ++k) v = sm[k] > v ? sm[k] : v;
+  if (j >= n) return;
+  const int32_t a = (int32_t)(uint32_t)v;
+  anc_out[j] = (*zero_w && anc_old) ? anc_old[a] : a;
 }
 
 enum SearchMode { SEARCH_SYSTEMATIC = 0, SEARCH_MULTINOMIAL = 1, SEARCH_SAMPLE = 2 };
@@ -379,19 +619,64 @@ __device__ __forceinline__ uint64_t slot_target(const SearchArgs& s, const DevSc
   return scale_u53(u53_bits(w.x, w.y), dev->S);
 }
 
-__global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs g, const DevScalars* dev) {
-  if (!*g.gate) return;
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= s.n_slots) return;
-  const uint64_t target = slot_target(s, dev, s.slot_lo + j) - dev->base;
-  int64_t lo = 0, hi = s.n_cdf - 1;
-  while (lo < hi) {  // first i with C[i] - base > target
+// first i in [lo, hi] with C[i] - base > target (C[hi] - base > target holds)
+__device__ __forceinline__ int64_t cdf_search(const uint64_t* C, uint64_t base, uint64_t target,
+                                              int64_t lo, int64_t hi) {
+  while (lo < hi) {
     const int64_t mid = lo + ((hi - lo) >> 1);
-    if (s.C[mid] - dev->base > target) hi = mid;
+    if (C[mid] - base > target) hi = mid;
     else lo = mid + 1;
   }
+  return lo;
+}
+
+constexpr int kSearchWin = 256;  // CDF entries a wave stages in LDS
+
+// Ancestor search.  Systematic targets are monotone in the slot, so a wave's
+// 64 slots need a contiguous CDF window: the wave finds the window's ends
+// with two (wave-uniform) binary searches, stages up to 256 entries in LDS
+// and each lane finishes with an 8-step LDS search.  Wider windows (many
+// zero-offspring particles between the wave's ancestors) and random targets
+// (multinomial, sampling) use a per-lane binary search over the global CDF.
+__global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs g, const DevScalars* dev) {
+  if (!*g.gate) return;
+  __shared__ uint64_t win[kBlock / 64][kSearchWin];
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t jc = j < s.n_slots ? j : s.n_slots - 1;  // clamp: padding lanes mirror the last slot
+  const uint64_t base = dev->base;
+  const uint64_t target = slot_target(s, dev, s.slot_lo + jc) - base;
+  const int64_t hi_all = s.n_cdf - 1;
+  int64_t a;
+  if (s.mode == SEARCH_SYSTEMATIC) {
+    const uint64_t t_lo = __shfl(target, 0, 64);
+    const uint64_t t_hi = __shfl(target, 63, 64);
+    const int64_t a_lo = cdf_search(s.C, base, t_lo, 0, hi_all);
+    const int64_t a_hi = cdf_search(s.C, base, t_hi, a_lo, hi_all);
+    if (a_hi - a_lo < kSearchWin) {
+#pragma unroll
+      for (int k = 0; k < kSearchWin / 64; ++k) {
+        const int64_t i = a_lo + lane + 64 * k;
+        win[w][lane + 64 * k] = i <= a_hi ? s.C[i] - base : ~0ull;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      int lo = 0, hi = (int)(a_hi - a_lo);
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (win[w][mid] > target) hi = mid;
+        else lo = mid + 1;
+      }
+      a = a_lo + lo;
+    } else {
+      a = cdf_search(s.C, base, target, a_lo, a_hi);
+    }
+  } else {
+    a = cdf_search(s.C, base, target, 0, hi_all);
+  }
+  if (j >= s.n_slots) return;
   const int zero = *g.zero_w;
-  s.anc_out[j] = (zero && s.anc_old) ? s.anc_old[lo] : (int32_t)lo;
+  s.anc_out[j] = (zero && s.anc_old) ? s.anc_old[a] : (int32_t)a;
 }
 
 __global__ void k_copy_anc(const int* gate, const int32_t* src, int32_t* dst, int64_t n) {

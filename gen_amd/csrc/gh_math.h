@@ -50,9 +50,11 @@ GH_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
-    const uint32_t hi0 = mulhi32(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi1 = mulhi32(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    // one 32x32->64 multiply per word pair (v_mad_u64_u32) gives hi and lo
+    const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c.z;
+    c = u32x4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
+              (uint32_t)p0};
   }
   return c;
 }
@@ -173,27 +175,25 @@ GH_HD double cos_kernel(double x) {
 }
 
 // sin(2*pi*u), cos(2*pi*u) for u in [0,1) (u a multiple of 2^-53).
+// Octant o = floor(8u), f = 8u - o (both exact).  Even octants evaluate the
+// kernels at f*pi/4, odd ones at (1-f)*pi/4 (1-f exact) with sin/cos swapped;
+// the quadrant then permutes and negates.  Written with selects so a wave
+// evaluates the two polynomials once, whatever its lanes' octants.
 GH_HD void sincos_2pi(double u, double* s, double* c) {
   const double v = u * 8.0;               // exact
   const double o = floor(v);              // octant 0..7
   const double f = v - o;                 // exact, in [0,1)
   const int oi = (int)o;
-  double ss, cc;
-  if (oi & 1) {
-    const double b = (1.0 - f) * 0x1.921fb54442d18p-1;  // 1-f exact
-    ss = cos_kernel(b);
-    cc = sin_kernel(b);
-  } else {
-    const double a = f * 0x1.921fb54442d18p-1;
-    ss = sin_kernel(a);
-    cc = cos_kernel(a);
-  }
-  switch (oi >> 1) {
-    case 0: *s = ss; *c = cc; break;
-    case 1: *s = cc; *c = -ss; break;
-    case 2: *s = -ss; *c = -cc; break;
-    default: *s = -cc; *c = ss; break;
-  }
+  const bool odd = (oi & 1) != 0;
+  const double a = (odd ? (1.0 - f) : f) * 0x1.921fb54442d18p-1;
+  const double sk = sin_kernel(a), ck = cos_kernel(a);
+  const double ss = odd ? ck : sk, cc = odd ? sk : ck;
+  const int q = oi >> 1;
+  // q=0: (ss, cc)  q=1: (cc, -ss)  q=2: (-ss, -cc)  q=3: (-cc, ss)
+  const double s0 = (q & 1) ? cc : ss;
+  const double c0 = (q & 1) ? ss : cc;
+  *s = (q >= 2) ? -s0 : s0;
+  *c = (q == 1 || q == 2) ? -c0 : c0;
 }
 
 // cos(x) for moderate |x| (< 2^19 * pi/2): fdlibm three-part pi/2 reduction.

@@ -44,9 +44,16 @@ struct LGParams {
   double cstR;        // -0.5 (dy log 2pi + log det R)
 };
 
-template <int D>
+// S: structure known at model-compile time (host detects exact zeros):
+//   bit 0 — chol(Q) is diagonal:   L z needs only the diagonal terms
+//   bit 1 — L_R^{-1} H is diagonal (dy == d): the residual needs only x_r
+// The skipped terms are exactly-zero matrix entries; the oracle applies the
+// same rule, so both paths stay bit-identical.
+template <int D, int S = 0>
 struct LGModel {
   static constexpr int kD = D;
+  // spill-free register budgets measured with tools/regs.py
+  static constexpr int kMinWaves = (D <= 4) ? 8 : (S == 3 ? 7 : 5);
   using Params = LGParams;
 
   __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, uint32_t stream,
@@ -64,11 +71,19 @@ struct LGModel {
   __device__ static double obs(const Params& p, const StepObs& o, const double* x) {
     if (!o.present) return 0.0;
     double quad = 0.0;
-    for (int r = 0; r < p.dy; ++r) {
-      double acc = o.v[r];
+    if (S & 2) {
 #pragma unroll
-      for (int j = 0; j < D; ++j) acc = fma(-p.M[r * D + j], x[j], acc);
-      quad = fma(acc, acc, quad);
+      for (int r = 0; r < D; ++r) {
+        const double acc = fma(-p.M[r * D + r], x[r], o.v[r]);
+        quad = fma(acc, acc, quad);
+      }
+    } else {
+      for (int r = 0; r < p.dy; ++r) {
+        double acc = o.v[r];
+#pragma unroll
+        for (int j = 0; j < D; ++j) acc = fma(-p.M[r * D + j], x[j], acc);
+        quad = fma(acc, acc, quad);
+      }
     }
     return p.cstR - 0.5 * quad;
   }
@@ -96,8 +111,12 @@ struct LGModel {
       double acc = p.b[i];
 #pragma unroll
       for (int k = 0; k < D; ++k) acc = fma(p.A[i * D + k], xp[k], acc);
+      if (S & 1) {
+        acc = fma(p.LQ[i * D + i], z[i], acc);
+      } else {
 #pragma unroll
-      for (int k = 0; k <= i; ++k) acc = fma(p.LQ[i * D + k], z[k], acc);
+        for (int k = 0; k <= i; ++k) acc = fma(p.LQ[i * D + k], z[k], acc);
+      }
       x[i] = acc;
     }
     return obs(p, o, x);
@@ -150,6 +169,7 @@ __device__ __forceinline__ int cat_sample_prod(const double* a, int sa, const do
 
 struct HMMModel {
   static constexpr int kD = 1;
+  static constexpr int kMinWaves = 8;
   using Params = HMMParams;
 
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
@@ -194,6 +214,7 @@ struct KitParams {
 
 struct KitModel {
   static constexpr int kD = 1;
+  static constexpr int kMinWaves = 8;
   using Params = KitParams;
 
   __device__ static double obs(const Params& p, const StepObs& o, double x) {

@@ -214,6 +214,7 @@ typedef struct {
   int family, d, dy, k, v;
   /* LGSSM */
   double *A, *b, *LQ, *M, *LR, *c, *mu0, *L0, cstR;
+  int lq_diag, m_diag;  /* exact-zero structure: skipped terms */
   /* HMM */
   double *prior, *T, *E, *logE;
   /* Kitagawa */
@@ -247,6 +248,12 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->L0 = malloc(sizeof(double) * d * d);
     if (chol(d, P0, m->L0)) return -2;
     m->cstR = gauss_cst(dy, m->LR);
+    m->lq_diag = 1;
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < i; ++j) if (m->LQ[i * d + j] != 0.0) m->lq_diag = 0;
+    m->m_diag = dy == d;
+    for (int r = 0; m->m_diag && r < dy; ++r)
+      for (int j = 0; j < d; ++j) if (j != r && m->M[r * d + j] != 0.0) m->m_diag = 0;
   } else if (family == ORC_HMM) {
     if (np < (int64_t)k + (int64_t)k * k + (int64_t)v * k) return -1;
     m->d = 1;
@@ -292,6 +299,13 @@ static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* 
 static double lgssm_obs(const model_t* m, const double* x, const obs_t* o) {
   if (!o->present) return 0.0;
   double quad = 0.0;
+  if (m->m_diag) {
+    for (int r = 0; r < m->dy; ++r) {
+      double acc = fma(-m->M[r * m->d + r], x[r], o->bt[r]);
+      quad = fma(acc, acc, quad);
+    }
+    return m->cstR - 0.5 * quad;
+  }
   for (int r = 0; r < m->dy; ++r) {
     double acc = o->bt[r];
     for (int j = 0; j < m->d; ++j) acc = fma(-m->M[r * m->d + j], x[j], acc);
@@ -364,7 +378,8 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
     for (int i = 0; i < d; ++i) {
       double acc = m->b[i];
       for (int k = 0; k < d; ++k) acc = fma(m->A[i * d + k], xp[k], acc);
-      for (int k = 0; k <= i; ++k) acc = fma(m->LQ[i * d + k], z[k], acc);
+      if (m->lq_diag) acc = fma(m->LQ[i * d + i], z[i], acc);
+      else for (int k = 0; k <= i; ++k) acc = fma(m->LQ[i * d + k], z[k], acc);
       x[i] = acc;
     }
     return lgssm_obs(m, x, o);

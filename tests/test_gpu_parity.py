@@ -101,6 +101,25 @@ def test_lgssm_parity(gh_ctx, d, thr):
         assert np.array_equal(st.states(t).T, orc.trajectory(t)), t
 
 
+def random_lgssm(d, dy, seed):
+    rng = np.random.default_rng(seed)
+    A = 0.5 * np.eye(d) + 0.1 * rng.standard_normal((d, d))
+    B = rng.standard_normal((d, d))
+    C = rng.standard_normal((dy, dy))
+    return gen.LinearGaussianSSM(A, 0.1 * B @ B.T + 0.05 * np.eye(d), rng.standard_normal((dy, d)),
+                                 0.2 * C @ C.T + 0.3 * np.eye(dy), rng.standard_normal(d), np.eye(d),
+                                 b=0.1 * rng.standard_normal(d), c=0.1 * rng.standard_normal(dy))
+
+
+@pytest.mark.parametrize("d,dy", [(4, 3), (10, 10), (3, 7)])
+def test_lgssm_dense_parity(gh_ctx, d, dy):
+    # dense Q, R, H (no structure specialisation) and non-zero offsets b, c
+    m = random_lgssm(d, dy, 11)
+    _, ys = m.simulate(12, np.random.default_rng(4))
+    st, orc = run_both(m, ys, 9001, seed=3)
+    assert_lml_close(st, orc)
+
+
 def test_lgssm_multinomial_parity(gh_ctx):
     m = gen.LinearGaussianSSM.benchmark(3)
     _, ys = m.simulate(10, np.random.default_rng(3))
@@ -189,6 +208,22 @@ def test_all_weights_minus_inf_is_numeric_error(gh_ctx):
     with pytest.raises(gen.GenHipError) as e:
         gen.maybe_resample(st)
     assert e.value.code == 3
+
+
+def test_parents_before_step_and_double_resample(gh_ctx):
+    # ancestors of a pending systematic resample are readable before the step
+    m = gen.LinearGaussianSSM.benchmark(3)
+    _, ys = m.simulate(3, np.random.default_rng(9))
+    n = 4099
+    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=8)
+    orc = O.OraclePF(m, n, 8)
+    orc.init(ys[0])
+    assert gen.maybe_resample(st, n + 1) and orc.maybe_resample(n + 1)[0]
+    assert np.array_equal(st.parents, orc.parents())
+    assert np.array_equal(st.states().T, orc.state())
+    gen.particle_filter_step(st, (2,), (gen.UnknownChange(),), {("chain", 2, "y"): ys[1]})
+    orc.step(ys[1])
+    assert np.array_equal(st.states().T, orc.state())
 
 
 def test_double_maybe_resample(gh_ctx):
