@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-history", action="store_true")
+    p.add_argument("--ess-threshold", type=float, default=None, help="default N/2 (the reference's default)")
     return p.parse_args()
 
 
@@ -105,7 +106,7 @@ def main():
         model, (1,), {("chain", 1, "y"): ys[0]}, n_global, seed=42, resampler=a.resampler,
         record_history=not a.no_history, history_capacity=T + 2, time_kernels=True,
     )
-    gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]))
+    gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold)
     ctx.synchronize()
     st.kernel_time_ms(reset=True)
     ess0, did0 = st.ess_history()
@@ -117,7 +118,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    gen.run_particle_filter(st, list(ys[1 + a.warmup : 1 + a.warmup + a.steps]))
+    gen.run_particle_filter(st, list(ys[1 + a.warmup : 1 + a.warmup + a.steps]), a.ess_threshold)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:

@@ -58,6 +58,7 @@ extern "C" const char* gh_version(void) { return "gen_hip 0.1.0 (gfx950)"; }
 // --------------------------------------------------------------- context
 struct gh_ctx {
   int device = 0;
+  int cus = 256;  // compute units
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int rank = 0, world = 1;
@@ -67,6 +68,7 @@ struct gh_ctx {
 static int ctx_setup(int device, void* stream, gh_ctx* c) {
   c->device = device;
   HIP_TRY(hipSetDevice(device));
+  HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
   if (stream) {
     c->stream = (hipStream_t)stream;
   } else {
@@ -268,6 +270,7 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
   if (m->family == GH_FAMILY_LGSSM) {
     const int d = m->d, dy = m->dy;
     double* q = m->dparams;
+    m->lg.base = m->dparams;
     m->lg.A = q; q += d * d;
     m->lg.b = q; q += d;
     m->lg.LQ = q; q += d * d;
@@ -276,6 +279,7 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->lg.L0 = q;
   } else if (m->family == GH_FAMILY_HMM) {
     const int K = m->k, V = m->v;
+    m->hmm.base = m->dparams;
     m->hmm.prior = m->dparams;
     m->hmm.T = m->dparams + K;
     m->hmm.E = m->dparams + K + K * K;
@@ -343,6 +347,8 @@ struct gh_pf {
   uint64_t* cmark = nullptr;      // systematic: tagged carry per step block
   uint64_t epoch = 0;             // resample counter for the tags
   bool marks_pending = false;     // last resample's ancestors only exist as marks
+  double thr_hint = 0.0;          // threshold the next maybe_resample! is expected to use
+  bool hint_valid = false;        // k_fold pre-evaluated the decision for thr_hint
   uint64_t* bsum = nullptr;
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
@@ -447,8 +453,13 @@ template <class Model>
 static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const StepObs& o,
                           const StepArgs& a, bool init) {
   const dim3 grid((unsigned)pf->nb_step), block(kBlock);
-  if (init) hipLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, p, o, a);
-  else hipLaunchKernelGGL((k_step<Model, false>), grid, block, 0, pf->s, p, o, a);
+  if (init) hipLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, pf->m->dparams, p, o, a);
+  else hipLaunchKernelGGL((k_step<Model, false>), grid, block, 0, pf->s, pf->m->dparams, p, o, a);
+  // single rank: pre-evaluate the next maybe_resample! for the threshold last used
+  const double hint = pf->ctx->world == 1 ? pf->thr_hint : 0.0;
+  hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_step,
+                     a.stats_out, pf->dev, init ? 0 : 1, hint, pf->n_global);
+  pf->hint_valid = hint > 0.0;
 }
 
 static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
@@ -536,7 +547,7 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   ALLOC(pf->logw, sizeof(double) * n);
   ALLOC(pf->C, sizeof(uint64_t) * n);
   ALLOC(pf->mark, sizeof(uint64_t) * n);
-  ALLOC(pf->cmark, sizeof(uint64_t) * pf->nb_step);
+  ALLOC(pf->cmark, sizeof(uint64_t) * ((n + 63) / 64));
   ALLOC(pf->bsum, sizeof(uint64_t) * pf->nb_scan);
   ALLOC(pf->pm, sizeof(double) * pf->nb_step);
   ALLOC(pf->ps, sizeof(double) * pf->nb_step);
@@ -569,7 +580,7 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
     if (hipMemcpyAsync(pf->dev, &z, sizeof z, hipMemcpyHostToDevice, pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init scalars"));
     if (hipMemsetAsync(pf->mark, 0, sizeof(uint64_t) * n, pf->s) != hipSuccess ||
-        hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * pf->nb_step, pf->s) != hipSuccess)
+        hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * ((n + 63) / 64), pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init marks"));
     if (hipStreamSynchronize(pf->s) != hipSuccess) return fail(set_err(GH_E_HIP, "sync"));
   }
@@ -683,9 +694,12 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   const bool fused = !second && n > 0;
   if (second && pf->marks_pending) CHECK(materialize_marks(pf));
   if (!fused) hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, pf->s, d, pf->dev);
+  const int fmode = !fused ? 0 : ((pf->hint_valid && pf->thr_hint == thr) ? 2 : 1);
+  pf->thr_hint = thr;
+  pf->hint_valid = false;
   if (n > 0)
     hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum,
-                       fused ? 1 : 0, d, pf->dev);
+                       fmode, d, pf->dev);
   if (R > 1) {
     hipLaunchKernelGGL(k_rank_total, dim3(1), dim3(kBlock), 0, pf->s, g.gate, pf->bsum, n > 0 ? pf->nb_scan : 0,
                        pf->dev);
@@ -698,7 +712,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   mk.cmark = pf->cmark;
   mk.epoch = ++pf->epoch;
   mk.n_global = pf->n_global;
-  mk.nb_step = pf->nb_step;
+  mk.n_groups = (pf->n + 63) / 64;
   mk.enabled = sys1 ? 1 : 0;
   CdfArgs ca{};
   ca.bsum = pf->bsum;
@@ -723,6 +737,9 @@ static int resample_enqueue(gh_pf* pf, double thr) {
                          pf->anc_scratch, anc_target, n);
     } else {
       pf->marks_pending = true;
+#if defined(GH_ABLATE_MARKS)  // timing-only variant: expand the marks in their own launch
+      CHECK(materialize_marks(pf));
+#endif
     }
   } else if (R == 1) {
     SearchArgs sa{};

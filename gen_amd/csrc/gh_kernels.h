@@ -38,9 +38,13 @@ struct DevScalars {
   int spend;           // sample_unweighted: weights are all equal
   int one;             // constant 1 (gate for unconditional launches)
   int error;           // gh_status raised on the device
-  unsigned ticket;     // last-block-done counter of k_step
-  unsigned ticket_q;   // ... of k_qsum
-  unsigned ticket_c;   // ... of k_cdf
+  unsigned ticket;     // (unused; kept for layout)
+  unsigned ticket_q;
+  unsigned ticket_c;
+  // decision pre-evaluated by k_fold for the threshold the host expects the
+  // next maybe_resample! to use (single rank); committed by k_qsum
+  double cM, cL, cess;
+  int cfire, cerr;
 
 };
 
@@ -49,7 +53,7 @@ struct StepArgs {
   int64_t ld_prev;
   int32_t* anc;          // ancestors for this step (read when a resample is pending;
                          // written here when they come from the systematic marks)
-  const uint64_t* mark;  // systematic range marks + per-block carries (mark_mode)
+  const uint64_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode)
   const uint64_t* carry;
   int mark_mode;
   const double* remote;  // multi-rank: states received from other ranks [D][ld_remote]
@@ -104,121 +108,95 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
   return (sm[0] + sm[1]) + (sm[2] + sm[3]);
 }
 
-// Combine per-block (m, s, s2) partials into the rank's triple.  Called by
-// the last block of k_step after the agent-scope acquire.
-__device__ void fold_partials(double* pm, double* ps, double* ps2, int nb,
-                              double* sm, double* out) {
-  double m = -INFINITY;
-  for (int b = threadIdx.x; b < nb; b += kBlock)
-    m = fmax(m, __hip_atomic_load(&pm[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const double M = block_max(m, sm);
-  double s = 0.0, s2 = 0.0;
-  if (M > -INFINITY) {
-    for (int b = threadIdx.x; b < nb; b += kBlock) {
-      const double mb = __hip_atomic_load(&pm[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (mb > -INFINITY) {
-        const double e = gh_exp(mb - M);
-        s += __hip_atomic_load(&ps[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * e;
-        s2 += __hip_atomic_load(&ps2[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) * (e * e);
-      }
-    }
-  }
-  s = block_sum(s, sm);
-  s2 = block_sum(s2, sm);
-  if (threadIdx.x == 0) {
-    out[0] = M;
-    out[1] = s;
-    out[2] = s2;
-  }
-}
-
 // ---------------------------------------------------------------- k_step
+// One particle per lane, 64-particle tiles per wave, 4 waves per block.
+// Systematic ancestors come from the range marks by a wave-level prefix max
+// seeded with the carry of the tile's 64-slot group (no block barrier).  Each
+// block writes one (max, sum e, sum e^2) partial with plain stores; k_fold
+// combines them in the next launch (a single-word ticket per block would
+// serialise ~4k atomics per 1M particles at the memory side).
 template <class Model, bool INIT>
-// occupancy target per model (waves per SIMD the register budget must allow)
-__global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(typename Model::Params p, StepObs o, StepArgs a) {
+__global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double* __restrict__ prm,
+                                                                    typename Model::Params p0, StepObs o,
+                                                                    StepArgs a) {
   constexpr int D = Model::kD;
-  __shared__ double sm[8];
-  __shared__ int am_last;
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const typename Model::Params p = p0.rebase(prm);
+  __shared__ double sm[3][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + w;
+  const int64_t j = tile * 64 + lane;
   int pend = 0, use_marks = 0;
   if (!INIT) {
     const int pending = a.dev->pending, fire = a.dev->fire;
     pend = pending | fire;
     use_marks = a.mark_mode && fire && !pending;
   }
-  int64_t src = j;
-  if (use_marks) {
-    // systematic ancestors from the range marks: block-wide prefix max seeded
-    // with the block's carry (the ancestor of its first slot)
-    __shared__ uint64_t smk[4];
-    uint64_t v = j < a.n ? a.mark[j] : 0;
-    const uint64_t c = a.carry[blockIdx.x];
-    v = v > c ? v : c;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint64_t u = __shfl_up(v, off, 64);
-      if (lane >= off && u > v) v = u;
-    }
-    if (lane == 63) smk[w] = v;
-    __syncthreads();
-    for (int k = 0; k < w; ++k) v = smk[k] > v ? smk[k] : v;
-    src = (int64_t)(uint32_t)v;
-    if (j < a.n) a.anc[j] = (int32_t)src;  // genealogy record
-  }
   double lw = -INFINITY;
-  if (j < a.n) {
-    double x[D];
-    double inc;
-    if (INIT) {
-      inc = Model::init(p, o, a.seed, (uint64_t)(a.lo + j), a.proposal, x);
-      lw = inc;
-    } else {
-      double xp[D];
-      if (pend && !use_marks) src = a.anc[j];
-      if (src >= 0) {
+  if (tile * 64 < a.n) {  // wave-uniform
+    int64_t src = j;
+    if (use_marks) {
+      uint64_t v = j < a.n ? a.mark[j] : 0;
+      const uint64_t c = a.carry[tile];
+      v = v > c ? v : c;
 #pragma unroll
-        for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
-      } else {
-#pragma unroll
-        for (int k = 0; k < D; ++k) xp[k] = a.remote[k * a.ld_remote + (-1 - src)];
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t u = __shfl_up(v, off, 64);
+        if (lane >= off && u > v) v = u;
       }
-      inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x);
-      lw = (pend ? 0.0 : a.logw[j]) + inc;
+      src = (int64_t)(uint32_t)v;
+      if (j < a.n) a.anc[j] = (int32_t)src;  // genealogy record
     }
+    if (j < a.n) {
+      double x[D];
+      if (INIT) {
+        lw = Model::init(p, o, a.seed, (uint64_t)(a.lo + j), a.proposal, x);
+      } else {
+        double xp[D];
+        if (pend && !use_marks) src = a.anc[j];
+        if (src >= 0) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.xout[k * a.ld_out + j] = x[k];
-    a.logw[j] = lw;
+          for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
+        } else {
+#pragma unroll
+          for (int k = 0; k < D; ++k) xp[k] = a.remote[k * a.ld_remote + (-1 - src)];
+        }
+        const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x);
+        lw = (pend ? 0.0 : a.logw[j]) + inc;
+      }
+#pragma unroll
+      for (int k = 0; k < D; ++k) a.xout[k * a.ld_out + j] = x[k];
+      a.logw[j] = lw;
+    }
   }
-  // block partials of (max, sum e, sum e^2)
-  const double mb = block_max(lw, sm);
+#if defined(GH_ABLATE_REDUCE)  // timing-only variant: no statistics at all
+  asm volatile("" ::"v"(lw));
+  return;
+#endif
+  // block partial: wave (max, sum, sum^2), then the 4 waves through LDS
+  const double mw = wave_max(lw);
   double e = 0.0;
-  if (mb > -INFINITY && lw > -INFINITY) e = gh_exp(lw - mb);
-  const double sb = block_sum(e, sm);
-  const double s2b = block_sum(e * e, sm);
-  if (threadIdx.x == 0) {
-    // Publish the three partials with 8-byte agent-scope (sc1) stores, drain
-    // them, then take a ticket.  No release fence: a fence would write back
-    // this XCD's whole L2 (the block's freshly written states) per block.
-    __hip_atomic_store(&a.pm[blockIdx.x], mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.ps[blockIdx.x], sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&a.ps2[blockIdx.x], s2b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev =
-        __hip_atomic_fetch_add(&a.dev->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    am_last = (prev == gridDim.x - 1);
+  if (lw > -INFINITY) e = gh_exp(lw - mw);
+  if (lw != lw) e = lw;  // NaN poisons the statistics
+  const double sw = wave_sum(e), s2w = wave_sum(e * e);
+  if (lane == 0) {
+    sm[0][w] = mw;
+    sm[1][w] = sw;
+    sm[2][w] = s2w;
   }
   __syncthreads();
-  if (!am_last) return;
-  // the last arriver reads every partial with sc1 loads (fold_partials)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  fold_partials(a.pm, a.ps, a.ps2, (int)gridDim.x, sm, a.stats_out);
   if (threadIdx.x == 0) {
-    __hip_atomic_store(&a.dev->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!INIT) {
-      a.dev->pending = 0;
-      a.dev->fire = 0;
-    }
+    double mb = -INFINITY, sb = 0.0, s2b = 0.0;
+    for (int k = 0; k < 4; ++k) mb = fmax(mb, sm[0][k]);
+    if (mb > -INFINITY)
+      for (int k = 0; k < 4; ++k)
+        if (sm[0][k] > -INFINITY) {
+          const double f = gh_exp(sm[0][k] - mb);
+          sb += sm[1][k] * f;
+          s2b += sm[2][k] * (f * f);
+        }
+    a.pm[blockIdx.x] = mb;
+    a.ps[blockIdx.x] = sb;
+    a.ps2[blockIdx.x] = s2b;
   }
 }
 
@@ -295,6 +273,84 @@ __global__ void k_decide(DecideArgs d, DevScalars* dev) {
   }
   const Decision r = decide(d, dev->pending != 0);
   commit_decision(d, r, dev, dev->pending);
+}
+
+// Fold the step kernel's block partials into the rank's (M, S, S2) and clear
+// the resample flags the step consumed (one 1024-thread block, partial loads
+// issued eight at a time).  On a single rank it also pre-evaluates the next
+// maybe_resample! decision for `thr_hint` (> 0), so k_qsum's blocks need not.
+__global__ __launch_bounds__(1024) void k_fold(const double* pm, const double* ps, const double* ps2, int nb,
+                                               double* stats_out, DevScalars* dev, int clear_flags,
+                                               double thr_hint, int64_t n_global) {
+  __shared__ double sm[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double m = -INFINITY;
+  for (int b0 = threadIdx.x; b0 < nb; b0 += 1024 * 8) {
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (b0 + 1024 * k < nb) ? pm[b0 + 1024 * k] : -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmax(m, v[k]);
+  }
+  m = wave_max(m);
+  if (lane == 0) sm[w] = m;
+  __syncthreads();
+  double M = -INFINITY;
+  for (int k = 0; k < 16; ++k) M = fmax(M, sm[k]);
+  double s = 0.0, s2 = 0.0;
+  if (M > -INFINITY) {
+    for (int b0 = threadIdx.x; b0 < nb; b0 += 1024 * 8) {
+      double mv[8], sv[8], s2v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int b = b0 + 1024 * k;
+        mv[k] = b < nb ? pm[b] : -INFINITY;
+        sv[k] = b < nb ? ps[b] : 0.0;
+        s2v[k] = b < nb ? ps2[b] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (mv[k] > -INFINITY) {
+          const double f = gh_exp(mv[k] - M);
+          s += sv[k] * f;
+          s2 += s2v[k] * (f * f);
+        }
+    }
+  }
+  s = wave_sum(s);
+  s2 = wave_sum(s2);
+  __syncthreads();
+  if (lane == 0) sm[w] = s;
+  __syncthreads();
+  double S = 0.0;
+  for (int k = 0; k < 16; ++k) S += sm[k];
+  __syncthreads();
+  if (lane == 0) sm[w] = s2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double S2 = 0.0;
+    for (int k = 0; k < 16; ++k) S2 += sm[k];
+    stats_out[0] = M;
+    stats_out[1] = S;
+    stats_out[2] = S2;
+    if (clear_flags) {
+      dev->pending = 0;
+      dev->fire = 0;
+    }
+    if (thr_hint > 0.0) {
+      DecideArgs d{};
+      d.stats_all = stats_out;
+      d.R = 1;
+      d.n_global = n_global;
+      d.thr = thr_hint;
+      const Decision r = decide(d, false);
+      dev->cM = r.M;
+      dev->cL = r.L;
+      dev->cess = r.ess;
+      dev->cfire = r.fire;
+      dev->cerr = r.err;
+    }
+  }
 }
 
 // ------------------------------------------------------ integer CDF kernels
@@ -384,7 +440,16 @@ __global__ __launch_bounds__(kBlock) void k_qsum(const double* logw, int64_t n, 
   __shared__ int sfire;
   if (fused) {
     if (threadIdx.x == 0) {
-      const Decision r = decide(d, false);
+      Decision r;
+      if (fused == 2) {  // pre-evaluated by k_fold for this threshold
+        r.M = dev->cM;
+        r.L = dev->cL;
+        r.ess = dev->cess;
+        r.fire = dev->cfire;
+        r.err = dev->cerr;
+      } else {
+        r = decide(d, false);
+      }
       if (blockIdx.x == 0) commit_decision(d, r, dev, 0);
       sM = r.M;
       sfire = r.fire;
@@ -450,10 +515,10 @@ __device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, 
 
 struct MarkArgs {
   uint64_t* mark;     // [n slots] tagged (epoch << 32 | ancestor) at each range start
-  uint64_t* cmark;    // [step blocks] tagged ancestor of the block's first slot
+  uint64_t* cmark;    // [64-slot groups] tagged ancestor of the group's first slot
   uint64_t epoch;     // resample counter (tags older marks as stale)
   int64_t n_global;
-  int64_t nb_step;    // step blocks (entries of cmark)
+  int64_t n_groups;   // 64-slot groups (entries of cmark)
   int enabled;        // systematic single-rank path
 };
 
@@ -552,11 +617,11 @@ __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, G
     s_i = e_i;
   }
   __syncthreads();
-  // step-block starts inside [first slot, last slot end) of this particle block
+  // 64-slot group starts inside [first slot, last slot end) of this particle block
   const int64_t s_lo = sfirst, s_hi = se[kScanTile - 1];
   const int64_t pbase = (int64_t)blockIdx.x * kScanTile;
-  for (int64_t b = (s_lo + kBlock - 1) / kBlock + threadIdx.x; b * kBlock < s_hi; b += kBlock) {
-    const int32_t slot = (int32_t)(b * kBlock);
+  for (int64_t b = (s_lo + 63) / 64 + threadIdx.x; b * 64 < s_hi; b += kBlock) {
+    const int32_t slot = (int32_t)(b * 64);
     int lo = 0, hi = kScanTile - 1;  // first particle p with se[p] > slot
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -567,27 +632,24 @@ __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, G
   }
 }
 
-// systematic ancestors: block-wide prefix max of the slot marks seeded with
-// the block's carry (no search at all)
+// systematic ancestors (materialised outside a step): wave-level prefix max
+// of the slot marks seeded with the carry of the 64-slot group
 __global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const int* zero_w,
                                                           const uint64_t* mark, const uint64_t* carry,
                                                           int64_t n, const int32_t* anc_old,
                                                           int32_t* anc_out) {
   if (!*gate) return;
-  __shared__ uint64_t sm[4];
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  if ((j & ~63LL) >= n) return;  // whole wave past the end
   uint64_t v = j < n ? mark[j] : 0;
-  const uint64_t c = carry[blockIdx.x];
+  const uint64_t c = carry[j >> 6];
   v = v > c ? v : c;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const uint64_t u = __shfl_up(v, off, 64);
     if (lane >= off && u > v) v = u;
   }
-  if (lane == 63) sm[w] = v;
-  __syncthreads();
-  for (int k = 0; k < w; ++k) v = sm[k] > v ? sm[k] : v;
   if (j >= n) return;
   const int32_t a = (int32_t)(uint32_t)v;
   anc_out[j] = (*zero_w && anc_old) ? anc_old[a] : a;

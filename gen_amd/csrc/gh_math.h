@@ -43,9 +43,12 @@ GH_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
   return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
 }
 
+#ifndef GH_PHILOX_ROUNDS
+#define GH_PHILOX_ROUNDS 10  // timing-only variants may lower it; the product uses 10
+#endif
 GH_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < GH_PHILOX_ROUNDS; ++r) {
     if (r) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
@@ -214,6 +217,11 @@ GH_HD double gh_cos(double x) {
 // ------------------------------------------------------------ normals
 // Box–Muller on one Philox block: two standard normals.
 GH_HD void normal_pair(u32x4 w, double* z0, double* z1) {
+#if defined(GH_ABLATE_BOXMULLER)  // timing-only variant: uniforms instead of normals
+  *z0 = u53(w.x, w.y) - 0.5;
+  *z1 = u53(w.z, w.w) - 0.5;
+  return;
+#endif
   const double u1 = 1.0 - u53(w.x, w.y);  // (0, 1]
   const double u2 = u53(w.z, w.w);        // [0, 1)
   const double r = sqrt(-2.0 * gh_log(u1));

@@ -33,7 +33,17 @@ struct StepObs {
 };
 
 // ------------------------------------------------------------------ LGSSM
+// Parameter blocks hold pointers into one device buffer.  rebase() re-derives
+// them from the kernel's `const double* __restrict__` argument so the
+// compiler can prove no store of the kernel clobbers them and reads them
+// through the scalar cache (s_load) instead of per-lane vector loads.
+template <class P>
+__device__ __forceinline__ const double* rebased(const P& p, const double* __restrict__ prm, const double* ptr) {
+  return prm + (ptr - p.base);
+}
+
 struct LGParams {
+  const double* base; // start of the device parameter buffer
   const double* A;    // d*d
   const double* b;    // d
   const double* LQ;   // d*d lower Cholesky factor of Q
@@ -42,6 +52,16 @@ struct LGParams {
   const double* L0;   // d*d lower Cholesky factor of P0
   int dy;
   double cstR;        // -0.5 (dy log 2pi + log det R)
+  __device__ LGParams rebase(const double* __restrict__ prm) const {
+    LGParams q = *this;
+    q.A = rebased(*this, prm, A);
+    q.b = rebased(*this, prm, b);
+    q.LQ = rebased(*this, prm, LQ);
+    q.M = rebased(*this, prm, M);
+    q.mu0 = rebased(*this, prm, mu0);
+    q.L0 = rebased(*this, prm, L0);
+    return q;
+  }
 };
 
 // S: structure known at model-compile time (host detects exact zeros):
@@ -53,7 +73,7 @@ template <int D, int S = 0>
 struct LGModel {
   static constexpr int kD = D;
   // spill-free register budgets measured with tools/regs.py
-  static constexpr int kMinWaves = (D <= 4) ? 8 : (S == 3 ? 7 : 5);
+  static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 10 ? (S == 3 ? 7 : 5) : 4);
   using Params = LGParams;
 
   __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, uint32_t stream,
@@ -125,12 +145,21 @@ struct LGModel {
 
 // -------------------------------------------------------------------- HMM
 struct HMMParams {
+  const double* base;
   const double* prior;  // k
   const double* T;      // k*k, T[new*k + prev]
   const double* E;      // v*k, E[x*k + z]
   const double* logE;   // v*k
   int k;
   int v;
+  __device__ HMMParams rebase(const double* __restrict__ prm) const {
+    HMMParams q = *this;
+    q.prior = rebased(*this, prm, prior);
+    q.T = rebased(*this, prm, T);
+    q.E = rebased(*this, prm, E);
+    q.logE = rebased(*this, prm, logE);
+    return q;
+  }
 };
 
 // inverse-CDF categorical draw over p[0], p[stride], ... (sequential sums)
@@ -210,6 +239,7 @@ struct KitParams {
   double sx;        // sqrt(var_x)
   double inv2vy;    // 1 / (2 var_y)
   double csty;      // -0.5 log(2 pi var_y)
+  __device__ KitParams rebase(const double* __restrict__) const { return *this; }
 };
 
 struct KitModel {

@@ -1,0 +1,50 @@
+"""Timing-only ablation variants of libgen_hip.so (never the product).
+
+build:  python tools/variants.py build
+run:    python tools/variants.py run   (on the GPU box; one process per variant)
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VARIANTS = {
+    "base": [],
+    "no_bm_philox1": ["GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
+    "no_ticket": ["GH_ABLATE_TICKET"],
+    "no_reduce": ["GH_ABLATE_REDUCE"],
+    "no_reduce_no_rng": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
+}
+BENCH_ARGS = os.environ.get("GH_VARIANT_ARGS", "--no-history --ess-threshold 1e-300 --particles 4194304 --steps 30").split()
+
+
+def main():
+    if sys.argv[1] == "build":
+        from gen_amd import build as gb
+
+        for name, defs in VARIANTS.items():
+            if len(sys.argv) > 2 and name not in sys.argv[2:]:
+                continue
+            gb.build_variant(name, defs)
+            print("built", name, flush=True)
+    else:
+        out = {}
+        for name in VARIANTS:
+            lib = os.path.join(ROOT, "gen_amd", "variants", f"{name}.so")
+            env = dict(os.environ, GEN_HIP_LIB=lib)
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + BENCH_ARGS,
+                               env=env, capture_output=True, text=True, timeout=300)
+            try:
+                d = json.loads(r.stdout.strip().splitlines()[-1])
+                out[name] = {"ms_per_step": d["ms_per_step"], "k_step_ms": d["roofline"]["kernel_avg_ms"],
+                             "value": d["value"]}
+            except Exception:
+                out[name] = {"error": r.stderr[-500:]}
+            print(name, out[name], flush=True)
+        json.dump(out, open(os.path.join(ROOT, "gpurun_out", "variants.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
