@@ -68,6 +68,7 @@ SIGNATURES = {
     "gh_ctx_create": (c_int, [c_int, c_void_p, POINTER(c_void_p)]),
     "gh_comm_unique_id": (c_int, [POINTER(c_uint8)]),
     "gh_ctx_create_dist": (c_int, [c_int, c_int, c_int, POINTER(c_uint8), c_void_p, POINTER(c_void_p)]),
+    "gh_ctx_create_hostcomm": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, POINTER(c_void_p)]),
     "gh_ctx_destroy": (c_int, [c_void_p]),
     "gh_ctx_rank": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
     "gh_ctx_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
@@ -91,6 +92,7 @@ SIGNATURES = {
     "gh_pf_sample_unweighted": (c_int, [c_void_p, c_int64, c_uint64, POINTER(c_int64)]),
     "gh_pf_get_ess_history": (c_int, [c_void_p, c_int, POINTER(c_double), POINTER(c_int32)]),
     "gh_pf_kernel_time": (c_int, [c_void_p, POINTER(c_double), POINTER(c_int64), c_int]),
+    "gh_sys_plan": (c_int, [c_int64, c_int, c_int, POINTER(c_uint64), c_uint64, POINTER(c_int64), POINTER(c_int64), POINTER(c_int64), POINTER(c_int64)]),
     "gh_is_run": (c_int, [c_void_p, POINTER(Obs), c_int, c_int64, c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
     "gh_last_error": (c_char_p, []),
     "gh_version": (c_char_p, []),

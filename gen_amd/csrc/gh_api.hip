@@ -63,6 +63,11 @@ struct gh_ctx {
   bool own_stream = false;
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
+  // host-staged transport (gh_ctx_create_hostcomm)
+  bool host_comm = false;
+  gh_host_comm hc{};
+  char* stage = nullptr;  // pinned staging buffer
+  size_t stage_bytes = 0;
 };
 
 static int ctx_setup(int device, void* stream, gh_ctx* c) {
@@ -117,10 +122,26 @@ extern "C" int gh_ctx_create_dist(int device, int rank, int world, const uint8_t
   return GH_OK;
 }
 
+extern "C" int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_host_comm* comm,
+                                      void* hip_stream, gh_ctx** out) {
+  if (!out || !comm || !comm->allgather || !comm->sendrecv || world < 1 || rank < 0 || rank >= world)
+    return set_err(GH_E_INVAL, "gh_ctx_create_hostcomm: bad argument (rank/world %d/%d)", rank, world);
+  gh_ctx* c = new gh_ctx();
+  int rc = ctx_setup(device, hip_stream, c);
+  if (rc) { delete c; return rc; }
+  c->rank = rank;
+  c->world = world;
+  c->host_comm = true;
+  c->hc = *comm;
+  *out = c;
+  return GH_OK;
+}
+
 extern "C" int gh_ctx_destroy(gh_ctx* c) {
   if (!c) return GH_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->stage) hipHostFree(c->stage);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
@@ -137,6 +158,92 @@ extern "C" int gh_ctx_rank(const gh_ctx* c, int* rank, int* world) {
 extern "C" int gh_ctx_stream(const gh_ctx* c, void** s) {
   if (!c || !s) return set_err(GH_E_INVAL, "null ctx");
   *s = (void*)c->stream;
+  return GH_OK;
+}
+
+// ---------------------------------------------------------- transport
+// Two collectives cover the path: an all-gather of a few words per rank and a
+// grouped point-to-point exchange of state rows.  RCCL runs them on the
+// context stream with no host synchronisation; the host-staged transport
+// copies through pinned memory and calls the user's functions.
+struct CommMsg {
+  int peer;
+  void* dptr;
+  size_t bytes;
+};
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static int stage_reserve(gh_ctx* c, size_t bytes) {
+  if (bytes <= c->stage_bytes) return GH_OK;
+  size_t nb = c->stage_bytes ? c->stage_bytes : (1 << 16);
+  while (nb < bytes) nb *= 2;
+  if (c->stage) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    hipHostFree(c->stage);
+    c->stage = nullptr;
+    c->stage_bytes = 0;
+  }
+  HIP_TRY(hipHostMalloc((void**)&c->stage, nb, hipHostMallocDefault));
+  c->stage_bytes = nb;
+  return GH_OK;
+}
+
+static int comm_allgather(gh_ctx* c, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
+  if (!c->host_comm) {
+    NCCL_TRY(ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, s));
+    return GH_OK;
+  }
+  const size_t off = align_up(bytes);
+  CHECK(stage_reserve(c, off + bytes * (size_t)c->world));
+  HIP_TRY(hipMemcpyAsync(c->stage, dsend, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->hc.allgather(c->hc.user, c->stage, c->stage + off, bytes))
+    return set_err(GH_E_RCCL, "host transport: allgather failed");
+  HIP_TRY(hipMemcpyAsync(drecv, c->stage + off, bytes * (size_t)c->world, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return GH_OK;
+}
+
+static int comm_exchange(gh_ctx* c, const std::vector<CommMsg>& sends, const std::vector<CommMsg>& recvs,
+                         hipStream_t s) {
+  if (sends.empty() && recvs.empty()) return GH_OK;
+  if (!c->host_comm) {
+    NCCL_TRY(ncclGroupStart());
+    for (const auto& m : sends) NCCL_TRY(ncclSend(m.dptr, m.bytes, ncclUint8, m.peer, c->comm, s));
+    for (const auto& m : recvs) NCCL_TRY(ncclRecv(m.dptr, m.bytes, ncclUint8, m.peer, c->comm, s));
+    NCCL_TRY(ncclGroupEnd());
+    return GH_OK;
+  }
+  size_t total = 0;
+  for (const auto& m : sends) total += align_up(m.bytes);
+  for (const auto& m : recvs) total += align_up(m.bytes);
+  CHECK(stage_reserve(c, total));
+  std::vector<int> sp, rp;
+  std::vector<const void*> sb;
+  std::vector<void*> rb;
+  std::vector<uint64_t> sn, rn;
+  size_t off = 0;
+  for (const auto& m : sends) {
+    HIP_TRY(hipMemcpyAsync(c->stage + off, m.dptr, m.bytes, hipMemcpyDeviceToHost, s));
+    sp.push_back(m.peer);
+    sb.push_back(c->stage + off);
+    sn.push_back(m.bytes);
+    off += align_up(m.bytes);
+  }
+  for (const auto& m : recvs) {
+    rp.push_back(m.peer);
+    rb.push_back(c->stage + off);
+    rn.push_back(m.bytes);
+    off += align_up(m.bytes);
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->hc.sendrecv(c->hc.user, (int)sp.size(), sp.data(), sb.data(), sn.data(), (int)rp.size(), rp.data(),
+                     rb.data(), rn.data()))
+    return set_err(GH_E_RCCL, "host transport: sendrecv failed");
+  for (size_t i = 0; i < recvs.size(); ++i)
+    HIP_TRY(hipMemcpyAsync(recvs[i].dptr, rb[i], recvs[i].bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
   return GH_OK;
 }
 
@@ -360,10 +467,11 @@ struct gh_pf {
   double* ess_hist = nullptr;     // [cap+2]
   int32_t* res_hist = nullptr;    // [cap+2]
   // multi-rank resample exchange
-  double* recv = nullptr;         // [D][n]
-  double* send = nullptr;         // [D][n]
-  int64_t* xslot = nullptr;       // [n] slots emitted by this rank
-  int32_t* xanc = nullptr;        // [n]
+  double* rows_recv = nullptr;    // [n][D+1] rows received for this rank's slots
+  double* rows_send = nullptr;    // [send_cap][D+1] rows this rank sends
+  int32_t* xanc = nullptr;        // [send_cap] local ancestors of the sent rows
+  int64_t send_cap = 0;
+  int64_t* gparent = nullptr;     // [n] global parent ids of the last exchange
   std::vector<void*> chunks;      // history allocations (record_history)
   // kernel timing
   std::vector<hipEvent_t> ev;
@@ -435,7 +543,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->logw); hipFree(pf->C); hipFree(pf->mark); hipFree(pf->cmark); hipFree(pf->bsum); hipFree(pf->pm); hipFree(pf->ps);
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
-  hipFree(pf->recv); hipFree(pf->send); hipFree(pf->xslot); hipFree(pf->xanc);
+  hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
   if (!pf->opts.record_history) {
     for (auto p : pf->xs) hipFree(p);
     for (auto p : pf->ancs) hipFree(p);
@@ -510,8 +618,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
 // after the step kernel: share the rank's (M, S, S2) with every rank
 static int share_stats(gh_pf* pf) {
   if (pf->ctx->world == 1) return GH_OK;
-  NCCL_TRY(ncclAllGather(pf->dev->stats, pf->stats_all, 3, ncclDouble, pf->ctx->comm, pf->s));
-  return GH_OK;
+  return comm_allgather(pf->ctx, pf->dev->stats, pf->stats_all, 3 * sizeof(double), pf->s);
 }
 
 extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles,
@@ -557,10 +664,10 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   ALLOC(pf->totals_all, sizeof(uint64_t) * ctx->world);
   ALLOC(pf->anc_scratch, sizeof(int32_t) * n);
   if (ctx->world > 1) {
-    ALLOC(pf->recv, sizeof(double) * pf->D * n);
-    ALLOC(pf->send, sizeof(double) * pf->D * n);
-    ALLOC(pf->xslot, sizeof(int64_t) * n);
-    ALLOC(pf->xanc, sizeof(int32_t) * n);
+    if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
+      return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
+    ALLOC(pf->rows_recv, sizeof(double) * (pf->D + 1) * n);
+    ALLOC(pf->gparent, sizeof(int64_t) * n);
   }
   if (!pf->opts.record_history) {
     for (int i = 0; i < 2; ++i) {
@@ -632,8 +739,8 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   a.mark = pf->mark;
   a.carry = pf->cmark;
   a.mark_mode = pf->marks_pending ? 1 : 0;
-  a.remote = pf->recv;
-  a.ld_remote = pf->n;
+  a.remote = pf->rows_recv;
+  a.ld_remote = pf->D + 1;
   a.xout = slot_x(pf, t);
   a.ld_out = pf->n;
   a.logw = pf->logw;
@@ -703,7 +810,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   if (R > 1) {
     hipLaunchKernelGGL(k_rank_total, dim3(1), dim3(kBlock), 0, pf->s, g.gate, pf->bsum, n > 0 ? pf->nb_scan : 0,
                        pf->dev);
-    NCCL_TRY(ncclAllGather(&pf->dev->local, pf->totals_all, 1, ncclUint64, pf->ctx->comm, pf->s));
+    CHECK(comm_allgather(pf->ctx, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
   }
   int32_t* anc_target = anc_for_step(pf, t + 1);
   const bool sys1 = R == 1 && pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
@@ -925,7 +1032,11 @@ extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
     for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->lo + i;
     return GH_OK;
   }
-  if (pf->ctx->world > 1) return set_err(GH_E_STATE, "multi-rank: parents are exchanged as (rank, index) pairs; not exported yet");
+  if (pf->ctx->world > 1) {
+    // gparent holds the most recent exchange, i.e. the resample before step s_last
+    HIP_TRY(hipMemcpy(out, pf->gparent, sizeof(int64_t) * pf->n, hipMemcpyDeviceToHost));
+    return GH_OK;
+  }
   std::vector<int32_t> a(pf->n);
   HIP_TRY(hipMemcpy(a.data(), anc_for_step(pf, s_last), sizeof(int32_t) * pf->n, hipMemcpyDeviceToHost));
   for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->lo + a[i];
@@ -1017,12 +1128,142 @@ extern "C" int gh_pf_kernel_time(gh_pf* pf, double* avg_ms, int64_t* nl, int res
 }
 
 // -------------------------------------------------- multi-rank exchange
-// Stub until the RCCL exchange lands: refuse loudly rather than compute wrong
-// ancestors.
+// Systematic resampling over R ranks.  Global slot j takes the
+// first particle whose global inclusive CDF exceeds T_j = floor((j S + o)/N);
+// T is monotone, so the slots rank r's particles cover form one contiguous
+// range [count(base_r), count(base_r + total_r)) with
+//   count(X) = #{j : T_j < X} = clamp(ceil((X N - o) / S), 0, N).
+// Intersecting those ranges with the slot blocks each rank owns gives every
+// rank the same plan: which slot range it sends to / receives from each peer.
+static int64_t sys_count_host(uint64_t X, uint64_t N, uint64_t S, uint64_t o) {
+  if (X == 0) return 0;
+  if (X >= S) return (int64_t)N;
+  const __int128 num = (__int128)X * N - (__int128)o;
+  if (num <= 0) return 0;
+  const __int128 j = (num + S - 1) / S;
+  return j > (__int128)N ? (int64_t)N : (int64_t)j;
+}
+
+static void sys_plan(int64_t N, int R, int q, const uint64_t* totals, uint64_t o, int64_t* send_lo,
+                     int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi) {
+  uint64_t S = 0;
+  for (int r = 0; r < R; ++r) S += totals[r];
+  std::vector<int64_t> cov_lo(R), cov_hi(R);
+  uint64_t base = 0;
+  for (int r = 0; r < R; ++r) {
+    cov_lo[r] = sys_count_host(base, (uint64_t)N, S, o);
+    base += totals[r];
+    cov_hi[r] = sys_count_host(base, (uint64_t)N, S, o);
+  }
+  const int64_t my_lo = split_lo(N, q, R), my_hi = split_lo(N, q + 1, R);
+  for (int r = 0; r < R; ++r) {
+    const int64_t dlo = split_lo(N, r, R), dhi = split_lo(N, r + 1, R);
+    int64_t a = cov_lo[q] > dlo ? cov_lo[q] : dlo, b = cov_hi[q] < dhi ? cov_hi[q] : dhi;
+    send_lo[r] = a;
+    send_hi[r] = b > a ? b : a;
+    a = cov_lo[r] > my_lo ? cov_lo[r] : my_lo;
+    b = cov_hi[r] < my_hi ? cov_hi[r] : my_hi;
+    recv_lo[r] = a;
+    recv_hi[r] = b > a ? b : a;
+  }
+}
+
+extern "C" int gh_sys_plan(int64_t n_global, int world, int rank, const uint64_t* totals, uint64_t offset,
+                           int64_t* send_lo, int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi) {
+  if (n_global < 1 || world < 1 || rank < 0 || rank >= world || !totals || !send_lo || !send_hi || !recv_lo ||
+      !recv_hi)
+    return set_err(GH_E_INVAL, "gh_sys_plan: bad argument");
+  uint64_t S = 0;
+  for (int r = 0; r < world; ++r) S += totals[r];
+  if (S == 0 || offset >= S) return set_err(GH_E_INVAL, "gh_sys_plan: offset must be < sum(totals) > 0");
+  sys_plan(n_global, world, rank, totals, offset, send_lo, send_hi, recv_lo, recv_hi);
+  return GH_OK;
+}
+
 static int exchange_states(gh_pf* pf, int32_t* anc_out) {
-  (void)pf;
-  (void)anc_out;
-  return set_err(GH_E_STATE, "multi-rank resampling exchange not built yet");
+  gh_ctx* c = pf->ctx;
+  const int R = c->world, q = c->rank;
+  const int D = pf->D;
+  const int t = pf->t;
+  // the plan needs the decision and the totals on the host: one round trip
+  DevScalars h;
+  std::vector<uint64_t> tot(R);
+  HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipMemcpyAsync(tot.data(), pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  if (h.error) return set_err(h.error, "maybe_resample: all log-weights are -Inf or NaN");
+  if (!h.fire) return GH_OK;
+  uint64_t S = 0;
+  for (int r = 0; r < R; ++r) S += tot[r];
+  const u32x4 w = rng_block(pf->seed, ~0ull, (uint32_t)t, STREAM_RESAMPLE, 0);
+  const uint64_t o = scale_u53(u53_bits(w.x, w.y), S);
+  std::vector<int64_t> slo(R), shi(R), rlo(R), rhi(R);
+  sys_plan(pf->n_global, R, q, tot.data(), o, slo.data(), shi.data(), rlo.data(), rhi.data());
+  // rows to send, packed by destination rank
+  int64_t n_send = 0;
+  for (int r = 0; r < R; ++r)
+    if (r != q) n_send += shi[r] - slo[r];
+  if (n_send > pf->send_cap) {
+    HIP_TRY(hipStreamSynchronize(pf->s));
+    hipFree(pf->rows_send);
+    hipFree(pf->xanc);
+    pf->rows_send = nullptr;
+    pf->xanc = nullptr;
+    pf->send_cap = 0;
+    int64_t cap = n_send + n_send / 4 + 64;
+    if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess ||
+        hipMalloc(&pf->xanc, sizeof(int32_t) * cap) != hipSuccess)
+      return set_err(GH_E_NOMEM, "exchange: cannot allocate %lld send rows", (long long)cap);
+    pf->send_cap = cap;
+  }
+  GateArgs g;
+  g.gate = &pf->dev->fire;
+  g.M = &pf->dev->M;
+  g.zero_w = &pf->dev->pending;
+  g.shift = quant_shift((uint64_t)pf->n_global);
+  SearchArgs sa{};
+  sa.C = pf->C;
+  sa.n_cdf = pf->n;
+  sa.n_global = pf->n_global;
+  sa.seed = pf->seed;
+  sa.t = (uint32_t)t;
+  sa.mode = SEARCH_SYSTEMATIC;
+  sa.anc_old = nullptr;
+  std::vector<CommMsg> sends, recvs;
+  const size_t row_bytes = sizeof(double) * (D + 1);
+  int64_t soff = 0;
+  for (int r = 0; r < R; ++r) {
+    const int64_t len = shi[r] - slo[r];
+    if (len <= 0) continue;
+    sa.slot_lo = slo[r];
+    sa.n_slots = len;
+    sa.anc_out = r == q ? anc_out + (slo[r] - pf->lo) : pf->xanc + soff;
+    hipLaunchKernelGGL(k_search, dim3((unsigned)((len + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s, sa, g,
+                       pf->dev);
+    if (r != q) {
+      sends.push_back({r, pf->rows_send + soff * (D + 1), (size_t)len * row_bytes});
+      soff += len;
+    }
+  }
+  if (n_send > 0)
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((n_send + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s,
+                       pf->xanc, n_send, slot_x(pf, t), pf->n, D, pf->lo, pf->rows_send);
+  int64_t roff = 0;
+  for (int r = 0; r < R; ++r) {
+    const int64_t len = rhi[r] - rlo[r];
+    if (r == q || len <= 0) continue;
+    recvs.push_back({r, pf->rows_recv + roff * (D + 1), (size_t)len * row_bytes});
+    hipLaunchKernelGGL(k_assign_remote, dim3((unsigned)((len + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s,
+                       anc_out + (rlo[r] - pf->lo), len, roff);
+    roff += len;
+  }
+  HIP_TRY(hipGetLastError());
+  CHECK(comm_exchange(c, sends, recvs, pf->s));
+  if (pf->n > 0)
+    hipLaunchKernelGGL(k_global_parents, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, anc_out, pf->n,
+                       pf->lo, pf->rows_recv, D, pf->gparent);
+  HIP_TRY(hipGetLastError());
+  return GH_OK;
 }
 
 // ------------------------------------------------------ importance sampling

@@ -56,8 +56,8 @@ struct StepArgs {
   const uint64_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode)
   const uint64_t* carry;
   int mark_mode;
-  const double* remote;  // multi-rank: states received from other ranks [D][ld_remote]
-  int64_t ld_remote;
+  const double* remote;  // multi-rank: rows received from other ranks, row r at
+  int64_t ld_remote;     // remote[r * ld_remote] = (x_0 .. x_{D-1}, global id)
   double* xout;          // [D][ld_out]
   int64_t ld_out;
   double* logw;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
           for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
         } else {
 #pragma unroll
-          for (int k = 0; k < D; ++k) xp[k] = a.remote[k * a.ld_remote + (-1 - src)];
+          for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
         }
         const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
@@ -739,6 +739,33 @@ __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs g, con
   if (j >= s.n_slots) return;
   const int zero = *g.zero_w;
   s.anc_out[j] = (zero && s.anc_old) ? s.anc_old[a] : (int32_t)a;
+}
+
+// ------------------------------------------------- multi-rank exchange
+// Rows sent to other ranks: row j = (x[:, anc[j]], global id of anc[j]).
+__global__ __launch_bounds__(kBlock) void k_pack_rows(const int32_t* anc, int64_t rows, const double* x,
+                                                      int64_t ldx, int D, int64_t lo, double* out) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= rows) return;
+  const int32_t a = anc[j];
+  double* r = out + j * (D + 1);
+  for (int k = 0; k < D; ++k) r[k] = x[k * ldx + a];
+  r[D] = __longlong_as_double(lo + a);
+}
+
+// slots fed by received rows: ancestor = -1 - (row index in the receive buffer)
+__global__ void k_assign_remote(int32_t* anc, int64_t len, int64_t row0) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < len) anc[j] = (int32_t)(-1 - (row0 + j));
+}
+
+// global parent ids of this rank's slots after an exchange
+__global__ void k_global_parents(const int32_t* anc, int64_t n, int64_t lo, const double* rows, int D,
+                                 int64_t* gparent) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const int32_t a = anc[j];
+  gparent[j] = a >= 0 ? lo + a : __double_as_longlong(rows[(int64_t)(-1 - a) * (D + 1) + D]);
 }
 
 __global__ void k_copy_anc(const int* gate, const int32_t* src, int32_t* dst, int64_t n) {

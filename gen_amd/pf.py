@@ -49,13 +49,21 @@ class OptimalProposal:
 class Context:
     """One GPU (and, for multi-GPU, one rank of an RCCL communicator)."""
 
-    def __init__(self, device: int | None = None, rank: int = 0, world: int = 1, unique_id: bytes | None = None):
+    def __init__(self, device: int | None = None, rank: int = 0, world: int = 1, unique_id: bytes | None = None,
+                 transport=None):
+        """`unique_id`: RCCL communicator id (Context.unique_id() on rank 0,
+        broadcast to the others).  `transport`: a host-staged transport
+        (gen_amd.transport.GlooTransport) used instead of RCCL."""
         lib = _lib.load()
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         self.device = device
+        self.transport = transport
         h = c_void_p()
-        if world > 1:
+        if transport is not None:
+            rank, world = transport.rank, transport.world
+            _lib.check(lib.gh_ctx_create_hostcomm(device, rank, world, byref(transport.struct), None, byref(h)))
+        elif world > 1:
             if unique_id is None or len(unique_id) != 128:
                 raise ValueError("multi-rank context needs the 128-byte RCCL unique id")
             buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)

@@ -53,7 +53,7 @@ typedef enum {
 typedef enum {
   /* x_1 ~ mvnormal(mu0, P0); x_t ~ mvnormal(A x_{t-1} + b, Q); y_t ~ mvnormal(H x_t + c, R)
      params (row-major doubles): A[d*d] b[d] Q[d*d] H[dy*d] c[dy] R[dy*dy] mu0[d] P0[d*d]
-     supported d: 1..8, 10, 12, 16; dy <= 32 */
+     supported d: 1..8, 10, 12, 16; dy <= 32.  Multi-rank filters use systematic resampling. */
   GH_FAMILY_LGSSM = 1,
   /* categorical HMM (test/inference/particle_filter.jl:50-78):
      z_1 ~ categorical(prior); z_t ~ categorical(T[:, z_{t-1}]); x_t ~ categorical(E[:, z_t])
@@ -109,6 +109,21 @@ int gh_ctx_create(int device, void* hip_stream /* NULL = own stream */, gh_ctx**
 int gh_comm_unique_id(uint8_t id[128]);
 int gh_ctx_create_dist(int device, int rank, int world, const uint8_t id[128], void* hip_stream,
                        gh_ctx** out);
+/* Host-staged transport (e.g. several ranks sharing one GPU, or a cluster
+   without RCCL peer access): the library stages device buffers through host
+   memory and calls these functions, which move host buffers between ranks.
+   Return 0 on success. */
+typedef struct {
+  void* user;
+  /* every rank contributes `bytes`; recv receives world*bytes in rank order */
+  int (*allgather)(void* user, const void* send, void* recv, uint64_t bytes);
+  /* point-to-point exchange: the calls of all ranks match pairwise */
+  int (*sendrecv)(void* user, int n_send, const int* send_peers, const void* const* send_bufs,
+                  const uint64_t* send_bytes, int n_recv, const int* recv_peers, void* const* recv_bufs,
+                  const uint64_t* recv_bytes);
+} gh_host_comm;
+int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_host_comm* comm, void* hip_stream,
+                           gh_ctx** out);
 int gh_ctx_destroy(gh_ctx* ctx);
 int gh_ctx_rank(const gh_ctx* ctx, int* rank, int* world);
 int gh_ctx_stream(const gh_ctx* ctx, void** hip_stream);
@@ -147,6 +162,14 @@ int gh_pf_sample_unweighted(gh_pf* pf, int64_t n_samples, uint64_t seed, int64_t
 int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int32_t* did);
 /* average duration (ms) of the step kernel over the timed launches (opts.time_kernels) */
 int gh_pf_kernel_time(gh_pf* pf, double* avg_ms, int64_t* n_launches, int reset);
+
+/* multi-rank systematic resampling plan (host only, no GPU): given every
+   rank's integer weight total and the shared offset o < sum(totals), the global
+   slot ranges rank `rank` sends to ([send_lo[r], send_hi[r])) and receives from
+   ([recv_lo[r], recv_hi[r])) each rank r; empty ranges have lo == hi.  This is
+   the plan gh_pf_maybe_resample follows; exposed for tests and integrators. */
+int gh_sys_plan(int64_t n_global, int world, int rank, const uint64_t* totals, uint64_t offset,
+                int64_t* send_lo, int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi);
 
 /* ---- importance sampling ---------------------------------------------------- */
 int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t seed,

@@ -1,0 +1,81 @@
+"""Multi-rank particle-filter worker (launched by tests/test_multirank.py).
+
+One process per rank (torch.distributed.run).  Every rank holds a shard of
+one filter; the ranks talk through the host-staged gloo transport (several
+ranks may share one GPU) or RCCL (one GPU per rank).  Each rank saves its
+shard of the final states, log-weights, parents and the log-ML estimate.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def build_model(name):
+    import gen_amd as gen
+
+    if name == "lg4":
+        return gen.LinearGaussianSSM.benchmark(4)
+    if name == "lg10":
+        return gen.LinearGaussianSSM.benchmark(10)
+    if name == "kit":
+        return gen.KitagawaSSM(10.0, 1.0)
+    raise ValueError(name)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--model", default="lg4")
+    p.add_argument("--n", type=int, default=3001)
+    p.add_argument("--T", type=int, default=8)
+    p.add_argument("--thr", type=float, default=0.0)
+    p.add_argument("--seed", type=int, default=9)
+    p.add_argument("--transport", default="gloo")
+    p.add_argument("--out", required=True)
+    a = p.parse_args()
+
+    import torch.distributed as dist
+
+    import gen_amd as gen
+    from gen_amd.transport import GlooTransport
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if a.transport == "gloo":
+        tr = GlooTransport()
+        ctx = gen.Context(device=0, transport=tr)
+    else:
+        uid = [gen.Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx = gen.Context(device=int(os.environ.get("LOCAL_RANK", "0")), rank=rank, world=world, unique_id=uid[0])
+    gen.set_default_context(ctx)
+    m = build_model(a.model)
+    _, ys = m.simulate(a.T, np.random.default_rng(5))
+    addr = m.obs_address
+    st = gen.initialize_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, seed=a.seed)
+    did = []
+    for t in range(2, a.T + 1):
+        did.append(gen.maybe_resample(st, a.thr if a.thr > 0 else None))
+        gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})
+    lml = gen.log_ml_estimate(st)
+    np.savez(
+        f"{a.out}.rank{rank}.npz",
+        states=st.states(),
+        logw=gen.get_log_weights(st),
+        parents=st.parents,
+        lml=lml,
+        did=np.array(did, dtype=np.int64),
+        lo=st.first,
+    )
+    st.close()
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

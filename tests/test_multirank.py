@@ -1,0 +1,251 @@
+"""Multi-rank particle filter.
+
+CPU tests (gloo, world_size 2..4):
+  * the product's exchange plan (gh_sys_plan, host code) against a brute-force
+    systematic resampler over the global CDF;
+  * the host transport callbacks (gen_amd.transport.GlooTransport) moving
+    bytes between two processes;
+  * the sharded oracle driven by the product's plan and real gloo messages
+    reproduces the single-rank oracle bit for bit.
+GPU test: 2 and 3 ranks sharing GPU 0 through the host transport reproduce
+the single-rank oracle (states, weights, parents bit-exact; log-ML 1e-9).
+"""
+import ctypes
+import os
+import socket
+import subprocess
+import sys
+from ctypes import POINTER, c_int64, c_uint64
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from gen_amd import _lib  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def plan(n, R, q, totals, o):
+    lib = _lib.load()
+    tot = np.ascontiguousarray(totals, dtype=np.uint64)
+    out = [np.zeros(R, dtype=np.int64) for _ in range(4)]
+    _lib.check(lib.gh_sys_plan(n, R, q, tot.ctypes.data_as(POINTER(c_uint64)), int(o),
+                               *[a.ctypes.data_as(POINTER(c_int64)) for a in out]))
+    return out
+
+
+def brute_source_rank(n, totals, o):
+    """rank owning the ancestor of every global slot (systematic, global CDF)."""
+    S = int(sum(int(t) for t in totals))
+    bounds = np.cumsum([int(t) for t in totals])
+    src = np.empty(n, dtype=np.int64)
+    for j in range(n):
+        T = (j * S + o) // n
+        src[j] = int(np.searchsorted(bounds, T, side="right"))
+    return src
+
+
+@pytest.mark.parametrize("R", [2, 3, 5, 8])
+def test_sys_plan_matches_bruteforce(R):
+    rng = np.random.default_rng(R)
+    for trial in range(30):
+        n = int(rng.integers(R, 400))
+        totals = rng.integers(0, 1 << 40, size=R).astype(np.uint64)
+        if trial % 3 == 0:
+            totals[rng.integers(0, R, size=R // 2 + 1)] = 0  # empty ranks
+        if totals.sum() == 0:
+            totals[0] = 7
+        S = int(sum(int(t) for t in totals))
+        o = int(rng.integers(0, S))
+        src = brute_source_rank(n, totals, o)
+        plans = [plan(n, R, q, totals, o) for q in range(R)]
+        for q in range(R):
+            slo, shi, rlo, rhi = plans[q]
+            lo, hi = (n * q) // R, (n * (q + 1)) // R
+            # every slot of q is received from exactly its source rank
+            got = np.full(hi - lo, -1)
+            for r in range(R):
+                got[rlo[r] - lo : rhi[r] - lo] = r
+            assert np.array_equal(got, src[lo:hi])
+            for r in range(R):
+                # what q sends to r is what r receives from q
+                assert (slo[r], shi[r]) == (plans[r][2][q], plans[r][3][q])
+
+
+def test_sys_plan_rejects_bad_arguments():
+    lib = _lib.load()
+    tot = np.array([0, 0], dtype=np.uint64)
+    z = np.zeros(2, dtype=np.int64)
+    p = z.ctypes.data_as(POINTER(c_int64))
+    rc = lib.gh_sys_plan(10, 2, 0, tot.ctypes.data_as(POINTER(c_uint64)), 0, p, p, p, p)
+    assert rc == 1
+    tot = np.array([5, 5], dtype=np.uint64)
+    rc = lib.gh_sys_plan(10, 2, 2, tot.ctypes.data_as(POINTER(c_uint64)), 0, p, p, p, p)
+    assert rc == 1
+
+
+def _run_workers(script_args, world, timeout=300):
+    env = dict(os.environ)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    env["MASTER_PORT"] = str(_free_port())
+    env["WORLD_SIZE"] = str(world)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    procs = []
+    for r in range(world):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable] + script_args, env=e, cwd=ROOT,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out.decode(errors="replace"))
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-4000:]
+    return outs
+
+
+_CPU_WORKER = r'''
+import os, sys, ctypes
+import numpy as np
+import torch, torch.distributed as dist
+sys.path.insert(0, os.environ["GH_ROOT"])
+from gen_amd import _lib, LinearGaussianSSM
+from gen_amd.transport import GlooTransport
+from oracle import oracle as O
+from tests.test_multirank import plan
+
+dist.init_process_group("gloo")
+rank, R = dist.get_rank(), dist.get_world_size()
+out = os.environ["GH_OUT"]
+
+# 1) transport callbacks through their C function pointers
+tr = GlooTransport()
+send = (ctypes.c_uint8 * 5)(*[rank * 10 + i for i in range(5)])
+recv = (ctypes.c_uint8 * (5 * R))()
+assert tr.struct.allgather(None, ctypes.addressof(send), ctypes.addressof(recv), 5) == 0
+assert list(recv) == [r * 10 + i for r in range(R) for i in range(5)]
+peers = [p for p in range(R) if p != rank]
+sb = [(ctypes.c_uint8 * (3 + rank))(*([rank + 1] * (3 + rank))) for _ in peers]
+rb = [(ctypes.c_uint8 * (3 + p))() for p in peers]
+IA = ctypes.c_int * len(peers); VA = ctypes.c_void_p * len(peers); UA = ctypes.c_uint64 * len(peers)
+rc = tr.struct.sendrecv(None, len(peers), IA(*peers), VA(*[ctypes.addressof(b) for b in sb]),
+                        UA(*[3 + rank] * len(peers)), len(peers), IA(*peers),
+                        VA(*[ctypes.addressof(b) for b in rb]), UA(*[3 + p for p in peers]))
+assert rc == 0
+for p, b in zip(peers, rb):
+    assert list(b) == [p + 1] * (3 + p)
+
+# 2) sharded oracle, routed by the product's plan over gloo
+m = LinearGaussianSSM.benchmark(4)
+_, ys = m.simulate(8, np.random.default_rng(5))
+n, seed = 3001, 9
+lo, hi = (n * rank) // R, (n * (rank + 1)) // R
+pf = O.OraclePF(m, n, seed, lo=lo, n_local=hi - lo)
+pf.init(ys[0])
+for t, y in enumerate(ys[1:], start=1):
+    st = torch.from_numpy(pf.local_stats())
+    allst = [torch.empty(3, dtype=torch.float64) for _ in range(R)]
+    dist.all_gather(allst, st)
+    dec, L, ess, M = O.combine_stats(torch.cat(allst).numpy(), n, n)
+    assert dec == 1
+    tot = torch.tensor([pf.qtotal(M)], dtype=torch.int64)
+    allt = [torch.empty(1, dtype=torch.int64) for _ in range(R)]
+    dist.all_gather(allt, tot)
+    totals = np.array([int(x.item()) for x in allt], dtype=np.uint64)
+    S = int(sum(int(x) for x in totals))
+    w = O.philox([0xFFFFFFFF, 0xFFFFFFFF, t, (3 << 16) | 0], [seed & 0xFFFFFFFF, seed >> 32])
+    u = ((w[0] >> 5) << 26) | (w[1] >> 6)
+    o = (u * S) >> 53
+    slo, shi, rlo, rhi = plan(n, R, rank, totals, o)
+    slots, ancs, sts = pf.emit(M, totals, rank)
+    reqs, bufs = [], []
+    for r in range(R):
+        if r == rank:
+            continue
+        sel = (slots >= slo[r]) & (slots < shi[r])
+        assert sel.sum() == shi[r] - slo[r]
+        if sel.sum():
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(slots[sel])), r))
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(ancs[sel])), r))
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(sts[sel])), r))
+        k = rhi[r] - rlo[r]
+        if k:
+            b = (torch.empty(k, dtype=torch.int64), torch.empty(k, dtype=torch.int64),
+                 torch.empty((k, m.d), dtype=torch.float64))
+            for x in b:
+                reqs.append(dist.irecv(x, r))
+            bufs.append(b)
+    for q in reqs:
+        q.wait()
+    own = (slots >= lo) & (slots < hi)
+    all_s = np.concatenate([slots[own]] + [b[0].numpy() for b in bufs])
+    all_a = np.concatenate([ancs[own]] + [b[1].numpy() for b in bufs])
+    all_x = np.concatenate([sts[own]] + [b[2].numpy() for b in bufs])
+    assert np.array_equal(np.sort(all_s), np.arange(lo, hi))
+    pf.apply(L, all_s, all_a, all_x)
+    pf.step(y)
+np.savez(f"{out}.rank{rank}.npz", states=pf.state(), parents=pf.parents())
+dist.barrier()
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.parametrize("R", [2, 3])
+def test_gloo_sharded_oracle_with_product_plan(tmp_path, R):
+    from gen_amd import LinearGaussianSSM
+    from oracle import oracle as O
+
+    script = tmp_path / "w.py"
+    script.write_text(_CPU_WORKER)
+    out = str(tmp_path / "o")
+    os.environ["GH_ROOT"] = ROOT
+    os.environ["GH_OUT"] = out
+    try:
+        _run_workers([str(script)], R, timeout=240)
+    finally:
+        os.environ.pop("GH_OUT", None)
+    m = LinearGaussianSSM.benchmark(4)
+    _, ys = m.simulate(8, np.random.default_rng(5))
+    ref = O.run_pf(m, ys, 3001, 9, thr=3001)
+    parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
+    assert np.array_equal(np.concatenate([p["states"] for p in parts], axis=1), ref.state())
+    assert np.array_equal(np.concatenate([p["parents"] for p in parts]), ref.parents())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,R,thr", [("lg4", 2, 3001.0), ("lg4", 3, 0.0), ("kit", 2, 0.0), ("lg10", 2, 3001.0)])
+def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr):
+    """R ranks share GPU 0 through the gloo host transport; the gathered shards
+    equal the single-rank oracle bit for bit (log-ML within 1e-9)."""
+    from oracle import oracle as O
+    from tests.mr_worker import build_model
+
+    out = str(tmp_path / "g")
+    n, T, seed = 3001, 8, 9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  "--thr", str(thr), "--seed", str(seed), "--out", out], R, timeout=400)
+    m = build_model(model)
+    _, ys = m.simulate(T, np.random.default_rng(5))
+    ref = O.run_pf(m, ys, n, seed, thr=thr if thr > 0 else None)
+    parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
+    states = np.concatenate([p["states"] for p in parts], axis=0)  # [n, d]
+    assert np.array_equal(states.T, ref.state())
+    assert np.array_equal(np.concatenate([p["logw"] for p in parts]), ref.log_weights())
+    assert np.array_equal(np.concatenate([p["parents"] for p in parts]), ref.parents())
+    lml = float(parts[0]["lml"])
+    assert all(float(p["lml"]) == lml for p in parts)
+    assert abs(lml - ref.log_ml_estimate()) <= 1e-9 * abs(ref.log_ml_estimate())
