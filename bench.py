@@ -173,7 +173,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "k_step<LGModel<10>,false>",
+            "kernel": f"k_step<LGModel<{a.d},3>,false>",
             "kernel_avg_ms": kms,
             "kernel_launches": kcount,
             "bytes_per_particle_step": bytes_pp,

@@ -563,6 +563,10 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
   const dim3 grid((unsigned)pf->nb_step), block(kBlock);
   if (init) hipLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, pf->m->dparams, p, o, a);
   else hipLaunchKernelGGL((k_step<Model, false>), grid, block, 0, pf->s, pf->m->dparams, p, o, a);
+}
+
+// fold the step kernel's block partials into the rank's (M, S, S2)
+static void launch_fold(gh_pf* pf, const StepArgs& a, bool init) {
   // single rank: pre-evaluate the next maybe_resample! for the threshold last used
   const double hint = pf->ctx->world == 1 ? pf->thr_hint : 0.0;
   hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_step,
@@ -598,8 +602,14 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
   return GH_OK;
 }
 
+// the step kernel (timed alone when opts.time_kernels), then the fold
 static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
-  if (!pf->opts.time_kernels) return launch_step(pf, o, a, init);
+  if (!pf->opts.time_kernels) {
+    CHECK(launch_step(pf, o, a, init));
+    launch_fold(pf, a, init);
+    HIP_TRY(hipGetLastError());
+    return GH_OK;
+  }
   if (pf->ev_used + 2 > pf->ev.size()) {
     for (int i = 0; i < 64; ++i) {
       hipEvent_t e;
@@ -612,6 +622,8 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   HIP_TRY(hipEventRecord(e0, pf->s));
   CHECK(launch_step(pf, o, a, init));
   HIP_TRY(hipEventRecord(e1, pf->s));
+  launch_fold(pf, a, init);
+  HIP_TRY(hipGetLastError());
   return GH_OK;
 }
 
