@@ -6,6 +6,7 @@
 // -> log_ml_estimate, with every per-particle loop moved to the device and
 // every decision (ESS test, resample) kept device-resident so that a whole
 // filter can be enqueued without a host round trip.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -559,10 +560,15 @@ extern "C" int gh_pf_destroy(gh_pf* pf) {
 // ----------------------------------------------------------- kernel launch
 template <class Model>
 static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const StepObs& o,
-                          const StepArgs& a, bool init) {
+                          const StepArgs& a, bool init, hipEvent_t e0, hipEvent_t e1) {
   const dim3 grid((unsigned)pf->nb_step), block(kBlock);
-  if (init) hipLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, pf->m->dparams, p, o, a);
-  else hipLaunchKernelGGL((k_step<Model, false>), grid, block, 0, pf->s, pf->m->dparams, p, o, a);
+  // the timed launch records its events at the kernel's own start and end
+  if (init)
+    hipExtLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, e0, e1, 0, (const double*)pf->m->dparams,
+                          p, o, a);
+  else
+    hipExtLaunchKernelGGL((k_step<Model, false>), grid, block, 0, pf->s, e0, e1, 0, (const double*)pf->m->dparams,
+                          p, o, a);
 }
 
 // fold the step kernel's block partials into the rank's (M, S, S2)
@@ -574,7 +580,8 @@ static void launch_fold(gh_pf* pf, const StepArgs& a, bool init) {
   pf->hint_valid = hint > 0.0;
 }
 
-static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
+static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init, hipEvent_t e0 = nullptr,
+                       hipEvent_t e1 = nullptr) {
   gh_model* m = pf->m;
   switch (m->family) {
     case GH_FAMILY_LGSSM:
@@ -582,10 +589,10 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
 #define GH_LG_CASE(DD)                                                                  \
   case DD:                                                                              \
     switch (m->lg_struct) {                                                             \
-      case 1: launch_step_t<LGModel<DD, 1>>(pf, m->lg, o, a, init); break;              \
-      case 2: launch_step_t<LGModel<DD, 2>>(pf, m->lg, o, a, init); break;              \
-      case 3: launch_step_t<LGModel<DD, 3>>(pf, m->lg, o, a, init); break;              \
-      default: launch_step_t<LGModel<DD, 0>>(pf, m->lg, o, a, init); break;             \
+      case 1: launch_step_t<LGModel<DD, 1>>(pf, m->lg, o, a, init, e0, e1); break;              \
+      case 2: launch_step_t<LGModel<DD, 2>>(pf, m->lg, o, a, init, e0, e1); break;              \
+      case 3: launch_step_t<LGModel<DD, 3>>(pf, m->lg, o, a, init, e0, e1); break;              \
+      default: launch_step_t<LGModel<DD, 0>>(pf, m->lg, o, a, init, e0, e1); break;             \
     }                                                                                   \
     break;
         GH_LG_CASE(1) GH_LG_CASE(2) GH_LG_CASE(3) GH_LG_CASE(4) GH_LG_CASE(5) GH_LG_CASE(6)
@@ -594,8 +601,8 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
         default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", m->d);
       }
       break;
-    case GH_FAMILY_HMM: launch_step_t<HMMModel>(pf, m->hmm, o, a, init); break;
-    case GH_FAMILY_KITAGAWA: launch_step_t<KitModel>(pf, m->kit, o, a, init); break;
+    case GH_FAMILY_HMM: launch_step_t<HMMModel>(pf, m->hmm, o, a, init, e0, e1); break;
+    case GH_FAMILY_KITAGAWA: launch_step_t<KitModel>(pf, m->kit, o, a, init, e0, e1); break;
     default: return set_err(GH_E_INVAL, "unknown family");
   }
   HIP_TRY(hipGetLastError());
@@ -619,9 +626,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   }
   hipEvent_t e0 = pf->ev[pf->ev_used], e1 = pf->ev[pf->ev_used + 1];
   pf->ev_used += 2;
-  HIP_TRY(hipEventRecord(e0, pf->s));
-  CHECK(launch_step(pf, o, a, init));
-  HIP_TRY(hipEventRecord(e1, pf->s));
+  CHECK(launch_step(pf, o, a, init, e0, e1));
   launch_fold(pf, a, init);
   HIP_TRY(hipGetLastError());
   return GH_OK;
