@@ -49,6 +49,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-history", action="store_true")
     p.add_argument("--ess-threshold", type=float, default=None, help="default N/2 (the reference's default)")
+    p.add_argument("--no-kernel-timing", action="store_true", help="no hipEvents around the step kernel")
     return p.parse_args()
 
 
@@ -104,7 +105,7 @@ def main():
     n_global = a.particles * world
     st = gen.initialize_particle_filter(
         model, (1,), {("chain", 1, "y"): ys[0]}, n_global, seed=42, resampler=a.resampler,
-        record_history=not a.no_history, history_capacity=T + 2, time_kernels=True,
+        record_history=not a.no_history, history_capacity=T + 2, time_kernels=not a.no_kernel_timing,
     )
     gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold)
     ctx.synchronize()
@@ -133,7 +134,7 @@ def main():
     lml = gen.log_ml_estimate(st)
 
     bytes_pp = 16 * a.d + 16 + 4.0 * n_res / max(1, a.steps)
-    achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9
+    achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
     if os.path.exists(pmc):

@@ -455,8 +455,10 @@ struct gh_pf {
   uint64_t* cmark = nullptr;      // systematic: tagged carry per step block
   uint64_t epoch = 0;             // resample counter for the tags
   bool marks_pending = false;     // last resample's ancestors only exist as marks
-  double thr_hint = 0.0;          // threshold the next maybe_resample! is expected to use
-  bool hint_valid = false;        // k_fold pre-evaluated the decision for thr_hint
+  bool stats_valid = false;       // stats_all holds the last step's (M, S, S2) (one rank)
+  uint64_t* tsum = nullptr;       // k_resample1: published tile totals
+  int rs_grid = 0;                // k_resample1 tiles (blocks)
+  int rs_cap = 0;                 // co-resident k_resample1 blocks on this device
   uint64_t* bsum = nullptr;
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
@@ -542,7 +544,7 @@ static void pf_free(gh_pf* pf) {
   for (auto c : pf->chunks) hipFree(c);
   for (auto e : pf->ev) hipEventDestroy(e);
   hipFree(pf->logw); hipFree(pf->C); hipFree(pf->mark); hipFree(pf->cmark); hipFree(pf->bsum); hipFree(pf->pm); hipFree(pf->ps);
-  hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->stats_all); hipFree(pf->totals_all);
+  hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->tsum); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
   if (!pf->opts.record_history) {
@@ -573,12 +575,23 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
 
 // fold the step kernel's block partials into the rank's (M, S, S2)
 static void launch_fold(gh_pf* pf, const StepArgs& a, bool init) {
-  // single rank: pre-evaluate the next maybe_resample! for the threshold last used
-  const double hint = pf->ctx->world == 1 ? pf->thr_hint : 0.0;
   hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_step,
-                     a.stats_out, pf->dev, init ? 0 : 1, hint, pf->n_global);
-  pf->hint_valid = hint > 0.0;
+                     a.stats_out, pf->dev, init ? 0 : 1, 0.0, pf->n_global);
 }
+
+// one rank: make stats_all current (the fold is otherwise done by k_resample1)
+static int ensure_stats(gh_pf* pf) {
+  if (pf->ctx->world > 1 || pf->stats_valid) return GH_OK;
+  hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_step,
+                     pf->stats_all, pf->dev, 0, 0.0, pf->n_global);
+  HIP_TRY(hipGetLastError());
+  pf->stats_valid = true;
+  return GH_OK;
+}
+
+// the device resample flags describe the current particles only if a
+// maybe_resample! was enqueued since the last step
+static int flags_live(const gh_pf* pf) { return pf->resample_calls > 0 ? 1 : 0; }
 
 static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init, hipEvent_t e0 = nullptr,
                        hipEvent_t e1 = nullptr) {
@@ -609,11 +622,14 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
   return GH_OK;
 }
 
-// the step kernel (timed alone when opts.time_kernels), then the fold
+// the step kernel (timed alone when opts.time_kernels).  Multi-rank: the
+// fold follows at once (its triple is all-gathered every step); one rank: the
+// next maybe_resample! folds inside k_resample1, other readers fold on demand.
 static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
+  pf->stats_valid = false;
   if (!pf->opts.time_kernels) {
     CHECK(launch_step(pf, o, a, init));
-    launch_fold(pf, a, init);
+    if (pf->ctx->world > 1) launch_fold(pf, a, init);
     HIP_TRY(hipGetLastError());
     return GH_OK;
   }
@@ -627,7 +643,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   hipEvent_t e0 = pf->ev[pf->ev_used], e1 = pf->ev[pf->ev_used + 1];
   pf->ev_used += 2;
   CHECK(launch_step(pf, o, a, init, e0, e1));
-  launch_fold(pf, a, init);
+  if (pf->ctx->world > 1) launch_fold(pf, a, init);
   HIP_TRY(hipGetLastError());
   return GH_OK;
 }
@@ -680,6 +696,15 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   ALLOC(pf->stats_all, sizeof(double) * 3 * ctx->world);
   ALLOC(pf->totals_all, sizeof(uint64_t) * ctx->world);
   ALLOC(pf->anc_scratch, sizeof(int32_t) * n);
+  pf->rs_grid = (int)((n + kRsTile - 1) / kRsTile);
+  ALLOC(pf->tsum, sizeof(uint64_t) * pf->rs_grid);
+  {
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_resample1<true>, kRsBlock, 0) != hipSuccess) occ = 0;
+    int occ2 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_resample1<false>, kRsBlock, 0) != hipSuccess) occ2 = 0;
+    pf->rs_cap = (occ < occ2 ? occ : occ2) * ctx->cus;
+  }
   if (ctx->world > 1) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
@@ -704,6 +729,7 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
     if (hipMemcpyAsync(pf->dev, &z, sizeof z, hipMemcpyHostToDevice, pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init scalars"));
     if (hipMemsetAsync(pf->mark, 0, sizeof(uint64_t) * n, pf->s) != hipSuccess ||
+        hipMemsetAsync(pf->tsum, 0, sizeof(uint64_t) * pf->rs_grid, pf->s) != hipSuccess ||
         hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * ((n + 63) / 64), pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init marks"));
     if (hipStreamSynchronize(pf->s) != hipSuccess) return fail(set_err(GH_E_HIP, "sync"));
@@ -756,6 +782,7 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   a.mark = pf->mark;
   a.carry = pf->cmark;
   a.mark_mode = pf->marks_pending ? 1 : 0;
+  a.resampled = flags_live(pf);
   a.remote = pf->rows_recv;
   a.ld_remote = pf->D + 1;
   a.xout = slot_x(pf, t);
@@ -815,12 +842,65 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   g.shift = quant_shift((uint64_t)pf->n_global);
   // The common case fuses the decision into the first resample kernel; a
   // second call without a step (or an empty shard) decides in its own launch.
+  const bool sys = pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
+  if (R == 1 && !second && n > 0 && pf->rs_grid <= pf->rs_cap && pf->nb_step <= kRsPart * kRsBlock) {
+    // one launch: fold + decision + quantise + one grid barrier + marks / CDF
+    Resample1Args ra{};
+    ra.pm = pf->pm;
+    ra.ps = pf->ps;
+    ra.ps2 = pf->ps2;
+    ra.nb_part = (int)pf->nb_step;
+    ra.logw = pf->logw;
+    ra.n = n;
+    ra.shift = g.shift;
+    ra.stats_out = pf->stats_all;
+    ra.dev = pf->dev;
+    ra.d = d;
+    ra.tsum = pf->tsum;
+    ra.mk.mark = pf->mark;
+    ra.mk.cmark = pf->cmark;
+    ra.mk.epoch = ++pf->epoch;
+    ra.mk.n_global = pf->n_global;
+    ra.mk.n_groups = (n + 63) / 64;
+    ra.mk.enabled = sys ? 1 : 0;
+    ra.C = pf->C;
+    ra.seed = pf->seed;
+    ra.t = (uint32_t)t;
+    // grid <= co-resident capacity of an idle device (rs_cap), so every block
+    // is eventually resident; the barrier wait is bounded as a backstop
+    if (sys)
+      hipLaunchKernelGGL(k_resample1<true>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra);
+    else
+      hipLaunchKernelGGL(k_resample1<false>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra);
+    pf->stats_valid = true;
+    if (sys) {
+      pf->marks_pending = true;
+#if defined(GH_ABLATE_MARKS)  // timing-only variant: expand the marks in their own launch
+      CHECK(materialize_marks(pf));
+#endif
+    } else {
+      SearchArgs sa{};
+      sa.C = pf->C;
+      sa.n_cdf = n;
+      sa.n_slots = n;
+      sa.slot_lo = 0;
+      sa.n_global = pf->n_global;
+      sa.seed = pf->seed;
+      sa.t = (uint32_t)t;
+      sa.mode = SEARCH_MULTINOMIAL;
+      sa.anc_old = nullptr;
+      sa.anc_out = anc_for_step(pf, t + 1);
+      hipLaunchKernelGGL(k_search, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, sa, g, pf->dev);
+    }
+    HIP_TRY(hipGetLastError());
+    pf->resample_calls++;
+    return GH_OK;
+  }
+  CHECK(ensure_stats(pf));
   const bool fused = !second && n > 0;
   if (second && pf->marks_pending) CHECK(materialize_marks(pf));
   if (!fused) hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, pf->s, d, pf->dev);
-  const int fmode = !fused ? 0 : ((pf->hint_valid && pf->thr_hint == thr) ? 2 : 1);
-  pf->thr_hint = thr;
-  pf->hint_valid = false;
+  const int fmode = fused ? 1 : 0;
   if (n > 0)
     hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum,
                        fmode, d, pf->dev);
@@ -929,9 +1009,10 @@ extern "C" int gh_pf_log_ml_estimate(gh_pf* pf, double* out) {
   if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
   DevScalars h;
   std::vector<double> st;
+  CHECK(ensure_stats(pf));
   CHECK(read_scalars(pf, &h, &st));
   if (h.error) return set_err(h.error, "log_ml_estimate: numeric error raised on the device");
-  if (h.pending | h.fire) {  // all weights are 0: logsumexp(w) - log N = 0
+  if (flags_live(pf) && (h.pending | h.fire)) {  // all weights are 0: logsumexp(w) - log N = 0
     *out = h.log_ml_est;
     return GH_OK;
   }
@@ -968,7 +1049,7 @@ extern "C" int gh_pf_get_log_weights(gh_pf* pf, double* out) {
   if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
   DevScalars h;
   CHECK(read_scalars(pf, &h, nullptr));
-  if (h.pending | h.fire) {
+  if (flags_live(pf) && (h.pending | h.fire)) {
     for (int64_t i = 0; i < pf->n; ++i) out[i] = 0.0;
     return GH_OK;
   }
@@ -1006,6 +1087,7 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   ta.ancs = dancs;
   ta.res_before = pf->res_hist;
   ta.anc_pending = (pf->ctx->world == 1 && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
+  ta.live = flags_live(pf);
   ta.n = n;
   ta.ld = n;
   ta.t_target = t;
@@ -1027,7 +1109,7 @@ extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {
   if (pf->ctx->world > 1) {
     DevScalars h;
     CHECK(read_scalars(pf, &h, nullptr));
-    if (h.pending | h.fire)
+    if (flags_live(pf) && (h.pending | h.fire))
       return set_err(GH_E_STATE, "multi-rank: states of a pending resample are materialised by the next step");
     HIP_TRY(hipMemcpy(out, slot_x(pf, pf->t), sizeof(double) * pf->D * pf->n, hipMemcpyDeviceToHost));
     return GH_OK;
@@ -1080,7 +1162,8 @@ extern "C" int gh_pf_sample_unweighted(gh_pf* pf, int64_t ns, uint64_t seed, int
   if (pf->ctx->world > 1) return set_err(GH_E_STATE, "sample_unweighted: single rank only");
   if (ns == 0) return GH_OK;
   const int64_t n = pf->n;
-  hipLaunchKernelGGL(k_prep_sample, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, 1);
+  CHECK(ensure_stats(pf));
+  hipLaunchKernelGGL(k_prep_sample, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, 1, flags_live(pf));
   GateArgs g;
   g.gate = &pf->dev->one;
   g.M = &pf->dev->sM;
@@ -1307,6 +1390,14 @@ extern "C" int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n
   gh_pf_destroy(pf);
   return rc;
 }
+
+#if defined(GH_RS_STAMPS)
+extern "C" int gh_debug_rs_stamps(uint64_t* out, int n) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rs_stamps), sizeof(uint64_t) * (size_t)n));
+  return GH_OK;
+}
+#endif
 
 // ------------------------------------------------------------ self tests
 extern "C" int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double* oe, double* ol,

@@ -33,6 +33,7 @@ struct DevScalars {
   uint64_t local;      // this rank's integer total
   uint64_t o, Qs, Rs;  // systematic offset, S / N, S % N
   double invN;         // 1 / N (division estimate, corrected exactly)
+  double invS;         // 1 / S (slot-count estimate, exact unless near an integer)
   int pending;         // a resample happened since the last step
   int fire;            // the current maybe_resample decided to resample
   int spend;           // sample_unweighted: weights are all equal
@@ -45,6 +46,7 @@ struct DevScalars {
   // next maybe_resample! to use (single rank); committed by k_qsum
   double cM, cL, cess;
   int cfire, cerr;
+  unsigned bar_gen;    // k_resample1 grid barriers completed
 
 };
 
@@ -56,6 +58,8 @@ struct StepArgs {
   const uint64_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode)
   const uint64_t* carry;
   int mark_mode;
+  int resampled;         // a maybe_resample! was enqueued since the last step
+                         // (otherwise the device flags are stale and ignored)
   const double* remote;  // multi-rank: rows received from other ranks, row r at
   int64_t ld_remote;     // remote[r * ld_remote] = (x_0 .. x_{D-1}, global id)
   double* xout;          // [D][ld_out]
@@ -74,19 +78,75 @@ struct StepArgs {
 };
 
 // ------------------------------------------------------------ reductions
+// Wave-level reductions and scans on DPP lane moves (quad_perm, row_shr,
+// row_bcast:15/31) instead of LDS-routed shuffles: each step is two
+// v_mov_dpp (64-bit payload) + the operation, a few cycles instead of an LDS
+// round trip.  Reductions leave the total in lane 63, read back with
+// readlane.  Integer sums, maxima and scans are exact in any order; the
+// floating sums only feed the statistics (log-ML / ESS), not the ancestors.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v, uint64_t old) {
+  const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)old, (int)(uint32_t)v, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(old >> 32), (int)(uint32_t)(v >> 32), CTRL, ROW_MASK,
+                                             0xf, false);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo;
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double v, double old) {
+  return as_f64(dpp_u64<CTRL, ROW_MASK>(as_u64(v), as_u64(old)));
+}
+__device__ __forceinline__ uint64_t readlane63_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <class Op>
+__device__ __forceinline__ double wave_reduce_f64(double v, Op op) {
+  v = op(v, dpp_f64<0xb1>(v, v));         // quad_perm [1,0,3,2]
+  v = op(v, dpp_f64<0x4e>(v, v));         // quad_perm [2,3,0,1]
+  v = op(v, dpp_f64<0x114>(v, v));        // row_shr:4
+  v = op(v, dpp_f64<0x118>(v, v));        // row_shr:8
+  v = op(v, dpp_f64<0x142, 0xa>(v, v));   // row_bcast:15
+  v = op(v, dpp_f64<0x143, 0xc>(v, v));   // row_bcast:31
+  return as_f64(readlane63_u64(as_u64(v)));
+}
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce_f64(v, [](double a, double b) { return fmax(a, b); });
 }
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce_f64(v, [](double a, double b) { return a + b; });
 }
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += dpp_u64<0xb1>(v, 0);
+  v += dpp_u64<0x4e>(v, 0);
+  v += dpp_u64<0x114>(v, 0);
+  v += dpp_u64<0x118>(v, 0);
+  v += dpp_u64<0x142, 0xa>(v, 0);
+  v += dpp_u64<0x143, 0xc>(v, 0);
+  return readlane63_u64(v);
+}
+// inclusive scans over the 64 lanes (lane order)
+__device__ __forceinline__ uint64_t wave_incl_sum_u64(uint64_t v) {
+  const int lane = threadIdx.x & 63, rl = lane & 15;
+  uint64_t t;
+  t = dpp_u64<0x111>(v, 0); if (rl >= 1) v += t;   // row_shr:1
+  t = dpp_u64<0x112>(v, 0); if (rl >= 2) v += t;   // row_shr:2
+  t = dpp_u64<0x114>(v, 0); if (rl >= 4) v += t;   // row_shr:4
+  t = dpp_u64<0x118>(v, 0); if (rl >= 8) v += t;   // row_shr:8
+  t = dpp_u64<0x142>(v, 0); if ((lane & 31) >= 16) v += t;  // row_bcast:15
+  t = dpp_u64<0x143>(v, 0); if (lane >= 32) v += t;         // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_incl_max_u64(uint64_t v) {
+  const int lane = threadIdx.x & 63, rl = lane & 15;
+  uint64_t t;
+  t = dpp_u64<0x111>(v, 0); if (rl >= 1 && t > v) v = t;
+  t = dpp_u64<0x112>(v, 0); if (rl >= 2 && t > v) v = t;
+  t = dpp_u64<0x114>(v, 0); if (rl >= 4 && t > v) v = t;
+  t = dpp_u64<0x118>(v, 0); if (rl >= 8 && t > v) v = t;
+  t = dpp_u64<0x142>(v, 0); if ((lane & 31) >= 16 && t > v) v = t;
+  t = dpp_u64<0x143>(v, 0); if (lane >= 32 && t > v) v = t;
   return v;
 }
 
@@ -126,7 +186,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + w;
   const int64_t j = tile * 64 + lane;
   int pend = 0, use_marks = 0;
-  if (!INIT) {
+  if (!INIT && a.resampled) {
     const int pending = a.dev->pending, fire = a.dev->fire;
     pend = pending | fire;
     use_marks = a.mark_mode && fire && !pending;
@@ -137,12 +197,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
     if (use_marks) {
       uint64_t v = j < a.n ? a.mark[j] : 0;
       const uint64_t c = a.carry[tile];
-      v = v > c ? v : c;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const uint64_t u = __shfl_up(v, off, 64);
-        if (lane >= off && u > v) v = u;
-      }
+      v = wave_incl_max_u64(v > c ? v : c);
       src = (int64_t)(uint32_t)v;
       if (j < a.n) a.anc[j] = (int32_t)src;  // genealogy record
     }
@@ -378,11 +433,7 @@ __device__ __forceinline__ uint64_t block_sum_u64(uint64_t s, uint64_t* sm) {
 // Block-wide (256 threads) inclusive scans of one value per thread.
 __device__ __forceinline__ uint64_t block_incl_sum_u64(uint64_t v, uint64_t* sm4) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint64_t u = __shfl_up(v, off, 64);
-    if (lane >= off) v += u;
-  }
+  v = wave_incl_sum_u64(v);
   __syncthreads();
   if (lane == 63) sm4[w] = v;
   __syncthreads();
@@ -391,11 +442,7 @@ __device__ __forceinline__ uint64_t block_incl_sum_u64(uint64_t v, uint64_t* sm4
 }
 __device__ __forceinline__ uint64_t block_incl_max_u64(uint64_t v, uint64_t* sm4) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint64_t u = __shfl_up(v, off, 64);
-    if (lane >= off && u > v) v = u;
-  }
+  v = wave_incl_max_u64(v);
   __syncthreads();
   if (lane == 63) sm4[w] = v;
   __syncthreads();
@@ -503,7 +550,7 @@ __device__ __forceinline__ uint64_t sys_target(const DevScalars* dev, uint64_t N
 
 // #{ j in [0, N) : T_j < X }: the first slot whose target reaches X.
 // Particle i owns the slots [count(C_{i-1}), count(C_i)).
-__device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, uint64_t X) {
+__device__ __forceinline__ int64_t sys_count_exact(const DevScalars* dev, uint64_t N, uint64_t X) {
   if (X == 0) return 0;
   if (X >= dev->S) return (int64_t)N;
   const double est = ((double)X * (double)N - (double)dev->o) / (double)dev->S;
@@ -511,6 +558,23 @@ __device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, 
   while (j > 0 && sys_target(dev, N, (uint64_t)(j - 1)) >= X) --j;
   while (j < (int64_t)N && sys_target(dev, N, (uint64_t)j) < X) ++j;
   return j;
+}
+
+// The same count from v = (X N - o) / S in floating point: count = ceil(v)
+// clamped to [0, N].  The computed v is within 5 N 2^-53 (< 2^-19 for
+// N < 2^31) of the exact quotient, so ceil is exact whenever v is more than
+// 2^-16 away from an integer; otherwise (probability ~2^-15) count exactly.
+__device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, uint64_t X) {
+  if (X == 0) return 0;
+  if (X >= dev->S) return (int64_t)N;
+  const double v = fma((double)X, (double)N, -(double)dev->o) * dev->invS;
+  const double fl = floor(v);
+  const double fr = v - fl;
+  if (fr > 0x1p-16 && fr < 1.0 - 0x1p-16) {
+    const double j = fl + 1.0;
+    return j <= 0.0 ? 0 : (j >= (double)N ? (int64_t)N : (int64_t)j);
+  }
+  return sys_count_exact(dev, N, X);
 }
 
 struct MarkArgs {
@@ -574,6 +638,7 @@ __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, G
     sd.Qs = S / (uint64_t)ca.n_global;
     sd.Rs = S % (uint64_t)ca.n_global;
     sd.invN = 1.0 / (double)ca.n_global;
+    sd.invS = 1.0 / (double)S;
     sboff = base + before;
     if (blockIdx.x == 0) {
       dev->S = sd.S;
@@ -644,15 +709,267 @@ __global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const
   if ((j & ~63LL) >= n) return;  // whole wave past the end
   uint64_t v = j < n ? mark[j] : 0;
   const uint64_t c = carry[j >> 6];
-  v = v > c ? v : c;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint64_t u = __shfl_up(v, off, 64);
-    if (lane >= off && u > v) v = u;
-  }
+  v = wave_incl_max_u64(v > c ? v : c);
+  (void)lane;
   if (j >= n) return;
   const int32_t a = (int32_t)(uint32_t)v;
   anc_out[j] = (*zero_w && anc_old) ? anc_old[a] : a;
+}
+
+// ----------------------------------------------- fused single-rank resample
+// maybe_resample! on one rank in ONE launch: every block folds
+// the step kernel's partials itself and takes the (identical) decision, so no
+// block waits for another to decide; if it fires, each block quantises its
+// 4096-particle tile, publishes the tile's integer total and crosses one grid
+// barrier; then it derives its CDF offset and the systematic constants from
+// the published totals and writes the range marks (or the CDF).  The grid is
+// co-resident (cooperative launch, grid <= resident capacity).
+constexpr int kRsBlock = 1024;
+constexpr int kRsItems = 4;
+constexpr int kRsTile = kRsBlock * kRsItems;  // particles per block
+constexpr int kRsPart = 4;                    // step partials per thread (nb_part <= 4096)
+
+struct Resample1Args {
+  const double* pm;        // step-kernel block partials
+  const double* ps;
+  const double* ps2;
+  int nb_part;
+  const double* logw;
+  int64_t n;
+  int shift;
+  double* stats_out;       // (M, S, S2) of this rank
+  DevScalars* dev;
+  DecideArgs d;
+  uint64_t* tsum;          // [grid] published tile totals (bit 63: generation parity)
+  MarkArgs mk;             // enabled: systematic marks; else write C
+  uint64_t* C;
+  uint64_t seed;
+  uint32_t t;
+};
+
+// 1024-thread block reductions (16 waves), result broadcast
+__device__ __forceinline__ double blk16_max(double v, double* sm) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = sm[0];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) r = fmax(r, sm[k]);
+  return r;
+}
+__device__ __forceinline__ double blk16_sum(double v, double* sm) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = sm[0];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) r += sm[k];
+  return r;
+}
+__device__ __forceinline__ uint64_t blk16_sum_u64(uint64_t v, uint64_t* sm) {
+  v = wave_sum_u64(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) r += sm[k];
+  return r;
+}
+// inclusive scan over the block's threads
+__device__ __forceinline__ uint64_t blk16_incl_u64(uint64_t v, uint64_t* sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_incl_sum_u64(v);
+  __syncthreads();
+  if (lane == 63) sm[w] = v;
+  __syncthreads();
+  for (int k = 0; k < w; ++k) v += sm[k];
+  return v;
+}
+
+#if defined(GH_RS_STAMPS)  // timing-only variant: per-block phase clocks
+__device__ uint64_t g_rs_stamps[1024 * 8];
+#define GH_RS_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_rs_stamps[blockIdx.x * 8 + (k)] = wall_clock64();
+#else
+#define GH_RS_STAMP(k)
+#endif
+
+template <bool MARKS>
+__global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
+  __shared__ double smd[16];
+  __shared__ uint64_t smu[16];
+  __shared__ DevScalars sd;
+  __shared__ uint64_t sbase;
+  __shared__ int32_t se[kRsTile];
+  __shared__ int64_t sfirst;
+  __shared__ unsigned sgen;
+  GH_RS_STAMP(0);
+  // barrier generation of this launch: read before this block publishes
+  if (threadIdx.x == 0) sgen = r.dev->bar_gen + 1;
+  // ---- fold the step partials (same order in every block: same result)
+  // this tile's log-weights are loaded up front, beside the partials
+  const int64_t i0 = (int64_t)blockIdx.x * kRsTile + (int64_t)threadIdx.x * kRsItems;
+  double lw[kRsItems];
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
+  double pmv[kRsPart], psv[kRsPart], ps2v[kRsPart];
+#pragma unroll
+  for (int k = 0; k < kRsPart; ++k) {
+    const int b = threadIdx.x + k * kRsBlock;
+    const bool ok = b < r.nb_part;
+    pmv[k] = ok ? r.pm[b] : -INFINITY;
+    psv[k] = ok ? r.ps[b] : 0.0;
+    ps2v[k] = ok ? r.ps2[b] : 0.0;
+  }
+  double m = pmv[0];
+#pragma unroll
+  for (int k = 1; k < kRsPart; ++k) m = fmax(m, pmv[k]);
+  const double M = blk16_max(m, smd);
+  GH_RS_STAMP(7);
+  double s1 = 0.0, s2 = 0.0;
+  if (M > -INFINITY) {
+#pragma unroll
+    for (int k = 0; k < kRsPart; ++k)
+      if (pmv[k] > -INFINITY) {
+        const double f = gh_exp(pmv[k] - M);
+        s1 += psv[k] * f;
+        s2 += ps2v[k] * (f * f);
+      }
+  }
+  const double S1 = blk16_sum(s1, smd);
+  const double S2 = blk16_sum(s2, smd);
+  // the resample test alone (ESS = S^2 / S2 < thr, exactly as decide()):
+  // block 0 commits the full decision (logsumexp, log-ML) at its end
+  __shared__ int sfire;
+  if (threadIdx.x == 0) {
+    const bool ok = M > -INFINITY && M != INFINITY && M == M;
+    sfire = ok && ((S1 * S1) / S2 < r.d.thr);
+  }
+  __syncthreads();
+  GH_RS_STAMP(1);
+  const int fire = sfire;
+  auto commit = [&]() {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      double st[3] = {M, S1, S2};
+      DecideArgs d = r.d;
+      d.stats_all = st;
+      d.R = 1;
+      const Decision dec = decide(d, false);
+      r.stats_out[0] = M;
+      r.stats_out[1] = S1;
+      r.stats_out[2] = S2;
+      r.dev->pending = 0;
+      commit_decision(r.d, dec, r.dev, 0);
+    }
+  };
+  if (!fire) {  // uniform over the grid: nobody publishes
+    commit();
+    return;
+  }
+  const double Mq = M;
+  // ---- quantise this block's tile (4 consecutive particles per thread)
+  uint64_t q[kRsItems];
+  uint64_t tsum = 0;
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    q[k] = (i0 + k < r.n) ? quantize_weight(lw[k], Mq, r.shift) : 0;
+    tsum += q[k];
+  }
+  const uint64_t incl = blk16_incl_u64(tsum, smu);
+  GH_RS_STAMP(2);
+  // ---- grid barrier: each tile total (< 2^62) is published as ONE 8-byte
+  // agent-scope store tagged in bit 63 with the generation's parity, and read
+  // back with agent-scope loads until every tag matches (the payload is its
+  // own flag: no counter, no fence)
+  const uint64_t kTag = 1ull << 63;
+  const uint64_t par = (sgen & 1u) ? kTag : 0ull;
+  if (threadIdx.x == kRsBlock - 1) st_sc1(&r.tsum[blockIdx.x], incl | par);
+  uint64_t before = 0, all = 0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kRsBlock) {
+    uint64_t v = ld_sc1(&r.tsum[b]);
+    unsigned spins = 0;  // bounded (~0.5 s): a grid that is not co-resident errors out
+    while ((v & kTag) != par) {
+      __builtin_amdgcn_s_sleep(1);
+      v = ld_sc1(&r.tsum[b]);
+      if (++spins == (1u << 22)) {
+        r.dev->error = 7;  // GH_E_STATE
+        break;
+      }
+    }
+    v &= ~kTag;
+    all += v;
+    if (b < (int)blockIdx.x) before += v;
+  }
+  GH_RS_STAMP(3);
+  before = blk16_sum_u64(before, smu);
+  all = blk16_sum_u64(all, smu);
+  if (threadIdx.x == 0) {
+    const uint64_t N = (uint64_t)r.d.n_global;
+    sd.S = all;
+    sd.base = 0;
+    sd.local = all;
+    const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
+    sd.o = scale_u53(u53_bits(w.x, w.y), all);
+    sd.invN = 1.0 / (double)N;
+    sd.Qs = udiv_n(all, N, sd.invN);
+    sd.Rs = all - sd.Qs * N;
+    sd.invS = 1.0 / (double)all;
+    sbase = before;
+    if (blockIdx.x == 0) {
+      r.dev->bar_gen = sgen;  // every block has published, so has read the old value
+      r.dev->S = sd.S;
+      r.dev->base = 0;
+      r.dev->local = sd.local;
+      r.dev->o = sd.o;
+      r.dev->Qs = sd.Qs;
+      r.dev->Rs = sd.Rs;
+      r.dev->invN = sd.invN;
+      r.dev->invS = sd.invS;
+    }
+  }
+  __syncthreads();
+  GH_RS_STAMP(4);
+  uint64_t run = sbase + incl - tsum;
+  if (!MARKS) {
+#pragma unroll
+    for (int k = 0; k < kRsItems; ++k) {
+      run += q[k];
+      if (i0 + k < r.n) r.C[i0 + k] = run;
+    }
+    commit();
+    return;
+  }
+  const uint64_t N = (uint64_t)r.mk.n_global;
+  int64_t s_i = sys_count(&sd, N, run);
+  if (threadIdx.x == 0) sfirst = s_i;
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    run += q[k];
+    const int64_t e_i = (i0 + k < r.n && q[k]) ? sys_count(&sd, N, run) : s_i;
+    se[threadIdx.x * kRsItems + k] = (int32_t)e_i;
+    if (e_i > s_i) r.mk.mark[s_i] = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
+    s_i = e_i;
+  }
+  __syncthreads();
+  GH_RS_STAMP(5);
+  // 64-slot groups starting inside this tile's slot span get their carry
+  const int64_t s_lo = sfirst, s_hi = se[kRsTile - 1];
+  const int64_t pbase = (int64_t)blockIdx.x * kRsTile;
+  for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
+    const int32_t slot = (int32_t)(g * 64);
+    int lo = 0, hi = kRsTile - 1;  // first particle p with se[p] > slot
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (se[mid] > slot) hi = mid;
+      else lo = mid + 1;
+    }
+    r.mk.cmark[g] = (r.mk.epoch << 32) | (uint64_t)(pbase + lo);
+  }
+  commit();
+  GH_RS_STAMP(6);
 }
 
 enum SearchMode { SEARCH_SYSTEMATIC = 0, SEARCH_MULTINOMIAL = 1, SEARCH_SAMPLE = 2 };
@@ -782,6 +1099,7 @@ struct TrajArgs {
   const int32_t* anc_pending; // ancestors of a resample pending after the last step
   int64_t n, ld;
   int t_target, t_cur, D;
+  int live;                   // the device resample flags are current
   double* out;                // [D][n]
 };
 
@@ -789,7 +1107,7 @@ __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevScalars* d
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= a.n) return;
   int64_t idx = j;
-  if ((dev->pending | dev->fire) && a.anc_pending) idx = a.anc_pending[idx];
+  if (a.live && (dev->pending | dev->fire) && a.anc_pending) idx = a.anc_pending[idx];
   for (int s = a.t_cur; s > a.t_target; --s)
     if (a.res_before[s]) idx = a.ancs[s - 1][idx];
   const double* x = a.xs[a.t_target - 1];
@@ -797,11 +1115,11 @@ __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevScalars* d
 }
 
 // sample_unweighted: prepare max / equal-weight flag from the current stats
-__global__ void k_prep_sample(DevScalars* dev, const double* stats_all, int R) {
+__global__ void k_prep_sample(DevScalars* dev, const double* stats_all, int R, int live) {
   if (threadIdx.x != 0) return;
   double M = -INFINITY;
   for (int r = 0; r < R; ++r) M = fmax(M, stats_all[3 * r]);
-  dev->spend = dev->pending | dev->fire;
+  dev->spend = live ? (dev->pending | dev->fire) : 0;
   dev->sM = dev->spend ? 0.0 : M;
   dev->one = 1;
 }

@@ -1,0 +1,33 @@
+"""Per-phase clocks of k_resample1 (variant build with GH_RS_STAMPS).
+
+python tools/rs_stamps.py   (on the GPU box, after `python tools/variants.py build rs_stamps`)
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["GEN_HIP_LIB"] = os.path.join(ROOT, "gen_amd", "variants", "rs_stamps.so")
+import gen_amd as gen  # noqa: E402
+from gen_amd import _lib  # noqa: E402
+
+ctx = gen.Context(device=0)
+gen.set_default_context(ctx)
+m = gen.LinearGaussianSSM.benchmark(10)
+_, ys = m.simulate(12, np.random.default_rng(2))
+st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, 1 << 20, seed=42, record_history=False)
+gen.run_particle_filter(st, list(ys[1:10]))
+ctx.synchronize()
+lib = _lib.load()
+buf = (ctypes.c_uint64 * (1024 * 8))()
+lib.gh_debug_rs_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+_lib.check(lib.gh_debug_rs_stamps(buf, 1024 * 8))
+a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[:256, :8].astype(np.int64)
+t0 = a[:, 0].min()
+rel = (a - t0) * 0.01  # wall_clock64 ticks at 100 MHz -> us
+names = {0: "start", 7: "max", 1: "decided", 2: "quantised", 3: "barrier", 4: "offsets", 5: "marks", 6: "end"}
+for k, nm in names.items():
+    print(f"{nm:10s} min {rel[:, k].min():7.2f} med {np.median(rel[:, k]):7.2f} max {rel[:, k].max():7.2f} us")

@@ -13,18 +13,19 @@ sys.path.insert(0, ROOT)
 VARIANTS = {
     "base": [],
     "no_bm_philox1": ["GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
-    "no_ticket": ["GH_ABLATE_TICKET"],
     "no_reduce": ["GH_ABLATE_REDUCE"],
     "no_reduce_no_rng": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
 }
-BENCH_ARGS = os.environ.get("GH_VARIANT_ARGS", "--no-history --ess-threshold 1e-300 --particles 4194304 --steps 30").split()
+# instrumented builds (not timed by `run`)
+EXTRA = {"rs_stamps": ["GH_RS_STAMPS"]}
+BENCH_ARGS = os.environ.get("GH_VARIANT_ARGS", "--steps 50").split()
 
 
 def main():
     if sys.argv[1] == "build":
         from gen_amd import build as gb
 
-        for name, defs in VARIANTS.items():
+        for name, defs in {**VARIANTS, **EXTRA}.items():
             if len(sys.argv) > 2 and name not in sys.argv[2:]:
                 continue
             gb.build_variant(name, defs)
