@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--no-history", action="store_true")
     p.add_argument("--ess-threshold", type=float, default=None, help="default N/2 (the reference's default)")
     p.add_argument("--no-kernel-timing", action="store_true", help="no hipEvents around the step kernel")
+    p.add_argument("--time-every", type=int, default=10,
+                   help="time every k-th step kernel with launch events (each timed launch adds queue packets)")
     return p.parse_args()
 
 
@@ -105,7 +107,7 @@ def main():
     n_global = a.particles * world
     st = gen.initialize_particle_filter(
         model, (1,), {("chain", 1, "y"): ys[0]}, n_global, seed=42, resampler=a.resampler,
-        record_history=not a.no_history, history_capacity=T + 2, time_kernels=not a.no_kernel_timing,
+        record_history=not a.no_history, history_capacity=T + 2, time_kernels=0 if a.no_kernel_timing else a.time_every,
     )
     gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold)
     ctx.synchronize()

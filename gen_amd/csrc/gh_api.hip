@@ -627,7 +627,9 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
 // next maybe_resample! folds inside k_resample1, other readers fold on demand.
 static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
   pf->stats_valid = false;
-  if (!pf->opts.time_kernels) {
+  // time_kernels = k > 0: time every k-th step kernel (events add queue packets)
+  const int every = pf->opts.time_kernels;
+  if (every <= 0 || (a.t - 1) % (uint32_t)every != 0) {
     CHECK(launch_step(pf, o, a, init));
     if (pf->ctx->world > 1) launch_fold(pf, a, init);
     HIP_TRY(hipGetLastError());

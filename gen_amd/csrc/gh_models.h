@@ -73,7 +73,11 @@ template <int D, int S = 0>
 struct LGModel {
   static constexpr int kD = D;
   // spill-free register budgets measured with tools/regs.py
+  #if defined(GH_LG10_WAVES)  // timing-only variants: occupancy target of the d<=10 diagonal case
+  static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 10 ? (S == 3 ? GH_LG10_WAVES : 5) : 4);
+#else
   static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 10 ? (S == 3 ? 7 : 5) : 4);
+#endif
   using Params = LGParams;
 
   __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, uint32_t stream,

@@ -271,7 +271,7 @@ class _TraceView:
 
 
 # --------------------------------------------------------------- the API
-def _opts(resampler: str, record_history: bool, history_capacity: int, time_kernels: bool) -> _lib.PFOpts:
+def _opts(resampler: str, record_history: bool, history_capacity: int, time_kernels: int) -> _lib.PFOpts:
     o = _lib.PFOpts()
     _lib.load().gh_pf_opts_default(byref(o))
     o.resampler = {"systematic": _lib.RESAMPLE_SYSTEMATIC, "multinomial": _lib.RESAMPLE_MULTINOMIAL}[resampler]
@@ -283,7 +283,7 @@ def _opts(resampler: str, record_history: bool, history_capacity: int, time_kern
 
 def initialize_particle_filter(model: Model, model_args: tuple, observations, *args, seed: int = 0,
                                resampler: str = "systematic", record_history: bool = True,
-                               history_capacity: int = 0, time_kernels: bool = False,
+                               history_capacity: int = 0, time_kernels: int = 0,
                                ctx: Context | None = None) -> ParticleFilterState:
     """initialize_particle_filter(model, model_args, observations, num_particles)
     initialize_particle_filter(model, model_args, observations, proposal, proposal_args, num_particles)"""

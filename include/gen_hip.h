@@ -100,7 +100,7 @@ typedef struct {
   int32_t record_history; /* 1: keep every step's states + genealogy (Gen trace semantics) */
   int32_t history_capacity; /* steps to preallocate when record_history (0 = grow) */
   int32_t block_size;     /* 0 = default (256) */
-  int32_t time_kernels;   /* 1: time every step kernel with hipEvents (gh_pf_kernel_time) */
+  int32_t time_kernels;   /* k > 0: time every k-th step kernel with hipEvents (gh_pf_kernel_time) */
   int32_t reserved[3];
 } gh_pf_opts;
 

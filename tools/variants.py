@@ -15,6 +15,8 @@ VARIANTS = {
     "no_bm_philox1": ["GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
     "no_reduce": ["GH_ABLATE_REDUCE"],
     "no_reduce_no_rng": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
+    "occ8": ["GH_LG10_WAVES=8"],
+    "occ6": ["GH_LG10_WAVES=6"],
 }
 # instrumented builds (not timed by `run`)
 EXTRA = {"rs_stamps": ["GH_RS_STAMPS"]}
@@ -32,7 +34,7 @@ def main():
             print("built", name, flush=True)
     else:
         out = {}
-        for name in VARIANTS:
+        for name in [v for v in VARIANTS if len(sys.argv) < 3 or v in sys.argv[2:]]:
             lib = os.path.join(ROOT, "gen_amd", "variants", f"{name}.so")
             env = dict(os.environ, GEN_HIP_LIB=lib)
             r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + BENCH_ARGS,
