@@ -758,6 +758,7 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   a.ps = pf->ps;
   a.ps2 = pf->ps2;
   a.stats_out = ctx->world == 1 ? pf->stats_all : pf->dev->stats;
+  a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
   rc = timed_step(pf, o, a, true);
   if (rc) return fail(rc);
   rc = share_stats(pf);
@@ -800,6 +801,7 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   a.ps = pf->ps;
   a.ps2 = pf->ps2;
   a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
+  a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
   CHECK(timed_step(pf, o, a, false));
   CHECK(share_stats(pf));
   pf->t = t;

@@ -60,6 +60,7 @@ struct StepArgs {
   int mark_mode;
   int resampled;         // a maybe_resample! was enqueued since the last step
                          // (otherwise the device flags are stale and ignored)
+  int buf;               // state slots < 4 GiB: address them by buffer descriptors
   const double* remote;  // multi-rank: rows received from other ranks, row r at
   int64_t ld_remote;     // remote[r * ld_remote] = (x_0 .. x_{D-1}, global id)
   double* xout;          // [D][ld_out]
@@ -168,6 +169,22 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
   return (sm[0] + sm[1]) + (sm[2] + sm[3]);
 }
 
+// ------------------------------------------------------- buffer accesses
+// A buffer descriptor (wave-uniform, from kernel arguments) + a 32-bit
+// per-lane byte offset + a uniform SGPR offset per state component: one
+// offset VGPR serves all d component loads/stores of a particle instead of d
+// 64-bit addresses.
+typedef unsigned int gh_v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gh_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)0xffffffff, 0x00020000);
+}
+__device__ __forceinline__ double buf_ld_f64(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gh_v2u, v), r, (int)voff, (int)soff, 0);
+}
+
 // ---------------------------------------------------------------- k_step
 // One particle per lane, 64-particle tiles per wave, 4 waves per block.
 // Systematic ancestors come from the range marks by a wave-level prefix max
@@ -208,7 +225,12 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
       } else {
         double xp[D];
         if (pend && !use_marks) src = a.anc[j];
-        if (src >= 0) {
+        if (src >= 0 && a.buf) {
+          const __amdgpu_buffer_rsrc_t rp = gh_rsrc(a.xprev);
+#pragma unroll
+          for (int k = 0; k < D; ++k)
+            xp[k] = buf_ld_f64(rp, (uint32_t)src * 8u, (uint32_t)k * (uint32_t)a.ld_prev * 8u);
+        } else if (src >= 0) {
 #pragma unroll
           for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
         } else {
@@ -218,8 +240,14 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
         const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
       }
+      if (a.buf) {
+        const __amdgpu_buffer_rsrc_t ro = gh_rsrc(a.xout);
 #pragma unroll
-      for (int k = 0; k < D; ++k) a.xout[k * a.ld_out + j] = x[k];
+        for (int k = 0; k < D; ++k) buf_st_f64(x[k], ro, (uint32_t)j * 8u, (uint32_t)k * (uint32_t)a.ld_out * 8u);
+      } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) a.xout[k * a.ld_out + j] = x[k];
+      }
       a.logw[j] = lw;
     }
   }
