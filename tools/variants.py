@@ -17,6 +17,10 @@ VARIANTS = {
     "no_reduce_no_rng": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
     "occ8": ["GH_LG10_WAVES=8"],
     "occ6": ["GH_LG10_WAVES=6"],
+    "occ5": ["GH_LG10_WAVES=5"],
+    "philox1": ["GH_PHILOX_ROUNDS=1"],
+    "no_bm": ["GH_ABLATE_BOXMULLER"],
+    "philox7": ["GH_PHILOX_ROUNDS=7"],
 }
 # instrumented builds (not timed by `run`)
 EXTRA = {"rs_stamps": ["GH_RS_STAMPS"]}
