@@ -475,6 +475,10 @@ struct gh_pf {
   int32_t* xanc = nullptr;        // [send_cap] local ancestors of the sent rows
   int64_t send_cap = 0;
   int64_t* gparent = nullptr;     // [n] global parent ids of the last exchange
+  hipStream_t aux = nullptr;      // multi-rank: side stream for the plan's D2H read
+  hipEvent_t ev_tot = nullptr;    // multi-rank: totals all-gathered
+  uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]]
+  int mark_mode = 1;              // 1: one-rank marks; 2: marks + received rows
   std::vector<void*> chunks;      // history allocations (record_history)
   // kernel timing
   std::vector<hipEvent_t> ev;
@@ -484,6 +488,14 @@ struct gh_pf {
 };
 
 static int64_t split_lo(int64_t n, int r, int R) { return (n * r) / R; }
+
+// device -> host copy ordered after everything enqueued on the filter's stream
+// (the stream is non-blocking, so a plain hipMemcpy could overtake it)
+static int d2h(gh_pf* pf, void* dst, const void* src, size_t bytes) {
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  return GH_OK;
+}
 
 static double* slot_x(gh_pf* pf, int t) {  // states of step t (1-based)
   return pf->opts.record_history ? pf->xs[t - 1] : pf->xs[t & 1];
@@ -547,6 +559,9 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->tsum); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
+  if (pf->aux) hipStreamDestroy(pf->aux);
+  if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
+  if (pf->h_plan) hipHostFree(pf->h_plan);
   if (!pf->opts.record_history) {
     for (auto p : pf->xs) hipFree(p);
     for (auto p : pf->ancs) hipFree(p);
@@ -712,6 +727,10 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
     ALLOC(pf->rows_recv, sizeof(double) * (pf->D + 1) * n);
     ALLOC(pf->gparent, sizeof(int64_t) * n);
+    if (hipStreamCreateWithFlags(&pf->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&pf->ev_tot, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void**)&pf->h_plan, sizeof(uint64_t) * (ctx->world + 1), hipHostMallocDefault) != hipSuccess)
+      return fail(set_err(GH_E_NOMEM, "multi-rank plan buffers"));
   }
   if (!pf->opts.record_history) {
     for (int i = 0; i < 2; ++i) {
@@ -784,7 +803,7 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   a.anc = anc_for_step(pf, t);
   a.mark = pf->mark;
   a.carry = pf->cmark;
-  a.mark_mode = pf->marks_pending ? 1 : 0;
+  a.mark_mode = pf->marks_pending ? pf->mark_mode : 0;
   a.resampled = flags_live(pf);
   a.remote = pf->rows_recv;
   a.ld_remote = pf->D + 1;
@@ -816,7 +835,8 @@ static int materialize_marks(gh_pf* pf) {
   if (!pf->marks_pending) return GH_OK;
   int32_t* anc_target = anc_for_step(pf, pf->t + 1);
   hipLaunchKernelGGL(k_sys_ancestors, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
-                     &pf->dev->pending, pf->mark, pf->cmark, pf->n, (const int32_t*)nullptr, anc_target);
+                     &pf->dev->pending, pf->mark, pf->cmark, pf->n, (const int32_t*)nullptr, anc_target,
+                     (const DevScalars*)pf->dev, pf->mark_mode);
   HIP_TRY(hipGetLastError());
   pf->marks_pending = false;
   return GH_OK;
@@ -824,6 +844,111 @@ static int materialize_marks(gh_pf* pf) {
 
 // multi-rank exchange of ancestor states; defined below
 static int exchange_states(gh_pf* pf, int32_t* anc_out);
+
+static void sys_plan(int64_t N, int R, int q, const uint64_t* totals, uint64_t o, int64_t* send_lo,
+                     int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi);
+
+// Multi-rank systematic resample: decision + quantise + rank
+// total (k_rank_a), all-gather of the totals, marks + outgoing rows
+// (k_rank_b).  The host reads the totals on a side stream while k_rank_b
+// runs, derives the row counts (gh_sys_plan's arithmetic) and posts the
+// grouped send/recv; the next step kernel reads own-slot ancestors from the
+// marks and the other slots from the received rows.
+static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
+  gh_ctx* c = pf->ctx;
+  const int R = c->world, q = c->rank;
+  const int D = pf->D;
+  if (pf->send_cap < 1) {
+    const int64_t cap = pf->n / 4 + 1024;
+    if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess)
+      return set_err(GH_E_NOMEM, "send rows");
+    pf->send_cap = cap;
+  }
+  RankAArgs ra{};
+  ra.logw = pf->logw;
+  ra.n = pf->n;
+  ra.shift = shift;
+  ra.dev = pf->dev;
+  ra.d = d;
+  ra.tsum = pf->tsum;
+  hipLaunchKernelGGL(k_rank_a, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra);
+  HIP_TRY(hipGetLastError());
+  CHECK(comm_allgather(c, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
+  HIP_TRY(hipEventRecord(pf->ev_tot, pf->s));
+  RankBArgs rb{};
+  rb.logw = pf->logw;
+  rb.n = pf->n;
+  rb.shift = shift;
+  rb.dev = pf->dev;
+  rb.tsum = pf->tsum;
+  rb.totals = pf->totals_all;
+  rb.R = R;
+  rb.rank = q;
+  rb.lo = pf->lo;
+  rb.seed = pf->seed;
+  rb.t = (uint32_t)t;
+  rb.mk.mark = pf->mark;
+  rb.mk.cmark = pf->cmark;
+  rb.mk.epoch = ++pf->epoch;
+  rb.mk.n_global = pf->n_global;
+  rb.mk.n_groups = (pf->n + 63) / 64;
+  rb.mk.enabled = 1;
+  rb.xprev = slot_x(pf, t);
+  rb.ldx = pf->n;
+  rb.D = D;
+  rb.rows = pf->rows_send;
+  rb.rows_cap = pf->send_cap;
+  hipLaunchKernelGGL(k_rank_b, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, rb);
+  HIP_TRY(hipGetLastError());
+  // the counts: decision + totals on the host, overlapping k_rank_b
+  HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_tot, 0));
+  HIP_TRY(hipMemcpyAsync(pf->h_plan, &pf->dev->fire, sizeof(int), hipMemcpyDeviceToHost, pf->aux));
+  HIP_TRY(hipMemcpyAsync(pf->h_plan + 1, pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->aux));
+  HIP_TRY(hipStreamSynchronize(pf->aux));
+  int fire = 0;
+  memcpy(&fire, pf->h_plan, sizeof(int));
+  pf->mark_mode = 2;
+  pf->marks_pending = true;  // harmless when it did not fire: k_step gates on the device flag
+  if (!fire) return GH_OK;
+  const uint64_t* tot = pf->h_plan + 1;
+  uint64_t S = 0;
+  for (int r = 0; r < R; ++r) S += tot[r];
+  if (S == 0) return GH_OK;  // the device raised GH_E_NUMERIC
+  const u32x4 w = rng_block(pf->seed, ~0ull, (uint32_t)t, STREAM_RESAMPLE, 0);
+  const uint64_t o = scale_u53(u53_bits(w.x, w.y), S);
+  std::vector<int64_t> slo(R), shi(R), rlo(R), rhi(R);
+  sys_plan(pf->n_global, R, q, tot, o, slo.data(), shi.data(), rlo.data(), rhi.data());
+  int64_t n_send = 0;
+  for (int r = 0; r < R; ++r)
+    if (r != q) n_send += shi[r] - slo[r];
+  if (n_send > pf->send_cap) {  // rows did not fit: grow and pack again
+    HIP_TRY(hipStreamSynchronize(pf->s));
+    hipFree(pf->rows_send);
+    pf->rows_send = nullptr;
+    pf->send_cap = 0;
+    const int64_t cap = n_send + n_send / 4 + 1024;
+    if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess)
+      return set_err(GH_E_NOMEM, "send rows");
+    pf->send_cap = cap;
+    rb.rows = pf->rows_send;
+    rb.rows_cap = cap;
+    hipLaunchKernelGGL(k_rank_b, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, rb);
+    HIP_TRY(hipGetLastError());
+  }
+  std::vector<CommMsg> sends, recvs;
+  const size_t row_bytes = sizeof(double) * (D + 1);
+  int64_t soff = 0, roff = 0;
+  for (int r = 0; r < R; ++r) {
+    if (r == q) continue;
+    const int64_t ls = shi[r] - slo[r], lr = rhi[r] - rlo[r];
+    if (ls > 0) sends.push_back({r, pf->rows_send + soff * (D + 1), (size_t)ls * row_bytes});
+    if (lr > 0) recvs.push_back({r, pf->rows_recv + roff * (D + 1), (size_t)lr * row_bytes});
+    soff += ls > 0 ? ls : 0;
+    roff += lr > 0 ? lr : 0;
+  }
+  CHECK(comm_exchange(c, sends, recvs, pf->s));
+  return GH_OK;
+}
 
 static int resample_enqueue(gh_pf* pf, double thr) {
   const int t = pf->t;
@@ -900,6 +1025,11 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     pf->resample_calls++;
     return GH_OK;
   }
+  if (R > 1 && R <= kMaxRanks && !second && n > 0 && sys && pf->rs_grid <= pf->rs_cap) {
+    CHECK(rank_resample(pf, d, g.shift, t));
+    pf->resample_calls++;
+    return GH_OK;
+  }
   CHECK(ensure_stats(pf));
   const bool fused = !second && n > 0;
   if (second && pf->marks_pending) CHECK(materialize_marks(pf));
@@ -940,7 +1070,8 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     // kernel expands them (no search, no ancestor array round trip)
     if (second) {
       hipLaunchKernelGGL(k_sys_ancestors, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, g.gate, g.zero_w,
-                         pf->mark, pf->cmark, n, (const int32_t*)anc_target, pf->anc_scratch);
+                         pf->mark, pf->cmark, n, (const int32_t*)anc_target, pf->anc_scratch,
+                         (const DevScalars*)pf->dev, 1);
       hipLaunchKernelGGL(k_copy_anc, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
                          pf->anc_scratch, anc_target, n);
     } else {
@@ -1057,7 +1188,7 @@ extern "C" int gh_pf_get_log_weights(gh_pf* pf, double* out) {
     for (int64_t i = 0; i < pf->n; ++i) out[i] = 0.0;
     return GH_OK;
   }
-  HIP_TRY(hipMemcpy(out, pf->logw, sizeof(double) * pf->n, hipMemcpyDeviceToHost));
+  CHECK(d2h(pf, out, pf->logw, sizeof(double) * pf->n));
   return GH_OK;
 }
 
@@ -1115,7 +1246,7 @@ extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {
     CHECK(read_scalars(pf, &h, nullptr));
     if (flags_live(pf) && (h.pending | h.fire))
       return set_err(GH_E_STATE, "multi-rank: states of a pending resample are materialised by the next step");
-    HIP_TRY(hipMemcpy(out, slot_x(pf, pf->t), sizeof(double) * pf->D * pf->n, hipMemcpyDeviceToHost));
+    CHECK(d2h(pf, out, slot_x(pf, pf->t), sizeof(double) * pf->D * pf->n));
     return GH_OK;
   }
   return gh_pf_get_trajectory(pf, pf->t, out);
@@ -1127,7 +1258,7 @@ extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
   // ParticleFilterState.parents: ancestors chosen by the most recent resample
   // (identity before the first one), as global 0-based ids.
   std::vector<int32_t> res(pf->cap + 2);
-  HIP_TRY(hipMemcpy(res.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2), hipMemcpyDeviceToHost));
+  CHECK(d2h(pf, res.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2)));
   int s_last = -1;
   for (int s = pf->t + 1; s >= 2 && s < pf->cap + 2; --s)
     if (res[s]) { s_last = s; break; }
@@ -1136,12 +1267,17 @@ extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
     return GH_OK;
   }
   if (pf->ctx->world > 1) {
-    // gparent holds the most recent exchange, i.e. the resample before step s_last
-    HIP_TRY(hipMemcpy(out, pf->gparent, sizeof(int64_t) * pf->n, hipMemcpyDeviceToHost));
+    // the most recent resample (before step s_last): local ancestors plus the
+    // global ids carried by the received rows
+    hipLaunchKernelGGL(k_global_parents, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s,
+                       (const int32_t*)anc_for_step(pf, s_last), pf->n, pf->lo, (const double*)pf->rows_recv,
+                       pf->D, pf->gparent);
+    HIP_TRY(hipGetLastError());
+    CHECK(d2h(pf, out, pf->gparent, sizeof(int64_t) * pf->n));
     return GH_OK;
   }
   std::vector<int32_t> a(pf->n);
-  HIP_TRY(hipMemcpy(a.data(), anc_for_step(pf, s_last), sizeof(int32_t) * pf->n, hipMemcpyDeviceToHost));
+  CHECK(d2h(pf, a.data(), anc_for_step(pf, s_last), sizeof(int32_t) * pf->n));
   for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->lo + a[i];
   return GH_OK;
 }
@@ -1151,8 +1287,8 @@ extern "C" int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int3
   const int T = pf->t < max_steps ? pf->t : max_steps;
   std::vector<double> e(pf->cap + 2);
   std::vector<int32_t> r(pf->cap + 2);
-  HIP_TRY(hipMemcpy(e.data(), pf->ess_hist, sizeof(double) * (pf->cap + 2), hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(r.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2), hipMemcpyDeviceToHost));
+  CHECK(d2h(pf, e.data(), pf->ess_hist, sizeof(double) * (pf->cap + 2)));
+  CHECK(d2h(pf, r.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2)));
   // ess[s-1]: ESS measured by maybe_resample after step s; did[s-1]: resampled then
   for (int s = 1; s <= T; ++s) {
     if (ess) ess[s - 1] = e[s];

@@ -46,7 +46,8 @@ struct DevScalars {
   // next maybe_resample! to use (single rank); committed by k_qsum
   double cM, cL, cess;
   int cfire, cerr;
-  unsigned bar_gen;    // k_resample1 grid barriers completed
+  unsigned bar_gen;    // k_resample1 / k_rank_a grid barriers completed
+  int64_t ra, rb;      // multi-rank: local slots [0, ra) and [rb, n) take received rows
 
 };
 
@@ -57,7 +58,7 @@ struct StepArgs {
                          // written here when they come from the systematic marks)
   const uint64_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode)
   const uint64_t* carry;
-  int mark_mode;
+  int mark_mode;          // 1: systematic marks (one rank); 2: marks + received rows (multi-rank)
   int resampled;         // a maybe_resample! was enqueued since the last step
                          // (otherwise the device flags are stale and ignored)
   int buf;               // state slots < 4 GiB: address them by buffer descriptors
@@ -216,6 +217,11 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
       const uint64_t c = a.carry[tile];
       v = wave_incl_max_u64(v > c ? v : c);
       src = (int64_t)(uint32_t)v;
+      if (a.mark_mode == 2) {  // slots outside [ra, rb) take the received rows in slot order
+        const int64_t ra = a.dev->ra, rb = a.dev->rb;
+        if (j < ra) src = -1 - j;
+        else if (j >= rb) src = -1 - (ra + (j - rb));
+      }
       if (j < a.n) a.anc[j] = (int32_t)src;  // genealogy record
     }
     if (j < a.n) {
@@ -730,7 +736,7 @@ __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, G
 __global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const int* zero_w,
                                                           const uint64_t* mark, const uint64_t* carry,
                                                           int64_t n, const int32_t* anc_old,
-                                                          int32_t* anc_out) {
+                                                          int32_t* anc_out, const DevScalars* dev, int mode) {
   if (!*gate) return;
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -740,7 +746,11 @@ __global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const
   v = wave_incl_max_u64(v > c ? v : c);
   (void)lane;
   if (j >= n) return;
-  const int32_t a = (int32_t)(uint32_t)v;
+  int32_t a = (int32_t)(uint32_t)v;
+  if (mode == 2) {  // multi-rank: slots outside [ra, rb) take received rows
+    if (j < dev->ra) a = (int32_t)(-1 - j);
+    else if (j >= dev->rb) a = (int32_t)(-1 - (dev->ra + (j - dev->rb)));
+  }
   anc_out[j] = (*zero_w && anc_old) ? anc_old[a] : a;
 }
 
@@ -998,6 +1008,216 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   }
   commit();
   GH_RS_STAMP(6);
+}
+
+// ------------------------------------------------ multi-rank resample (R > 1)
+// DESIGN.md §7.  Phase A (before the all-gather of the rank totals): every
+// block takes the decision from the all-gathered (M, S, S2) triples, then
+// quantises its tile, publishes the tile total and crosses one grid barrier
+// (as k_resample1); block 0 leaves the rank total in dev->local.
+struct RankAArgs {
+  const double* logw;
+  int64_t n;
+  int shift;
+  DevScalars* dev;
+  DecideArgs d;      // stats_all = the R all-gathered triples
+  uint64_t* tsum;    // [grid] tile totals (bit 63: generation parity)
+};
+
+__global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
+  __shared__ uint64_t smu[16];
+  __shared__ int sfire;
+  __shared__ double sM;
+  __shared__ unsigned sgen;
+  if (threadIdx.x == 0) {
+    sgen = r.dev->bar_gen + 1;
+    const Decision dec = decide(r.d, false);
+    sfire = dec.fire;
+    sM = dec.M;
+    if (blockIdx.x == 0) {
+      r.dev->pending = 0;
+      commit_decision(r.d, dec, r.dev, 0);
+    }
+  }
+  __syncthreads();
+  if (!sfire) return;
+  const double M = sM;
+  const int64_t i0 = (int64_t)blockIdx.x * kRsTile + (int64_t)threadIdx.x * kRsItems;
+  uint64_t tsum = 0;
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) tsum += (i0 + k < r.n) ? quantize_weight(r.logw[i0 + k], M, r.shift) : 0;
+  const uint64_t tot = blk16_sum_u64(tsum, smu);
+  const uint64_t kTag = 1ull << 63;
+  const uint64_t par = (sgen & 1u) ? kTag : 0ull;
+  if (threadIdx.x == 0) st_sc1(&r.tsum[blockIdx.x], tot | par);
+  uint64_t all = 0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kRsBlock) {
+    uint64_t v = ld_sc1(&r.tsum[b]);
+    unsigned spins = 0;
+    while ((v & kTag) != par) {
+      __builtin_amdgcn_s_sleep(1);
+      v = ld_sc1(&r.tsum[b]);
+      if (++spins == (1u << 22)) {
+        r.dev->error = 7;
+        break;
+      }
+    }
+    all += v & ~kTag;
+  }
+  all = blk16_sum_u64(all, smu);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    r.dev->local = all;
+    r.dev->bar_gen = sgen;
+  }
+}
+
+// Phase B (after the all-gather): every block derives the global systematic
+// constants and the slot coverage of every rank from the totals (the same
+// integers on every rank), re-quantises its tile, and for each particle's
+// slot range writes a range mark where the slots are this rank's own and a
+// state row (x, global id) where they belong to another rank, packed by
+// destination rank and slot.  Slots of this rank covered by other ranks are
+// [0, ra) and [rb, n): the step kernel reads them from the received rows.
+constexpr int kMaxRanks = 64;
+struct RankBArgs {
+  const double* logw;
+  int64_t n;
+  int shift;
+  DevScalars* dev;
+  const uint64_t* tsum;   // tile totals of phase A (tagged)
+  const uint64_t* totals; // [R] all-gathered rank totals
+  int R, rank;
+  int64_t lo;             // global id of this rank's first particle
+  uint64_t seed;
+  uint32_t t;
+  MarkArgs mk;            // marks / carries in this rank's local slot space
+  const double* xprev;    // [D][ldx] states of the current step
+  int64_t ldx;
+  int D;
+  double* rows;           // send rows [(D+1)] per slot
+  int64_t rows_cap;
+};
+
+__global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
+  if (!r.dev->fire) return;
+  __shared__ uint64_t smu[16];
+  __shared__ DevScalars sd;
+  __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
+  __shared__ int64_t sown_lo, sown_hi, sra, srb;
+  __shared__ uint64_t sbase;
+  __shared__ int32_t se[kRsTile];
+  __shared__ int64_t sfirst;
+  const int R = r.R, q = r.rank;
+  const uint64_t N = (uint64_t)r.mk.n_global;
+  // tile offset within the rank
+  uint64_t before = 0;
+  for (int b = threadIdx.x; b < (int)blockIdx.x; b += kRsBlock) before += r.tsum[b] & ~(1ull << 63);
+  before = blk16_sum_u64(before, smu);
+  if (threadIdx.x == 0) {
+    uint64_t S = 0, base = 0;
+    for (int k = 0; k < R; ++k) {
+      if (k < q) base += r.totals[k];
+      S += r.totals[k];
+    }
+    sd.S = S;
+    sd.base = base;
+    sd.local = r.totals[q];
+    const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
+    sd.o = scale_u53(u53_bits(w.x, w.y), S);
+    sd.invN = 1.0 / (double)N;
+    sd.Qs = udiv_n(S, N, sd.invN);
+    sd.Rs = S - sd.Qs * N;
+    sd.invS = 1.0 / (double)S;
+    const int64_t cov_lo = sys_count_exact(&sd, N, base);
+    const int64_t cov_hi = sys_count_exact(&sd, N, base + sd.local);
+    const int64_t own_lo = r.lo, own_hi = r.lo + r.n;
+    // rows this rank sends: destination blocks in rank order (lower ranks,
+    // then higher ranks), each the part of [cov_lo, cov_hi) it owns
+    int64_t soff = 0;
+    for (int k = 0; k < R; ++k) {
+      const int64_t dlo = (int64_t)(((__int128)N * k) / R), dhi = (int64_t)(((__int128)N * (k + 1)) / R);
+      const int64_t a = cov_lo > dlo ? cov_lo : dlo, b = cov_hi < dhi ? cov_hi : dhi;
+      sdst_lo[k] = dlo;
+      sseg_lo[k] = a;
+      ssoff[k] = soff;
+      if (k != q && b > a) soff += b - a;
+    }
+    sown_lo = own_lo;
+    sown_hi = own_hi;
+    const int64_t ca = cov_lo < own_lo ? own_lo : (cov_lo > own_hi ? own_hi : cov_lo);
+    const int64_t cb = cov_hi < own_lo ? own_lo : (cov_hi > own_hi ? own_hi : cov_hi);
+    sra = ca - own_lo;
+    srb = cb - own_lo;
+    sbase = base + before;
+    if (blockIdx.x == 0) {
+      r.dev->S = S;
+      r.dev->base = base;
+      r.dev->o = sd.o;
+      r.dev->Qs = sd.Qs;
+      r.dev->Rs = sd.Rs;
+      r.dev->invN = sd.invN;
+      r.dev->invS = sd.invS;
+      r.dev->ra = sra;
+      r.dev->rb = srb;
+    }
+  }
+  __syncthreads();
+  const double M = r.dev->M;
+  const int64_t i0 = (int64_t)blockIdx.x * kRsTile + (int64_t)threadIdx.x * kRsItems;
+  uint64_t qv[kRsItems];
+  uint64_t tsum = 0;
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    qv[k] = (i0 + k < r.n) ? quantize_weight(r.logw[i0 + k], M, r.shift) : 0;
+    tsum += qv[k];
+  }
+  const uint64_t incl = blk16_incl_u64(tsum, smu);
+  uint64_t run = sbase + incl - tsum;
+  const int64_t own_lo = sown_lo, own_hi = sown_hi;
+  auto clamp_own = [&](int64_t s) { return s < own_lo ? own_lo : (s > own_hi ? own_hi : s); };
+  int64_t s0 = sys_count(&sd, N, run);
+  if (threadIdx.x == 0) sfirst = clamp_own(s0) - own_lo;
+#pragma unroll
+  for (int k = 0; k < kRsItems; ++k) {
+    run += qv[k];
+    const int64_t i = i0 + k;
+    const int64_t s1 = (i < r.n && qv[k]) ? sys_count(&sd, N, run) : s0;
+    const int64_t l0 = clamp_own(s0), l1 = clamp_own(s1);
+    se[threadIdx.x * kRsItems + k] = (int32_t)(l1 - own_lo);
+    if (l1 > l0) r.mk.mark[l0 - own_lo] = (r.mk.epoch << 32) | (uint64_t)i;
+    // slots of other ranks: state rows, by destination then slot
+    for (int64_t sl = s0; sl < s1; ++sl) {
+      if (sl >= own_lo && sl < own_hi) {
+        sl = own_hi - 1;  // skip the own block
+        continue;
+      }
+      int dst = (int)(((__int128)sl * R) / (int64_t)N);  // owner of global slot sl
+      while (dst + 1 < R && sdst_lo[dst + 1] <= sl) ++dst;
+      while (dst > 0 && sdst_lo[dst] > sl) --dst;
+      const int64_t row = ssoff[dst] + (sl - sseg_lo[dst]);
+      if (row < r.rows_cap) {
+        double* rw = r.rows + row * (r.D + 1);
+        for (int c = 0; c < r.D; ++c) rw[c] = r.xprev[c * r.ldx + i];
+        rw[r.D] = __longlong_as_double(r.lo + i);
+      }
+    }
+    s0 = s1;
+  }
+  __syncthreads();
+  // carries of the 64-slot groups (local slot space) starting in this tile's
+  // own-slot span
+  const int64_t s_lo = sfirst, s_hi = se[kRsTile - 1];
+  const int64_t pbase = (int64_t)blockIdx.x * kRsTile;
+  for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
+    const int32_t slot = (int32_t)(g * 64);
+    int lo = 0, hi = kRsTile - 1;  // first particle p with se[p] > slot
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (se[mid] > slot) hi = mid;
+      else lo = mid + 1;
+    }
+    r.mk.cmark[g] = (r.mk.epoch << 32) | (uint64_t)(pbase + lo);
+  }
 }
 
 enum SearchMode { SEARCH_SYSTEMATIC = 0, SEARCH_MULTINOMIAL = 1, SEARCH_SAMPLE = 2 };

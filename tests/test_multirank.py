@@ -227,15 +227,18 @@ def test_gloo_sharded_oracle_with_product_plan(tmp_path, R):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,R,thr", [("lg4", 2, 3001.0), ("lg4", 3, 0.0), ("kit", 2, 0.0), ("lg10", 2, 3001.0)])
-def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr):
+@pytest.mark.parametrize("model,R,thr,n", [("lg4", 2, 3001.0, 3001), ("lg4", 3, 0.0, 3001), ("kit", 2, 0.0, 3001),
+                                            ("lg10", 2, 3001.0, 3001), ("lg4", 2, 1e9, 20011), ("kit", 4, 1e9, 4003)])
+def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr, n):
     """R ranks share GPU 0 through the gloo host transport; the gathered shards
-    equal the single-rank oracle bit for bit (log-ML within 1e-9)."""
+    equal the single-rank oracle bit for bit (log-ML within 1e-9).  n = 20011
+    spans several 4096-particle tiles per rank; R = 4 with the peaked
+    Kitagawa weights moves rows across several ranks."""
     from oracle import oracle as O
     from tests.mr_worker import build_model
 
     out = str(tmp_path / "g")
-    n, T, seed = 3001, 8, 9
+    T, seed = 8, 9
     _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
                   "--thr", str(thr), "--seed", str(seed), "--out", out], R, timeout=400)
     m = build_model(model)
