@@ -19,6 +19,7 @@
 
 #include "../../include/gen_hip.h"
 #include "gh_kernels.h"
+#include "gh_pmmh.h"
 
 using namespace gh;
 
@@ -1538,6 +1539,100 @@ extern "C" int gh_debug_rs_stamps(uint64_t* out, int n) {
   return GH_OK;
 }
 #endif
+
+// ------------------------------------------------------------------ PMMH
+extern "C" int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T,
+                           int n_iters, int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml,
+                           int32_t* accepts, double* hist, double* kernel_ms) {
+  if (!ctx || !ys || !lvx || !lvy || !lml || !accepts || T < 1 || n_iters < 0 || n_chains < 0 || chain0 < 0)
+    return set_err(GH_E_INVAL, "gh_pmmh_run: bad argument");
+  if (n_inner < 64 || n_inner > kPmmhMaxInner || n_inner % 64)
+    return set_err(GH_E_INVAL, "gh_pmmh_run: n_inner must be a multiple of 64 in 64..%d", kPmmhMaxInner);
+  if (chain0 + n_chains > (1LL << 22))
+    return set_err(GH_E_INVAL, "gh_pmmh_run: chain ids must stay below 2^22");
+  if (iter0 < 0 || ((int64_t)iter0 + n_iters) * 4 + 1 >= (1LL << 32))
+    return set_err(GH_E_INVAL, "gh_pmmh_run: too many iterations");
+  if (n_chains == 0) return GH_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  std::vector<double> ct(T);
+  for (int t = 1; t <= T; ++t) ct[t - 1] = 8.0 * gh_cos(1.2 * (double)t);
+  const size_t nc = (size_t)n_chains;
+  double *d_ys = nullptr, *d_ct = nullptr, *d_vx = nullptr, *d_vy = nullptr, *d_ml = nullptr, *d_hist = nullptr;
+  int32_t* d_acc = nullptr;
+  auto cleanup = [&]() {
+    hipFree(d_ys); hipFree(d_ct); hipFree(d_vx); hipFree(d_vy); hipFree(d_ml); hipFree(d_acc); hipFree(d_hist);
+  };
+#define PM_ALLOC(p, bytes) \
+  if (hipMalloc(&(p), (bytes)) != hipSuccess) { cleanup(); return set_err(GH_E_NOMEM, "gh_pmmh_run: %s", #p); }
+  PM_ALLOC(d_ys, sizeof(double) * T);
+  PM_ALLOC(d_ct, sizeof(double) * T);
+  PM_ALLOC(d_vx, sizeof(double) * nc);
+  PM_ALLOC(d_vy, sizeof(double) * nc);
+  PM_ALLOC(d_ml, sizeof(double) * nc);
+  PM_ALLOC(d_acc, sizeof(int32_t) * 4 * nc);
+  if (hist) PM_ALLOC(d_hist, sizeof(double) * 2 * nc * (size_t)(n_iters > 0 ? n_iters : 1));
+#undef PM_ALLOC
+  int rc = GH_OK;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  do {
+    if (hipMemcpyAsync(d_ys, ys, sizeof(double) * T, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_ct, ct.data(), sizeof(double) * T, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_pmmh_run: upload");
+      break;
+    }
+    if (!init &&
+        (hipMemcpyAsync(d_vx, lvx, sizeof(double) * nc, hipMemcpyHostToDevice, s) != hipSuccess ||
+         hipMemcpyAsync(d_vy, lvy, sizeof(double) * nc, hipMemcpyHostToDevice, s) != hipSuccess ||
+         hipMemcpyAsync(d_ml, lml, sizeof(double) * nc, hipMemcpyHostToDevice, s) != hipSuccess)) {
+      rc = set_err(GH_E_HIP, "gh_pmmh_run: upload state");
+      break;
+    }
+    PmmhArgs a{};
+    a.ys = d_ys;
+    a.ct = d_ct;
+    a.T = T;
+    a.n_iters = n_iters;
+    a.iter0 = iter0;
+    a.seed = seed;
+    a.chain0 = chain0;
+    a.n_chains = n_chains;
+    a.lvx = d_vx;
+    a.lvy = d_vy;
+    a.lml = d_ml;
+    a.accepts = d_acc;
+    a.hist = d_hist;
+    a.init = init ? 1 : 0;
+    if (kernel_ms) {
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+    }
+    hipExtLaunchKernelGGL(k_pmmh, dim3((unsigned)n_chains), dim3((unsigned)n_inner), 0, s, e0, e1, 0, a);
+    if (hipGetLastError() != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_pmmh_run: launch");
+      break;
+    }
+    if (hipMemcpyAsync(lvx, d_vx, sizeof(double) * nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(lvy, d_vy, sizeof(double) * nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(lml, d_ml, sizeof(double) * nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(accepts, d_acc, sizeof(int32_t) * 4 * nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (hist && hipMemcpyAsync(hist, d_hist, sizeof(double) * 2 * nc * n_iters, hipMemcpyDeviceToHost, s) !=
+                     hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_pmmh_run: download");
+      break;
+    }
+    if (kernel_ms) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, e0, e1);
+      *kernel_ms = ms;
+    }
+  } while (0);
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  cleanup();
+  return rc;
+}
 
 // ------------------------------------------------------------ self tests
 extern "C" int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double* oe, double* ol,

@@ -16,6 +16,8 @@
  *   gh_pf_get_parents       ParticleFilterState.parents  src/inference/particle_filter.jl:23
  *   gh_pf_sample_unweighted sample_unweighted_traces     src/inference/particle_filter.jl:62-70
  *   gh_is_run               importance_sampling          src/inference/importance.jl:20-52
+ *   gh_pmmh_run             PMMH (mh over a PF-estimated  examples/pmmh/example.jl:20-79,
+ *                           likelihood)                   examples/pmmh/pf.jl:14-73
  *   gh_model_create         a Static-DSL model + Unfold  src/static_ir/, src/modeling_library/unfold/
  *
  * Conventions
@@ -175,6 +177,20 @@ int gh_sys_plan(int64_t n_global, int world, int rank, const uint64_t* totals, u
 int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t seed,
               double* host_log_norm_weights /* may be NULL */, double* host_states /* may be NULL */,
               double* lml);
+
+/* ---- particle-marginal MH (config C5) ------------------------------------------
+   examples/pmmh/example.jl:20-79: log var_x, log var_y ~ normal(0, 2); the
+   likelihood is the log-ML estimate of an inner particle filter with n_inner
+   particles on the Kitagawa model (examples/pmmh/pf.jl:14-73); each
+   iteration applies mh(select(:var_x)), mh(select(:var_y)) and the two
+   random-walk moves (sd sqrt(0.5)) (src/inference/mh.jl:14-62).  One
+   workgroup per chain, chains [chain0, chain0 + n_chains) (a rank's share).
+   init = 1 draws the start from the prior (generate); otherwise lvx / lvy /
+   lml hold the state to continue from, after iter0 iterations.  Host buffers; hist (nullable) gets
+   [n_chains][n_iters][2]; accepts [n_chains][4] counts per move. */
+int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T,
+                int n_iters, int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml, int32_t* accepts,
+                double* hist, double* kernel_ms);
 
 /* ---- diagnostics ------------------------------------------------------------ */
 const char* gh_last_error(void);

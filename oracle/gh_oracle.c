@@ -699,3 +699,127 @@ int orc_importance_sampling(int family, int d, int dy, int k, int v, const doubl
   model_free(&m);
   return 0;
 }
+
+/* ----------------------------------------------------------------- PMMH */
+/* Particle-marginal MH over the Kitagawa model (examples/pmmh/example.jl:
+   20-79 with the ParticleFilterCombinator of examples/pmmh/pf.jl:14-73 and
+   mh.jl:14-62).  Random-number layout and move order: gen_amd/csrc/gh_pmmh.h
+   (DESIGN.md §9). */
+static double pmmh_filter(uint64_t seed, uint64_t c, uint32_t u, double lvx, double lvy, int N,
+                          const double* ys, const double* ct, int T, double* x, double* lw, double* xp,
+                          uint64_t* C) {
+  double var_x = orc_exp(lvx), var_y = orc_exp(lvy);
+  double sx = sqrt(var_x), inv2vy = 1.0 / (2.0 * var_y);
+  double csty = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * var_y);
+  uint64_t cid = ((uint64_t)u << 32) | (c << 10);
+  double logN = orc_log((double)N);
+  int shift = qshift((uint64_t)N);
+  double z[2];
+  for (int p = 0; p < N; ++p) {
+    orc_normals(seed, cid | (uint64_t)p, 1, S_INIT, 1, z);
+    x[p] = 0.0 + 5.0 * z[0];
+    double diff = ys[0] - x[p] * x[p] / 20.0;
+    lw[p] = -(diff * diff) * inv2vy + csty;
+  }
+  double log_ml = 0.0;
+  for (int t = 2; t <= T; ++t) {
+    double M = -INFINITY, S = 0.0, S2 = 0.0;
+    for (int p = 0; p < N; ++p) M = fmax(M, lw[p]);
+    for (int p = 0; p < N; ++p) {
+      double e = lw[p] > -INFINITY ? orc_exp(lw[p] - M) : 0.0;
+      S += e;
+      S2 += e * e;
+    }
+    int fire = (S * S) / S2 < (double)N / 2.0;
+    if (fire) {
+      log_ml += (M + orc_log(S)) - logN;
+      uint64_t acc = 0;
+      for (int p = 0; p < N; ++p) { acc += quantize(lw[p], M, shift); C[p] = acc; }
+      uint32_t w[4];
+      rng(seed, cid, (uint32_t)(t - 1), S_RESAMPLE, 0, w);
+      uint64_t o = scale_u53(bits53(w[0], w[1]), acc);
+      uint64_t Qs = acc / (uint64_t)N, Rs = acc % (uint64_t)N;
+      for (int j = 0; j < N; ++j) {
+        uint64_t target = (uint64_t)j * Qs + ((uint64_t)j * Rs + o) / (uint64_t)N;
+        int a = 0;
+        while (C[a] <= target) ++a;
+        xp[j] = x[a];
+      }
+    } else {
+      for (int p = 0; p < N; ++p) xp[p] = x[p];
+    }
+    for (int p = 0; p < N; ++p) {
+      orc_normals(seed, cid | (uint64_t)p, (uint32_t)t, S_STEP, 1, z);
+      double v = xp[p];
+      double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + ct[t - 1];
+      x[p] = mean + sx * z[0];
+      double diff = ys[t - 1] - x[p] * x[p] / 20.0;
+      lw[p] = (fire ? 0.0 : lw[p]) + (-(diff * diff) * inv2vy + csty);
+    }
+  }
+  double M = -INFINITY, S = 0.0;
+  for (int p = 0; p < N; ++p) M = fmax(M, lw[p]);
+  for (int p = 0; p < N; ++p) S += lw[p] > -INFINITY ? orc_exp(lw[p] - M) : 0.0;
+  return log_ml + (M + orc_log(S)) - logN;
+}
+
+int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T, int n_iters,
+                 int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml, int32_t* accepts,
+                 double* hist) {
+  if (n_inner < 1 || n_inner > 1024 || T < 1) return 1;
+  double* x = malloc(sizeof(double) * n_inner);
+  double* lw = malloc(sizeof(double) * n_inner);
+  double* xp = malloc(sizeof(double) * n_inner);
+  uint64_t* C = malloc(sizeof(uint64_t) * n_inner);
+  double* ct = malloc(sizeof(double) * T);
+  for (int t = 1; t <= T; ++t) ct[t - 1] = 8.0 * orc_cos(1.2 * (double)t);
+  const double sd_rw = 0x1.6a09e667f3bcdp-1;
+  for (int64_t cl = 0; cl < n_chains; ++cl) {
+    uint64_t c = (uint64_t)(chain0 + cl);
+    double vx, vy, ml;
+    if (init) {
+      double z[2];
+      orc_normals(seed, c << 10, 0, S_MH, 2, z);
+      vx = 0.0 + 2.0 * z[0];
+      vy = 0.0 + 2.0 * z[1];
+      ml = pmmh_filter(seed, c, 0, vx, vy, n_inner, ys, ct, T, x, lw, xp, C);
+    } else {
+      vx = lvx[cl]; vy = lvy[cl]; ml = lml[cl];
+    }
+    int acc[4] = {0, 0, 0, 0};
+    for (int k = 0; k < n_iters; ++k) {
+      for (int m = 0; m < 4; ++m) {
+        uint32_t u = 1u + 4u * (uint32_t)(iter0 + k) + (uint32_t)m;
+        uint64_t cid = ((uint64_t)u << 32) | (c << 10);
+        double z[2];
+        orc_normals(seed, cid, 0, S_MH, 2, z);
+        uint32_t wa[4];
+        rng(seed, cid, 0, S_MH, 1, wa);
+        double logu = orc_log(unif53(wa[0], wa[1]));
+        int on_x = (m & 1) == 0;
+        double cur = on_x ? vx : vy, prop, alpha, ml_new;
+        if (m < 2) {
+          prop = 0.0 + 2.0 * z[0];
+          ml_new = pmmh_filter(seed, c, u, on_x ? prop : vx, on_x ? vy : prop, n_inner, ys, ct, T, x, lw, xp, C);
+          alpha = ml_new - ml;
+        } else {
+          prop = cur + sd_rw * z[0];
+          ml_new = pmmh_filter(seed, c, u, on_x ? prop : vx, on_x ? vy : prop, n_inner, ys, ct, T, x, lw, xp, C);
+          double weight = (orc_normal_logpdf(prop, 0.0, 2.0) - orc_normal_logpdf(cur, 0.0, 2.0)) + (ml_new - ml);
+          double fwd = orc_normal_logpdf(prop, cur, sd_rw), bwd = orc_normal_logpdf(cur, prop, sd_rw);
+          alpha = (weight - fwd) + bwd;
+        }
+        if (logu < alpha) {
+          if (on_x) vx = prop; else vy = prop;
+          ml = ml_new;
+          acc[m] += 1;
+        }
+      }
+      if (hist) { hist[(cl * n_iters + k) * 2] = vx; hist[(cl * n_iters + k) * 2 + 1] = vy; }
+    }
+    lvx[cl] = vx; lvy[cl] = vy; lml[cl] = ml;
+    for (int m = 0; m < 4; ++m) accepts[cl * 4 + m] = acc[m];
+  }
+  free(x); free(lw); free(xp); free(C); free(ct);
+  return 0;
+}

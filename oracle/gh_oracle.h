@@ -87,6 +87,12 @@ int orc_importance_sampling(int family, int d, int dy, int k, int v, const doubl
                             int64_t n, uint64_t seed, double* log_norm_weights, double* states,
                             double* lml);
 
+/* particle-marginal MH (config C5): chains [chain0, chain0 + n_chains) of the
+   Kitagawa PMMH of examples/pmmh/example.jl; see gen_amd/csrc/gh_pmmh.h */
+int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T, int n_iters,
+                 int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml, int32_t* accepts,
+                 double* hist);
+
 /* static weight helpers used by the golden-vector tests */
 double orc_normal_logpdf(double x, double mu, double std);
 

@@ -62,6 +62,7 @@ def lib():
             "orc_pf_resample_apply": (None, [V, c_double, I64, POINTER(c_int64), POINTER(c_int64), D]),
             "orc_importance_sampling": (I, [I, I, I, I, I, D, I64, D, I, I, I64, U64, D, D, D]),
             "orc_normal_logpdf": (c_double, [c_double, c_double, c_double]),
+            "orc_pmmh_run": (I, [I64, I64, I, D, I, I, I, U64, I, D, D, D, POINTER(ctypes.c_int32), D]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -235,3 +236,21 @@ def run_pf(model, ys, n, seed, thr=None, resampler=SYSTEMATIC, proposal=DEFAULT,
         pf.maybe_resample(thr)
         pf.step(y, proposal)
     return pf
+
+
+def pmmh_run(ys, n_chains, n_inner, n_iters, seed, chain0=0, iter0=0, state=None, history=False):
+    """CPU PMMH (orc_pmmh_run): returns (lvx, lvy, lml, accepts[n,4], hist)."""
+    ys = np.ascontiguousarray(np.asarray(ys, dtype=np.float64))
+    if state is None:
+        lvx, lvy, lml = np.zeros(n_chains), np.zeros(n_chains), np.zeros(n_chains)
+        init = 1
+    else:
+        lvx, lvy, lml = (np.array(a, dtype=np.float64) for a in state)
+        init = 0
+    acc = np.zeros((n_chains, 4), dtype=np.int32)
+    hist = np.zeros((n_chains, max(n_iters, 1), 2)) if history else None
+    rc = lib().orc_pmmh_run(chain0, n_chains, n_inner, _d(ys), ys.size, n_iters, iter0, seed, init, _d(lvx),
+                            _d(lvy), _d(lml), acc.ctypes.data_as(POINTER(ctypes.c_int32)), _d(hist))
+    if rc:
+        raise ValueError("oracle PMMH failed")
+    return lvx, lvy, lml, acc, hist
