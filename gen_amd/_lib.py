@@ -96,6 +96,8 @@ SIGNATURES = {
     "gh_pmmh_run": (c_int, [c_void_p, c_int64, c_int64, c_int, POINTER(c_double), c_int, c_int, c_int, c_uint64, c_int,
                             POINTER(c_double), POINTER(c_double), POINTER(c_double), POINTER(c_int32),
                             POINTER(c_double), POINTER(c_double)]),
+    "gh_coal_run": (c_int, [c_void_p, c_int64, c_int64, POINTER(c_double), c_int, c_int, c_int, c_uint64, c_int,
+                            POINTER(c_double), POINTER(c_int32), POINTER(c_int32), POINTER(c_double)]),
     "gh_is_run": (c_int, [c_void_p, POINTER(Obs), c_int, c_int64, c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
     "gh_last_error": (c_char_p, []),
     "gh_version": (c_char_p, []),

@@ -20,6 +20,7 @@
 #include "../../include/gen_hip.h"
 #include "gh_kernels.h"
 #include "gh_pmmh.h"
+#include "gh_coal.h"
 
 using namespace gh;
 
@@ -1620,6 +1621,81 @@ extern "C" int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_
                      hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess) {
       rc = set_err(GH_E_HIP, "gh_pmmh_run: download");
+      break;
+    }
+    if (kernel_ms) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, e0, e1);
+      *kernel_ms = ms;
+    }
+  } while (0);
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  cleanup();
+  return rc;
+}
+
+// ------------------------------------------------------------------ coal
+extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const double* events, int E, int n_iters,
+                           int iter0, uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist,
+                           double* kernel_ms) {
+  if (!ctx || !events || !state || !accepts || E < 1 || E > kCoalMaxEvents || n_iters < 0 || iter0 < 0 ||
+      n_chains < 0 || chain0 < 0)
+    return set_err(GH_E_INVAL, "gh_coal_run: bad argument (events 1..%d)", kCoalMaxEvents);
+  for (int i = 1; i < E; ++i)
+    if (!(events[i] >= events[i - 1])) return set_err(GH_E_INVAL, "gh_coal_run: events must be sorted");
+  if (!(events[E - 1] > 0.0)) return set_err(GH_E_INVAL, "gh_coal_run: the window [0, T] is empty");
+  if (n_chains == 0) return GH_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = ctx->stream;
+  const size_t nc = (size_t)n_chains;
+  double *d_ev = nullptr, *d_st = nullptr;
+  int32_t *d_acc = nullptr, *d_kh = nullptr;
+  auto cleanup = [&]() { hipFree(d_ev); hipFree(d_st); hipFree(d_acc); hipFree(d_kh); };
+  if (hipMalloc(&d_ev, sizeof(double) * E) != hipSuccess || hipMalloc(&d_st, sizeof(double) * 2 * kCoalW * nc) != hipSuccess ||
+      hipMalloc(&d_acc, sizeof(int32_t) * 3 * nc) != hipSuccess ||
+      (khist && n_iters > 0 && hipMalloc(&d_kh, sizeof(int32_t) * nc * n_iters) != hipSuccess)) {
+    cleanup();
+    return set_err(GH_E_NOMEM, "gh_coal_run: device buffers");
+  }
+  int rc = GH_OK;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  do {
+    if (hipMemcpyAsync(d_ev, events, sizeof(double) * E, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(d_st, 0, sizeof(double) * 2 * kCoalW * nc, s) != hipSuccess ||
+        (!init && hipMemcpy2DAsync(d_st, sizeof(double) * 2 * kCoalW, state, sizeof(double) * kCoalW,
+                                   sizeof(double) * kCoalW, nc, hipMemcpyHostToDevice, s) != hipSuccess)) {
+      rc = set_err(GH_E_HIP, "gh_coal_run: upload");
+      break;
+    }
+    CoalArgs a{};
+    a.events = d_ev;
+    a.E = E;
+    a.T = events[E - 1];
+    a.chain0 = chain0;
+    a.n_chains = n_chains;
+    a.seed = seed;
+    a.n_iters = n_iters;
+    a.iter0 = iter0;
+    a.init = init ? 1 : 0;
+    a.state = d_st;
+    a.accepts = d_acc;
+    a.khist = d_kh;
+    if (kernel_ms) {
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+    }
+    hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, e0, e1, 0, a);
+    if (hipGetLastError() != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_coal_run: launch");
+      break;
+    }
+    if (hipMemcpy2DAsync(state, sizeof(double) * kCoalW, d_st, sizeof(double) * 2 * kCoalW, sizeof(double) * kCoalW,
+                         nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(accepts, d_acc, sizeof(int32_t) * 3 * nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (d_kh && hipMemcpyAsync(khist, d_kh, sizeof(int32_t) * nc * n_iters, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_coal_run: download");
       break;
     }
     if (kernel_ms) {

@@ -18,6 +18,8 @@
  *   gh_is_run               importance_sampling          src/inference/importance.jl:20-52
  *   gh_pmmh_run             PMMH (mh over a PF-estimated  examples/pmmh/example.jl:20-79,
  *                           likelihood)                   examples/pmmh/pf.jl:14-73
+ *   gh_coal_run             involutive (RJ) MH chains     examples/coal/coal.jl:126-336,
+ *                                                         src/inference/mh.jl:85-98
  *   gh_model_create         a Static-DSL model + Unfold  src/static_ir/, src/modeling_library/unfold/
  *
  * Conventions
@@ -191,6 +193,18 @@ int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t 
 int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T,
                 int n_iters, int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml, int32_t* accepts,
                 double* hist, double* kernel_ms);
+
+/* ---- reversible-jump MH on the coal change-point model (config C3) ---------------
+   examples/coal/coal.jl:47-62 model, mcmc_step (:329-336) = rate_move,
+   position_move (k > 0), birth_death_move, each an involutive MH step
+   (src/inference/mh.jl:85-98, trace_translators.jl:848-876).  One thread per
+   chain; events sorted, T = events[E-1].  state: host [n_chains][68] rows
+   (k, score, cp[32], h[33], pad), written on return and read when init == 0
+   (continuing after iter0 iterations).  accepts [n_chains][3]; khist
+   (nullable) [n_chains][n_iters] = k after each iteration. */
+int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const double* events, int E, int n_iters,
+                int iter0, uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist,
+                double* kernel_ms);
 
 /* ---- diagnostics ------------------------------------------------------------ */
 const char* gh_last_error(void);

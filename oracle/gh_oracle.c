@@ -823,3 +823,204 @@ int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys
   free(x); free(lw); free(xp); free(C); free(ct);
   return 0;
 }
+
+/* ------------------------------------------------------------------ coal */
+/* Reversible-jump MH on the coal change-point model (config C3): a plain
+   restatement of gen_amd/csrc/gh_coal.h (which cites examples/coal/coal.jl
+   and poisson_process.jl line by line); spec DESIGN.md §7c. */
+#define COAL_KMAX 32
+#define COAL_W 68
+#define COAL_THETA (1.0 / 200.0)
+
+static double coal_u(uint64_t seed, uint64_t c, uint32_t step, uint32_t d) {
+  uint32_t w[4];
+  rng(seed, c, step, S_MH, d, w);
+  return unif53(w[0], w[1]);
+}
+
+static int coal_upper(const double* ev, int E, double x) {
+  int lo = 0, hi = E;
+  while (lo < hi) { int mid = (lo + hi) >> 1; if (ev[mid] <= x) lo = mid + 1; else hi = mid; }
+  return lo;
+}
+
+static double coal_score(const double* s, const double* ev, int E, double T) {
+  int k = (int)s[0];
+  const double* cp = s + 2;
+  const double* h = s + 2 + COAL_KMAX;
+  double lf = 0.0;
+  for (int j = 2; j <= k; ++j) lf += orc_log((double)j);
+  double lp = ((double)k * orc_log(3.0) - 3.0) - lf;
+  double lower = 0.0, l_lower = orc_log(T);
+  for (int i = 1; i <= k; ++i) {
+    double x = cp[i - 1];
+    if (!(x > lower && x < T)) return -INFINITY;
+    double m = (double)(k - i + 1);
+    double l_x = orc_log(T - x);
+    lp += ((m - 1.0) * l_x + orc_log(m)) - m * l_lower;
+    lower = x;
+    l_lower = l_x;
+  }
+  double l_theta = orc_log(COAL_THETA);
+  for (int i = 1; i <= k + 1; ++i) {
+    double x = h[i - 1];
+    if (!(x > 0.0)) return -INFINITY;
+    lp += -l_theta - x / COAL_THETA;
+  }
+  double A = 0.0, B = 0.0, b_lo = 0.0;
+  int c_lo = 0;
+  for (int i = 1; i <= k + 1; ++i) {
+    double b_hi = i <= k ? cp[i - 1] : T;
+    int c_hi = coal_upper(ev, E, b_hi);
+    A += (double)(c_hi - c_lo) * orc_log(h[i - 1]);
+    B += (b_hi - b_lo) * h[i - 1];
+    b_lo = b_hi;
+    c_lo = c_hi;
+  }
+  return lp + (A - B);
+}
+
+static void coal_copy(const double* src, double* dst) {
+  int k = (int)src[0];
+  dst[0] = src[0];
+  for (int i = 0; i < k; ++i) dst[2 + i] = src[2 + i];
+  for (int i = 0; i <= k; ++i) dst[2 + COAL_KMAX + i] = src[2 + COAL_KMAX + i];
+}
+
+static void coal_init(uint64_t seed, uint64_t c, double T, int E, double* s) {
+  for (int att = 0; att < 64; ++att) {
+    uint32_t d0 = 100u * (uint32_t)att;
+    double u = coal_u(seed, c, 0, d0);
+    double p = orc_exp(-3.0), cum = p;
+    int k = 0;
+    while (u >= cum && k < 200) { ++k; p = p * (3.0 / (double)k); cum += p; }
+    if (k > COAL_KMAX) continue;
+    int ok = 1;
+    double lower = 0.0;
+    for (int i = 1; i <= k; ++i) {
+      double q = coal_u(seed, c, 0, d0 + 1u + (uint32_t)i);
+      double m = (double)(k - i + 1);
+      double x = T - (T - lower) * orc_exp(orc_log(1.0 - q) / m);
+      if (!(x > lower && x < T)) ok = 0;
+      s[2 + i - 1] = x;
+      lower = x;
+    }
+    for (int i = 1; i <= k + 1; ++i) {
+      double q = coal_u(seed, c, 0, d0 + 40u + (uint32_t)i);
+      double x = -COAL_THETA * orc_log(1.0 - q);
+      if (!(x > 0.0)) ok = 0;
+      s[2 + COAL_KMAX + i - 1] = x;
+    }
+    if (!ok) continue;
+    s[0] = (double)k;
+    return;
+  }
+  s[0] = 0.0;
+  s[2 + COAL_KMAX] = (double)E / T;
+}
+
+int orc_coal_run(int64_t chain0, int64_t n_chains, const double* ev, int E, int n_iters, int iter0,
+                 uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist) {
+  if (E < 1) return 1;
+  double T = ev[E - 1];
+  double prop[COAL_W];
+  for (int64_t cl = 0; cl < n_chains; ++cl) {
+    uint64_t c = (uint64_t)(chain0 + cl);
+    double* cur = state + cl * COAL_W;
+    if (init) {
+      memset(cur, 0, sizeof(double) * COAL_W);
+      coal_init(seed, c, T, E, cur);
+      cur[1] = coal_score(cur, ev, E, T);
+    }
+    int acc[3] = {0, 0, 0};
+    for (int it = 0; it < n_iters; ++it) {
+      uint32_t step = (uint32_t)(iter0 + it + 1);
+      { /* rate move */
+        int k = (int)cur[0];
+        int i = (int)(coal_u(seed, c, step, 0) * (double)(k + 1)) + 1;
+        double h = cur[2 + COAL_KMAX + i - 1];
+        double lo = h / 2.0, hi = h * 2.0;
+        double nh = lo + (hi - lo) * coal_u(seed, c, step, 1);
+        coal_copy(cur, prop);
+        prop[2 + COAL_KMAX + i - 1] = nh;
+        double sn = coal_score(prop, ev, E, T);
+        double fwd = -orc_log((double)(k + 1)) - orc_log(hi - lo);
+        double bwd = -orc_log((double)(k + 1)) - orc_log(nh * 2.0 - nh / 2.0);
+        double alpha = ((sn - cur[1]) + bwd) - fwd;
+        if (orc_log(coal_u(seed, c, step, 2)) < alpha) { cur[2 + COAL_KMAX + i - 1] = nh; cur[1] = sn; acc[0]++; }
+      }
+      if ((int)cur[0] > 0) { /* position move */
+        int k = (int)cur[0];
+        int i = (int)(coal_u(seed, c, step, 3) * (double)k) + 1;
+        double lower = i == 1 ? 0.0 : cur[2 + i - 2];
+        double upper = i == k ? T : cur[2 + i];
+        double ncp = lower + (upper - lower) * coal_u(seed, c, step, 4);
+        coal_copy(cur, prop);
+        prop[2 + i - 1] = ncp;
+        double sn = coal_score(prop, ev, E, T);
+        double fwd = -orc_log((double)k) - orc_log(upper - lower), bwd = fwd;
+        double alpha = ((sn - cur[1]) + bwd) - fwd;
+        if (orc_log(coal_u(seed, c, step, 5)) < alpha) { cur[2 + i - 1] = ncp; cur[1] = sn; acc[1]++; }
+      }
+      { /* birth / death move */
+        int k = (int)cur[0];
+        int birth = k == 0 || coal_u(seed, c, step, 6) < 0.5;
+        double alpha = -INFINITY, sn = -INFINITY;
+        if (birth) {
+          int i = (int)(coal_u(seed, c, step, 7) * (double)(k + 1)) + 1;
+          double lower = i == 1 ? 0.0 : cur[2 + i - 2];
+          double upper = i == k + 1 ? T : cur[2 + i - 1];
+          double ncp = lower + (upper - lower) * coal_u(seed, c, step, 8);
+          double uu = coal_u(seed, c, step, 9);
+          double d_prev = ncp - lower, d_next = upper - ncp;
+          if (k < COAL_KMAX && d_prev > 0.0 && d_next > 0.0 && uu > 0.0) {
+            double h = cur[2 + COAL_KMAX + i - 1];
+            double d_total = d_prev + d_next;
+            double lr = orc_log(1.0 - uu) - orc_log(uu);
+            double hp = orc_exp(orc_log(h) - (d_next / d_total) * lr);
+            double hn = orc_exp(orc_log(h) + (d_prev / d_total) * lr);
+            prop[0] = (double)(k + 1);
+            for (int j = 1; j < i; ++j) prop[2 + j - 1] = cur[2 + j - 1];
+            prop[2 + i - 1] = ncp;
+            for (int j = i + 1; j <= k + 1; ++j) prop[2 + j - 1] = cur[2 + j - 2];
+            for (int j = 1; j < i; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j - 1];
+            prop[2 + COAL_KMAX + i - 1] = hp;
+            prop[2 + COAL_KMAX + i] = hn;
+            for (int j = i + 2; j <= k + 2; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j - 2];
+            sn = coal_score(prop, ev, E, T);
+            double fwd = ((k > 0 ? orc_log(0.5) : 0.0) - orc_log((double)(k + 1))) - orc_log(upper - lower);
+            double bwd = orc_log(0.5) - orc_log((double)(k + 1));
+            double logj = 2.0 * orc_log(hp + hn) - orc_log(h);
+            alpha = (((sn - cur[1]) + bwd) - fwd) + logj;
+          }
+        } else {
+          int i = (int)(coal_u(seed, c, step, 7) * (double)k) + 1;
+          double cpd = cur[2 + i - 1];
+          double lower = i == 1 ? 0.0 : cur[2 + i - 2];
+          double upper = i == k ? T : cur[2 + i];
+          double d_prev = cpd - lower, d_next = upper - cpd;
+          if (d_prev > 0.0 && d_next > 0.0) {
+            double hp = cur[2 + COAL_KMAX + i - 1], hn = cur[2 + COAL_KMAX + i];
+            double d_total = d_prev + d_next;
+            double h = orc_exp((d_prev / d_total) * orc_log(hp) + (d_next / d_total) * orc_log(hn));
+            prop[0] = (double)(k - 1);
+            for (int j = 1; j < i; ++j) prop[2 + j - 1] = cur[2 + j - 1];
+            for (int j = i; j <= k - 1; ++j) prop[2 + j - 1] = cur[2 + j];
+            for (int j = 1; j < i; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j - 1];
+            prop[2 + COAL_KMAX + i - 1] = h;
+            for (int j = i + 1; j <= k; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j];
+            sn = coal_score(prop, ev, E, T);
+            double fwd = orc_log(0.5) - orc_log((double)k);
+            double bwd = ((k - 1 > 0 ? orc_log(0.5) : 0.0) - orc_log((double)k)) - orc_log(upper - lower);
+            double logj = orc_log(h) - 2.0 * orc_log(hp + hn);
+            alpha = (((sn - cur[1]) + bwd) - fwd) + logj;
+          }
+        }
+        if (orc_log(coal_u(seed, c, step, 10)) < alpha) { coal_copy(prop, cur); cur[1] = sn; acc[2]++; }
+      }
+      if (khist) khist[cl * n_iters + it] = (int32_t)cur[0];
+    }
+    for (int m = 0; m < 3; ++m) accepts[cl * 3 + m] = acc[m];
+  }
+  return 0;
+}

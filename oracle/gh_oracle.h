@@ -93,6 +93,12 @@ int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys
                  int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml, int32_t* accepts,
                  double* hist);
 
+/* reversible-jump MH on the coal change-point model (config C3): chains
+   [chain0, chain0 + n_chains); state rows of 68 doubles (k, score, cp[32],
+   h[33], pad); see gen_amd/csrc/gh_coal.h */
+int orc_coal_run(int64_t chain0, int64_t n_chains, const double* events, int E, int n_iters, int iter0,
+                 uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist);
+
 /* static weight helpers used by the golden-vector tests */
 double orc_normal_logpdf(double x, double mu, double std);
 

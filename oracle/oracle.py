@@ -63,6 +63,7 @@ def lib():
             "orc_importance_sampling": (I, [I, I, I, I, I, D, I64, D, I, I, I64, U64, D, D, D]),
             "orc_normal_logpdf": (c_double, [c_double, c_double, c_double]),
             "orc_pmmh_run": (I, [I64, I64, I, D, I, I, I, U64, I, D, D, D, POINTER(ctypes.c_int32), D]),
+            "orc_coal_run": (I, [I64, I64, D, I, I, I, U64, I, D, POINTER(ctypes.c_int32), POINTER(ctypes.c_int32)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -254,3 +255,20 @@ def pmmh_run(ys, n_chains, n_inner, n_iters, seed, chain0=0, iter0=0, state=None
     if rc:
         raise ValueError("oracle PMMH failed")
     return lvx, lvy, lml, acc, hist
+
+
+COAL_W = 68
+
+
+def coal_run(events, n_chains, n_iters, seed, chain0=0, iter0=0, state=None, khist=False):
+    """CPU RJMCMC on the coal model (orc_coal_run): (state[n,68], accepts[n,3], khist)."""
+    ev = np.ascontiguousarray(np.asarray(events, dtype=np.float64))
+    st = np.zeros((n_chains, COAL_W)) if state is None else np.array(state, dtype=np.float64)
+    acc = np.zeros((n_chains, 3), dtype=np.int32)
+    kh = np.zeros((n_chains, max(n_iters, 1)), dtype=np.int32) if khist else None
+    rc = lib().orc_coal_run(chain0, n_chains, _d(ev), ev.size, n_iters, iter0, seed, 1 if state is None else 0,
+                            _d(st), acc.ctypes.data_as(POINTER(ctypes.c_int32)),
+                            None if kh is None else kh.ctypes.data_as(POINTER(ctypes.c_int32)))
+    if rc:
+        raise ValueError("oracle coal failed")
+    return st, acc, kh

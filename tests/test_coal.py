@@ -1,0 +1,73 @@
+"""Reversible-jump MH on the coal change-point model (config C3).
+
+CPU: the oracle (orc_coal_run) is deterministic, continues across calls
+exactly, keeps every state inside the model's support with a consistent
+cached score, and its posterior over k matches the reference analysis (Green
+1995, the source of examples/coal: mass on 1..7 change points, mode 2-3).
+GPU: one thread per chain reproduces the oracle bit for bit (states, scores,
+acceptance counts, k histories).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+
+EV = json.load(open(os.path.join(ROOT, "tests", "golden", "coal_events.json")))
+EVENTS = np.array(EV["events"])
+
+
+def _valid(st):
+    T = EVENTS[-1]
+    for row in st:
+        k = int(row[0])
+        cp = row[2 : 2 + k]
+        h = row[34 : 34 + k + 1]
+        assert 0 <= k <= 32
+        assert np.all(np.diff(np.concatenate([[0.0], cp, [T]])) > 0)
+        assert np.all(h > 0)
+
+
+def test_fixture():
+    assert EV["n"] == 190 and EVENTS[0] == 0.0 and np.all(np.diff(EVENTS) >= 0)
+
+
+def test_oracle_coal_deterministic_continues_and_valid():
+    a = O.coal_run(EVENTS, 8, 60, seed=3, chain0=4, khist=True)
+    b = O.coal_run(EVENTS, 8, 60, seed=3, chain0=4, khist=True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    c1 = O.coal_run(EVENTS, 8, 25, seed=3, chain0=4)
+    c2 = O.coal_run(EVENTS, 8, 35, seed=3, chain0=4, iter0=25, state=c1[0])
+    assert np.array_equal(c2[0], a[0]) and np.array_equal(c1[1] + c2[1], a[1])
+    _valid(a[0])
+
+
+def test_oracle_coal_posterior_over_k():
+    st, acc, kh = O.coal_run(EVENTS, 32, 3000, seed=1, khist=True)
+    post = np.bincount(kh[:, 1000:].ravel(), minlength=33) / kh[:, 1000:].size
+    assert post[0] < 0.01  # a single rate is ruled out by the data
+    assert post[1:8].sum() > 0.97
+    assert 2 <= int(np.argmax(post)) <= 3
+    rates = acc.sum(axis=0) / (32 * 3000)
+    assert np.all((rates > 0.05) & (rates < 0.8)), rates
+
+
+@pytest.mark.gpu
+def test_gpu_coal_matches_oracle(gh_ctx):
+    from gen_amd.coal import CoalChains
+
+    ref = O.coal_run(EVENTS, 300, 30, seed=11, chain0=7, khist=True)
+    ch = CoalChains(EVENTS, 300, seed=11, chain0=7, ctx=gh_ctx)
+    kh = ch.run(30, k_history=True)
+    assert np.array_equal(ch.state, ref[0])
+    assert np.array_equal(ch.accepts, ref[1])
+    assert np.array_equal(kh, ref[2])
+    ch.run(20)
+    ref2 = O.coal_run(EVENTS, 300, 20, seed=11, chain0=7, iter0=30, state=ref[0])
+    assert np.array_equal(ch.state, ref2[0])
