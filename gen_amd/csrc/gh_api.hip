@@ -459,8 +459,8 @@ struct gh_pf {
   bool marks_pending = false;     // last resample's ancestors only exist as marks
   bool stats_valid = false;       // stats_all holds the last step's (M, S, S2) (one rank)
   uint64_t* tsum = nullptr;       // k_resample1: published tile totals
-  int rs_grid = 0;                // k_resample1 tiles (blocks)
-  int rs_cap = 0;                 // co-resident k_resample1 blocks on this device
+  int rs_grid = 0;                // k_resample1 / k_rank_* tiles (blocks); 0: not usable
+  int rs_it = 0;                  // particles per thread of those kernels (4, 8 or 16)
   uint64_t* bsum = nullptr;
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
@@ -490,6 +490,43 @@ struct gh_pf {
 };
 
 static int64_t split_lo(int64_t n, int r, int R) { return (n * r) / R; }
+
+// Tile size of the one-launch resample kernels: the smallest 1024 x IT tile
+// whose grid fits the co-resident capacity (their grid barrier needs every
+// block resident), IT = 4 only while the step partials fit its registers.
+template <class K>
+static int occ_blocks(K kernel) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kRsBlock, 0) != hipSuccess) occ = 0;
+  return occ;
+}
+template <int IT>
+static int resample_cap(int cus) {
+  int o = occ_blocks(k_resample1<true, IT>);
+  int o2 = occ_blocks(k_resample1<false, IT>);
+  int o3 = occ_blocks(k_rank_a<IT>);
+  if (o2 < o) o = o2;
+  if (o3 < o) o = o3;
+  return o * cus;
+}
+static void pick_resample_tiles(gh_pf* pf, int64_t n) {
+  const int cus = pf->ctx->cus;
+  const int64_t grid4 = (n + 4 * kRsBlock - 1) / (4 * kRsBlock);
+  const int64_t grid8 = (n + 8 * kRsBlock - 1) / (8 * kRsBlock);
+  const int64_t grid16 = (n + 16 * kRsBlock - 1) / (16 * kRsBlock);
+  pf->rs_grid = 0;
+  pf->rs_it = 0;
+  if (pf->nb_step <= kRsPart * kRsBlock && grid4 <= resample_cap<4>(cus)) {
+    pf->rs_it = 4;
+    pf->rs_grid = (int)grid4;
+  } else if (grid8 <= resample_cap<8>(cus)) {
+    pf->rs_it = 8;
+    pf->rs_grid = (int)grid8;
+  } else if (grid16 <= resample_cap<16>(cus)) {
+    pf->rs_it = 16;
+    pf->rs_grid = (int)grid16;
+  }
+}
 
 // device -> host copy ordered after everything enqueued on the filter's stream
 // (the stream is non-blocking, so a plain hipMemcpy could overtake it)
@@ -715,15 +752,8 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   ALLOC(pf->stats_all, sizeof(double) * 3 * ctx->world);
   ALLOC(pf->totals_all, sizeof(uint64_t) * ctx->world);
   ALLOC(pf->anc_scratch, sizeof(int32_t) * n);
-  pf->rs_grid = (int)((n + kRsTile - 1) / kRsTile);
-  ALLOC(pf->tsum, sizeof(uint64_t) * pf->rs_grid);
-  {
-    int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_resample1<true>, kRsBlock, 0) != hipSuccess) occ = 0;
-    int occ2 = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, k_resample1<false>, kRsBlock, 0) != hipSuccess) occ2 = 0;
-    pf->rs_cap = (occ < occ2 ? occ : occ2) * ctx->cus;
-  }
+  ALLOC(pf->tsum, sizeof(uint64_t) * ((n + kRsTile - 1) / kRsTile));
+  pick_resample_tiles(pf, n);
   if (ctx->world > 1) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
@@ -850,6 +880,14 @@ static int exchange_states(gh_pf* pf, int32_t* anc_out);
 static void sys_plan(int64_t N, int R, int q, const uint64_t* totals, uint64_t o, int64_t* send_lo,
                      int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi);
 
+static void launch_rank_b(gh_pf* pf, const RankBArgs& rb) {
+  switch (pf->rs_it) {
+    case 4: hipLaunchKernelGGL(k_rank_b<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, rb); break;
+    case 8: hipLaunchKernelGGL(k_rank_b<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, rb); break;
+    default: hipLaunchKernelGGL(k_rank_b<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, rb); break;
+  }
+}
+
 // Multi-rank systematic resample: decision + quantise + rank
 // total (k_rank_a), all-gather of the totals, marks + outgoing rows
 // (k_rank_b).  The host reads the totals on a side stream while k_rank_b
@@ -873,7 +911,11 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   ra.dev = pf->dev;
   ra.d = d;
   ra.tsum = pf->tsum;
-  hipLaunchKernelGGL(k_rank_a, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra);
+  switch (pf->rs_it) {
+    case 4: hipLaunchKernelGGL(k_rank_a<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
+    case 8: hipLaunchKernelGGL(k_rank_a<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
+    default: hipLaunchKernelGGL(k_rank_a<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
+  }
   HIP_TRY(hipGetLastError());
   CHECK(comm_allgather(c, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
   HIP_TRY(hipEventRecord(pf->ev_tot, pf->s));
@@ -900,7 +942,7 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.D = D;
   rb.rows = pf->rows_send;
   rb.rows_cap = pf->send_cap;
-  hipLaunchKernelGGL(k_rank_b, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, rb);
+  launch_rank_b(pf, rb);
   HIP_TRY(hipGetLastError());
   // the counts: decision + totals on the host, overlapping k_rank_b
   HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_tot, 0));
@@ -934,7 +976,7 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
     pf->send_cap = cap;
     rb.rows = pf->rows_send;
     rb.rows_cap = cap;
-    hipLaunchKernelGGL(k_rank_b, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, rb);
+    launch_rank_b(pf, rb);
     HIP_TRY(hipGetLastError());
   }
   std::vector<CommMsg> sends, recvs;
@@ -974,7 +1016,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   // The common case fuses the decision into the first resample kernel; a
   // second call without a step (or an empty shard) decides in its own launch.
   const bool sys = pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
-  if (R == 1 && !second && n > 0 && pf->rs_grid <= pf->rs_cap && pf->nb_step <= kRsPart * kRsBlock) {
+  if (R == 1 && !second && n > 0 && pf->rs_grid > 0) {
     // one launch: fold + decision + quantise + one grid barrier + marks / CDF
     Resample1Args ra{};
     ra.pm = pf->pm;
@@ -999,10 +1041,17 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     ra.t = (uint32_t)t;
     // grid <= co-resident capacity of an idle device (rs_cap), so every block
     // is eventually resident; the barrier wait is bounded as a backstop
-    if (sys)
-      hipLaunchKernelGGL(k_resample1<true>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra);
-    else
-      hipLaunchKernelGGL(k_resample1<false>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra);
+    const dim3 grid((unsigned)pf->rs_grid), blk(kRsBlock);
+#define GH_RS1(SYS, IT) hipLaunchKernelGGL((k_resample1<SYS, IT>), grid, blk, 0, pf->s, ra)
+    switch (pf->rs_it * 2 + (sys ? 1 : 0)) {
+      case 9: GH_RS1(true, 4); break;
+      case 8: GH_RS1(false, 4); break;
+      case 17: GH_RS1(true, 8); break;
+      case 16: GH_RS1(false, 8); break;
+      case 33: GH_RS1(true, 16); break;
+      default: GH_RS1(false, 16); break;
+    }
+#undef GH_RS1
     pf->stats_valid = true;
     if (sys) {
       pf->marks_pending = true;
@@ -1027,7 +1076,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     pf->resample_calls++;
     return GH_OK;
   }
-  if (R > 1 && R <= kMaxRanks && !second && n > 0 && sys && pf->rs_grid <= pf->rs_cap) {
+  if (R > 1 && R <= kMaxRanks && !second && n > 0 && sys && pf->rs_grid > 0) {
     CHECK(rank_resample(pf, d, g.shift, t));
     pf->resample_calls++;
     return GH_OK;

@@ -835,13 +835,13 @@ __device__ uint64_t g_rs_stamps[1024 * 8];
 #define GH_RS_STAMP(k)
 #endif
 
-template <bool MARKS>
+template <bool MARKS, int IT>
 __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   __shared__ double smd[16];
   __shared__ uint64_t smu[16];
   __shared__ DevScalars sd;
   __shared__ uint64_t sbase;
-  __shared__ int32_t se[kRsTile];
+  __shared__ int32_t se[(kRsBlock * IT)];
   __shared__ int64_t sfirst;
   __shared__ unsigned sgen;
   GH_RS_STAMP(0);
@@ -849,32 +849,47 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   if (threadIdx.x == 0) sgen = r.dev->bar_gen + 1;
   // ---- fold the step partials (same order in every block: same result)
   // this tile's log-weights are loaded up front, beside the partials
-  const int64_t i0 = (int64_t)blockIdx.x * kRsTile + (int64_t)threadIdx.x * kRsItems;
-  double lw[kRsItems];
+  const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
+  double lw[IT];
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
-  double pmv[kRsPart], psv[kRsPart], ps2v[kRsPart];
+  for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
+  double M, s1 = 0.0, s2 = 0.0;
+  if constexpr (IT <= kRsPart) {  // the partials fit in registers: one round trip
+    double pmv[kRsPart], psv[kRsPart], ps2v[kRsPart];
 #pragma unroll
-  for (int k = 0; k < kRsPart; ++k) {
-    const int b = threadIdx.x + k * kRsBlock;
-    const bool ok = b < r.nb_part;
-    pmv[k] = ok ? r.pm[b] : -INFINITY;
-    psv[k] = ok ? r.ps[b] : 0.0;
-    ps2v[k] = ok ? r.ps2[b] : 0.0;
-  }
-  double m = pmv[0];
+    for (int k = 0; k < kRsPart; ++k) {
+      const int b = threadIdx.x + k * kRsBlock;
+      const bool ok = b < r.nb_part;
+      pmv[k] = ok ? r.pm[b] : -INFINITY;
+      psv[k] = ok ? r.ps[b] : 0.0;
+      ps2v[k] = ok ? r.ps2[b] : 0.0;
+    }
+    double m = pmv[0];
 #pragma unroll
-  for (int k = 1; k < kRsPart; ++k) m = fmax(m, pmv[k]);
-  const double M = blk16_max(m, smd);
-  GH_RS_STAMP(7);
-  double s1 = 0.0, s2 = 0.0;
-  if (M > -INFINITY) {
+    for (int k = 1; k < kRsPart; ++k) m = fmax(m, pmv[k]);
+    M = blk16_max(m, smd);
+    GH_RS_STAMP(7);
+    if (M > -INFINITY) {
 #pragma unroll
-    for (int k = 0; k < kRsPart; ++k)
-      if (pmv[k] > -INFINITY) {
-        const double f = gh_exp(pmv[k] - M);
-        s1 += psv[k] * f;
-        s2 += ps2v[k] * (f * f);
+      for (int k = 0; k < kRsPart; ++k)
+        if (pmv[k] > -INFINITY) {
+          const double f = gh_exp(pmv[k] - M);
+          s1 += psv[k] * f;
+          s2 += ps2v[k] * (f * f);
+        }
+    }
+  } else {  // larger sets: max pass, then a sum pass over the (cache-hot) partials
+    double m = -INFINITY;
+    for (int b = threadIdx.x; b < r.nb_part; b += kRsBlock) m = fmax(m, r.pm[b]);
+    M = blk16_max(m, smd);
+    if (M > -INFINITY)
+      for (int b = threadIdx.x; b < r.nb_part; b += kRsBlock) {
+        const double mb = r.pm[b];
+        if (mb > -INFINITY) {
+          const double f = gh_exp(mb - M);
+          s1 += r.ps[b] * f;
+          s2 += r.ps2[b] * (f * f);
+        }
       }
   }
   const double S1 = blk16_sum(s1, smd);
@@ -909,10 +924,10 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   }
   const double Mq = M;
   // ---- quantise this block's tile (4 consecutive particles per thread)
-  uint64_t q[kRsItems];
+  uint64_t q[IT];
   uint64_t tsum = 0;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     q[k] = (i0 + k < r.n) ? quantize_weight(lw[k], Mq, r.shift) : 0;
     tsum += q[k];
   }
@@ -973,7 +988,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   uint64_t run = sbase + incl - tsum;
   if (!MARKS) {
 #pragma unroll
-    for (int k = 0; k < kRsItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
       run += q[k];
       if (i0 + k < r.n) r.C[i0 + k] = run;
     }
@@ -984,21 +999,21 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   int64_t s_i = sys_count(&sd, N, run);
   if (threadIdx.x == 0) sfirst = s_i;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     run += q[k];
     const int64_t e_i = (i0 + k < r.n && q[k]) ? sys_count(&sd, N, run) : s_i;
-    se[threadIdx.x * kRsItems + k] = (int32_t)e_i;
+    se[threadIdx.x * IT + k] = (int32_t)e_i;
     if (e_i > s_i) r.mk.mark[s_i] = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
     s_i = e_i;
   }
   __syncthreads();
   GH_RS_STAMP(5);
   // 64-slot groups starting inside this tile's slot span get their carry
-  const int64_t s_lo = sfirst, s_hi = se[kRsTile - 1];
-  const int64_t pbase = (int64_t)blockIdx.x * kRsTile;
+  const int64_t s_lo = sfirst, s_hi = se[(kRsBlock * IT) - 1];
+  const int64_t pbase = (int64_t)blockIdx.x * (kRsBlock * IT);
   for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
     const int32_t slot = (int32_t)(g * 64);
-    int lo = 0, hi = kRsTile - 1;  // first particle p with se[p] > slot
+    int lo = 0, hi = (kRsBlock * IT) - 1;  // first particle p with se[p] > slot
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (se[mid] > slot) hi = mid;
@@ -1024,6 +1039,7 @@ struct RankAArgs {
   uint64_t* tsum;    // [grid] tile totals (bit 63: generation parity)
 };
 
+template <int IT>
 __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
   __shared__ uint64_t smu[16];
   __shared__ int sfire;
@@ -1042,10 +1058,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
   __syncthreads();
   if (!sfire) return;
   const double M = sM;
-  const int64_t i0 = (int64_t)blockIdx.x * kRsTile + (int64_t)threadIdx.x * kRsItems;
+  const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
   uint64_t tsum = 0;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) tsum += (i0 + k < r.n) ? quantize_weight(r.logw[i0 + k], M, r.shift) : 0;
+  for (int k = 0; k < IT; ++k) tsum += (i0 + k < r.n) ? quantize_weight(r.logw[i0 + k], M, r.shift) : 0;
   const uint64_t tot = blk16_sum_u64(tsum, smu);
   const uint64_t kTag = 1ull << 63;
   const uint64_t par = (sgen & 1u) ? kTag : 0ull;
@@ -1098,6 +1114,7 @@ struct RankBArgs {
   int64_t rows_cap;
 };
 
+template <int IT>
 __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   if (!r.dev->fire) return;
   __shared__ uint64_t smu[16];
@@ -1105,7 +1122,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
   __shared__ int64_t sown_lo, sown_hi, sra, srb;
   __shared__ uint64_t sbase;
-  __shared__ int32_t se[kRsTile];
+  __shared__ int32_t se[(kRsBlock * IT)];
   __shared__ int64_t sfirst;
   const int R = r.R, q = r.rank;
   const uint64_t N = (uint64_t)r.mk.n_global;
@@ -1163,11 +1180,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   }
   __syncthreads();
   const double M = r.dev->M;
-  const int64_t i0 = (int64_t)blockIdx.x * kRsTile + (int64_t)threadIdx.x * kRsItems;
-  uint64_t qv[kRsItems];
+  const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
+  uint64_t qv[IT];
   uint64_t tsum = 0;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     qv[k] = (i0 + k < r.n) ? quantize_weight(r.logw[i0 + k], M, r.shift) : 0;
     tsum += qv[k];
   }
@@ -1178,12 +1195,12 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   int64_t s0 = sys_count(&sd, N, run);
   if (threadIdx.x == 0) sfirst = clamp_own(s0) - own_lo;
 #pragma unroll
-  for (int k = 0; k < kRsItems; ++k) {
+  for (int k = 0; k < IT; ++k) {
     run += qv[k];
     const int64_t i = i0 + k;
     const int64_t s1 = (i < r.n && qv[k]) ? sys_count(&sd, N, run) : s0;
     const int64_t l0 = clamp_own(s0), l1 = clamp_own(s1);
-    se[threadIdx.x * kRsItems + k] = (int32_t)(l1 - own_lo);
+    se[threadIdx.x * IT + k] = (int32_t)(l1 - own_lo);
     if (l1 > l0) r.mk.mark[l0 - own_lo] = (r.mk.epoch << 32) | (uint64_t)i;
     // slots of other ranks: state rows, by destination then slot
     for (int64_t sl = s0; sl < s1; ++sl) {
@@ -1206,11 +1223,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __syncthreads();
   // carries of the 64-slot groups (local slot space) starting in this tile's
   // own-slot span
-  const int64_t s_lo = sfirst, s_hi = se[kRsTile - 1];
-  const int64_t pbase = (int64_t)blockIdx.x * kRsTile;
+  const int64_t s_lo = sfirst, s_hi = se[(kRsBlock * IT) - 1];
+  const int64_t pbase = (int64_t)blockIdx.x * (kRsBlock * IT);
   for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
     const int32_t slot = (int32_t)(g * 64);
-    int lo = 0, hi = kRsTile - 1;  // first particle p with se[p] > slot
+    int lo = 0, hi = (kRsBlock * IT) - 1;  // first particle p with se[p] > slot
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (se[mid] > slot) hi = mid;

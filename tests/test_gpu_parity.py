@@ -192,6 +192,16 @@ def test_lgssm_full_size_first_steps_bitexact(gh_ctx):
     assert_lml_close(st, orc)
 
 
+@pytest.mark.parametrize("n", [1_500_007, 4_200_001])
+def test_kitagawa_large_tiles_bitexact(gh_ctx, n):
+    """Past 2^20 particles the one-launch resample kernel takes 8 / 16
+    particles per thread (the C4 shard size is 2^21 per GPU)."""
+    m = gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(3, np.random.default_rng(4))
+    st, orc = run_both(m, ys, n, seed=5, thr=n, check_every_step=False)
+    assert_lml_close(st, orc)
+
+
 # ------------------------------------------------------------- edge cases
 def test_single_particle(gh_ctx):
     m = gen.KitagawaSSM()
