@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--particles", type=int, default=1 << 20, help="particles per GPU")
     p.add_argument("--d", type=int, default=10)
+    p.add_argument("--model", default="lgssm", choices=["lgssm", "kitagawa"],
+                   help="lgssm: C2 (the headline); kitagawa: the C4 nonlinear SSM")
     p.add_argument("--resampler", default="systematic")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -101,9 +103,12 @@ def main():
         ctx = gen.Context(device=0)
     gen.set_default_context(ctx)
 
-    model = gen.LinearGaussianSSM.benchmark(a.d)
+    if a.model == "lgssm":
+        model = gen.LinearGaussianSSM.benchmark(a.d)
+    else:
+        model = gen.KitagawaSSM(10.0, 1.0)  # examples/pmmh/run.jl:69 (var_x = 10, var_y = 1)
     T = a.warmup + a.steps + 1
-    _, ys = model.simulate(T, np.random.default_rng(2))
+    _, ys = model.simulate(T, np.random.default_rng(2 if a.model == "lgssm" else 3))
     n_global = a.particles * world
     st = gen.initialize_particle_filter(
         model, (1,), {("chain", 1, "y"): ys[0]}, n_global, seed=42, resampler=a.resampler,
@@ -135,7 +140,8 @@ def main():
     n_res = int(did[a.warmup : a.warmup + a.steps].sum())  # resamples ahead of the timed steps
     lml = gen.log_ml_estimate(st)
 
-    bytes_pp = 16 * a.d + 16 + 4.0 * n_res / max(1, a.steps)
+    d = a.d if a.model == "lgssm" else 1
+    bytes_pp = 16 * d + 16 + 4.0 * n_res / max(1, a.steps)
     achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
@@ -147,7 +153,8 @@ def main():
 
     value = n_global * a.steps / dt
     out = {
-        "metric": "particle-steps/sec (whole node) + log-ML error vs CPU ref, 1M-particle SSM",
+        "metric": ("particle-steps/sec (whole node) + log-ML error vs CPU ref, 1M-particle SSM" if a.model == "lgssm"
+                   else "particle-steps/sec (whole node), nonlinear SSM (C4)"),
         "value": value,
         "unit": "particle-steps/s",
         "n_gpus": world,
@@ -160,10 +167,11 @@ def main():
         "dtype": "f64",
         "data": "synthetic (observations simulated from the model, numpy seed 2)",
         "config": {
-            "workload": f"C2: {a.d}-dim linear-Gaussian SSM bootstrap PF, {a.particles} particles/GPU, "
+            "workload": (f"C2: {a.d}-dim linear-Gaussian SSM bootstrap PF" if a.model == "lgssm" else
+                         "C4: Kitagawa nonlinear SSM bootstrap PF") + f", {a.particles} particles/GPU, "
                         f"systematic resampling at ESS<N/2, record_history={not a.no_history}",
             "particles_global": n_global,
-            "d": a.d,
+            "d": d,
             "resampler": a.resampler,
             "parallelism": f"particle-dp{world}",
             "resample_steps_timed": n_res,
@@ -176,7 +184,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": f"k_step<LGModel<{a.d},3>,false>",
+            "kernel": f"k_step<LGModel<{a.d},3>,false>" if a.model == "lgssm" else "k_step<KitModel,false>",
             "kernel_avg_ms": kms,
             "kernel_launches": kcount,
             "bytes_per_particle_step": bytes_pp,
