@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--no-history", action="store_true")
     p.add_argument("--ess-threshold", type=float, default=None, help="default N/2 (the reference's default)")
     p.add_argument("--no-kernel-timing", action="store_true", help="no hipEvents around the step kernel")
+    p.add_argument("--transport", default="rccl", choices=["rccl", "gloo"],
+                   help="multi-GPU collectives: RCCL (default) or the host-staged gloo transport "
+                        "(ranks may share a GPU; a correctness rehearsal, not a benchmark)")
     p.add_argument("--time-every", type=int, default=10,
                    help="time every k-th step kernel with launch events (each timed launch adds queue packets)")
     return p.parse_args()
@@ -96,9 +99,16 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo")
-        uid = [gen.Context.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx = gen.Context(device=local, rank=rank, world=world, unique_id=uid[0])
+        if a.transport == "gloo":
+            import torch
+
+            from gen_amd.transport import GlooTransport
+
+            ctx = gen.Context(device=local % max(1, torch.cuda.device_count()), transport=GlooTransport())
+        else:
+            uid = [gen.Context.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            ctx = gen.Context(device=local, rank=rank, world=world, unique_id=uid[0])
     else:
         ctx = gen.Context(device=0)
     gen.set_default_context(ctx)
@@ -145,7 +155,7 @@ def main():
     achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20:  # the profiled config
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
@@ -165,7 +175,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (observations simulated from the model, numpy seed 2)",
+        "data": f"synthetic (observations simulated from the model, numpy seed {2 if a.model == 'lgssm' else 3})",
         "config": {
             "workload": (f"C2: {a.d}-dim linear-Gaussian SSM bootstrap PF" if a.model == "lgssm" else
                          "C4: Kitagawa nonlinear SSM bootstrap PF") + f", {a.particles} particles/GPU, "
@@ -197,6 +207,8 @@ def main():
     st.close()
     if dist is not None:
         dist.barrier()
+    ctx.close()
+    if dist is not None:
         dist.destroy_process_group()
 
 
