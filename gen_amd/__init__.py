@@ -23,6 +23,7 @@ from .pf import (
     maybe_resample,
     maybe_resample_async,
     particle_filter_step,
+    rejuvenate,
     run_particle_filter,
     sample_unweighted_traces,
     set_default_context,
@@ -34,6 +35,6 @@ __all__ = [
     "Context", "NoChange", "OptimalProposal", "ParticleFilterState", "UnknownChange", "default_context",
     "get_log_weights", "get_traces", "importance_resampling", "importance_sampling",
     "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",
-    "particle_filter_step", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
+    "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
     "GenHipError",
 ]

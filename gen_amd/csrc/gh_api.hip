@@ -21,6 +21,7 @@
 #include "gh_kernels.h"
 #include "gh_pmmh.h"
 #include "gh_coal.h"
+#include "gh_rejuv.h"
 
 using namespace gh;
 
@@ -481,6 +482,11 @@ struct gh_pf {
   hipEvent_t ev_tot = nullptr;    // multi-rank: totals all-gathered
   uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]]
   int mark_mode = 1;              // 1: one-rank marks; 2: marks + received rows
+  // rejuvenation (gh_pf_rejuvenate): the current step's observation and the
+  // MH moves already applied at this step (their draw windows)
+  StepObs last_obs{};
+  uint32_t rejuv_moves = 0;
+  unsigned long long* acc_count = nullptr;
   std::vector<void*> chunks;      // history allocations (record_history)
   // kernel timing
   std::vector<hipEvent_t> ev;
@@ -598,6 +604,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->tsum); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
+  hipFree(pf->acc_count);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
   if (pf->h_plan) hipHostFree(pf->h_plan);
@@ -815,6 +822,7 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   rc = share_stats(pf);
   if (rc) return fail(rc);
   pf->t = 1;
+  pf->last_obs = o;
   *out = pf;
   return GH_OK;
 }
@@ -858,6 +866,8 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   pf->t = t;
   pf->resample_calls = 0;
   pf->marks_pending = false;
+  pf->last_obs = o;
+  pf->rejuv_moves = 0;
   return GH_OK;
 }
 
@@ -1330,6 +1340,91 @@ extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
   std::vector<int32_t> a(pf->n);
   CHECK(d2h(pf, a.data(), anc_for_step(pf, s_last), sizeof(int32_t) * pf->n));
   for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->lo + a[i];
+  return GH_OK;
+}
+
+// ------------------------------------------------------------ rejuvenation
+template <class Model>
+static void launch_rejuv_t(gh_pf* pf, const typename Model::Params& p, const RejuvArgs& a, bool init) {
+  const dim3 grid((unsigned)pf->nb_step), block(kBlock);
+  if (init)
+    hipLaunchKernelGGL((k_rejuv<Model, true>), grid, block, 0, pf->s, (const double*)pf->m->dparams, p,
+                       pf->last_obs, a);
+  else
+    hipLaunchKernelGGL((k_rejuv<Model, false>), grid, block, 0, pf->s, (const double*)pf->m->dparams, p,
+                       pf->last_obs, a);
+}
+
+static int launch_rejuv(gh_pf* pf, const RejuvArgs& a, bool init) {
+  gh_model* m = pf->m;
+  switch (m->family) {
+    case GH_FAMILY_LGSSM:
+      switch (m->d) {
+#define GH_LG_CASE(DD)                                                       \
+  case DD:                                                                   \
+    switch (m->lg_struct) {                                                  \
+      case 1: launch_rejuv_t<LGModel<DD, 1>>(pf, m->lg, a, init); break;     \
+      case 2: launch_rejuv_t<LGModel<DD, 2>>(pf, m->lg, a, init); break;     \
+      case 3: launch_rejuv_t<LGModel<DD, 3>>(pf, m->lg, a, init); break;     \
+      default: launch_rejuv_t<LGModel<DD, 0>>(pf, m->lg, a, init); break;    \
+    }                                                                        \
+    break;
+        GH_LG_CASE(1) GH_LG_CASE(2) GH_LG_CASE(3) GH_LG_CASE(4) GH_LG_CASE(5) GH_LG_CASE(6)
+        GH_LG_CASE(7) GH_LG_CASE(8) GH_LG_CASE(10) GH_LG_CASE(12) GH_LG_CASE(16)
+#undef GH_LG_CASE
+        default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", m->d);
+      }
+      break;
+    case GH_FAMILY_HMM: launch_rejuv_t<HMMModel>(pf, m->hmm, a, init); break;
+    case GH_FAMILY_KITAGAWA: launch_rejuv_t<KitModel>(pf, m->kit, a, init); break;
+    default: return set_err(GH_E_INVAL, "unknown family");
+  }
+  HIP_TRY(hipGetLastError());
+  return GH_OK;
+}
+
+// mh(trace, select(x_t)) on every particle (gh_rejuv.h).  The states of step t
+// are rewritten in place; the parent states are those step t consumed: the
+// previous slot through the step's ancestors, or rows received from other
+// ranks (still resident until the next exchange).
+extern "C" int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  if (n_moves < 0) return set_err(GH_E_INVAL, "gh_pf_rejuvenate: n_moves < 0");
+  if (pf->resample_calls > 0)
+    return set_err(GH_E_STATE, "gh_pf_rejuvenate: call after a step and before maybe_resample");
+  if ((uint64_t)pf->rejuv_moves + (uint64_t)n_moves > kRejuvMaxMoves)
+    return set_err(GH_E_INVAL, "gh_pf_rejuvenate: more than %u moves at one step", kRejuvMaxMoves);
+  HIP_TRY(hipSetDevice(pf->ctx->device));
+  if (!pf->acc_count) HIP_TRY(hipMalloc(&pf->acc_count, sizeof(unsigned long long)));
+  HIP_TRY(hipMemsetAsync(pf->acc_count, 0, sizeof(unsigned long long), pf->s));
+  const int t = pf->t;
+  if (n_moves > 0 && pf->n > 0) {
+    RejuvArgs a{};
+    if (t >= 2) {
+      a.xprev = slot_x(pf, t - 1);
+      a.ld_prev = pf->n;
+      a.anc = anc_for_step(pf, t);
+      a.res = pf->res_hist + t;
+      a.remote = pf->rows_recv;
+      a.ld_remote = pf->D + 1;
+    }
+    a.x = slot_x(pf, t);
+    a.ld = pf->n;
+    a.n = pf->n;
+    a.lo = pf->lo;
+    a.seed = pf->seed;
+    a.t = (uint32_t)t;
+    a.move0 = pf->rejuv_moves;
+    a.n_moves = n_moves;
+    a.accepted = pf->acc_count;
+    CHECK(launch_rejuv(pf, a, t == 1));
+  }
+  pf->rejuv_moves += (uint32_t)n_moves;
+  if (accepted) {
+    unsigned long long h = 0;
+    CHECK(d2h(pf, &h, pf->acc_count, sizeof h));
+    *accepted = (int64_t)h;
+  }
   return GH_OK;
 }
 

@@ -24,6 +24,13 @@ namespace gh {
 
 constexpr int kMaxObs = 32;
 
+// Where a particle's draws come from: the step / init streams for the filter,
+// the MH stream (with a per-move draw offset) for rejuvenation proposals.
+struct Draw {
+  uint32_t stream;
+  uint32_t base;  // first draw index
+};
+
 // per-step observation, passed by value in the kernel arguments
 struct StepObs {
   double v[kMaxObs];  // LGSSM: L_R^{-1}(y - c); Kitagawa: y; HMM: symbol
@@ -80,12 +87,11 @@ struct LGModel {
 #endif
   using Params = LGParams;
 
-  __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, uint32_t stream,
-                                 double* z) {
+  __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, Draw dr, double* z) {
 #pragma unroll
     for (int j = 0; 2 * j < D; ++j) {
       double a, b;
-      normal_pair(rng_block(seed, pid, step, stream, (uint32_t)j), &a, &b);
+      normal_pair(rng_block(seed, pid, step, dr.stream, dr.base + (uint32_t)j), &a, &b);
       z[2 * j] = a;
       if (2 * j + 1 < D) z[2 * j + 1] = b;
     }
@@ -112,10 +118,12 @@ struct LGModel {
     return p.cstR - 0.5 * quad;
   }
 
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return obs(p, o, x); }
+
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
-                                int /*proposal*/, double* x) {
+                                int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
     double z[D + 1];
-    normals(seed, pid, 1, STREAM_INIT, z);
+    normals(seed, pid, 1, dr, z);
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       double acc = p.mu0[i];
@@ -127,9 +135,10 @@ struct LGModel {
   }
 
   __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
-                                uint32_t t, int /*proposal*/, const double* xp, double* x) {
+                                uint32_t t, int /*proposal*/, const double* xp, double* x,
+                                Draw dr = {STREAM_STEP, 0}) {
     double z[D + 1];
-    normals(seed, pid, t, STREAM_STEP, z);
+    normals(seed, pid, t, dr, z);
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       double acc = p.b[i];
@@ -205,9 +214,12 @@ struct HMMModel {
   static constexpr int kMinWaves = 8;
   using Params = HMMParams;
 
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) {
+    return o.present ? p.logE[o.sym * p.k + (int)x[0]] : 0.0;
+  }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
-                                int proposal, double* x) {
-    const u32x4 w = rng_block(seed, pid, 1, STREAM_INIT, 0);
+                                int proposal, double* x, Draw dr = {STREAM_INIT, 0}) {
+    const u32x4 w = rng_block(seed, pid, 1, dr.stream, dr.base);
     const double u = u53(w.x, w.y);
     if (proposal == 1 && o.present) {
       double total;
@@ -221,8 +233,9 @@ struct HMMModel {
   }
 
   __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
-                                uint32_t t, int proposal, const double* xp, double* x) {
-    const u32x4 w = rng_block(seed, pid, t, STREAM_STEP, 0);
+                                uint32_t t, int proposal, const double* xp, double* x,
+                                Draw dr = {STREAM_STEP, 0}) {
+    const u32x4 w = rng_block(seed, pid, t, dr.stream, dr.base);
     const double u = u53(w.x, w.y);
     const int zp = (int)xp[0];
     if (proposal == 1 && o.present) {
@@ -256,17 +269,19 @@ struct KitModel {
     const double diff = o.v[0] - x * x / 20.0;
     return -(diff * diff) * p.inv2vy + p.csty;
   }
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return obs(p, o, x[0]); }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
-                                int /*proposal*/, double* x) {
+                                int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
     double z0, z1;
-    normal_pair(rng_block(seed, pid, 1, STREAM_INIT, 0), &z0, &z1);
+    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1);
     x[0] = p.mu1 + p.s1 * z0;
     return obs(p, o, x[0]);
   }
   __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
-                                uint32_t t, int /*proposal*/, const double* xp, double* x) {
+                                uint32_t t, int /*proposal*/, const double* xp, double* x,
+                                Draw dr = {STREAM_STEP, 0}) {
     double z0, z1;
-    normal_pair(rng_block(seed, pid, t, STREAM_STEP, 0), &z0, &z1);
+    normal_pair(rng_block(seed, pid, t, dr.stream, dr.base), &z0, &z1);
     const double v = xp[0];
     const double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
     x[0] = mean + p.sx * z0;

@@ -1,0 +1,88 @@
+// gh_rejuv.h — rejuvenation moves on the particles of a filter.
+//
+// The reference leaves rejuvenation to the caller: after a step it applies
+// an MH kernel to every trace, typically
+//     state.traces[i], _ = mh(state.traces[i], select(:x => t))
+// (src/inference/mh.jl:14-26, selection form: regenerate the selected choices
+// from their prior; accept iff log(rand()) < weight), and the particle's log
+// weight is left as it is (mh keeps the target of the trace).  Regenerating the
+// current latent x_t from its prior given x_{t-1} gives
+//     weight = log p(y_t | x'_t) - log p(y_t | x_t)
+// because the transition density cancels between the new score and the
+// proposal.  At t = 1 the prior is the initial-state distribution.
+//
+// One particle per lane; the current state and its parent's state live in
+// registers for all moves.  Move m of step t draws its proposal from the MH
+// stream at draw offset (move0 + m) * kRejuvDraws and its acceptance uniform
+// from the last draw of that window.
+#pragma once
+#include "gh_kernels.h"
+
+namespace gh {
+
+constexpr uint32_t kRejuvDraws = 16;      // draw window per move (LG d <= 16 uses 8)
+constexpr uint32_t kRejuvMaxMoves = 4096; // 16-bit draw field / kRejuvDraws
+
+struct RejuvArgs {
+  const double* xprev;    // [D][ld_prev] states of step t-1 (t >= 2)
+  int64_t ld_prev;
+  const int32_t* anc;     // ancestors consumed by step t (valid when *res)
+  const int32_t* res;     // res_hist + t: a resample preceded step t
+  const double* remote;   // multi-rank rows received by the last exchange
+  int64_t ld_remote;
+  double* x;              // [D][ld] states of step t, rewritten in place
+  int64_t ld;
+  int64_t n, lo;
+  uint64_t seed;
+  uint32_t t;
+  uint32_t move0;         // moves already applied at this step
+  int n_moves;
+  unsigned long long* accepted;  // accepted moves (summed over particles)
+};
+
+template <class Model, bool INIT>
+__global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm, typename Model::Params p0,
+                                                  StepObs o, RejuvArgs a) {
+  constexpr int D = Model::kD;
+  const typename Model::Params p = p0.rebase(prm);
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  unsigned acc = 0;
+  if (j < a.n) {
+    const uint64_t pid = (uint64_t)(a.lo + j);
+    double x[D], xp[D], y[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) x[k] = a.x[k * a.ld + j];
+    if (!INIT) {
+      const int64_t src = *a.res ? (int64_t)a.anc[j] : j;
+      if (src >= 0) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
+      } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
+      }
+    }
+    double ll = Model::loglik(p, o, x);
+    for (int m = 0; m < a.n_moves; ++m) {
+      const uint32_t base = (a.move0 + (uint32_t)m) * kRejuvDraws;
+      const Draw dr{STREAM_MH, base};
+      // the prior proposal's weight increment is the observation log-density
+      const double ll2 = INIT ? Model::init(p, o, a.seed, pid, 0, y, dr)
+                              : Model::step(p, o, a.seed, pid, a.t, 0, xp, y, dr);
+      const u32x4 w = rng_block(a.seed, pid, a.t, STREAM_MH, base + kRejuvDraws - 1);
+      const double logu = gh_log(u53(w.x, w.y));
+      if (logu < ll2 - ll) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[k] = y[k];
+        ll = ll2;
+        ++acc;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) a.x[k * a.ld + j] = x[k];
+  }
+  const uint64_t tot = wave_sum_u64((uint64_t)acc);
+  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(a.accepted, (unsigned long long)tot);
+}
+
+}  // namespace gh

@@ -378,6 +378,17 @@ def sample_unweighted_traces(state: ParticleFilterState, num_samples: int, seed:
     return [tr[i] for i in idx], idx
 
 
+def rejuvenate(state: ParticleFilterState, n_moves: int = 1) -> int:
+    """Rejuvenation between steps: for every particle i, n_moves times
+    ``state.traces[i], _ = mh(state.traces[i], select(:chain => t => :x))``
+    (src/inference/mh.jl:14-26) on the current step t.  Weights are unchanged.
+    Call after a step and before maybe_resample.  Returns the accepted moves
+    summed over this rank's particles."""
+    acc = c_int64()
+    _lib.check(_lib.load().gh_pf_rejuvenate(state.h, int(n_moves), byref(acc)))
+    return int(acc.value)
+
+
 def importance_sampling(model: Model, model_args: tuple, observations, *args, seed: int = 0,
                         ctx: Context | None = None):
     """(traces, log_normalized_weights, lml_est) (importance.jl:20-52)."""

@@ -15,6 +15,8 @@
  *   gh_pf_get_trajectory    get_traces (SoA columns)     src/inference/particle_filter.jl:31-34
  *   gh_pf_get_parents       ParticleFilterState.parents  src/inference/particle_filter.jl:23
  *   gh_pf_sample_unweighted sample_unweighted_traces     src/inference/particle_filter.jl:62-70
+ *   gh_pf_rejuvenate        mh(trace, select(x_t)) on    src/inference/mh.jl:14-26 (applied per
+ *                           every particle               particle, as callers of the PF do)
  *   gh_is_run               importance_sampling          src/inference/importance.jl:20-52
  *   gh_pmmh_run             PMMH (mh over a PF-estimated  examples/pmmh/example.jl:20-79,
  *                           likelihood)                   examples/pmmh/pf.jl:14-73
@@ -162,6 +164,14 @@ int gh_pf_get_parents(gh_pf* pf, int64_t* host_out /* n_local, global ids */);
    genealogy back from the current step (record_history required) */
 int gh_pf_get_trajectory(gh_pf* pf, int t, double* host_out /* [d][n_local] */);
 int gh_pf_sample_unweighted(gh_pf* pf, int64_t n_samples, uint64_t seed, int64_t* host_idx);
+/* Rejuvenation: n_moves MH moves on every particle, each regenerating the
+   current latent x_t from its prior given x_{t-1} (x_1 from the initial
+   distribution) and accepting with log(rand()) < log p(y_t|x'_t) - log p(y_t|x_t).
+   Log weights are unchanged.  Call after gh_pf_init / gh_pf_step and before
+   gh_pf_maybe_resample (GH_E_STATE otherwise); at most 4096 moves per step.
+   *accepted (optional, synchronises) = accepted moves summed over the local
+   particles. */
+int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted);
 /* per-step resampling record: ess and did_resample for steps 1..t */
 int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int32_t* did);
 /* average duration (ms) of the step kernel over the timed launches (opts.time_kernels) */

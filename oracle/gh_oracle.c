@@ -140,10 +140,11 @@ double orc_cos(double x) {
 }
 
 /* n standard normals for (id, step, stream): Box–Muller on Philox blocks */
-void orc_normals(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, int n, double* z) {
+static void normals_at(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, uint32_t base, int n,
+                       double* z) {
   for (int j = 0; 2 * j < n; ++j) {
     uint32_t w[4];
-    rng(seed, id, step, stream, (uint32_t)j, w);
+    rng(seed, id, step, stream, base + (uint32_t)j, w);
     double u1 = 1.0 - unif53(w[0], w[1]);
     double u2 = unif53(w[2], w[3]);
     double r = sqrt(-2.0 * orc_log(u1));
@@ -152,6 +153,9 @@ void orc_normals(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, int
     z[2 * j] = r * c;
     if (2 * j + 1 < n) z[2 * j + 1] = r * s;
   }
+}
+void orc_normals(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, int n, double* z) {
+  normals_at(seed, id, step, stream, 0, n, z);
 }
 
 static uint64_t scale_u53(uint64_t u, uint64_t S) {
@@ -330,11 +334,13 @@ static int cat_sample(const double* p, int K, int stride, double u) {
 }
 
 /* generate at t = 1: writes x[d], returns the log weight */
+/* draws come from (stream, base + j): the filter uses (S_INIT / S_STEP, 0),
+   rejuvenation moves (S_MH, 16 * move) */
 static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
-                            int proposal, double* x) {
+                            int proposal, double* x, uint32_t stream, uint32_t base) {
   if (m->family == ORC_LGSSM) {
     double z[64];
-    orc_normals(seed, pid, 1, S_INIT, m->d, z);
+    normals_at(seed, pid, 1, stream, base, m->d, z);
     for (int i = 0; i < m->d; ++i) {
       double acc = m->mu0[i];
       for (int k = 0; k <= i; ++k) acc = fma(m->L0[i * m->d + k], z[k], acc);
@@ -343,14 +349,14 @@ static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const
     return lgssm_obs(m, x, o);
   } else if (m->family == ORC_KITAGAWA) {
     double z[2];
-    orc_normals(seed, pid, 1, S_INIT, 1, z);
+    normals_at(seed, pid, 1, stream, base, 1, z);
     x[0] = m->mu1 + m->s1 * z[0];
     if (!o->present) return 0.0;
     double diff = o->bt[0] - x[0] * x[0] / 20.0;
     return -(diff * diff) * m->inv2vy + m->csty;
   } else {
     uint32_t w[4];
-    rng(seed, pid, 1, S_INIT, 0, w);
+    rng(seed, pid, 1, stream, base, w);
     double u = unif53(w[0], w[1]);
     int K = m->k;
     if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
@@ -370,10 +376,11 @@ static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const
 
 /* update at step t >= 2 from previous latent xp: writes x, returns increment */
 static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t,
-                            const obs_t* o, int proposal, const double* xp, double* x) {
+                            const obs_t* o, int proposal, const double* xp, double* x, uint32_t stream,
+                            uint32_t base) {
   if (m->family == ORC_LGSSM) {
     double z[64];
-    orc_normals(seed, pid, t, S_STEP, m->d, z);
+    normals_at(seed, pid, t, stream, base, m->d, z);
     int d = m->d;
     for (int i = 0; i < d; ++i) {
       double acc = m->b[i];
@@ -385,7 +392,7 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
     return lgssm_obs(m, x, o);
   } else if (m->family == ORC_KITAGAWA) {
     double z[2];
-    orc_normals(seed, pid, t, S_STEP, 1, z);
+    normals_at(seed, pid, t, stream, base, 1, z);
     double v = xp[0];
     double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o->ct;
     x[0] = mean + m->sx * z[0];
@@ -394,7 +401,7 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
     return -(diff * diff) * m->inv2vy + m->csty;
   } else {
     uint32_t w[4];
-    rng(seed, pid, t, S_STEP, 0, w);
+    rng(seed, pid, t, stream, base, w);
     double u = unif53(w[0], w[1]);
     int K = m->k, zp = (int)xp[0];
     if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
@@ -426,6 +433,8 @@ struct orc_pf {
   double* anc_state;    /* [d][n] ancestor states after a (distributed) resample */
   int pending;          /* resampled since the last step */
   double log_ml_est;
+  obs_t obs;            /* observation of the current step (rejuvenation) */
+  uint32_t moves;       /* rejuvenation moves applied at the current step */
   /* history */
   int cap;
   double** hx;
@@ -481,13 +490,15 @@ int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
   int D = pf->m.d;
   double x[64];
   for (int64_t i = 0; i < pf->n; ++i) {
-    pf->logw[i] = particle_init(&pf->m, pf->seed, (uint64_t)(pf->lo + i), &o, proposal, x);
+    pf->logw[i] = particle_init(&pf->m, pf->seed, (uint64_t)(pf->lo + i), &o, proposal, x, S_INIT, 0);
     for (int k = 0; k < D; ++k) pf->x[(size_t)k * pf->n + i] = x[k];
     pf->anc[i] = pf->lo + i;
   }
   pf->t = 1;
   pf->pending = 0;
   pf->log_ml_est = 0.0;
+  pf->obs = o;
+  pf->moves = 0;
   record(pf);
   return 0;
 }
@@ -503,13 +514,15 @@ int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
   double xp[64], x[64];
   for (int64_t i = 0; i < n; ++i) {
     for (int k = 0; k < D; ++k) xp[k] = pf->xprev[(size_t)k * n + i];
-    double inc = particle_step(&pf->m, pf->seed, (uint64_t)(pf->lo + i), t, &o, proposal, xp, x);
+    double inc = particle_step(&pf->m, pf->seed, (uint64_t)(pf->lo + i), t, &o, proposal, xp, x, S_STEP, 0);
     for (int k = 0; k < D; ++k) pf->x[(size_t)k * n + i] = x[k];
     pf->logw[i] = (pf->pending ? 0.0 : pf->logw[i]) + inc;
   }
   int was = pf->pending;
   pf->pending = 0;
   pf->t = (int)t;
+  pf->obs = o;
+  pf->moves = 0;
   record(pf);
   if (pf->record_history) {
     pf->hres[t - 1] = was;
@@ -518,6 +531,57 @@ int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
       for (int64_t i = 0; i < n; ++i) pf->hanc[t - 1][i] = (int32_t)pf->anc[i];
     }
   }
+  return 0;
+}
+
+/* log p(y_t | x_t): the step's weight increment under the prior proposal */
+static double model_loglik(const model_t* m, const obs_t* o, const double* x) {
+  if (m->family == ORC_LGSSM) return lgssm_obs(m, x, o);
+  if (!o->present) return 0.0;
+  if (m->family == ORC_KITAGAWA) {
+    double diff = o->bt[0] - x[0] * x[0] / 20.0;
+    return -(diff * diff) * m->inv2vy + m->csty;
+  }
+  return m->logE[(int)o->bt[0] * m->k + (int)x[0]];
+}
+
+/* Rejuvenation: mh(trace, select(x_t)) on every particle (src/inference/mh.jl:14-26):
+   regenerate x_t from its prior given the parent state x_{t-1} (the states the
+   last step read, pf->xprev), weight = log p(y|x') - log p(y|x), accept iff
+   log(u) < weight.  Move m uses the MH stream's draws [16 m, 16 m + 8) for the
+   proposal and draw 16 m + 15 for u. */
+int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted) {
+  if (pf->pending || pf->t < 1 || n_moves < 0 || pf->moves + (uint32_t)n_moves > 4096) return -1;
+  const int D = pf->m.d;
+  const int64_t n = pf->n;
+  const uint32_t t = (uint32_t)pf->t;
+  int64_t acc = 0;
+  double x[64], xp[64], y[64];
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t pid = (uint64_t)(pf->lo + i);
+    for (int k = 0; k < D; ++k) x[k] = pf->x[(size_t)k * n + i];
+    if (t >= 2)
+      for (int k = 0; k < D; ++k) xp[k] = pf->xprev[(size_t)k * n + i];
+    double ll = model_loglik(&pf->m, &pf->obs, x);
+    for (int m = 0; m < n_moves; ++m) {
+      const uint32_t base = (pf->moves + (uint32_t)m) * 16u;
+      const double ll2 = t == 1 ? particle_init(&pf->m, pf->seed, pid, &pf->obs, 0, y, S_MH, base)
+                                : particle_step(&pf->m, pf->seed, pid, t, &pf->obs, 0, xp, y, S_MH, base);
+      uint32_t w[4];
+      rng(pf->seed, pid, t, S_MH, base + 15u, w);
+      const double logu = orc_log(unif53(w[0], w[1]));
+      if (logu < ll2 - ll) {
+        for (int k = 0; k < D; ++k) x[k] = y[k];
+        ll = ll2;
+        ++acc;
+      }
+    }
+    for (int k = 0; k < D; ++k) pf->x[(size_t)k * n + i] = x[k];
+  }
+  pf->moves += (uint32_t)n_moves;
+  if (pf->record_history && pf->hx && pf->hx[t - 1])
+    memcpy(pf->hx[t - 1], pf->x, sizeof(double) * (size_t)D * n);
+  if (accepted) *accepted = acc;
   return 0;
 }
 
@@ -687,7 +751,7 @@ int orc_importance_sampling(int family, int d, int dy, int k, int v, const doubl
   double x[64];
   double M = -INFINITY;
   for (int64_t i = 0; i < n; ++i) {
-    lnw[i] = particle_init(&m, seed, (uint64_t)i, &o, proposal, x);
+    lnw[i] = particle_init(&m, seed, (uint64_t)i, &o, proposal, x, S_INIT, 0);
     for (int kk = 0; kk < m.d; ++kk) states[(size_t)kk * n + i] = x[kk];
     if (lnw[i] > M) M = lnw[i];
   }

@@ -60,6 +60,9 @@ int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal);
 int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal);
 /* single-rank maybe_resample!: returns 1/0, or -1 on numeric error */
 int orc_pf_maybe_resample(orc_pf* pf, double ess_threshold, double* ess_out);
+/* rejuvenation: n_moves mh(trace, select(x_t)) moves per particle (src/inference/mh.jl:14-26);
+   -1 if a resample is pending */
+int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted);
 double orc_pf_log_ml_estimate(orc_pf* pf);
 void orc_pf_get_log_weights(orc_pf* pf, double* out);     /* n_local */
 void orc_pf_get_state(orc_pf* pf, double* out);           /* [d][n_local] */

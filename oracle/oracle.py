@@ -49,6 +49,7 @@ def lib():
             "orc_pf_init": (I, [V, D, I, I]),
             "orc_pf_step": (I, [V, D, I, I]),
             "orc_pf_maybe_resample": (I, [V, c_double, D]),
+            "orc_pf_rejuvenate": (I, [V, I, POINTER(c_int64)]),
             "orc_pf_log_ml_estimate": (c_double, [V]),
             "orc_pf_get_log_weights": (None, [V, D]),
             "orc_pf_get_state": (None, [V, D]),
@@ -140,6 +141,13 @@ class OraclePF:
         if r < 0:
             raise FloatingPointError("oracle: all log-weights are -Inf/NaN")
         return bool(r), ess.value
+
+    def rejuvenate(self, n_moves):
+        """n_moves mh(trace, select(x_t)) moves on every particle; returns accepted moves."""
+        acc = c_int64()
+        if lib().orc_pf_rejuvenate(self.h, n_moves, ctypes.byref(acc)):
+            raise RuntimeError("oracle: rejuvenate after a resample / too many moves")
+        return acc.value
 
     def log_ml_estimate(self):
         return lib().orc_pf_log_ml_estimate(self.h)

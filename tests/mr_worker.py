@@ -35,6 +35,7 @@ def main():
     p.add_argument("--thr", type=float, default=0.0)
     p.add_argument("--seed", type=int, default=9)
     p.add_argument("--transport", default="gloo")
+    p.add_argument("--rejuv", type=int, default=0, help="rejuvenation moves after init and every step")
     p.add_argument("--out", required=True)
     a = p.parse_args()
 
@@ -57,10 +58,14 @@ def main():
     _, ys = m.simulate(a.T, np.random.default_rng(5))
     addr = m.obs_address
     st = gen.initialize_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, seed=a.seed)
+    if a.rejuv:
+        gen.rejuvenate(st, a.rejuv)
     did = []
     for t in range(2, a.T + 1):
         did.append(gen.maybe_resample(st, a.thr if a.thr > 0 else None))
         gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})
+        if a.rejuv:
+            gen.rejuvenate(st, a.rejuv)
     lml = gen.log_ml_estimate(st)
     np.savez(
         f"{a.out}.rank{rank}.npz",
