@@ -6,7 +6,7 @@ inference API (src/inference/particle_filter.jl, importance.jl); see
 DESIGN.md.  Importing it does not touch the GPU; the first call does.
 """
 from .choicemap import ChoiceMap, EmptyChoiceMap, choicemap
-from .models import DiscreteHMM, KitagawaSSM, LinearGaussianSSM, Model
+from .models import BayesianLinearRegression, DiscreteHMM, KitagawaSSM, LinearGaussianSSM, Model
 from .pf import (
     Context,
     NoChange,
@@ -31,7 +31,7 @@ from .pf import (
 from ._lib import GenHipError
 
 __all__ = [
-    "ChoiceMap", "EmptyChoiceMap", "choicemap", "DiscreteHMM", "KitagawaSSM", "LinearGaussianSSM", "Model",
+    "ChoiceMap", "EmptyChoiceMap", "choicemap", "BayesianLinearRegression", "DiscreteHMM", "KitagawaSSM", "LinearGaussianSSM", "Model",
     "Context", "NoChange", "OptimalProposal", "ParticleFilterState", "UnknownChange", "default_context",
     "get_log_weights", "get_traces", "importance_resampling", "importance_sampling",
     "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",

@@ -23,7 +23,7 @@ STATUS = {
     7: "GH_E_STATE",
 }
 
-FAMILY_LGSSM, FAMILY_HMM, FAMILY_KITAGAWA = 1, 2, 3
+FAMILY_LGSSM, FAMILY_HMM, FAMILY_KITAGAWA, FAMILY_REGRESSION = 1, 2, 3, 4
 RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = 0, 1
 PROPOSAL_DEFAULT, PROPOSAL_OPTIMAL = 0, 1
 

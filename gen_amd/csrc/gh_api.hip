@@ -301,6 +301,7 @@ struct gh_model {
   int lg_struct = 0;  // LGModel<D, S> structure bits (gh_models.h)
   HMMParams hmm{};
   KitParams kit{};
+  RegParams reg{};
 };
 
 static bool lg_supported(int d) { return (d >= 1 && d <= 8) || d == 10 || d == 12 || d == 16; }
@@ -372,6 +373,23 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->kit.inv2vy = 1.0 / (2.0 * p[3]);
     m->kit.csty = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * p[3]);
     h.push_back(0.0);
+  } else if (desc->family == GH_FAMILY_REGRESSION) {
+    const int n = desc->dy;
+    if (n < 1 || n > kMaxObs) return fail(GH_E_INVAL, "regression: dy (data points) must be in 1..32");
+    if (desc->n_params < 5 + (int64_t)n) return fail(GH_E_INVAL, "regression: need mu_s sd_s mu_i sd_i sigma x[dy]");
+    if (!(p[1] > 0.0) || !(p[3] > 0.0) || !(p[4] > 0.0))
+      return fail(GH_E_INVAL, "regression: standard deviations must be > 0");
+    m->d = 2;
+    m->reg.mu_s = p[0];
+    m->reg.sd_s = p[1];
+    m->reg.mu_i = p[2];
+    m->reg.sd_i = p[3];
+    const double var = p[4] * p[4];
+    m->reg.inv2v = 1.0 / (2.0 * var);
+    m->reg.cst = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * var);
+    m->reg.n = n;
+    for (int i = 0; i < n; ++i) m->reg.xs[i] = p[5 + i];
+    h.push_back(0.0);
   } else {
     return fail(GH_E_INVAL, "unknown family");
   }
@@ -425,6 +443,9 @@ static int make_obs(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
     double r[kMaxObs];
     for (int i = 0; i < m->dy; ++i) r[i] = in->values[i] - m->c[i];
     fwdsub(m->dy, 1, m->LR.data(), r, o->v);
+  } else if (m->family == GH_FAMILY_REGRESSION) {
+    if (in->n_values != m->dy) return set_err(GH_E_INVAL, "observation has %d values, expected %d", in->n_values, m->dy);
+    for (int i = 0; i < m->dy; ++i) o->v[i] = in->values[i];
   } else if (m->family == GH_FAMILY_HMM) {
     const double s = in->values[0];
     if (!(s >= 0.0) || s >= (double)m->v || s != floor(s))
@@ -677,6 +698,10 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
       break;
     case GH_FAMILY_HMM: launch_step_t<HMMModel>(pf, m->hmm, o, a, init, e0, e1); break;
     case GH_FAMILY_KITAGAWA: launch_step_t<KitModel>(pf, m->kit, o, a, init, e0, e1); break;
+    case GH_FAMILY_REGRESSION:
+      if (!init) return set_err(GH_E_INVAL, "the regression model has no time steps");
+      launch_step_t<RegModel>(pf, m->reg, o, a, init, e0, e1);
+      break;
     default: return set_err(GH_E_INVAL, "unknown family");
   }
   HIP_TRY(hipGetLastError());
@@ -833,6 +858,8 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
   if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family != GH_FAMILY_HMM)
     return set_err(GH_E_INVAL, "the optimal proposal is implemented for HMM only");
+  if (pf->m->family == GH_FAMILY_REGRESSION)
+    return set_err(GH_E_INVAL, "the regression model has no time steps (particle_filter_step needs an Unfold)");
   const int t = pf->t + 1;
   CHECK(grow_for_step(pf, t));
   StepObs o;
@@ -1377,6 +1404,7 @@ static int launch_rejuv(gh_pf* pf, const RejuvArgs& a, bool init) {
       break;
     case GH_FAMILY_HMM: launch_rejuv_t<HMMModel>(pf, m->hmm, a, init); break;
     case GH_FAMILY_KITAGAWA: launch_rejuv_t<KitModel>(pf, m->kit, a, init); break;
+    case GH_FAMILY_REGRESSION: launch_rejuv_t<RegModel>(pf, m->reg, a, init); break;
     default: return set_err(GH_E_INVAL, "unknown family");
   }
   HIP_TRY(hipGetLastError());

@@ -289,4 +289,50 @@ struct KitModel {
   }
 };
 
+// ------------------------------------------------- Bayesian linear regression
+// examples/regression/quickstart.jl:3-9 (config C1):
+//   slope ~ normal(mu_s, sd_s); intercept ~ normal(mu_i, sd_i);
+//   y_i ~ normal(slope * x_i + intercept, sigma), i = 1..n (n <= kMaxObs)
+// A static model (no Unfold): generate only (importance sampling), plus
+// rejuvenation moves at t = 1.  State = (slope, intercept).
+struct RegParams {
+  double mu_s, sd_s, mu_i, sd_i;
+  double inv2v;  // 1 / (2 sigma^2)
+  double cst;    // -0.5 log(2 pi sigma^2)
+  int n;
+  double xs[kMaxObs];
+  __device__ RegParams rebase(const double* __restrict__) const { return *this; }
+};
+
+struct RegModel {
+  static constexpr int kD = 2;
+  static constexpr int kMinWaves = 8;
+  using Params = RegParams;
+
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) {
+    if (!o.present) return 0.0;
+    double s = 0.0;
+    for (int i = 0; i < p.n; ++i) {
+      const double diff = o.v[i] - (x[0] * p.xs[i] + x[1]);
+      s += -(diff * diff) * p.inv2v + p.cst;
+    }
+    return s;
+  }
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
+    double z0, z1;
+    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1);
+    x[0] = p.mu_s + p.sd_s * z0;
+    x[1] = p.mu_i + p.sd_i * z1;
+    return loglik(p, o, x);
+  }
+  // no time structure: the host refuses particle_filter_step for this family
+  __device__ static double step(const Params&, const StepObs&, uint64_t, uint64_t, uint32_t, int,
+                                const double* xp, double* x, Draw = {STREAM_STEP, 0}) {
+    x[0] = xp[0];
+    x[1] = xp[1];
+    return 0.0;
+  }
+};
+
 }  // namespace gh

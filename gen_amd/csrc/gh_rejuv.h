@@ -12,16 +12,21 @@
 // proposal.  At t = 1 the prior is the initial-state distribution.
 //
 // One particle per lane; the current state and its parent's state live in
-// registers for all moves.  Move m of step t draws its proposal from the MH
-// stream at draw offset (move0 + m) * kRejuvDraws and its acceptance uniform
-// from the last draw of that window.
+// registers for all moves.  Move w (counted from the step) draws its proposal
+// from draw window (w mod 4096) * kRejuvDraws of stream STREAM_MH + 16 (w / 4096)
+// and its acceptance uniform from the last draw of that window;
+// the first 4096 moves use the MH stream itself.
 #pragma once
 #include "gh_kernels.h"
 
 namespace gh {
 
-constexpr uint32_t kRejuvDraws = 16;      // draw window per move (LG d <= 16 uses 8)
-constexpr uint32_t kRejuvMaxMoves = 4096; // 16-bit draw field / kRejuvDraws
+constexpr uint32_t kRejuvDraws = 16;           // draw window per move (LG d <= 16 uses 8)
+constexpr uint32_t kRejuvMaxMoves = 1u << 24;  // 4096 windows x 4096 stream blocks
+
+__device__ __host__ __forceinline__ Draw rejuv_draw(uint32_t w) {
+  return Draw{(uint32_t)STREAM_MH + ((w >> 12) << 4), (w & 4095u) * kRejuvDraws};
+}
 
 struct RejuvArgs {
   const double* xprev;    // [D][ld_prev] states of step t-1 (t >= 2)
@@ -64,12 +69,11 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
     }
     double ll = Model::loglik(p, o, x);
     for (int m = 0; m < a.n_moves; ++m) {
-      const uint32_t base = (a.move0 + (uint32_t)m) * kRejuvDraws;
-      const Draw dr{STREAM_MH, base};
+      const Draw dr = rejuv_draw(a.move0 + (uint32_t)m);
       // the prior proposal's weight increment is the observation log-density
       const double ll2 = INIT ? Model::init(p, o, a.seed, pid, 0, y, dr)
                               : Model::step(p, o, a.seed, pid, a.t, 0, xp, y, dr);
-      const u32x4 w = rng_block(a.seed, pid, a.t, STREAM_MH, base + kRejuvDraws - 1);
+      const u32x4 w = rng_block(a.seed, pid, a.t, dr.stream, dr.base + kRejuvDraws - 1);
       const double logu = gh_log(u53(w.x, w.y));
       if (logu < ll2 - ll) {
 #pragma unroll

@@ -11,6 +11,7 @@ Address schemes follow the reference programs they mirror:
   DiscreteHMM        :z_init, :x_init, :chain => t-1 => :z / :x
                      (test/inference/particle_filter.jl:66-78)
   KitagawaSSM        :chain => t => :x / :y   (examples/pmmh/model.jl:40-50)
+  BayesianLinearRegression  :slope, :intercept, "y-$i"   (examples/regression/quickstart.jl:3-9)
 """
 from __future__ import annotations
 
@@ -27,6 +28,7 @@ class Model:
     v: int = 0
     latent_name = "x"
     obs_name = "y"
+    static = False  # True: no Unfold (generate only, model_args are the data)
 
     def params(self) -> np.ndarray:
         raise NotImplementedError
@@ -36,6 +38,18 @@ class Model:
 
     def latent_address(self, t: int):
         return ("chain", t, self.latent_name)
+
+    def obs_from_choicemap(self, cm, t: int):
+        """The observation of step t in a choice map (None if absent).  Any
+        other constrained address would update or delete an existing choice,
+        which the PF step forbids (particle_filter.jl:168-170)."""
+        addr = self.obs_address(t)
+        for a, _ in cm:
+            if a != addr:
+                raise _lib.GenHipError(
+                    2, f"constraint at {a}: only {addr} may be constrained in step {t} (discard must be empty)"
+                )
+        return cm.get(addr)
 
     def obs_values(self, value) -> np.ndarray:
         return np.ascontiguousarray(np.atleast_1d(np.asarray(value, dtype=np.float64)).ravel())
@@ -162,3 +176,78 @@ class KitagawaSSM(Model):
             xs[t - 1] = x
             ys[t - 1] = rng.normal(x * x / 20.0, np.sqrt(self.var_y))
         return xs, ys
+
+
+class BayesianLinearRegression(Model):
+    """examples/regression/quickstart.jl:3-9 (config C1), a static model:
+        slope = @trace(normal(mu_s, sd_s), :slope)
+        intercept = @trace(normal(mu_i, sd_i), :intercept)
+        @trace(normal(slope * x_i + intercept, sigma), "y-$i")   for i = 1..n
+    State (d = 2) = (slope, intercept); at most 32 data points per model."""
+
+    family = _lib.FAMILY_REGRESSION
+    d = 2
+    static = True
+
+    def __init__(self, xs, prior_slope=(0.0, 2.0), prior_intercept=(0.0, 10.0), sigma: float = 1.0):
+        self.xs = np.ascontiguousarray(np.asarray(xs, dtype=np.float64).ravel())
+        self.dy = self.xs.size
+        if not 1 <= self.dy <= 32:
+            raise ValueError("1..32 data points")
+        self.mu_s, self.sd_s = map(float, prior_slope)
+        self.mu_i, self.sd_i = map(float, prior_intercept)
+        self.sigma = float(sigma)
+
+    def params(self):
+        return np.concatenate([[self.mu_s, self.sd_s, self.mu_i, self.sd_i, self.sigma], self.xs])
+
+    def obs_address(self, t: int = 1):
+        return None  # several addresses: "y-1" .. "y-n"
+
+    def y_address(self, i: int):
+        return (f"y-{i}",)
+
+    def obs_from_choicemap(self, cm, t: int):
+        ys = np.full(self.dy, np.nan)
+        seen = 0
+        for a, v in cm:
+            name = a[0] if len(a) == 1 and isinstance(a[0], str) else None
+            i = int(name[2:]) if name and name.startswith("y-") and name[2:].isdigit() else 0
+            if not 1 <= i <= self.dy:
+                raise _lib.GenHipError(2, f"constraint at {a}: the model observes \"y-1\" .. \"y-{self.dy}\" only")
+            ys[i - 1] = float(v)
+            seen += 1
+        if seen == 0:
+            return None
+        if seen != self.dy:
+            raise _lib.GenHipError(1, "constrain every y-i (partial observations are not lowered)")
+        return ys
+
+    def constraints(self, ys):
+        return {self.y_address(i + 1): float(y) for i, y in enumerate(ys)}
+
+    def log_marginal(self, ys) -> float:
+        """Exact log p(ys): y ~ N(X m0, X S0 X' + sigma^2 I), X = [x 1]."""
+        X = np.stack([self.xs, np.ones_like(self.xs)], axis=1)
+        m0 = np.array([self.mu_s, self.mu_i])
+        S0 = np.diag([self.sd_s**2, self.sd_i**2])
+        C = X @ S0 @ X.T + self.sigma**2 * np.eye(self.dy)
+        r = np.asarray(ys, dtype=np.float64) - X @ m0
+        _, logdet = np.linalg.slogdet(C)
+        return float(-0.5 * (r @ np.linalg.solve(C, r) + logdet + self.dy * np.log(2 * np.pi)))
+
+    def posterior(self, ys):
+        """Exact posterior mean and covariance of (slope, intercept)."""
+        X = np.stack([self.xs, np.ones_like(self.xs)], axis=1)
+        P0 = np.diag([1 / self.sd_s**2, 1 / self.sd_i**2])
+        P = P0 + X.T @ X / self.sigma**2
+        S = np.linalg.inv(P)
+        mean = S @ (P0 @ np.array([self.mu_s, self.mu_i]) + X.T @ np.asarray(ys) / self.sigma**2)
+        return mean, S
+
+    @staticmethod
+    def quickstart() -> tuple["BayesianLinearRegression", np.ndarray]:
+        """The model and literal data of quickstart.jl:26-27."""
+        xs = np.arange(1.0, 11.0)
+        ys = np.array([8.23, 5.87, 3.99, 2.59, 0.23, -0.66, -3.53, -6.91, -7.24, -9.90])
+        return BayesianLinearRegression(xs), ys

@@ -136,16 +136,7 @@ def _step_obs(model: Model, t: int, observations) -> tuple[_lib.Obs, np.ndarray 
         val = None
     elif isinstance(observations, (ChoiceMap, dict)):
         cm = observations if isinstance(observations, ChoiceMap) else ChoiceMap(observations)
-        addr = model.obs_address(t)
-        for a, _ in cm:
-            if a != addr:
-                # Any other constrained address would update or delete an
-                # existing choice, which the PF step forbids
-                # (particle_filter.jl:168-170) or the model does not have.
-                raise _lib.GenHipError(
-                    2, f"constraint at {a}: only {addr} may be constrained in step {t} (discard must be empty)"
-                )
-        val = cm.get(addr)
+        val = model.obs_from_choicemap(cm, t)
     else:
         val = observations
     if val is None:
@@ -293,7 +284,7 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
         proposal, _, num_particles = args
     else:
         raise TypeError("expected (num_particles) or (proposal, proposal_args, num_particles)")
-    if tuple(model_args)[:1] not in ((1,), ()):
+    if not model.static and tuple(model_args)[:1] not in ((1,), ()):
         raise _lib.GenHipError(1, "the particle filter starts at model_args = (1,)")
     ctx = ctx or default_context()
     mh = ctx.model_handle(model)

@@ -68,7 +68,14 @@ typedef enum {
   /* nonlinear "Kitagawa" SSM (examples/pmmh/model.jl:9-13,40-46):
      x_1 ~ normal(mu1, s1); x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sqrt(var_x));
      y_t ~ normal(x_t^2/20, sqrt(var_y));  params: mu1 s1 var_x var_y */
-  GH_FAMILY_KITAGAWA = 3
+  GH_FAMILY_KITAGAWA = 3,
+  /* Bayesian linear regression (examples/regression/quickstart.jl:3-9), a static
+     model (generate / importance sampling / rejuvenation; no steps):
+     slope ~ normal(mu_s, sd_s); intercept ~ normal(mu_i, sd_i);
+     y_i ~ normal(slope x_i + intercept, sigma), i = 1..dy (dy <= 32 data points)
+     params: mu_s sd_s mu_i sd_i sigma x[dy]; the observation is y[dy];
+     state (d = 2) = (slope, intercept) */
+  GH_FAMILY_REGRESSION = 4
 } gh_family;
 
 typedef enum { GH_RESAMPLE_SYSTEMATIC = 0, GH_RESAMPLE_MULTINOMIAL = 1 } gh_resampler;
@@ -168,7 +175,7 @@ int gh_pf_sample_unweighted(gh_pf* pf, int64_t n_samples, uint64_t seed, int64_t
    current latent x_t from its prior given x_{t-1} (x_1 from the initial
    distribution) and accepting with log(rand()) < log p(y_t|x'_t) - log p(y_t|x_t).
    Log weights are unchanged.  Call after gh_pf_init / gh_pf_step and before
-   gh_pf_maybe_resample (GH_E_STATE otherwise); at most 4096 moves per step.
+   gh_pf_maybe_resample (GH_E_STATE otherwise); at most 2^24 moves per step.
    *accepted (optional, synchronises) = accepted moves summed over the local
    particles. */
 int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted);

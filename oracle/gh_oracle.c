@@ -223,6 +223,9 @@ typedef struct {
   double *prior, *T, *E, *logE;
   /* Kitagawa */
   double mu1, s1, sx, inv2vy, csty;
+  /* regression (quickstart.jl:3-9): priors, 1/(2 sigma^2), -0.5 log(2 pi sigma^2), xs */
+  double mu_s, sd_s, mu_i, sd_i, inv2v, cst;
+  double xs[32];
 } model_t;
 
 static void model_free(model_t* m) {
@@ -273,6 +276,14 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->sx = sqrt(p[2]);
     m->inv2vy = 1.0 / (2.0 * p[3]);
     m->csty = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * p[3]);
+  } else if (family == ORC_REGRESSION) {
+    if (dy < 1 || dy > 32 || np < 5 + (int64_t)dy) return -1;
+    m->d = 2;
+    m->mu_s = p[0]; m->sd_s = p[1]; m->mu_i = p[2]; m->sd_i = p[3];
+    double var = p[4] * p[4];
+    m->inv2v = 1.0 / (2.0 * var);
+    m->cst = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * var);
+    for (int i = 0; i < dy; ++i) m->xs[i] = p[5 + i];
   } else {
     return -1;
   }
@@ -295,6 +306,8 @@ static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* 
     double r[64];
     for (int i = 0; i < m->dy; ++i) r[i] = y[i] - m->c[i];
     fwdsub(m->dy, 1, m->LR, r, o->bt);
+  } else if (m->family == ORC_REGRESSION) {
+    for (int i = 0; i < m->dy; ++i) o->bt[i] = y[i];
   } else {
     o->bt[0] = y[0];
   }
@@ -334,10 +347,28 @@ static int cat_sample(const double* p, int K, int stride, double u) {
 }
 
 /* generate at t = 1: writes x[d], returns the log weight */
+/* sum_i normal(y_i; slope x_i + intercept, sigma) logpdf, in data order */
+static double reg_loglik(const model_t* m, const obs_t* o, const double* x) {
+  if (!o->present) return 0.0;
+  double s = 0.0;
+  for (int i = 0; i < m->dy; ++i) {
+    double diff = o->bt[i] - (x[0] * m->xs[i] + x[1]);
+    s += -(diff * diff) * m->inv2v + m->cst;
+  }
+  return s;
+}
+
 /* draws come from (stream, base + j): the filter uses (S_INIT / S_STEP, 0),
    rejuvenation moves (S_MH, 16 * move) */
 static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
                             int proposal, double* x, uint32_t stream, uint32_t base) {
+  if (m->family == ORC_REGRESSION) {
+    double z[2];
+    normals_at(seed, pid, 1, stream, base, 2, z);
+    x[0] = m->mu_s + m->sd_s * z[0];
+    x[1] = m->mu_i + m->sd_i * z[1];
+    return reg_loglik(m, o, x);
+  }
   if (m->family == ORC_LGSSM) {
     double z[64];
     normals_at(seed, pid, 1, stream, base, m->d, z);
@@ -504,6 +535,7 @@ int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
 }
 
 int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+  if (pf->m.family == ORC_REGRESSION) return -1; /* a static model has no steps */
   uint32_t t = (uint32_t)(pf->t + 1);
   obs_t o;
   obs_build(&pf->m, (int)t, obs, has_obs, &o);
@@ -537,6 +569,7 @@ int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
 /* log p(y_t | x_t): the step's weight increment under the prior proposal */
 static double model_loglik(const model_t* m, const obs_t* o, const double* x) {
   if (m->family == ORC_LGSSM) return lgssm_obs(m, x, o);
+  if (m->family == ORC_REGRESSION) return reg_loglik(m, o, x);
   if (!o->present) return 0.0;
   if (m->family == ORC_KITAGAWA) {
     double diff = o->bt[0] - x[0] * x[0] / 20.0;
@@ -548,10 +581,10 @@ static double model_loglik(const model_t* m, const obs_t* o, const double* x) {
 /* Rejuvenation: mh(trace, select(x_t)) on every particle (src/inference/mh.jl:14-26):
    regenerate x_t from its prior given the parent state x_{t-1} (the states the
    last step read, pf->xprev), weight = log p(y|x') - log p(y|x), accept iff
-   log(u) < weight.  Move m uses the MH stream's draws [16 m, 16 m + 8) for the
-   proposal and draw 16 m + 15 for u. */
+   log(u) < weight.  Move w of the step uses stream S_MH + 16 (w / 4096), draws
+   [16 (w mod 4096), +8) for the proposal and draw 16 (w mod 4096) + 15 for u. */
 int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted) {
-  if (pf->pending || pf->t < 1 || n_moves < 0 || pf->moves + (uint32_t)n_moves > 4096) return -1;
+  if (pf->pending || pf->t < 1 || n_moves < 0 || (uint64_t)pf->moves + (uint64_t)n_moves > (1u << 24)) return -1;
   const int D = pf->m.d;
   const int64_t n = pf->n;
   const uint32_t t = (uint32_t)pf->t;
@@ -564,11 +597,12 @@ int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted) {
       for (int k = 0; k < D; ++k) xp[k] = pf->xprev[(size_t)k * n + i];
     double ll = model_loglik(&pf->m, &pf->obs, x);
     for (int m = 0; m < n_moves; ++m) {
-      const uint32_t base = (pf->moves + (uint32_t)m) * 16u;
-      const double ll2 = t == 1 ? particle_init(&pf->m, pf->seed, pid, &pf->obs, 0, y, S_MH, base)
-                                : particle_step(&pf->m, pf->seed, pid, t, &pf->obs, 0, xp, y, S_MH, base);
+      const uint32_t mv = pf->moves + (uint32_t)m;
+      const uint32_t stream = (uint32_t)S_MH + ((mv >> 12) << 4), base = (mv & 4095u) * 16u;
+      const double ll2 = t == 1 ? particle_init(&pf->m, pf->seed, pid, &pf->obs, 0, y, stream, base)
+                                : particle_step(&pf->m, pf->seed, pid, t, &pf->obs, 0, xp, y, stream, base);
       uint32_t w[4];
-      rng(pf->seed, pid, t, S_MH, base + 15u, w);
+      rng(pf->seed, pid, t, stream, base + 15u, w);
       const double logu = orc_log(unif53(w[0], w[1]));
       if (logu < ll2 - ll) {
         for (int k = 0; k < D; ++k) x[k] = y[k];

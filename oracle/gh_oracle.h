@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-enum { ORC_LGSSM = 1, ORC_HMM = 2, ORC_KITAGAWA = 3 };
+enum { ORC_LGSSM = 1, ORC_HMM = 2, ORC_KITAGAWA = 3, ORC_REGRESSION = 4 };
 enum { ORC_SYSTEMATIC = 0, ORC_MULTINOMIAL = 1 };
 enum { ORC_PROPOSAL_DEFAULT = 0, ORC_PROPOSAL_OPTIMAL = 1 };
 

@@ -17,7 +17,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-LGSSM, HMM, KITAGAWA = 1, 2, 3
+LGSSM, HMM, KITAGAWA, REGRESSION = 1, 2, 3, 4
 SYSTEMATIC, MULTINOMIAL = 0, 1
 DEFAULT, OPTIMAL = 0, 1
 
@@ -104,7 +104,7 @@ class OraclePF:
     def __init__(self, model, n_global, seed, resampler=SYSTEMATIC, lo=0, n_local=None, record_history=True):
         fam, d, dy, k, v, p = model_args(model)
         self._p = p
-        self.d = d if fam == LGSSM else 1
+        self.d = d if fam in (LGSSM, REGRESSION) else 1
         self.n_global = n_global
         self.lo = lo
         self.n = n_global if n_local is None else n_local
@@ -226,7 +226,7 @@ def combine_stats(stats, n_global, thr):
 def importance_sampling(model, y, n, seed, proposal=DEFAULT):
     fam, d, dy, k, v, p = model_args(model)
     a = None if y is None else np.ascontiguousarray(np.atleast_1d(np.asarray(y, dtype=np.float64)))
-    dd = d if fam == LGSSM else 1
+    dd = d if fam in (LGSSM, REGRESSION) else 1
     lnw = np.empty(n)
     st = np.empty((dd, n))
     lml = c_double()

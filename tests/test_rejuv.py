@@ -129,7 +129,7 @@ def test_gpu_rejuvenation_state_errors(gh_ctx):
     gen.particle_filter_step(st, (2,), (gen.UnknownChange(),), {m.obs_address(2): ys[1]})
     gen.rejuvenate(st, 4000)
     with pytest.raises(gen.GenHipError):
-        gen.rejuvenate(st, 97)  # 4096 moves per step at most
+        gen.rejuvenate(st, (1 << 24) - 3999)  # 2^24 moves per step at most
     assert gen.rejuvenate(st, 0) == 0
 
 
