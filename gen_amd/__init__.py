@@ -11,6 +11,11 @@ from .pf import (
     Context,
     NoChange,
     OptimalProposal,
+    conditional_particle_filter_step,
+    conditional_smc,
+    get_particle,
+    initialize_conditional_particle_filter,
+    particle_gibbs,
     ParticleFilterState,
     UnknownChange,
     default_context,
@@ -36,5 +41,6 @@ __all__ = [
     "get_log_weights", "get_traces", "importance_resampling", "importance_sampling",
     "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",
     "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
-    "GenHipError",
+    "conditional_particle_filter_step", "conditional_smc", "get_particle", "initialize_conditional_particle_filter",
+    "particle_gibbs", "GenHipError",
 ]

@@ -22,6 +22,7 @@
 #include "gh_pmmh.h"
 #include "gh_coal.h"
 #include "gh_rejuv.h"
+#include "gh_csmc.h"
 
 using namespace gh;
 
@@ -508,6 +509,9 @@ struct gh_pf {
   StepObs last_obs{};
   uint32_t rejuv_moves = 0;
   unsigned long long* acc_count = nullptr;
+  // conditional SMC (gh_csmc.h): particle 0 is pinned to a given trajectory
+  bool cond = false;
+  double* pin = nullptr;          // [D] this step's distinguished state, [D] its new log weight
   std::vector<void*> chunks;      // history allocations (record_history)
   // kernel timing
   std::vector<hipEvent_t> ev;
@@ -625,7 +629,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->tsum); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
-  hipFree(pf->acc_count);
+  hipFree(pf->acc_count); hipFree(pf->pin);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
   if (pf->h_plan) hipHostFree(pf->h_plan);
@@ -675,20 +679,21 @@ static int ensure_stats(gh_pf* pf) {
 // maybe_resample! was enqueued since the last step
 static int flags_live(const gh_pf* pf) { return pf->resample_calls > 0 ? 1 : 0; }
 
-static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init, hipEvent_t e0 = nullptr,
-                       hipEvent_t e1 = nullptr) {
-  gh_model* m = pf->m;
+// Call f(Model{}, params) with the device model type of m (the one switch
+// over families and instantiated LGSSM shapes).
+template <class F>
+static int with_model(const gh_model* m, F&& f) {
   switch (m->family) {
     case GH_FAMILY_LGSSM:
       switch (m->d) {
-#define GH_LG_CASE(DD)                                                                  \
-  case DD:                                                                              \
-    switch (m->lg_struct) {                                                             \
-      case 1: launch_step_t<LGModel<DD, 1>>(pf, m->lg, o, a, init, e0, e1); break;              \
-      case 2: launch_step_t<LGModel<DD, 2>>(pf, m->lg, o, a, init, e0, e1); break;              \
-      case 3: launch_step_t<LGModel<DD, 3>>(pf, m->lg, o, a, init, e0, e1); break;              \
-      default: launch_step_t<LGModel<DD, 0>>(pf, m->lg, o, a, init, e0, e1); break;             \
-    }                                                                                   \
+#define GH_LG_CASE(DD)                                   \
+  case DD:                                               \
+    switch (m->lg_struct) {                              \
+      case 1: f(LGModel<DD, 1>{}, m->lg); break;         \
+      case 2: f(LGModel<DD, 2>{}, m->lg); break;         \
+      case 3: f(LGModel<DD, 3>{}, m->lg); break;         \
+      default: f(LGModel<DD, 0>{}, m->lg); break;        \
+    }                                                    \
     break;
         GH_LG_CASE(1) GH_LG_CASE(2) GH_LG_CASE(3) GH_LG_CASE(4) GH_LG_CASE(5) GH_LG_CASE(6)
         GH_LG_CASE(7) GH_LG_CASE(8) GH_LG_CASE(10) GH_LG_CASE(12) GH_LG_CASE(16)
@@ -696,14 +701,21 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
         default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", m->d);
       }
       break;
-    case GH_FAMILY_HMM: launch_step_t<HMMModel>(pf, m->hmm, o, a, init, e0, e1); break;
-    case GH_FAMILY_KITAGAWA: launch_step_t<KitModel>(pf, m->kit, o, a, init, e0, e1); break;
-    case GH_FAMILY_REGRESSION:
-      if (!init) return set_err(GH_E_INVAL, "the regression model has no time steps");
-      launch_step_t<RegModel>(pf, m->reg, o, a, init, e0, e1);
-      break;
+    case GH_FAMILY_HMM: f(HMMModel{}, m->hmm); break;
+    case GH_FAMILY_KITAGAWA: f(KitModel{}, m->kit); break;
+    case GH_FAMILY_REGRESSION: f(RegModel{}, m->reg); break;
     default: return set_err(GH_E_INVAL, "unknown family");
   }
+  return GH_OK;
+}
+
+static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init, hipEvent_t e0 = nullptr,
+                       hipEvent_t e1 = nullptr) {
+  if (!init && pf->m->family == GH_FAMILY_REGRESSION)
+    return set_err(GH_E_INVAL, "the regression model has no time steps");
+  CHECK(with_model(pf->m, [&](auto model, const auto& p) {
+    launch_step_t<decltype(model)>(pf, p, o, a, init, e0, e1);
+  }));
   HIP_TRY(hipGetLastError());
   return GH_OK;
 }
@@ -742,8 +754,63 @@ static int share_stats(gh_pf* pf) {
   return comm_allgather(pf->ctx, pf->dev->stats, pf->stats_all, 3 * sizeof(double), pf->s);
 }
 
+// Conditional SMC: pin particle 0 around the step kernel (gh_csmc.h).  pre =
+// before the step (saves the new weight), post = after it.
+static int pin_launch(gh_pf* pf, const StepObs& o, bool init, bool pre) {
+  PinArgs a{};
+  a.ref = pf->pin;
+  a.w0 = pf->pin + pf->D;
+  a.dev = pf->dev;
+  a.resampled = flags_live(pf);
+  a.x = slot_x(pf, init ? 1 : pf->t + 1);
+  a.ld = pf->n;
+  a.logw = pf->logw;
+  a.n = pf->n;
+  a.pm = pf->pm;
+  a.ps = pf->ps;
+  a.ps2 = pf->ps2;
+  if (pre) {
+    CHECK(with_model(pf->m, [&](auto model, const auto& p) {
+      using M = decltype(model);
+      if (init)
+        hipLaunchKernelGGL((k_pin_pre<M, true>), dim3(1), dim3(64), 0, pf->s, (const double*)pf->m->dparams, p, o, a);
+      else
+        hipLaunchKernelGGL((k_pin_pre<M, false>), dim3(1), dim3(64), 0, pf->s, (const double*)pf->m->dparams, p, o,
+                           a);
+    }));
+  } else {
+    hipLaunchKernelGGL(k_pin_post, dim3(1), dim3(kBlock), 0, pf->s, a, pf->D);
+  }
+  HIP_TRY(hipGetLastError());
+  return GH_OK;
+}
+
+static int pin_upload(gh_pf* pf, const double* ref) {
+  if (!pf->pin) HIP_TRY(hipMalloc(&pf->pin, sizeof(double) * (pf->D + 1)));
+  HIP_TRY(hipMemcpyAsync(pf->pin, ref, sizeof(double) * pf->D, hipMemcpyHostToDevice, pf->s));
+  return GH_OK;
+}
+
+static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles, uint64_t seed,
+                        const gh_pf_opts* opts, const double* pin_ref, gh_pf** out);
+
 extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles,
                           uint64_t seed, const gh_pf_opts* opts, gh_pf** out) {
+  return pf_init_impl(m, obs, proposal, n_particles, seed, opts, nullptr, out);
+}
+
+extern "C" int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_particles, uint64_t seed,
+                                      const gh_pf_opts* opts, const double* ref_x1, gh_pf** out) {
+  if (!m || !ref_x1 || !out) return set_err(GH_E_INVAL, "gh_pf_init_conditional: null argument");
+  if (!opts || opts->resampler != GH_RESAMPLE_MULTINOMIAL)
+    return set_err(GH_E_INVAL, "conditional SMC uses multinomial resampling (examples/pmmh/smc.jl:132)");
+  if (m->ctx->world != 1) return set_err(GH_E_INVAL, "conditional SMC runs on one rank");
+  if (m->family == GH_FAMILY_REGRESSION) return set_err(GH_E_INVAL, "conditional SMC needs a state-space model");
+  return pf_init_impl(m, obs, GH_PROPOSAL_DEFAULT, n_particles, seed, opts, ref_x1, out);
+}
+
+static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles, uint64_t seed,
+                        const gh_pf_opts* opts, const double* pin_ref, gh_pf** out) {
   if (!m || !out) return set_err(GH_E_INVAL, "gh_pf_init: null argument");
   if (n_particles < 1 || n_particles > 0x7fffffffLL)
     return set_err(GH_E_INVAL, "gh_pf_init: num_particles must be in 1..2^31-1");
@@ -844,6 +911,13 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
   a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
   rc = timed_step(pf, o, a, true);
   if (rc) return fail(rc);
+  if (pin_ref) {
+    pf->cond = true;
+    rc = pin_upload(pf, pin_ref);
+    if (!rc) rc = pin_launch(pf, o, true, true);
+    if (!rc) rc = pin_launch(pf, o, true, false);
+    if (rc) return fail(rc);
+  }
   rc = share_stats(pf);
   if (rc) return fail(rc);
   pf->t = 1;
@@ -854,7 +928,20 @@ extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t 
 
 static int grow_for_step(gh_pf* pf, int t) { return ensure_capacity(pf, t + 1); }
 
+static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double* pin_ref);
+
 extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
+  if (pf && pf->cond) return set_err(GH_E_STATE, "a conditional filter steps with gh_pf_step_conditional");
+  return pf_step_impl(pf, obs, proposal, nullptr);
+}
+
+extern "C" int gh_pf_step_conditional(gh_pf* pf, const gh_obs* obs, const double* ref_xt) {
+  if (!pf || !ref_xt) return set_err(GH_E_INVAL, "gh_pf_step_conditional: null argument");
+  if (!pf->cond) return set_err(GH_E_STATE, "gh_pf_step_conditional on a filter not made by gh_pf_init_conditional");
+  return pf_step_impl(pf, obs, GH_PROPOSAL_DEFAULT, ref_xt);
+}
+
+static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double* pin_ref) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
   if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family != GH_FAMILY_HMM)
     return set_err(GH_E_INVAL, "the optimal proposal is implemented for HMM only");
@@ -888,7 +975,12 @@ extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   a.ps2 = pf->ps2;
   a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
   a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
+  if (pin_ref) {
+    CHECK(pin_upload(pf, pin_ref));
+    CHECK(pin_launch(pf, o, false, true));
+  }
   CHECK(timed_step(pf, o, a, false));
+  if (pin_ref) CHECK(pin_launch(pf, o, false, false));
   CHECK(share_stats(pf));
   pf->t = t;
   pf->resample_calls = 0;
@@ -1198,6 +1290,9 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
   if (pf->t < 1) return set_err(GH_E_STATE, "maybe_resample before init");
   if (!(thr > 0.0)) thr = (double)pf->n_global / 2.0;
   CHECK(resample_enqueue(pf, thr));
+  // conditional SMC: the distinguished particle's parent is itself (smc.jl:139);
+  // the ancestor array is only read if the resample fired
+  if (pf->cond) HIP_TRY(hipMemsetAsync(anc_for_step(pf, pf->t + 1), 0, sizeof(int32_t), pf->s));
   if (did || ess) {
     DevScalars h;
     HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
@@ -1383,30 +1478,7 @@ static void launch_rejuv_t(gh_pf* pf, const typename Model::Params& p, const Rej
 }
 
 static int launch_rejuv(gh_pf* pf, const RejuvArgs& a, bool init) {
-  gh_model* m = pf->m;
-  switch (m->family) {
-    case GH_FAMILY_LGSSM:
-      switch (m->d) {
-#define GH_LG_CASE(DD)                                                       \
-  case DD:                                                                   \
-    switch (m->lg_struct) {                                                  \
-      case 1: launch_rejuv_t<LGModel<DD, 1>>(pf, m->lg, a, init); break;     \
-      case 2: launch_rejuv_t<LGModel<DD, 2>>(pf, m->lg, a, init); break;     \
-      case 3: launch_rejuv_t<LGModel<DD, 3>>(pf, m->lg, a, init); break;     \
-      default: launch_rejuv_t<LGModel<DD, 0>>(pf, m->lg, a, init); break;    \
-    }                                                                        \
-    break;
-        GH_LG_CASE(1) GH_LG_CASE(2) GH_LG_CASE(3) GH_LG_CASE(4) GH_LG_CASE(5) GH_LG_CASE(6)
-        GH_LG_CASE(7) GH_LG_CASE(8) GH_LG_CASE(10) GH_LG_CASE(12) GH_LG_CASE(16)
-#undef GH_LG_CASE
-        default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", m->d);
-      }
-      break;
-    case GH_FAMILY_HMM: launch_rejuv_t<HMMModel>(pf, m->hmm, a, init); break;
-    case GH_FAMILY_KITAGAWA: launch_rejuv_t<KitModel>(pf, m->kit, a, init); break;
-    case GH_FAMILY_REGRESSION: launch_rejuv_t<RegModel>(pf, m->reg, a, init); break;
-    default: return set_err(GH_E_INVAL, "unknown family");
-  }
+  CHECK(with_model(pf->m, [&](auto model, const auto& p) { launch_rejuv_t<decltype(model)>(pf, p, a, init); }));
   HIP_TRY(hipGetLastError());
   return GH_OK;
 }
@@ -1420,6 +1492,7 @@ extern "C" int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted) {
   if (n_moves < 0) return set_err(GH_E_INVAL, "gh_pf_rejuvenate: n_moves < 0");
   if (pf->resample_calls > 0)
     return set_err(GH_E_STATE, "gh_pf_rejuvenate: call after a step and before maybe_resample");
+  if (pf->cond) return set_err(GH_E_STATE, "gh_pf_rejuvenate: the distinguished particle of a conditional filter is fixed");
   if ((uint64_t)pf->rejuv_moves + (uint64_t)n_moves > kRejuvMaxMoves)
     return set_err(GH_E_INVAL, "gh_pf_rejuvenate: more than %u moves at one step", kRejuvMaxMoves);
   HIP_TRY(hipSetDevice(pf->ctx->device));

@@ -187,6 +187,37 @@ __device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, u
 }
 
 // ---------------------------------------------------------------- k_step
+// Block partial of the step kernel: wave (max, sum, sum^2), then the 4 waves
+// through LDS; thread 0 stores the block's triple.
+__device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double* pm, double* ps, double* ps2) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double mw = wave_max(lw);
+  double e = 0.0;
+  if (lw > -INFINITY) e = gh_exp(lw - mw);
+  if (lw != lw) e = lw;  // NaN poisons the statistics
+  const double sw = wave_sum(e), s2w = wave_sum(e * e);
+  if (lane == 0) {
+    sm[0][w] = mw;
+    sm[1][w] = sw;
+    sm[2][w] = s2w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double mb = -INFINITY, sb = 0.0, s2b = 0.0;
+    for (int k = 0; k < 4; ++k) mb = fmax(mb, sm[0][k]);
+    if (mb > -INFINITY)
+      for (int k = 0; k < 4; ++k)
+        if (sm[0][k] > -INFINITY) {
+          const double f = gh_exp(sm[0][k] - mb);
+          sb += sm[1][k] * f;
+          s2b += sm[2][k] * (f * f);
+        }
+    *pm = mb;
+    *ps = sb;
+    *ps2 = s2b;
+  }
+}
+
 // One particle per lane, 64-particle tiles per wave, 4 waves per block.
 // Systematic ancestors come from the range marks by a wave-level prefix max
 // seeded with the carry of the tile's 64-slot group (no block barrier).  Each
@@ -261,32 +292,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   asm volatile("" ::"v"(lw));
   return;
 #endif
-  // block partial: wave (max, sum, sum^2), then the 4 waves through LDS
-  const double mw = wave_max(lw);
-  double e = 0.0;
-  if (lw > -INFINITY) e = gh_exp(lw - mw);
-  if (lw != lw) e = lw;  // NaN poisons the statistics
-  const double sw = wave_sum(e), s2w = wave_sum(e * e);
-  if (lane == 0) {
-    sm[0][w] = mw;
-    sm[1][w] = sw;
-    sm[2][w] = s2w;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double mb = -INFINITY, sb = 0.0, s2b = 0.0;
-    for (int k = 0; k < 4; ++k) mb = fmax(mb, sm[0][k]);
-    if (mb > -INFINITY)
-      for (int k = 0; k < 4; ++k)
-        if (sm[0][k] > -INFINITY) {
-          const double f = gh_exp(sm[0][k] - mb);
-          sb += sm[1][k] * f;
-          s2b += sm[2][k] * (f * f);
-        }
-    a.pm[blockIdx.x] = mb;
-    a.ps[blockIdx.x] = sb;
-    a.ps2[blockIdx.x] = s2b;
-  }
+  block_partial(lw, sm, a.pm + blockIdx.x, a.ps + blockIdx.x, a.ps2 + blockIdx.x);
 }
 
 // --------------------------------------------------------------- decision

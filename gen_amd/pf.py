@@ -380,6 +380,90 @@ def rejuvenate(state: ParticleFilterState, n_moves: int = 1) -> int:
     return int(acc.value)
 
 
+# ------------------------------------------------------ conditional SMC
+def _ref_state(model: Model, x) -> np.ndarray:
+    a = np.ascontiguousarray(np.atleast_1d(np.asarray(x, dtype=np.float64)).ravel())
+    if a.size != model.d:
+        raise _lib.GenHipError(1, f"a reference state has {model.d} values, got {a.size}")
+    return a
+
+
+def initialize_conditional_particle_filter(model: Model, model_args: tuple, observations, num_particles: int,
+                                           reference_x1, seed: int = 0, record_history: bool = True,
+                                           history_capacity: int = 0, ctx: Context | None = None
+                                           ) -> ParticleFilterState:
+    """conditional_smc's initialisation (examples/pmmh/smc.jl:110-119):
+    particle 0 is the distinguished particle, pinned to reference_x1 with
+    weight init_score = log p(y_1 | x_1); multinomial resampling."""
+    if tuple(model_args)[:1] not in ((1,), ()):
+        raise _lib.GenHipError(1, "the particle filter starts at model_args = (1,)")
+    ctx = ctx or default_context()
+    mh = ctx.model_handle(model)
+    obs, keep = _step_obs(model, 1, observations)
+    ref = _ref_state(model, reference_x1)
+    h = c_void_p()
+    opts = _opts("multinomial", record_history, history_capacity, 0)
+    _lib.check(_lib.load().gh_pf_init_conditional(mh, byref(obs), int(num_particles), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                                  byref(opts), _lib.dptr(ref), byref(h)))
+    del keep
+    return ParticleFilterState(ctx, model, h, int(num_particles))
+
+
+def conditional_particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: tuple, observations,
+                                     reference_xt) -> None:
+    """One step of conditional_smc (smc.jl:138-147): the distinguished particle
+    takes reference_xt, its own parent, weight += log p(y_t | x_t)."""
+    t = state.t + 1
+    if tuple(new_args)[:1] != (t,):
+        raise _lib.GenHipError(1, f"new_args must extend the Unfold by one step: expected ({t},), got {new_args}")
+    obs, keep = _step_obs(state.model, t, observations)
+    ref = _ref_state(state.model, reference_xt)
+    _lib.check(_lib.load().gh_pf_step_conditional(state.h, byref(obs), _lib.dptr(ref)))
+    del keep
+
+
+def conditional_smc(model: Model, observations_per_step, num_particles: int, reference, seed: int = 0,
+                    ess_threshold: float | None = None, ctx: Context | None = None) -> ParticleFilterState:
+    """conditional_smc(scheme, distinguished_particle) (smc.jl:100-151) with the
+    model's own proposal: the whole sweep, reference = [T, d] trajectory."""
+    T = len(observations_per_step)
+    ref = np.asarray(reference, dtype=np.float64).reshape(T, -1)
+    addr = model.obs_address
+    st = initialize_conditional_particle_filter(model, (1,), {addr(1): observations_per_step[0]}, num_particles,
+                                                ref[0], seed=seed, history_capacity=T, ctx=ctx)
+    for t in range(2, T + 1):
+        maybe_resample_async(st, ess_threshold)
+        conditional_particle_filter_step(st, (t,), (UnknownChange(),), {addr(t): observations_per_step[t - 1]},
+                                         ref[t - 1])
+    return st
+
+
+def get_particle(state: ParticleFilterState, index: int) -> np.ndarray:
+    """get_particle(result, final_index) (smc.jl:153-163): the [T, d] trajectory
+    of one final particle, following its ancestors back."""
+    T = state.t
+    return np.stack([state.states(t)[index] for t in range(1, T + 1)])
+
+
+def particle_gibbs(model: Model, observations_per_step, num_particles: int, reference, num_sweeps: int,
+                   seed: int = 0, ess_threshold: float | None = None, ctx: Context | None = None):
+    """Particle Gibbs: repeat {conditional_smc; draw a final particle with
+    probability proportional to its weight; take its trajectory as the next
+    reference}.  Returns the list of references after each sweep and the
+    log-ML estimates of the sweeps."""
+    refs, lmls = [], []
+    ref = np.asarray(reference, dtype=np.float64)
+    for k in range(num_sweeps):
+        st = conditional_smc(model, observations_per_step, num_particles, ref, seed=seed + 1000003 * k,
+                             ess_threshold=ess_threshold, ctx=ctx)
+        _, idx = sample_unweighted_traces(st, 1, seed=seed + 1000003 * k + 1)
+        ref = get_particle(st, int(idx[0]))
+        refs.append(ref)
+        lmls.append(log_ml_estimate(st))
+        st.close()
+    return refs, lmls
+
+
 def importance_sampling(model: Model, model_args: tuple, observations, *args, seed: int = 0,
                         ctx: Context | None = None):
     """(traces, log_normalized_weights, lml_est) (importance.jl:20-52)."""

@@ -17,6 +17,8 @@
  *   gh_pf_sample_unweighted sample_unweighted_traces     src/inference/particle_filter.jl:62-70
  *   gh_pf_rejuvenate        mh(trace, select(x_t)) on    src/inference/mh.jl:14-26 (applied per
  *                           every particle               particle, as callers of the PF do)
+ *   gh_pf_init_conditional /
+ *   gh_pf_step_conditional  conditional_smc              examples/pmmh/smc.jl:100-151
  *   gh_is_run               importance_sampling          src/inference/importance.jl:20-52
  *   gh_pmmh_run             PMMH (mh over a PF-estimated  examples/pmmh/example.jl:20-79,
  *                           likelihood)                   examples/pmmh/pf.jl:14-73
@@ -179,6 +181,15 @@ int gh_pf_sample_unweighted(gh_pf* pf, int64_t n_samples, uint64_t seed, int64_t
    *accepted (optional, synchronises) = accepted moves summed over the local
    particles. */
 int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted);
+/* Conditional SMC (examples/pmmh/smc.jl:100-151, the particle-Gibbs sweep):
+   particle 0 is the distinguished particle, pinned to ref_x1 at init and to
+   ref_xt at each step, its parent always itself, its weight the observation
+   log-density of the given state (init_score / forward_score of the model's
+   own proposal).  Requires opts->resampler == GH_RESAMPLE_MULTINOMIAL and one
+   rank.  Such a filter steps only with gh_pf_step_conditional. */
+int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_particles, uint64_t seed,
+                           const gh_pf_opts* opts, const double* ref_x1 /* [d] */, gh_pf** out);
+int gh_pf_step_conditional(gh_pf* pf, const gh_obs* obs, const double* ref_xt /* [d] */);
 /* per-step resampling record: ess and did_resample for steps 1..t */
 int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int32_t* did);
 /* average duration (ms) of the step kernel over the timed launches (opts.time_kernels) */

@@ -465,6 +465,7 @@ struct orc_pf {
   int pending;          /* resampled since the last step */
   double log_ml_est;
   obs_t obs;            /* observation of the current step (rejuvenation) */
+  int cond;             /* conditional SMC: particle 0 is pinned (smc.jl:100-151) */
   uint32_t moves;       /* rejuvenation moves applied at the current step */
   /* history */
   int cap;
@@ -515,7 +516,9 @@ static void record(orc_pf* pf) {
   memcpy(pf->hx[t - 1], pf->x, sizeof(double) * sz);
 }
 
-int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+static double model_loglik(const model_t* m, const obs_t* o, const double* x);
+
+static int init_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, const double* ref) {
   obs_t o;
   obs_build(&pf->m, 1, obs, has_obs, &o);
   int D = pf->m.d;
@@ -525,6 +528,11 @@ int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
     for (int k = 0; k < D; ++k) pf->x[(size_t)k * pf->n + i] = x[k];
     pf->anc[i] = pf->lo + i;
   }
+  if (ref) {  /* distinguished particle: given state, weight init_score (smc.jl:114-115) */
+    for (int k = 0; k < D; ++k) pf->x[(size_t)k * pf->n] = ref[k];
+    pf->logw[0] = model_loglik(&pf->m, &o, ref);
+    pf->cond = 1;
+  }
   pf->t = 1;
   pf->pending = 0;
   pf->log_ml_est = 0.0;
@@ -533,8 +541,15 @@ int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
   record(pf);
   return 0;
 }
+int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+  return init_impl(pf, obs, has_obs, proposal, NULL);
+}
+int orc_pf_init_conditional(orc_pf* pf, const double* obs, int has_obs, const double* ref) {
+  if (pf->resampler != ORC_MULTINOMIAL || pf->lo != 0 || pf->n != pf->n_global) return -1;
+  return init_impl(pf, obs, has_obs, 0, ref);
+}
 
-int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+static int step_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, const double* ref) {
   if (pf->m.family == ORC_REGRESSION) return -1; /* a static model has no steps */
   uint32_t t = (uint32_t)(pf->t + 1);
   obs_t o;
@@ -543,12 +558,17 @@ int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
   int64_t n = pf->n;
   double* src = pf->pending ? pf->anc_state : pf->x;
   memcpy(pf->xprev, src, sizeof(double) * D * n);
+  const double w0_old = n > 0 ? pf->logw[0] : 0.0;
   double xp[64], x[64];
   for (int64_t i = 0; i < n; ++i) {
     for (int k = 0; k < D; ++k) xp[k] = pf->xprev[(size_t)k * n + i];
     double inc = particle_step(&pf->m, pf->seed, (uint64_t)(pf->lo + i), t, &o, proposal, xp, x, S_STEP, 0);
     for (int k = 0; k < D; ++k) pf->x[(size_t)k * n + i] = x[k];
     pf->logw[i] = (pf->pending ? 0.0 : pf->logw[i]) + inc;
+  }
+  if (ref) {  /* distinguished particle: parent itself, weight += forward_score (smc.jl:138-141) */
+    for (int k = 0; k < D; ++k) pf->x[(size_t)k * n] = ref[k];
+    pf->logw[0] = (pf->pending ? 0.0 : w0_old) + model_loglik(&pf->m, &o, ref);
   }
   int was = pf->pending;
   pf->pending = 0;
@@ -564,6 +584,15 @@ int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
     }
   }
   return 0;
+}
+
+int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+  if (pf->cond) return -1;
+  return step_impl(pf, obs, has_obs, proposal, NULL);
+}
+int orc_pf_step_conditional(orc_pf* pf, const double* obs, int has_obs, const double* ref) {
+  if (!pf->cond) return -1;
+  return step_impl(pf, obs, has_obs, 0, ref);
 }
 
 /* log p(y_t | x_t): the step's weight increment under the prior proposal */
@@ -584,7 +613,7 @@ static double model_loglik(const model_t* m, const obs_t* o, const double* x) {
    log(u) < weight.  Move w of the step uses stream S_MH + 16 (w / 4096), draws
    [16 (w mod 4096), +8) for the proposal and draw 16 (w mod 4096) + 15 for u. */
 int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted) {
-  if (pf->pending || pf->t < 1 || n_moves < 0 || (uint64_t)pf->moves + (uint64_t)n_moves > (1u << 24)) return -1;
+  if (pf->cond || pf->pending || pf->t < 1 || n_moves < 0 || (uint64_t)pf->moves + (uint64_t)n_moves > (1u << 24)) return -1;
   const int D = pf->m.d;
   const int64_t n = pf->n;
   const uint32_t t = (uint32_t)pf->t;
@@ -727,6 +756,10 @@ void orc_pf_resample_apply(orc_pf* pf, double L, int64_t count, const int64_t* s
   }
   pf->log_ml_est += L - orc_log((double)pf->n_global);
   pf->pending = 1;
+  if (pf->cond && pf->n > 0) {  /* the distinguished particle's parent is itself (smc.jl:139) */
+    pf->anc[0] = 0;
+    for (int k = 0; k < D; ++k) pf->anc_state[(size_t)k * pf->n] = pf->x[(size_t)k * pf->n];
+  }
 }
 
 int orc_pf_maybe_resample(orc_pf* pf, double thr, double* ess_out) {

@@ -63,6 +63,11 @@ int orc_pf_maybe_resample(orc_pf* pf, double ess_threshold, double* ess_out);
 /* rejuvenation: n_moves mh(trace, select(x_t)) moves per particle (src/inference/mh.jl:14-26);
    -1 if a resample is pending */
 int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted);
+/* conditional SMC (examples/pmmh/smc.jl:100-151): particle 0 pinned to ref
+   (multinomial resampler, one shard); a conditional filter steps only with
+   orc_pf_step_conditional.  -1 on misuse */
+int orc_pf_init_conditional(orc_pf* pf, const double* obs, int has_obs, const double* ref);
+int orc_pf_step_conditional(orc_pf* pf, const double* obs, int has_obs, const double* ref);
 double orc_pf_log_ml_estimate(orc_pf* pf);
 void orc_pf_get_log_weights(orc_pf* pf, double* out);     /* n_local */
 void orc_pf_get_state(orc_pf* pf, double* out);           /* [d][n_local] */

@@ -50,6 +50,8 @@ def lib():
             "orc_pf_step": (I, [V, D, I, I]),
             "orc_pf_maybe_resample": (I, [V, c_double, D]),
             "orc_pf_rejuvenate": (I, [V, I, POINTER(c_int64)]),
+            "orc_pf_init_conditional": (I, [V, D, I, D]),
+            "orc_pf_step_conditional": (I, [V, D, I, D]),
             "orc_pf_log_ml_estimate": (c_double, [V]),
             "orc_pf_get_log_weights": (None, [V, D]),
             "orc_pf_get_state": (None, [V, D]),
@@ -132,7 +134,20 @@ class OraclePF:
 
     def step(self, y, proposal=DEFAULT):
         a, has = self._obs(y)
-        lib().orc_pf_step(self.h, _d(a), has, proposal)
+        if lib().orc_pf_step(self.h, _d(a), has, proposal):
+            raise ValueError("oracle: this filter does not take plain steps")
+
+    def init_conditional(self, y, ref):
+        a, has = self._obs(y)
+        r = np.ascontiguousarray(np.atleast_1d(np.asarray(ref, dtype=np.float64)))
+        if lib().orc_pf_init_conditional(self.h, _d(a), has, _d(r)):
+            raise ValueError("oracle: conditional SMC needs the multinomial resampler on one shard")
+
+    def step_conditional(self, y, ref):
+        a, has = self._obs(y)
+        r = np.ascontiguousarray(np.atleast_1d(np.asarray(ref, dtype=np.float64)))
+        if lib().orc_pf_step_conditional(self.h, _d(a), has, _d(r)):
+            raise ValueError("oracle: not a conditional filter")
 
     def maybe_resample(self, thr=None):
         thr = self.n_global / 2 if thr is None else thr
@@ -244,6 +259,17 @@ def run_pf(model, ys, n, seed, thr=None, resampler=SYSTEMATIC, proposal=DEFAULT,
     for y in ys[1:]:
         pf.maybe_resample(thr)
         pf.step(y, proposal)
+    return pf
+
+
+def run_csmc(model, ys, n, seed, reference, thr=None):
+    """conditional_smc (examples/pmmh/smc.jl:100-151) on the oracle; reference [T, d]."""
+    ref = np.asarray(reference, dtype=np.float64).reshape(len(ys), -1)
+    pf = OraclePF(model, n, seed, MULTINOMIAL)
+    pf.init_conditional(ys[0], ref[0])
+    for t in range(1, len(ys)):
+        pf.maybe_resample(thr)
+        pf.step_conditional(ys[t], ref[t])
     return pf
 
 
