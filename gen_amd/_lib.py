@@ -106,6 +106,7 @@ SIGNATURES = {
     "gh_last_error": (c_char_p, []),
     "gh_version": (c_char_p, []),
     "gh_selftest_math": (c_int, [c_void_p, c_int64, POINTER(c_double), POINTER(c_double), POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
+    "gh_selftest_boxmuller": (c_int, [c_void_p, c_int64, POINTER(ctypes.c_uint32), POINTER(c_double)]),
     "gh_selftest_normals": (c_int, [c_void_p, c_uint64, c_int64, c_uint32, c_uint32, c_int, POINTER(c_double)]),
 }
 

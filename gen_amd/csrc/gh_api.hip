@@ -1975,6 +1975,32 @@ extern "C" int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double
   return GH_OK;
 }
 
+extern "C" int gh_selftest_boxmuller(gh_ctx* ctx, int64_t n, const uint32_t* words, double* out) {
+  if (!ctx || n < 0 || (n && (!words || !out))) return set_err(GH_E_INVAL, "gh_selftest_boxmuller: bad argument");
+  if (n == 0) return GH_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  uint32_t* dw = nullptr;
+  double* dout = nullptr;
+  if (hipMalloc(&dw, sizeof(uint32_t) * 3 * n) != hipSuccess || hipMalloc(&dout, sizeof(double) * 4 * n) != hipSuccess) {
+    hipFree(dw);
+    return set_err(GH_E_NOMEM, "gh_selftest_boxmuller");
+  }
+  int rc = GH_OK;
+  if (hipMemcpyAsync(dw, words, sizeof(uint32_t) * 3 * n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    rc = set_err(GH_E_HIP, "copy");
+  if (!rc) {
+    hipLaunchKernelGGL(k_selftest_boxmuller, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       ctx->stream, n, (const uint32_t*)dw, dout);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(out, dout, sizeof(double) * 4 * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      rc = set_err(GH_E_HIP, "gh_selftest_boxmuller");
+  }
+  hipFree(dw);
+  hipFree(dout);
+  return rc;
+}
+
 extern "C" int gh_selftest_normals(gh_ctx* ctx, uint64_t seed, int64_t n, uint32_t step, uint32_t stream,
                                    int dim, double* out) {
   if (!ctx || n <= 0 || dim <= 0) return set_err(GH_E_INVAL, "bad argument");

@@ -1407,15 +1407,37 @@ __global__ void k_selftest_math(int64_t n, const double* in, double* oe, double*
   od[i] = x / in[(i + 1) % n];
 }
 
+// Box–Muller stages for given words: u1, r, z0, z1 per triple
+__global__ void k_selftest_boxmuller(int64_t n, const uint32_t* w, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t a = w[3 * i], b = w[3 * i + 1], c = w[3 * i + 2];
+  const double u1 = one_minus_u53(a, b);
+  out[4 * i] = u1;
+  out[4 * i + 1] = sqrt_radius(-2.0 * gh_log_unit(u1));
+  double z0, z1;
+  box_muller(a, b, c, &z0, &z1);
+  out[4 * i + 2] = z0;
+  out[4 * i + 3] = z1;
+}
+
 __global__ void k_selftest_normals(uint64_t seed, int64_t n, uint32_t step, uint32_t stream,
                                    int dim, double* out) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  for (int j = 0; 2 * j < dim; ++j) {
+  // the multi-block layout of normals_n (pair p = words 3p..3p+2)
+  for (int p = 0; 2 * p < dim; ++p) {
+    uint32_t wd[3];
+    for (int q = 0; q < 3; ++q) {
+      const int k = 3 * p + q;
+      const u32x4 w = rng_block(seed, (uint64_t)i, step, stream, (uint32_t)(k >> 2));
+      const int r = k & 3;
+      wd[q] = r == 0 ? w.x : r == 1 ? w.y : r == 2 ? w.z : w.w;
+    }
     double a, b;
-    normal_pair(rng_block(seed, (uint64_t)i, step, stream, (uint32_t)j), &a, &b);
-    out[i * dim + 2 * j] = a;
-    if (2 * j + 1 < dim) out[i * dim + 2 * j + 1] = b;
+    box_muller(wd[0], wd[1], wd[2], &a, &b);
+    out[i * dim + 2 * p] = a;
+    if (2 * p + 1 < dim) out[i * dim + 2 * p + 1] = b;
   }
 }
 

@@ -214,22 +214,125 @@ GH_HD double gh_cos(double x) {
   }
 }
 
+// sin(2 pi c / 2^32), cos(2 pi c / 2^32) for a 32-bit angle word c: the
+// octant is c's top three bits, the fraction f = (c mod 2^29) 2^-29 (odd
+// octants use 1 - f, formed exactly in integers), one rounding in
+// a = f' (pi/4 2^-29); sin/cos are swapped when bit 29 ^ bit 30 and negated by
+// the quadrant (sign-bit flips).  Same kernels as sincos_2pi, no floor/convert
+// round trip and half the selects.
+GH_HD void sincos_2pi_u32(uint32_t c, double* s, double* co) {
+  const uint32_t fi = c & 0x1FFFFFFFu;
+  const uint32_t fo = ((c >> 29) & 1u) ? (0x20000000u - fi) : fi;
+  const double a = (double)fo * 0x1.921fb54442d18p-30;
+  const double sk = sin_kernel(a), ck = cos_kernel(a);
+  const bool swap = (((c >> 29) ^ (c >> 30)) & 1u) != 0;
+  const double s0 = swap ? ck : sk, c0 = swap ? sk : ck;
+  const uint64_t sgn_s = (uint64_t)(c >> 31) << 63;
+  const uint64_t sgn_c = (uint64_t)(((c >> 30) ^ (c >> 31)) & 1u) << 63;
+  *s = as_f64(as_u64(s0) ^ sgn_s);
+  *co = as_f64(as_u64(c0) ^ sgn_c);
+}
+
+// 1 - u53(a, b) in (0, 1], exactly: the 53-bit integer K = hi 2^32 + lo is
+// never formed; 1 - hi 2^-21 and then - lo 2^-53 are both exact.
+GH_HD double one_minus_u53(uint32_t a, uint32_t b) {
+  const uint32_t hi = a >> 11;
+  const uint32_t lo = ((a << 21) & 0xFC000000u) | (b >> 6);
+  return fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0));
+}
+
+// gh_log restricted to x in [2^-53, 1] (normal, positive, finite): the same
+// arithmetic without the special-case branches, so bit-identical to gh_log
+// there.
+GH_HD double gh_log_unit(double x) {
+  const uint64_t bits = as_u64(x);
+  int k = (int)(bits >> 52) - 1023;
+  double m = as_f64((bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+  if (m > 0x1.6a09e667f3bcdp+0) {
+    m *= 0.5;
+    k += 1;
+  }
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
+  const double t2 = z * (6.666666666666735130e-01 +
+                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)k;
+  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+
+// IEEE sqrt for x = 0 or x in [2^-767, inf): on the device the correctly
+// rounded rsq + Newton sequence the compiler emits for sqrt, minus its
+// small-input scaling and class fix-up (x here is -2 log(u1) in [0, 75]);
+// tests/test_gpu_parity.py checks it against the host's sqrt.
+GH_HD double sqrt_radius(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  double d = fma(-g, g, x);
+  h = fma(h, r, h);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  g = fma(d, h, g);
+  return x == 0.0 ? x : g;
+#else
+  return sqrt(x);
+#endif
+}
+
 // ------------------------------------------------------------ normals
-// Box–Muller on one Philox block: two standard normals.
-GH_HD void normal_pair(u32x4 w, double* z0, double* z1) {
+// Box–Muller on three 32-bit words: radius from the 53-bit uniform of (a, b),
+// angle from the 32-bit word c.  Four Philox words per block
+// serve 4/3 pairs, so d normals take ceil(3 ceil(d/2) / 4) blocks.
+GH_HD void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1) {
 #if defined(GH_ABLATE_BOXMULLER)  // timing-only variant: uniforms instead of normals
-  *z0 = u53(w.x, w.y) - 0.5;
-  *z1 = u53(w.z, w.w) - 0.5;
+  *z0 = u53(a, b) - 0.5;
+  *z1 = (double)c * 0x1p-32 - 0.5;
   return;
 #endif
-  const double u1 = 1.0 - u53(w.x, w.y);  // (0, 1]
-  const double u2 = u53(w.z, w.w);        // [0, 1)
-  const double r = sqrt(-2.0 * gh_log(u1));
-  double s, c;
-  sincos_2pi(u2, &s, &c);
-  *z0 = r * c;
+  const double u1 = one_minus_u53(a, b);  // (0, 1]
+  const double r = sqrt_radius(-2.0 * gh_log_unit(u1));
+  double s, co;
+  sincos_2pi_u32(c, &s, &co);
+  *z0 = r * co;
   *z1 = r * s;
 }
+
+// two standard normals from one Philox block (words x, y, z)
+GH_HD void normal_pair(u32x4 w, double* z0, double* z1) { box_muller(w.x, w.y, w.z, z0, z1); }
+
+// n standard normals from consecutive blocks draw0, draw0+1, ...: pair p takes
+// words 3p, 3p+1, 3p+2 of the concatenated blocks.
+#if defined(__HIPCC__)
+template <int N>
+__device__ __forceinline__ void normals_n(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream,
+                                          uint32_t draw0, double* z) {
+  constexpr int kPairs = (N + 1) / 2, kBlocks = (3 * kPairs + 3) / 4;
+  uint32_t wd[4 * kBlocks];
+#pragma unroll
+  for (int b = 0; b < kBlocks; ++b) {
+    const u32x4 w = rng_block(seed, id, step, stream, draw0 + (uint32_t)b);
+    wd[4 * b] = w.x;
+    wd[4 * b + 1] = w.y;
+    wd[4 * b + 2] = w.z;
+    wd[4 * b + 3] = w.w;
+  }
+#pragma unroll
+  for (int p = 0; p < kPairs; ++p) {
+    double a, c;
+    box_muller(wd[3 * p], wd[3 * p + 1], wd[3 * p + 2], &a, &c);
+    z[2 * p] = a;
+    if (2 * p + 1 < N) z[2 * p + 1] = c;
+  }
+}
+#endif
 
 // (u53 * S) >> 53 without overflow: floor(u * S) for the integer CDF.
 GH_HD uint64_t scale_u53(uint64_t u, uint64_t S) {

@@ -88,13 +88,7 @@ struct LGModel {
   using Params = LGParams;
 
   __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, Draw dr, double* z) {
-#pragma unroll
-    for (int j = 0; 2 * j < D; ++j) {
-      double a, b;
-      normal_pair(rng_block(seed, pid, step, dr.stream, dr.base + (uint32_t)j), &a, &b);
-      z[2 * j] = a;
-      if (2 * j + 1 < D) z[2 * j + 1] = b;
-    }
+    normals_n<D>(seed, pid, step, dr.stream, dr.base, z);
   }
 
   // mvnormal(H x + c, R) logpdf with the Cholesky factor applied on the host

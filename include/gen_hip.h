@@ -241,6 +241,9 @@ const char* gh_version(void);
    GPU so tests can compare them bit-for-bit with the CPU oracle */
 int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double* out_exp, double* out_log,
                      double* out_sqrt, double* out_div);
+/* Box–Muller stages for n word triples (a, b, c): out[4i..4i+3] =
+   (1 - u53(a, b), sqrt(-2 log(.)), z0, z1) as the kernels compute them */
+int gh_selftest_boxmuller(gh_ctx* ctx, int64_t n, const uint32_t* words, double* out);
 int gh_selftest_normals(gh_ctx* ctx, uint64_t seed, int64_t n, uint32_t step, uint32_t stream,
                         int dim, double* out /* [n][dim] */);
 

@@ -139,19 +139,49 @@ double orc_cos(double x) {
   }
 }
 
-/* n standard normals for (id, step, stream): Box–Muller on Philox blocks */
+/* sin/cos(2 pi c 2^-32) of a 32-bit angle word: octant = top
+   three bits, fraction in integers, 1 - f exact for odd octants. */
+void orc_sincos_2pi_u32(uint32_t c, double* s, double* co) {
+  uint32_t fi = c & 0x1FFFFFFFu;
+  uint32_t fo = ((c >> 29) & 1u) ? (0x20000000u - fi) : fi;
+  double a = (double)fo * 0x1.921fb54442d18p-30;
+  double sk = ksin(a), ck = kcos(a);
+  int swap = (int)(((c >> 29) ^ (c >> 30)) & 1u);
+  double s0 = swap ? ck : sk, c0 = swap ? sk : ck;
+  *s = (c >> 31) ? -s0 : s0;
+  *co = (((c >> 30) ^ (c >> 31)) & 1u) ? -c0 : c0;
+}
+
+/* Box–Muller on three words: radius from 1 - u53(a, b) (exact), angle word c */
+static void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1) {
+  uint32_t hi = a >> 11, lo = ((a << 21) & 0xFC000000u) | (b >> 6);
+  double u1 = fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0)); /* = 1 - u53(a, b) */
+  double r = sqrt(-2.0 * orc_log(u1));
+  double s, co;
+  orc_sincos_2pi_u32(c, &s, &co);
+  *z0 = r * co;
+  *z1 = r * s;
+}
+
+void orc_box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1) { box_muller(a, b, c, z0, z1); }
+
+/* n standard normals for (id, step, stream) from blocks base, base+1, ...:
+   pair p takes words 3p, 3p+1, 3p+2 of the concatenated blocks */
 static void normals_at(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, uint32_t base, int n,
                        double* z) {
-  for (int j = 0; 2 * j < n; ++j) {
-    uint32_t w[4];
-    rng(seed, id, step, stream, base + (uint32_t)j, w);
-    double u1 = 1.0 - unif53(w[0], w[1]);
-    double u2 = unif53(w[2], w[3]);
-    double r = sqrt(-2.0 * orc_log(u1));
-    double s, c;
-    orc_sincos_2pi(u2, &s, &c);
-    z[2 * j] = r * c;
-    if (2 * j + 1 < n) z[2 * j + 1] = r * s;
+  uint32_t w[4];
+  int cur = -1;
+  for (int p = 0; 2 * p < n; ++p) {
+    uint32_t wd[3];
+    for (int q = 0; q < 3; ++q) {
+      int k = 3 * p + q;
+      if ((k >> 2) != cur) { cur = k >> 2; rng(seed, id, step, stream, base + (uint32_t)cur, w); }
+      wd[q] = w[k & 3];
+    }
+    double a, c;
+    box_muller(wd[0], wd[1], wd[2], &a, &c);
+    z[2 * p] = a;
+    if (2 * p + 1 < n) z[2 * p + 1] = c;
   }
 }
 void orc_normals(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, int n, double* z) {

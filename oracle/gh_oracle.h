@@ -49,6 +49,8 @@ double orc_exp(double x);
 double orc_log(double x);
 double orc_cos(double x);
 void orc_sincos_2pi(double u, double* s, double* c);
+void orc_sincos_2pi_u32(uint32_t c, double* s, double* co);
+void orc_box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1);
 void orc_normals(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, int n, double* z);
 
 /* particle filter over particles [lo, lo+n_local) of a global set of n_global */

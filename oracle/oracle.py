@@ -43,6 +43,8 @@ def lib():
             "orc_log": (c_double, [c_double]),
             "orc_cos": (c_double, [c_double]),
             "orc_sincos_2pi": (None, [c_double, D, D]),
+            "orc_sincos_2pi_u32": (None, [U32, D, D]),
+            "orc_box_muller": (None, [U32, U32, U32, D, D]),
             "orc_normals": (None, [U64, U64, U32, U32, I, D]),
             "orc_pf_create": (V, [I, I, I, I, I, D, I64, I64, I64, I64, U64, I, I]),
             "orc_pf_destroy": (None, [V]),
@@ -86,6 +88,17 @@ def philox(ctr, key):
     o = (c_uint32 * 4)()
     lib().orc_philox4x32_10(c, k, o)
     return list(o)
+
+
+def box_muller_words(words):
+    """[n, 3] uint32 words -> [n, 2] normals (the oracle's Box–Muller)."""
+    out = np.empty((len(words), 2))
+    a, b = c_double(), c_double()
+    f = lib().orc_box_muller
+    for i, (x, y, z) in enumerate(np.asarray(words, dtype=np.uint64)):
+        f(int(x), int(y), int(z), ctypes.byref(a), ctypes.byref(b))
+        out[i] = a.value, b.value
+    return out
 
 
 def normals(seed, id_, step, stream, n):

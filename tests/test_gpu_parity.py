@@ -50,6 +50,35 @@ def test_device_math_is_bit_identical_to_oracle(gh_ctx):
         assert np.array_equal(od.view(np.uint64), (x / np.roll(x, -1)).view(np.uint64))
 
 
+def test_device_box_muller_stages_are_bit_identical(gh_ctx):
+    """1 - u53 (exact), the radius through the device's scaling-free sqrt and
+    the unit-interval log, and the normals, against the host (IEEE sqrt) and
+    the oracle, over random words plus the radius extremes (u1 = 1: r = 0;
+    u1 = 2^-53: r^2 = 73.6)."""
+    import ctypes
+
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    n = 1 << 21
+    w = rng.integers(0, 1 << 32, (n, 3), dtype=np.uint64).astype(np.uint32)
+    w[:4, :2] = [[0, 0], [0, 63], [0xFFFFFFFF, 0xFFFFFFFF], [0xFFFFFFFF, 0xFFFFFFC0]]
+    out = np.empty((n, 4))
+    _lib.check(lib.gh_selftest_boxmuller(gh_ctx.h, n, w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                         _lib.dptr(out)))
+    k = ((w[:, 0].astype(np.uint64) >> 5) << 26) | (w[:, 1].astype(np.uint64) >> 6)
+    u1 = 1.0 - k.astype(np.float64) * 2.0**-53
+    assert np.array_equal(out[:, 0], u1)
+    L = O.lib()
+    logs = np.array([L.orc_log(v) for v in u1[:200000]])
+    r = np.sqrt(-2.0 * logs)
+    assert np.array_equal(out[:200000, 1].view(np.uint64), r.view(np.uint64))
+    assert out[0, 1] == 0.0 and out[0, 2] == 0.0
+    assert abs(out[2, 1] - math.sqrt(-2.0 * math.log(2.0**-53))) < 1e-14
+    # the normals equal the oracle's Box-Muller on the same words
+    zr = O.box_muller_words(w[:50000])
+    assert np.array_equal(out[:50000, 2:].view(np.uint64), zr.view(np.uint64))
+
+
 def test_device_normals_are_bit_identical(gh_ctx):
     lib = _lib.load()
     n, dim = 4096, 10

@@ -56,9 +56,35 @@ def test_trig():
         assert abs(c.value - math.cos(2 * math.pi * u)) < 2e-15
 
 
+def test_trig_u32_angle_words():
+    """sincos of a 32-bit angle word (the Box–Muller angle): every octant
+    boundary and random words against libm at 2 pi c 2^-32."""
+    import ctypes
+
+    L = O.lib()
+    rng = np.random.default_rng(2)
+    words = list(rng.integers(0, 1 << 32, 20000, dtype=np.uint64))
+    words += [k << 29 for k in range(8)] + [(k << 29) - 1 for k in range(1, 8)] + [0xFFFFFFFF, 1]
+    s, c = ctypes.c_double(), ctypes.c_double()
+    for w in words:
+        L.orc_sincos_2pi_u32(int(w), ctypes.byref(s), ctypes.byref(c))
+        ang = 2 * math.pi * (int(w) / 2.0**32)
+        assert abs(s.value - math.sin(ang)) < 2e-15 and abs(c.value - math.cos(ang)) < 2e-15, w
+    L.orc_sincos_2pi_u32(0, ctypes.byref(s), ctypes.byref(c))
+    assert (s.value, c.value) == (0.0, 1.0)
+
+
 def test_normals_are_standard():
+    from scipy import stats
+
     z = np.concatenate([O.normals(7, i, 3, 2, 10) for i in range(20000)])
     assert abs(z.mean()) < 0.01 and abs(z.var() - 1) < 0.01
+    assert stats.kstest(z, "norm").pvalue > 1e-3
+    # each coordinate of the d = 10 layout (pairs straddle Philox blocks) is standard
+    zz = z.reshape(-1, 10)
+    for k in range(10):
+        assert stats.kstest(zz[:, k], "norm").pvalue > 1e-4, k
+    assert np.max(np.abs(np.corrcoef(zz.T) - np.eye(10))) < 0.04
     # the same counter gives the same draws, a different one different draws
     assert np.array_equal(O.normals(7, 5, 3, 2, 10), O.normals(7, 5, 3, 2, 10))
     assert not np.array_equal(O.normals(7, 5, 3, 2, 10), O.normals(7, 5, 4, 2, 10))

@@ -16,6 +16,7 @@ VARIANTS = {
     "no_reduce": ["GH_ABLATE_REDUCE"],
     "no_reduce_no_rng": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
     "occ8": ["GH_LG10_WAVES=8"],
+    "occ4": ["GH_LG10_WAVES=4"],
     "occ6": ["GH_LG10_WAVES=6"],
     "occ5": ["GH_LG10_WAVES=5"],
     "philox1": ["GH_PHILOX_ROUNDS=1"],
