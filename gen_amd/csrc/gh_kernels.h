@@ -103,14 +103,28 @@ __device__ __forceinline__ uint64_t readlane63_u64(uint64_t v) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Lane moves for reductions read at lane 63 only: lane 63's operands are
+// always valid sources, so the other lanes may take garbage — a plain
+// v_mov_dpp (bound_ctrl, no "old" operand) needs no register copy per step.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint64_t dpp_red_u64(uint64_t v) {
+  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, ROW_MASK, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, ROW_MASK, 0xf, true);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint64_t)(uint32_t)lo;
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_red_f64(double v) {
+  return as_f64(dpp_red_u64<CTRL, ROW_MASK>(as_u64(v)));
+}
+
 template <class Op>
 __device__ __forceinline__ double wave_reduce_f64(double v, Op op) {
-  v = op(v, dpp_f64<0xb1>(v, v));         // quad_perm [1,0,3,2]
-  v = op(v, dpp_f64<0x4e>(v, v));         // quad_perm [2,3,0,1]
-  v = op(v, dpp_f64<0x114>(v, v));        // row_shr:4
-  v = op(v, dpp_f64<0x118>(v, v));        // row_shr:8
-  v = op(v, dpp_f64<0x142, 0xa>(v, v));   // row_bcast:15
-  v = op(v, dpp_f64<0x143, 0xc>(v, v));   // row_bcast:31
+  v = op(v, dpp_red_f64<0xb1>(v));         // quad_perm [1,0,3,2]
+  v = op(v, dpp_red_f64<0x4e>(v));         // quad_perm [2,3,0,1]
+  v = op(v, dpp_red_f64<0x114>(v));        // row_shr:4
+  v = op(v, dpp_red_f64<0x118>(v));        // row_shr:8
+  v = op(v, dpp_red_f64<0x142, 0xa>(v));   // row_bcast:15
+  v = op(v, dpp_red_f64<0x143, 0xc>(v));   // row_bcast:31
   return as_f64(readlane63_u64(as_u64(v)));
 }
 __device__ __forceinline__ double wave_max(double v) {
@@ -120,12 +134,12 @@ __device__ __forceinline__ double wave_sum(double v) {
   return wave_reduce_f64(v, [](double a, double b) { return a + b; });
 }
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-  v += dpp_u64<0xb1>(v, 0);
-  v += dpp_u64<0x4e>(v, 0);
-  v += dpp_u64<0x114>(v, 0);
-  v += dpp_u64<0x118>(v, 0);
-  v += dpp_u64<0x142, 0xa>(v, 0);
-  v += dpp_u64<0x143, 0xc>(v, 0);
+  v += dpp_red_u64<0xb1>(v);
+  v += dpp_red_u64<0x4e>(v);
+  v += dpp_red_u64<0x114>(v);
+  v += dpp_red_u64<0x118>(v);
+  v += dpp_red_u64<0x142, 0xa>(v);
+  v += dpp_red_u64<0x143, 0xc>(v);
   return readlane63_u64(v);
 }
 // inclusive scans over the 64 lanes (lane order)
@@ -187,34 +201,29 @@ __device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, u
 }
 
 // ---------------------------------------------------------------- k_step
-// Block partial of the step kernel: wave (max, sum, sum^2), then the 4 waves
-// through LDS; thread 0 stores the block's triple.
+// Block partial of the step kernel: the block max first (wave DPP max, then
+// the 4 waves through LDS), then every lane's e = exp(lw - max) and the wave
+// sums of e and e^2 — partial sums on one reference, so the 4 waves add
+// without rescaling; thread 0 stores the block's triple.
 __device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double* pm, double* ps, double* ps2) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const double mw = wave_max(lw);
+  if (lane == 0) sm[0][w] = mw;
+  __syncthreads();
+  const double mb = fmax(fmax(sm[0][0], sm[0][1]), fmax(sm[0][2], sm[0][3]));
   double e = 0.0;
-  if (lw > -INFINITY) e = gh_exp(lw - mw);
+  if (lw > -INFINITY) e = gh_exp_nonpos(lw - mb);
   if (lw != lw) e = lw;  // NaN poisons the statistics
   const double sw = wave_sum(e), s2w = wave_sum(e * e);
   if (lane == 0) {
-    sm[0][w] = mw;
     sm[1][w] = sw;
     sm[2][w] = s2w;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double mb = -INFINITY, sb = 0.0, s2b = 0.0;
-    for (int k = 0; k < 4; ++k) mb = fmax(mb, sm[0][k]);
-    if (mb > -INFINITY)
-      for (int k = 0; k < 4; ++k)
-        if (sm[0][k] > -INFINITY) {
-          const double f = gh_exp(sm[0][k] - mb);
-          sb += sm[1][k] * f;
-          s2b += sm[2][k] * (f * f);
-        }
     *pm = mb;
-    *ps = sb;
-    *ps2 = s2b;
+    *ps = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
+    *ps2 = (sm[2][0] + sm[2][1]) + (sm[2][2] + sm[2][3]);
   }
 }
 

@@ -118,6 +118,36 @@ GH_HD double gh_exp(double x) {
   return ldexp_exact(p, (int)k);
 }
 
+// gh_exp for x <= 0 (or NaN), branch-free: the same reduction, polynomial
+// and 2^k scaling as gh_exp (so the same results), with the underflow cut and
+// the subnormal scaling done by selects.  Used where whole waves evaluate it.
+GH_HD double gh_exp_nonpos(double x) {
+  const bool tiny = x < -745.5;
+  const double xc = tiny ? 0.0 : x;
+  const double k = rint(xc * 0x1.71547652b82fep+0);
+  double r = fma(-k, 0x1.62e42fee00000p-1, xc);
+  r = fma(-k, 0x1.a39ef35793c76p-33, r);
+  double p = 0x1.6124613a86d09p-33;
+  p = fma(p, r, 0x1.1eed8eff8d898p-29);
+  p = fma(p, r, 0x1.ae64567f544e4p-26);
+  p = fma(p, r, 0x1.27e4fb7789f5cp-22);
+  p = fma(p, r, 0x1.71de3a556c734p-19);
+  p = fma(p, r, 0x1.a01a01a01a01ap-16);
+  p = fma(p, r, 0x1.a01a01a01a01ap-13);
+  p = fma(p, r, 0x1.6c16c16c16c17p-10);
+  p = fma(p, r, 0x1.1111111111111p-7);
+  p = fma(p, r, 0x1.5555555555555p-5);
+  p = fma(p, r, 0x1.5555555555555p-3);
+  p = fma(p, r, 0x1.0000000000000p-1);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const int ki = (int)k;
+  const bool sub = ki <= -1022;
+  const double sc = as_f64((uint64_t)((sub ? ki + 600 : ki) + 1023) << 52);
+  const double res = (p * sc) * (sub ? 0x1p-600 : 1.0);
+  return tiny ? 0.0 : res;
+}
+
 // ------------------------------------------------------------------- log
 // fdlibm e_log.c structure: x = 2^k m, m in [sqrt2/2, sqrt2), f = m-1,
 // s = f/(2+f), log(1+f) = f - hfsq + s (hfsq + R(s^2)).
