@@ -56,8 +56,14 @@ GH_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
     // one 32x32->64 multiply per word pair (v_mad_u64_u32) gives hi and lo
     const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c.z;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // three-input xor in one v_bitop3_b32 (truth table 0x96)
+    c = u32x4{(uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c.y, k0, 0x96), (uint32_t)p1,
+              (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c.w, k1, 0x96), (uint32_t)p0};
+#else
     c = u32x4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1,
               (uint32_t)p0};
+#endif
   }
   return c;
 }
