@@ -32,6 +32,10 @@ def hipcc_cmd(out: str = LIB, extra: list[str] | None = None) -> list[str]:
         "-std=c++17",
         "-ffp-contract=off",
         "-fno-fast-math",
+        # keep constant materialisation next to its uses inside the persistent
+        # loops (hoisted fp64 polynomial constants otherwise spill)
+        "-mllvm",
+        "-disable-machine-licm",
         "-fPIC",
         "-shared",
         "-Wall",

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -648,7 +649,9 @@ extern "C" int gh_pf_destroy(gh_pf* pf) {
 // ----------------------------------------------------------- kernel launch
 template <class Model>
 static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const StepObs& o,
-                          const StepArgs& a, bool init, hipEvent_t e0, hipEvent_t e1) {
+                          const StepArgs& a0, bool init, hipEvent_t e0, hipEvent_t e1) {
+  StepArgs a = a0;
+  a.nvb = pf->nb_step;
   const dim3 grid((unsigned)pf->nb_step), block(kBlock);
   // the timed launch records its events at the kernel's own start and end
   if (init)

@@ -68,6 +68,7 @@ struct StepArgs {
   int64_t ld_out;
   double* logw;
   int64_t n;             // particles on this rank
+  int64_t nvb;           // virtual blocks of kBlock particles (= partial count)
   int64_t lo;            // global id of the first one
   uint64_t seed;
   uint32_t t;            // 1-based step index
@@ -201,15 +202,27 @@ __device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, u
 }
 
 // ---------------------------------------------------------------- k_step
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// accesses (lgkmcnt) but not for its global stores, so the states a wave has
+// just written drain while it computes the next tile.  (__syncthreads()'s
+// release fence would emit vmcnt(0) and expose every store's latency.)
+#if defined(GH_STEP_SYNCBAR)  // timing-only variant: the fenced barrier
+__device__ __forceinline__ void lds_barrier() { __syncthreads(); }
+#else
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#endif
+
 // Block partial of the step kernel: the block max first (wave DPP max, then
 // the 4 waves through LDS), then every lane's e = exp(lw - max) and the wave
 // sums of e and e^2 — partial sums on one reference, so the 4 waves add
-// without rescaling; thread 0 stores the block's triple.
+// without rescaling; thread 0 stores the block's triple.  Safe to call in a
+// loop on the same `sm`: sm[0] is read before the second barrier, sm[1..2]
+// (thread 0) before thread 0 reaches the next call's first barrier.
 __device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double* pm, double* ps, double* ps2) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const double mw = wave_max(lw);
   if (lane == 0) sm[0][w] = mw;
-  __syncthreads();
+  lds_barrier();
   const double mb = fmax(fmax(sm[0][0], sm[0][1]), fmax(sm[0][2], sm[0][3]));
   double e = 0.0;
   if (lw > -INFINITY) e = gh_exp_nonpos(lw - mb);
@@ -219,7 +232,7 @@ __device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double
     sm[1][w] = sw;
     sm[2][w] = s2w;
   }
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) {
     *pm = mb;
     *ps = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
@@ -227,12 +240,17 @@ __device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double
   }
 }
 
-// One particle per lane, 64-particle tiles per wave, 4 waves per block.
-// Systematic ancestors come from the range marks by a wave-level prefix max
-// seeded with the carry of the tile's 64-slot group (no block barrier).  Each
-// block writes one (max, sum e, sum e^2) partial with plain stores; k_fold
-// combines them in the next launch (a single-word ticket per block would
-// serialise ~4k atomics per 1M particles at the memory side).
+// One particle per lane, 64-particle tiles per wave, 4 waves per block, one
+// 256-particle block per workgroup (straight-line code: a persistent
+// grid-stride loop was measured slower — the loop-invariant parameters,
+// observations and descriptors hoisted out of it spill).  Systematic ancestors
+// come from the range marks by a wave-level prefix max seeded with the carry
+// of the tile's 64-slot group (no block barrier).  The Box–Muller log table is
+// copied into LDS once per block.  Each block writes one (max, sum e, sum e^2)
+// partial with plain stores; k_resample1 / k_fold combine them in the next
+// launch (a per-block ticket would serialise ~4k atomics per 1M particles at
+// the memory side), and the block barrier waits for LDS only, so a block's
+// state stores are not waited for before it retires.
 template <class Model, bool INIT>
 __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double* __restrict__ prm,
                                                                     typename Model::Params p0, StepObs o,
@@ -240,8 +258,13 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   constexpr int D = Model::kD;
   const typename Model::Params p = p0.rebase(prm);
   __shared__ double sm[3][4];
+  __shared__ double logtab[kLogTabDoubles];
+  load_log_tab(logtab);
+  lds_barrier();
+  const Draw dr_init{STREAM_INIT, 0, logtab}, dr_step{STREAM_STEP, 0, logtab};
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t tile = (int64_t)blockIdx.x * (kBlock / 64) + w;
+  const int64_t vb = blockIdx.x;
+  const int64_t tile = vb * (kBlock / 64) + w;
   const int64_t j = tile * 64 + lane;
   int pend = 0, use_marks = 0;
   if (!INIT && a.resampled) {
@@ -267,23 +290,25 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
     if (j < a.n) {
       double x[D];
       if (INIT) {
-        lw = Model::init(p, o, a.seed, (uint64_t)(a.lo + j), a.proposal, x);
+        lw = Model::init(p, o, a.seed, (uint64_t)(a.lo + j), a.proposal, x, dr_init);
       } else {
         double xp[D];
         if (pend && !use_marks) src = a.anc[j];
-        if (src >= 0 && a.buf) {
+        // one load sequence per uniform case (no per-lane branch: values
+        // defined on divergent paths make the register allocator spill)
+        if (a.buf && a.mark_mode != 2) {  // local rows, slots < 4 GiB: buffer loads
           const __amdgpu_buffer_rsrc_t rp = gh_rsrc(a.xprev);
 #pragma unroll
           for (int k = 0; k < D; ++k)
             xp[k] = buf_ld_f64(rp, (uint32_t)src * 8u, (uint32_t)k * (uint32_t)a.ld_prev * 8u);
-        } else if (src >= 0) {
+        } else {  // general: a local column (stride ld_prev) or a received row (stride 1)
+          const bool loc = src >= 0;
+          const double* q = loc ? a.xprev + src : a.remote + (-1 - src) * a.ld_remote;
+          const int64_t st = loc ? a.ld_prev : 1;
 #pragma unroll
-          for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
-        } else {
-#pragma unroll
-          for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
+          for (int k = 0; k < D; ++k) xp[k] = q[k * st];
         }
-        const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x);
+        const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x, dr_step);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
       }
       if (a.buf) {
@@ -301,7 +326,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   asm volatile("" ::"v"(lw));
   return;
 #endif
-  block_partial(lw, sm, a.pm + blockIdx.x, a.ps + blockIdx.x, a.ps2 + blockIdx.x);
+  block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
 }
 
 // --------------------------------------------------------------- decision

@@ -20,6 +20,8 @@
 #include <stdint.h>
 #include <math.h>
 
+#include "gh_tables.h"
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define GH_HD __host__ __device__ __forceinline__
@@ -277,28 +279,67 @@ GH_HD double one_minus_u53(uint32_t a, uint32_t b) {
   return fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0));
 }
 
-// gh_log restricted to x in [2^-53, 1] (normal, positive, finite): the same
-// arithmetic without the special-case branches, so bit-identical to gh_log
-// there.
-GH_HD double gh_log_unit(double x) {
-  const uint64_t bits = as_u64(x);
-  int k = (int)(bits >> 52) - 1023;
-  double m = as_f64((bits & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
-  if (m > 0x1.6a09e667f3bcdp+0) {
-    m *= 0.5;
-    k += 1;
+// Table-driven log for x in [2^-53, 1] (normal, positive, finite), the
+// Box–Muller radius: x = 2^e m, bin i = top 7 mantissa bits,
+// bins i >= 53 take m/2 and k = e + 1, so the reduced m lies in
+// [0.70703125, 1.4140625); r = fma(m, invc_i, -1) (|r| <= 2^-8, one rounding),
+// log x = k ln2 + logc_i + log1p(r), log1p(r) = r + r^2 Q(r) with the Taylor
+// terms through r^7 (truncation < 0.2 ulp).  No division and no branches;
+// the table (tools/gen_tables.py) is shared with the oracle.
+#if defined(__HIPCC__)
+__constant__ double gh_log_tab_dev[256] = GH_LOG_TABLE_INIT;
+#endif
+static const double gh_log_tab_host[256] = GH_LOG_TABLE_INIT;
+#if defined(__HIPCC__)
+// Copy the log table into a block's LDS (kLogTabDoubles doubles); callers
+// barrier before the first read.  Per-lane table reads then are ds_read_b128
+// instead of vector-memory loads.
+constexpr int kLogTabDoubles = 256;
+__device__ __forceinline__ void load_log_tab(double* lds) {
+  for (int i = threadIdx.x; i < kLogTabDoubles / 2; i += blockDim.x) {
+    const double2 v = reinterpret_cast<const double2*>(gh_log_tab_dev)[i];
+    reinterpret_cast<double2*>(lds)[i] = v;
   }
-  const double f = m - 1.0;
-  const double s = f / (2.0 + f);
-  const double z = s * s;
-  const double w = z * z;
-  const double t1 = w * (3.999999999940941908e-01 + w * (2.222219843214978396e-01 + w * 1.531383769920937332e-01));
-  const double t2 = z * (6.666666666666735130e-01 +
-                         w * (2.857142874366239149e-01 + w * (1.818357216161805012e-01 + w * 1.479819860511658591e-01)));
-  const double R = t2 + t1;
-  const double hfsq = 0.5 * f * f;
-  const double dk = (double)k;
-  return dk * 6.93147180369123816490e-01 - ((hfsq - (s * (hfsq + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+#endif
+
+GH_HD double gh_log_unit(double x, const double* tab = nullptr) {
+  if (!tab) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    tab = gh_log_tab_dev;
+#else
+    tab = gh_log_tab_host;
+#endif
+  }
+  const uint64_t bits = as_u64(x);
+  const uint32_t hi = (uint32_t)(bits >> 32);
+  const uint32_t i = (hi >> 13) & 127u;
+  const uint32_t up = i >= 53u ? 1u : 0u;
+  const int k = (int)(hi >> 20) - 1023 + (int)up;
+  // m: x's mantissa under exponent 0 (bins < 53) or -1 (bins >= 53)
+  const double m = as_f64((bits & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(1023u - up) << 52));
+  double invc, logc;
+#if defined(__HIP_DEVICE_COMPILE__)
+  {
+    const double2 e = reinterpret_cast<const double2*>(tab)[i];
+    invc = e.x;
+    logc = e.y;
+  }
+#else
+  invc = tab[2 * i];
+  logc = tab[2 * i + 1];
+#endif
+  const double r = fma(m, invc, -1.0);
+  const double r2 = r * r;
+  double q = fma(0x1.2492492492492p-3, r, -0x1.5555555555555p-3);  // 1/7, -1/6
+  q = fma(q, r, 0x1.999999999999ap-3);                            // 1/5
+  q = fma(q, r, -0x1.0p-2);                                       // -1/4
+  q = fma(q, r, 0x1.5555555555555p-2);                            // 1/3
+  q = fma(q, r, -0x1.0p-1);                                       // -1/2
+  const double kd = (double)k;
+  const double h = fma(kd, 0x1.62e42fefa3800p-1, logc);           // ln2 high part: k ln2hi exact
+  const double l = fma(kd, 0x1.ef35793c76730p-45, r);             // ln2 low part
+  return h + fma(r2, q, l);
 }
 
 // IEEE sqrt for x = 0 or x in [2^-767, inf): on the device the correctly
@@ -327,14 +368,14 @@ GH_HD double sqrt_radius(double x) {
 // Box–Muller on three 32-bit words: radius from the 53-bit uniform of (a, b),
 // angle from the 32-bit word c.  Four Philox words per block
 // serve 4/3 pairs, so d normals take ceil(3 ceil(d/2) / 4) blocks.
-GH_HD void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1) {
+GH_HD void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1, const double* tab = nullptr) {
 #if defined(GH_ABLATE_BOXMULLER)  // timing-only variant: uniforms instead of normals
   *z0 = u53(a, b) - 0.5;
   *z1 = (double)c * 0x1p-32 - 0.5;
   return;
 #endif
   const double u1 = one_minus_u53(a, b);  // (0, 1]
-  const double r = sqrt_radius(-2.0 * gh_log_unit(u1));
+  const double r = sqrt_radius(-2.0 * gh_log_unit(u1, tab));
   double s, co;
   sincos_2pi_u32(c, &s, &co);
   *z0 = r * co;
@@ -349,7 +390,7 @@ GH_HD void normal_pair(u32x4 w, double* z0, double* z1) { box_muller(w.x, w.y, w
 #if defined(__HIPCC__)
 template <int N>
 __device__ __forceinline__ void normals_n(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream,
-                                          uint32_t draw0, double* z) {
+                                          uint32_t draw0, double* z, const double* tab = nullptr) {
   constexpr int kPairs = (N + 1) / 2, kBlocks = (3 * kPairs + 3) / 4;
   uint32_t wd[4 * kBlocks];
 #pragma unroll
@@ -363,7 +404,7 @@ __device__ __forceinline__ void normals_n(uint64_t seed, uint64_t id, uint32_t s
 #pragma unroll
   for (int p = 0; p < kPairs; ++p) {
     double a, c;
-    box_muller(wd[3 * p], wd[3 * p + 1], wd[3 * p + 2], &a, &c);
+    box_muller(wd[3 * p], wd[3 * p + 1], wd[3 * p + 2], &a, &c, tab);
     z[2 * p] = a;
     if (2 * p + 1 < N) z[2 * p + 1] = c;
   }

@@ -28,7 +28,8 @@ constexpr int kMaxObs = 32;
 // the MH stream (with a per-move draw offset) for rejuvenation proposals.
 struct Draw {
   uint32_t stream;
-  uint32_t base;  // first draw index
+  uint32_t base;               // first draw index
+  const double* tab = nullptr;  // log table for Box–Muller (LDS copy; nullptr: constant memory)
 };
 
 // per-step observation, passed by value in the kernel arguments
@@ -83,13 +84,10 @@ struct LGModel {
   #if defined(GH_LG10_WAVES)  // timing-only variants: occupancy target of the d<=10 diagonal case
   static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 10 ? (S == 3 ? GH_LG10_WAVES : 5) : 4);
 #else
-  static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 10 ? (S == 3 ? 7 : 5) : 4);
+  static constexpr int kMinWaves =
+      (D <= 3) ? 8 : (D <= 5 ? 7 : (D < 10 ? (S == 3 && D != 7 ? 6 : 5) : (D == 10 ? (S == 3 ? 7 : 5) : 4)));
 #endif
   using Params = LGParams;
-
-  __device__ static void normals(uint64_t seed, uint64_t pid, uint32_t step, Draw dr, double* z) {
-    normals_n<D>(seed, pid, step, dr.stream, dr.base, z);
-  }
 
   // mvnormal(H x + c, R) logpdf with the Cholesky factor applied on the host
   __device__ static double obs(const Params& p, const StepObs& o, const double* x) {
@@ -117,7 +115,7 @@ struct LGModel {
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
     double z[D + 1];
-    normals(seed, pid, 1, dr, z);
+    normals_n<D>(seed, pid, 1, dr.stream, dr.base, z, dr.tab);
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       double acc = p.mu0[i];
@@ -132,7 +130,7 @@ struct LGModel {
                                 uint32_t t, int /*proposal*/, const double* xp, double* x,
                                 Draw dr = {STREAM_STEP, 0}) {
     double z[D + 1];
-    normals(seed, pid, t, dr, z);
+    normals_n<D>(seed, pid, t, dr.stream, dr.base, z, dr.tab);
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       double acc = p.b[i];

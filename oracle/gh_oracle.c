@@ -8,6 +8,7 @@
  * separately, exactly as in the HIP kernels.
  */
 #include "gh_oracle.h"
+#include "../gen_amd/csrc/gh_tables.h"
 
 #include <math.h>
 #include <stdlib.h>
@@ -152,11 +153,35 @@ void orc_sincos_2pi_u32(uint32_t c, double* s, double* co) {
   *co = (((c >> 30) ^ (c >> 31)) & 1u) ? -c0 : c0;
 }
 
+/* Table-driven log of x in [2^-53, 1] (the table is the shared
+   data of gen_amd/csrc/gh_tables.h, made by tools/gen_tables.py):
+   log x = k ln2 + logc_i + log1p(r), r = fma(m, invc_i, -1),
+   log1p(r) = r + r^2 (-1/2 + r/3 - r^2/4 + r^3/5 - r^4/6 + r^5/7). */
+static const double log_tab[256] = GH_LOG_TABLE_INIT;
+double orc_log_unit(double x) {
+  uint64_t b = u64_of(x);
+  uint32_t i = (uint32_t)(b >> 45) & 127u;
+  int up = i >= 53;
+  int k = (int)(b >> 52) - 1023 + up;
+  double m = f64_of((b & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(1023 - up) << 52));
+  double r = fma(m, log_tab[2 * i], -1.0);
+  double r2 = r * r;
+  double q = fma(0x1.2492492492492p-3, r, -0x1.5555555555555p-3);
+  q = fma(q, r, 0x1.999999999999ap-3);
+  q = fma(q, r, -0x1.0p-2);
+  q = fma(q, r, 0x1.5555555555555p-2);
+  q = fma(q, r, -0x1.0p-1);
+  double kd = (double)k;
+  double h = fma(kd, 0x1.62e42fefa3800p-1, log_tab[2 * i + 1]);
+  double l = fma(kd, 0x1.ef35793c76730p-45, r);
+  return h + fma(r2, q, l);
+}
+
 /* Box–Muller on three words: radius from 1 - u53(a, b) (exact), angle word c */
 static void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1) {
   uint32_t hi = a >> 11, lo = ((a << 21) & 0xFC000000u) | (b >> 6);
   double u1 = fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0)); /* = 1 - u53(a, b) */
-  double r = sqrt(-2.0 * orc_log(u1));
+  double r = sqrt(-2.0 * orc_log_unit(u1));
   double s, co;
   orc_sincos_2pi_u32(c, &s, &co);
   *z0 = r * co;

@@ -47,6 +47,7 @@ typedef struct orc_pf orc_pf;
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 double orc_exp(double x);
 double orc_log(double x);
+double orc_log_unit(double x); /* x in [2^-53, 1]: the Box–Muller radius log (table-driven) */
 double orc_cos(double x);
 void orc_sincos_2pi(double u, double* s, double* c);
 void orc_sincos_2pi_u32(uint32_t c, double* s, double* co);

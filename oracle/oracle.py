@@ -41,6 +41,7 @@ def lib():
             "orc_philox4x32_10": (None, [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
             "orc_exp": (c_double, [c_double]),
             "orc_log": (c_double, [c_double]),
+            "orc_log_unit": (c_double, [c_double]),
             "orc_cos": (c_double, [c_double]),
             "orc_sincos_2pi": (None, [c_double, D, D]),
             "orc_sincos_2pi_u32": (None, [U32, D, D]),

@@ -42,6 +42,21 @@ def test_exp_log_within_one_ulp_of_libm():
     assert L.orc_exp(-1000.0) == 0.0 and L.orc_exp(800.0) == math.inf
 
 
+def test_unit_log_within_one_ulp_of_libm():
+    """The table-driven Box-Muller log over [2^-53, 1]: every bin, both bins
+    touching 1 (no cancellation near 1), the ends of the interval."""
+    L = O.lib()
+    rng = np.random.default_rng(5)
+    k = rng.integers(1, 1 << 53, 40000, dtype=np.uint64)
+    u = np.concatenate([1.0 - k.astype(np.float64) * 2.0**-53, rng.uniform(0, 1, 20000) + 2.0**-53,
+                        2.0 ** -rng.uniform(0, 53, 20000), 1.0 - 2.0 ** -np.arange(1, 54),
+                        [1.0, 2.0**-53, 0.5, 0.70703125, 0.7071067811865476, np.nextafter(1.0, 0)]])
+    lg = np.array([L.orc_log_unit(x) for x in u])
+    ref = np.log(u)
+    assert np.all(np.abs(lg - ref) <= np.spacing(np.abs(ref)))
+    assert L.orc_log_unit(1.0) == 0.0
+
+
 def test_trig():
     L = O.lib()
     rng = np.random.default_rng(1)

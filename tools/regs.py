@@ -9,9 +9,9 @@ import sys
 ROOT = __file__.rsplit("/tools/", 1)[0]
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
        f"-I{ROOT}/include", "--cuda-device-only", "-c", f"{ROOT}/gen_amd/csrc/gh_api.hip", "-o", "/tmp/_regs.o",
-       "-Rpass-analysis=kernel-resource-usage"] + [a for a in sys.argv[1:] if a.startswith("-D")]
+       "-Rpass-analysis=kernel-resource-usage", "-mllvm", "-disable-machine-licm"] + [x for a in sys.argv[1:] if a.startswith("-mllvm=") for x in ("-mllvm", a[7:])] + [a for a in sys.argv[1:] if a.startswith("-D")]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
-filt = [a for a in sys.argv[1:] if not a.startswith("-D")]
+filt = [a for a in sys.argv[1:] if not a.startswith(("-D", "-mllvm="))]
 cur = None
 rows = []
 for line in out.splitlines():

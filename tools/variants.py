@@ -16,16 +16,17 @@ VARIANTS = {
     "no_reduce": ["GH_ABLATE_REDUCE"],
     "no_reduce_no_rng": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
     "occ8": ["GH_LG10_WAVES=8"],
-    "occ4": ["GH_LG10_WAVES=4"],
     "occ6": ["GH_LG10_WAVES=6"],
-    "occ5": ["GH_LG10_WAVES=5"],
     "philox1": ["GH_PHILOX_ROUNDS=1"],
     "no_bm": ["GH_ABLATE_BOXMULLER"],
     "philox7": ["GH_PHILOX_ROUNDS=7"],
+    "syncbar": ["GH_STEP_SYNCBAR"],
 }
 # instrumented builds (not timed by `run`)
 EXTRA = {"rs_stamps": ["GH_RS_STAMPS"]}
 BENCH_ARGS = os.environ.get("GH_VARIANT_ARGS", "--steps 50").split()
+# GH_VARIANT_SCRIPT=tools/bench_pmmh.py times another workload with the same variants
+BENCH_SCRIPT = os.environ.get("GH_VARIANT_SCRIPT", "bench.py")
 
 
 def main():
@@ -42,12 +43,13 @@ def main():
         for name in [v for v in VARIANTS if len(sys.argv) < 3 or v in sys.argv[2:]]:
             lib = os.path.join(ROOT, "gen_amd", "variants", f"{name}.so")
             env = dict(os.environ, GEN_HIP_LIB=lib)
-            r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + BENCH_ARGS,
+            r = subprocess.run([sys.executable, os.path.join(ROOT, BENCH_SCRIPT)] +
+                               (["--no-cpu-baseline"] if BENCH_SCRIPT == "bench.py" else []) + BENCH_ARGS,
                                env=env, capture_output=True, text=True, timeout=300)
             try:
                 d = json.loads(r.stdout.strip().splitlines()[-1])
-                out[name] = {"ms_per_step": d["ms_per_step"], "k_step_ms": d["roofline"]["kernel_avg_ms"],
-                             "value": d["value"]}
+                out[name] = ({"ms_per_step": d["ms_per_step"], "k_step_ms": d["roofline"]["kernel_avg_ms"],
+                              "value": d["value"]} if "roofline" in d else {"value": d["value"]})
             except Exception:
                 out[name] = {"error": r.stderr[-500:]}
             print(name, out[name], flush=True)
