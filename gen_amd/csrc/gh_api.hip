@@ -548,13 +548,15 @@ static void pick_resample_tiles(gh_pf* pf, int64_t n) {
   const int64_t grid16 = (n + 16 * kRsBlock - 1) / (16 * kRsBlock);
   pf->rs_grid = 0;
   pf->rs_it = 0;
-  if (pf->nb_step <= kRsPart * kRsBlock && grid4 <= resample_cap<4>(cus)) {
+  // k_resample1's wave 0 polls every tile total: at most 64 * kRsPoll tiles
+  const int64_t gmax = 64 * kRsPoll;
+  if (pf->nb_step <= kRsPart * kRsBlock && grid4 <= std::min<int64_t>(gmax, resample_cap<4>(cus))) {
     pf->rs_it = 4;
     pf->rs_grid = (int)grid4;
-  } else if (grid8 <= resample_cap<8>(cus)) {
+  } else if (grid8 <= std::min<int64_t>(gmax, resample_cap<8>(cus))) {
     pf->rs_it = 8;
     pf->rs_grid = (int)grid8;
-  } else if (grid16 <= resample_cap<16>(cus)) {
+  } else if (grid16 <= std::min<int64_t>(gmax, resample_cap<16>(cus))) {
     pf->rs_it = 16;
     pf->rs_grid = (int)grid16;
   }

@@ -806,6 +806,7 @@ constexpr int kRsBlock = 1024;
 constexpr int kRsItems = 4;
 constexpr int kRsTile = kRsBlock * kRsItems;  // particles per block
 constexpr int kRsPart = 4;                    // step partials per thread (nb_part <= 4096)
+constexpr int kRsPoll = 8;                    // tile totals polled per lane of wave 0 (grid <= 512)
 
 struct Resample1Args {
   const double* pm;        // step-kernel block partials
@@ -846,6 +847,24 @@ __device__ __forceinline__ double blk16_sum(double v, double* sm) {
   for (int k = 1; k < 16; ++k) r += sm[k];
   return r;
 }
+// two sums in one pass (same per-value order as blk16_sum; sm holds 32)
+__device__ __forceinline__ void blk16_sum2(double* a, double* b, double* sm) {
+  const double wa = wave_sum(*a), wb = wave_sum(*b);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    sm[threadIdx.x >> 6] = wa;
+    sm[16 + (threadIdx.x >> 6)] = wb;
+  }
+  __syncthreads();
+  double ra = sm[0], rb = sm[16];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    ra += sm[k];
+    rb += sm[16 + k];
+  }
+  *a = ra;
+  *b = rb;
+}
 __device__ __forceinline__ uint64_t blk16_sum_u64(uint64_t v, uint64_t* sm) {
   v = wave_sum_u64(v);
   __syncthreads();
@@ -877,7 +896,7 @@ __device__ uint64_t g_rs_stamps[1024 * 8];
 
 template <bool MARKS, int IT>
 __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
-  __shared__ double smd[16];
+  __shared__ double smd[32];
   __shared__ uint64_t smu[16];
   __shared__ DevScalars sd;
   __shared__ uint64_t sbase;
@@ -911,12 +930,14 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     GH_RS_STAMP(7);
     if (M > -INFINITY) {
 #pragma unroll
-      for (int k = 0; k < kRsPart; ++k)
+      for (int k = 0; k < kRsPart; ++k) {
+        // pm - M <= 0: the branch-free exp (same values as gh_exp there)
+        const double f = gh_exp_nonpos(pmv[k] - M);
         if (pmv[k] > -INFINITY) {
-          const double f = gh_exp(pmv[k] - M);
           s1 += psv[k] * f;
           s2 += ps2v[k] * (f * f);
         }
+      }
     }
   } else {  // larger sets: max pass, then a sum pass over the (cache-hot) partials
     double m = -INFINITY;
@@ -932,8 +953,8 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
         }
       }
   }
-  const double S1 = blk16_sum(s1, smd);
-  const double S2 = blk16_sum(s2, smd);
+  blk16_sum2(&s1, &s2, smd);
+  const double S1 = s1, S2 = s2;
   // the resample test alone (ESS = S^2 / S2 < thr, exactly as decide()):
   // block 0 commits the full decision (logsumexp, log-ML) at its end
   __shared__ int sfire;
@@ -968,7 +989,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   uint64_t tsum = 0;
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
-    q[k] = (i0 + k < r.n) ? quantize_weight(lw[k], Mq, r.shift) : 0;
+    q[k] = (i0 + k < r.n) ? quantize_weight_nonpos(lw[k], Mq, r.shift) : 0;
     tsum += q[k];
   }
   const uint64_t incl = blk16_incl_u64(tsum, smu);
@@ -980,50 +1001,72 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   const uint64_t kTag = 1ull << 63;
   const uint64_t par = (sgen & 1u) ? kTag : 0ull;
   if (threadIdx.x == kRsBlock - 1) st_sc1(&r.tsum[blockIdx.x], incl | par);
-  uint64_t before = 0, all = 0;
-  for (int b = threadIdx.x; b < (int)gridDim.x; b += kRsBlock) {
-    uint64_t v = ld_sc1(&r.tsum[b]);
-    unsigned spins = 0;  // bounded (~0.5 s): a grid that is not co-resident errors out
-    while ((v & kTag) != par) {
-      __builtin_amdgcn_s_sleep(1);
-      v = ld_sc1(&r.tsum[b]);
-      if (++spins == (1u << 22)) {
+  if (threadIdx.x < 64) {  // wave 0 reads every tile total (DPP sums, no block reduction)
+    const u32x4 wr = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);  // independent of the totals
+    // the grid is at most kRsPoll * 64 blocks (host-checked): each lane polls
+    // its kRsPoll tiles together (one round trip per sweep, not per tile)
+    uint64_t v[kRsPoll];
+    bool ok[kRsPoll];
+#pragma unroll
+    for (int k = 0; k < kRsPoll; ++k) {
+      const int b = threadIdx.x + 64 * k;
+      ok[k] = b >= (int)gridDim.x;
+      v[k] = 0;
+    }
+    for (unsigned spins = 0;; ++spins) {  // bounded (~0.5 s): a grid that is not co-resident errors out
+#pragma unroll
+      for (int k = 0; k < kRsPoll; ++k)
+        if (!ok[k]) v[k] = ld_sc1(&r.tsum[threadIdx.x + 64 * k]);
+      bool all_ok = true;
+#pragma unroll
+      for (int k = 0; k < kRsPoll; ++k) {
+        ok[k] = ok[k] || (v[k] & kTag) == par;
+        all_ok = all_ok && ok[k];
+      }
+      if (__builtin_amdgcn_ballot_w64(!all_ok) == 0) break;
+      if (spins == (1u << 22)) {
         r.dev->error = 7;  // GH_E_STATE
         break;
       }
+      __builtin_amdgcn_s_sleep(1);
     }
-    v &= ~kTag;
-    all += v;
-    if (b < (int)blockIdx.x) before += v;
-  }
-  GH_RS_STAMP(3);
-  before = blk16_sum_u64(before, smu);
-  all = blk16_sum_u64(all, smu);
-  if (threadIdx.x == 0) {
-    const uint64_t N = (uint64_t)r.d.n_global;
-    sd.S = all;
-    sd.base = 0;
-    sd.local = all;
-    const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
-    sd.o = scale_u53(u53_bits(w.x, w.y), all);
-    sd.invN = 1.0 / (double)N;
-    sd.Qs = udiv_n(all, N, sd.invN);
-    sd.Rs = all - sd.Qs * N;
-    sd.invS = 1.0 / (double)all;
-    sbase = before;
-    if (blockIdx.x == 0) {
-      r.dev->bar_gen = sgen;  // every block has published, so has read the old value
-      r.dev->S = sd.S;
-      r.dev->base = 0;
-      r.dev->local = sd.local;
-      r.dev->o = sd.o;
-      r.dev->Qs = sd.Qs;
-      r.dev->Rs = sd.Rs;
-      r.dev->invN = sd.invN;
-      r.dev->invS = sd.invS;
+    GH_RS_STAMP(3);
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int k = 0; k < kRsPoll; ++k) {
+      const int b = threadIdx.x + 64 * k;
+      if (b >= (int)gridDim.x) continue;
+      const uint64_t x = v[k] & ~kTag;
+      all += x;
+      if (b < (int)blockIdx.x) before += x;
+    }
+    all = wave_sum_u64(all);
+    before = wave_sum_u64(before);
+    if (threadIdx.x == 0) {
+      const uint64_t N = (uint64_t)r.d.n_global;
+      sd.S = all;
+      sd.base = 0;
+      sd.local = all;
+      sd.o = scale_u53(u53_bits(wr.x, wr.y), all);
+      sd.invN = 1.0 / (double)N;
+      sd.Qs = udiv_n(all, N, sd.invN);
+      sd.Rs = all - sd.Qs * N;
+      sd.invS = 1.0 / (double)all;
+      sbase = before;
+      if (blockIdx.x == 0) {
+        r.dev->bar_gen = sgen;  // every block has published, so has read the old value
+        r.dev->S = sd.S;
+        r.dev->base = 0;
+        r.dev->local = sd.local;
+        r.dev->o = sd.o;
+        r.dev->Qs = sd.Qs;
+        r.dev->Rs = sd.Rs;
+        r.dev->invN = sd.invN;
+        r.dev->invS = sd.invS;
+      }
     }
   }
-  __syncthreads();
+  lds_barrier();
   GH_RS_STAMP(4);
   uint64_t run = sbase + incl - tsum;
   if (!MARKS) {
@@ -1046,7 +1089,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     if (e_i > s_i) r.mk.mark[s_i] = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
     s_i = e_i;
   }
-  __syncthreads();
+  lds_barrier();  // se[] only; the mark stores need not have landed
   GH_RS_STAMP(5);
   // 64-slot groups starting inside this tile's slot span get their carry
   const int64_t s_lo = sfirst, s_hi = se[(kRsBlock * IT) - 1];

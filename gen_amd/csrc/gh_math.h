@@ -436,6 +436,13 @@ GH_HD uint64_t quantize_weight(double lw, double M, int shift) {
   return (uint64_t)(e * as_f64((uint64_t)(shift + 1023) << 52));
 }
 
+// quantize_weight for lw - M <= 0 (always the case: M is the maximum), with
+// the branch-free exp (identical values)
+GH_HD uint64_t quantize_weight_nonpos(double lw, double M, int shift) {
+  const double e = gh_exp_nonpos(lw - M);
+  return (uint64_t)(e * as_f64((uint64_t)(shift + 1023) << 52));
+}
+
 constexpr double LOG_2PI = 0x1.d67f1c864beb4p+0;
 
 }  // namespace gh

@@ -48,7 +48,7 @@ BODY_KERNEL(k_div_fixup_f64, double, seed + c, asm volatile("v_div_fixup_f64 %0,
 BODY_KERNEL(k_log_f32, float, (float)seed + c, asm volatile("v_log_f32 %0, %0" : "+v"(v[c])))
 
 int main() {
-  const int grid = 256 * 4 * 7;  // 7 waves per SIMD (256-thread blocks = 4 waves)
+  const int grid = 256 * 7;  // 7 blocks of 4 waves per CU = 7 waves per SIMD (256 CUs)
   void* out;
   long long* clk;
   hipMalloc(&out, (size_t)grid * 256 * 8);
