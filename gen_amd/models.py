@@ -112,6 +112,24 @@ class LinearGaussianSSM(Model):
             ys[t] = rng.multivariate_normal(self.H @ x + self.c, self.R)
         return xs, ys
 
+    def kalman_log_marginal(self, ys) -> float:
+        """Exact log p(y_1..T) by the Kalman filter (host, numpy): the value
+        Gen's CPU particle filter estimates for this model (the analytic
+        reference of the C2 log-ML error)."""
+        mu, P = self.mu0.copy(), self.P0.copy()
+        ll = 0.0
+        for t, y in enumerate(np.atleast_2d(ys)):
+            if t > 0:
+                mu = self.A @ mu + self.b
+                P = self.A @ P @ self.A.T + self.Q
+            S = self.H @ P @ self.H.T + self.R
+            r = y - (self.H @ mu + self.c)
+            ll += -0.5 * (len(y) * np.log(2 * np.pi) + np.linalg.slogdet(S)[1] + r @ np.linalg.solve(S, r))
+            K = P @ self.H.T @ np.linalg.inv(S)
+            mu = mu + K @ r
+            P = P - K @ self.H @ P
+        return float(ll)
+
     @staticmethod
     def benchmark(d: int = 10, seed: int = 1) -> "LinearGaussianSSM":
         """The C2 synthetic model of SURVEY.md §8(d): A = 0.9 I + 0.01 G rescaled to
