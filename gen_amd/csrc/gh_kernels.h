@@ -245,8 +245,8 @@ __device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double
 // grid-stride loop was measured slower — the loop-invariant parameters,
 // observations and descriptors hoisted out of it spill).  Systematic ancestors
 // come from the range marks by a wave-level prefix max seeded with the carry
-// of the tile's 64-slot group (no block barrier).  The Box–Muller log table is
-// copied into LDS once per block.  Each block writes one (max, sum e, sum e^2)
+// of the tile's 64-slot group (no block barrier).  The Box–Muller log and angle
+// tables are copied into LDS once per block.  Each block writes one (max, sum e, sum e^2)
 // partial with plain stores; k_resample1 / k_fold combine them in the next
 // launch (a per-block ticket would serialise ~4k atomics per 1M particles at
 // the memory side), and the block barrier waits for LDS only, so a block's
@@ -258,8 +258,8 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   constexpr int D = Model::kD;
   const typename Model::Params p = p0.rebase(prm);
   __shared__ double sm[3][4];
-  __shared__ double logtab[kLogTabDoubles];
-  load_log_tab(logtab);
+  __shared__ double logtab[kMathTabDoubles];
+  load_math_tab(logtab);
   lds_barrier();
   const Draw dr_init{STREAM_INIT, 0, logtab}, dr_step{STREAM_STEP, 0, logtab};
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

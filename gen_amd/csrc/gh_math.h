@@ -252,23 +252,64 @@ GH_HD double gh_cos(double x) {
   }
 }
 
-// sin(2 pi c / 2^32), cos(2 pi c / 2^32) for a 32-bit angle word c: the
-// octant is c's top three bits, the fraction f = (c mod 2^29) 2^-29 (odd
-// octants use 1 - f, formed exactly in integers), one rounding in
-// a = f' (pi/4 2^-29); sin/cos are swapped when bit 29 ^ bit 30 and negated by
-// the quadrant (sign-bit flips).  Same kernels as sincos_2pi, no floor/convert
-// round trip and half the selects.
-GH_HD void sincos_2pi_u32(uint32_t c, double* s, double* co) {
-  const uint32_t fi = c & 0x1FFFFFFFu;
-  const uint32_t fo = ((c >> 29) & 1u) ? (0x20000000u - fi) : fi;
-  const double a = (double)fo * 0x1.921fb54442d18p-30;
-  const double sk = sin_kernel(a), ck = cos_kernel(a);
-  const bool swap = (((c >> 29) ^ (c >> 30)) & 1u) != 0;
-  const double s0 = swap ? ck : sk, c0 = swap ? sk : ck;
-  const uint64_t sgn_s = (uint64_t)(c >> 31) << 63;
-  const uint64_t sgn_c = (uint64_t)(((c >> 30) ^ (c >> 31)) & 1u) << 63;
-  *s = as_f64(as_u64(s0) ^ sgn_s);
-  *co = as_f64(as_u64(c0) ^ sgn_c);
+// Constant tables of the Box–Muller (tools/gen_tables.py, shared with the
+// oracle): [0, 256) the log bins {invc, logc}, [256, 768) {sin, cos}(2 pi j/256).
+constexpr int kMathTabDoubles = 768;
+constexpr int kTrigOff = 256;
+static const double gh_math_tab_host[kMathTabDoubles] = {GH_LOG_TABLE_DATA, GH_TRIG_TABLE_DATA};
+#if defined(__HIPCC__)
+__constant__ double gh_math_tab_dev[kMathTabDoubles] = {GH_LOG_TABLE_DATA, GH_TRIG_TABLE_DATA};
+// Copy the tables into a block's LDS (kMathTabDoubles doubles); callers
+// barrier before the first read.  Per-lane table reads then are ds_read_b128
+// instead of vector-memory loads.
+__device__ __forceinline__ void load_math_tab(double* lds) {
+  for (int i = threadIdx.x; i < kMathTabDoubles / 2; i += blockDim.x)
+    reinterpret_cast<double2*>(lds)[i] = reinterpret_cast<const double2*>(gh_math_tab_dev)[i];
+}
+#endif
+GH_HD const double* math_tab(const double* tab) {
+  if (tab) return tab;
+#if defined(__HIP_DEVICE_COMPILE__)
+  return gh_math_tab_dev;
+#else
+  return gh_math_tab_host;
+#endif
+}
+// both doubles of table entry i (16 bytes) in one load
+GH_HD void tab_pair(const double* t, uint32_t i, double* a, double* b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double2 e = reinterpret_cast<const double2*>(t)[i];
+  *a = e.x;
+  *b = e.y;
+#else
+  *a = t[2 * i];
+  *b = t[2 * i + 1];
+#endif
+}
+
+// sin(2 pi c / 2^32), cos(2 pi c / 2^32) for a 32-bit angle word c, table
+// driven: j = the nearest of 256 table angles (c + 2^23) >> 24 (mod 256),
+// residual d = (int32)(c - j 2^24) (2 pi 2^-32), |d| <= pi/256, one rounding;
+// sin d = d + d^3 (-1/6 + d^2 (1/120 - d^2/5040)), cos d - 1 =
+// d^2 (-1/2 + d^2 (1/24 - d^2/720)) (truncation < 1e-20), then the rotation
+// s = s_j + (s_j (cos d - 1) + c_j sin d), c = c_j + (c_j (cos d - 1) - s_j sin d).
+// No branches, no selects; |error| < 4e-16.
+GH_HD void sincos_2pi_u32(uint32_t c, double* s, double* co, const double* tab = nullptr) {
+  const double* t = math_tab(tab) + kTrigOff;
+  const uint32_t j = ((c + 0x800000u) >> 24) & 255u;
+  const int32_t di = (int32_t)(c - (j << 24));
+  const double d = (double)di * 0x1.921fb54442d18p-30;
+  const double d2 = d * d;
+  double ps = fma(d2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);
+  ps = fma(d2, ps, -0x1.5555555555555p-3);
+  const double sd = fma(d * d2, ps, d);
+  double pc = fma(d2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5);
+  pc = fma(d2, pc, -0.5);
+  const double cm1 = d2 * pc;
+  double sj, cj;
+  tab_pair(t, j, &sj, &cj);
+  *s = sj + fma(sj, cm1, cj * sd);
+  *co = cj + fma(cj, cm1, -(sj * sd));
 }
 
 // 1 - u53(a, b) in (0, 1], exactly: the 53-bit integer K = hi 2^32 + lo is
@@ -286,31 +327,8 @@ GH_HD double one_minus_u53(uint32_t a, uint32_t b) {
 // log x = k ln2 + logc_i + log1p(r), log1p(r) = r + r^2 Q(r) with the Taylor
 // terms through r^7 (truncation < 0.2 ulp).  No division and no branches;
 // the table (tools/gen_tables.py) is shared with the oracle.
-#if defined(__HIPCC__)
-__constant__ double gh_log_tab_dev[256] = GH_LOG_TABLE_INIT;
-#endif
-static const double gh_log_tab_host[256] = GH_LOG_TABLE_INIT;
-#if defined(__HIPCC__)
-// Copy the log table into a block's LDS (kLogTabDoubles doubles); callers
-// barrier before the first read.  Per-lane table reads then are ds_read_b128
-// instead of vector-memory loads.
-constexpr int kLogTabDoubles = 256;
-__device__ __forceinline__ void load_log_tab(double* lds) {
-  for (int i = threadIdx.x; i < kLogTabDoubles / 2; i += blockDim.x) {
-    const double2 v = reinterpret_cast<const double2*>(gh_log_tab_dev)[i];
-    reinterpret_cast<double2*>(lds)[i] = v;
-  }
-}
-#endif
-
 GH_HD double gh_log_unit(double x, const double* tab = nullptr) {
-  if (!tab) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    tab = gh_log_tab_dev;
-#else
-    tab = gh_log_tab_host;
-#endif
-  }
+  const double* t = math_tab(tab);
   const uint64_t bits = as_u64(x);
   const uint32_t hi = (uint32_t)(bits >> 32);
   const uint32_t i = (hi >> 13) & 127u;
@@ -319,16 +337,7 @@ GH_HD double gh_log_unit(double x, const double* tab = nullptr) {
   // m: x's mantissa under exponent 0 (bins < 53) or -1 (bins >= 53)
   const double m = as_f64((bits & 0x000FFFFFFFFFFFFFull) | ((uint64_t)(1023u - up) << 52));
   double invc, logc;
-#if defined(__HIP_DEVICE_COMPILE__)
-  {
-    const double2 e = reinterpret_cast<const double2*>(tab)[i];
-    invc = e.x;
-    logc = e.y;
-  }
-#else
-  invc = tab[2 * i];
-  logc = tab[2 * i + 1];
-#endif
+  tab_pair(t, i, &invc, &logc);
   const double r = fma(m, invc, -1.0);
   const double r2 = r * r;
   double q = fma(0x1.2492492492492p-3, r, -0x1.5555555555555p-3);  // 1/7, -1/6
@@ -377,7 +386,7 @@ GH_HD void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1
   const double u1 = one_minus_u53(a, b);  // (0, 1]
   const double r = sqrt_radius(-2.0 * gh_log_unit(u1, tab));
   double s, co;
-  sincos_2pi_u32(c, &s, &co);
+  sincos_2pi_u32(c, &s, &co, tab);
   *z0 = r * co;
   *z1 = r * s;
 }

@@ -140,24 +140,35 @@ double orc_cos(double x) {
   }
 }
 
-/* sin/cos(2 pi c 2^-32) of a 32-bit angle word: octant = top
-   three bits, fraction in integers, 1 - f exact for odd octants. */
+/* sin/cos(2 pi c 2^-32) of a 32-bit angle word, table driven:
+   nearest of 256 table angles j = (c + 2^23) >> 24 mod 256, residual
+   d = (int32)(c - j 2^24) * (2 pi 2^-32), short Taylor polynomials of sin d and
+   cos d - 1, rotation by the table's {sin, cos}(2 pi j / 256).  The table data
+   is gen_amd/csrc/gh_tables.h (tools/gen_tables.py). */
+static const double math_tab[768] = {GH_LOG_TABLE_DATA, GH_TRIG_TABLE_DATA};
+
 void orc_sincos_2pi_u32(uint32_t c, double* s, double* co) {
-  uint32_t fi = c & 0x1FFFFFFFu;
-  uint32_t fo = ((c >> 29) & 1u) ? (0x20000000u - fi) : fi;
-  double a = (double)fo * 0x1.921fb54442d18p-30;
-  double sk = ksin(a), ck = kcos(a);
-  int swap = (int)(((c >> 29) ^ (c >> 30)) & 1u);
-  double s0 = swap ? ck : sk, c0 = swap ? sk : ck;
-  *s = (c >> 31) ? -s0 : s0;
-  *co = (((c >> 30) ^ (c >> 31)) & 1u) ? -c0 : c0;
+  const double* t = math_tab + 256;
+  uint32_t j = ((c + 0x800000u) >> 24) & 255u;
+  int32_t di = (int32_t)(c - (j << 24));
+  double d = (double)di * 0x1.921fb54442d18p-30;
+  double d2 = d * d;
+  double ps = fma(d2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);
+  ps = fma(d2, ps, -0x1.5555555555555p-3);
+  double sd = fma(d * d2, ps, d);
+  double pc = fma(d2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5);
+  pc = fma(d2, pc, -0.5);
+  double cm1 = d2 * pc;
+  double sj = t[2 * j], cj = t[2 * j + 1];
+  *s = sj + fma(sj, cm1, cj * sd);
+  *co = cj + fma(cj, cm1, -(sj * sd));
 }
 
 /* Table-driven log of x in [2^-53, 1] (the table is the shared
    data of gen_amd/csrc/gh_tables.h, made by tools/gen_tables.py):
    log x = k ln2 + logc_i + log1p(r), r = fma(m, invc_i, -1),
    log1p(r) = r + r^2 (-1/2 + r/3 - r^2/4 + r^3/5 - r^4/6 + r^5/7). */
-static const double log_tab[256] = GH_LOG_TABLE_INIT;
+static const double* log_tab = math_tab;
 double orc_log_unit(double x) {
   uint64_t b = u64_of(x);
   uint32_t i = (uint32_t)(b >> 45) & 127u;
