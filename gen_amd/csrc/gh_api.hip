@@ -482,7 +482,10 @@ struct gh_pf {
   uint64_t epoch = 0;             // resample counter for the tags
   bool marks_pending = false;     // last resample's ancestors only exist as marks
   bool stats_valid = false;       // stats_all holds the last step's (M, S, S2) (one rank)
-  uint64_t* tsum = nullptr;       // k_resample1: published tile totals
+  uint64_t* tsum = nullptr;       // k_resample1: published tile totals (+ tile sums, 3 x n_tiles)
+  int64_t n_tiles = 0;
+  bool max_only = false;          // the last step wrote block maxima only (sums left to k_resample1)
+  bool step_max_only = false;     // gh_pf_run: the next step may write block maxima only
   int rs_grid = 0;                // k_resample1 / k_rank_* tiles (blocks); 0: not usable
   int rs_it = 0;                  // particles per thread of those kernels (4, 8 or 16)
   uint64_t* bsum = nullptr;
@@ -673,6 +676,8 @@ static void launch_fold(gh_pf* pf, const StepArgs& a, bool init) {
 // one rank: make stats_all current (the fold is otherwise done by k_resample1)
 static int ensure_stats(gh_pf* pf) {
   if (pf->ctx->world > 1 || pf->stats_valid) return GH_OK;
+  if (pf->max_only)  // cannot happen: a max-only step is always followed by the fused resample
+    return set_err(GH_E_STATE, "internal: step partials hold block maxima only");
   hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_step,
                      pf->stats_all, pf->dev, 0, 0.0, pf->n_global);
   HIP_TRY(hipGetLastError());
@@ -856,7 +861,9 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   ALLOC(pf->stats_all, sizeof(double) * 3 * ctx->world);
   ALLOC(pf->totals_all, sizeof(uint64_t) * ctx->world);
   ALLOC(pf->anc_scratch, sizeof(int32_t) * n);
-  ALLOC(pf->tsum, sizeof(uint64_t) * ((n + kRsTile - 1) / kRsTile));
+  // tile totals, then the tile sums of e and e^2 (k_resample1 sums-in-pass)
+  pf->n_tiles = (n + kRsTile - 1) / kRsTile;
+  ALLOC(pf->tsum, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles));
   pick_resample_tiles(pf, n);
   if (ctx->world > 1) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
@@ -886,7 +893,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     if (hipMemcpyAsync(pf->dev, &z, sizeof z, hipMemcpyHostToDevice, pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init scalars"));
     if (hipMemsetAsync(pf->mark, 0, sizeof(uint64_t) * n, pf->s) != hipSuccess ||
-        hipMemsetAsync(pf->tsum, 0, sizeof(uint64_t) * pf->rs_grid, pf->s) != hipSuccess ||
+        hipMemsetAsync(pf->tsum, 0, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles), pf->s) != hipSuccess ||
         hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * ((n + 63) / 64), pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init marks"));
     if (hipStreamSynchronize(pf->s) != hipSuccess) return fail(set_err(GH_E_HIP, "sync"));
@@ -980,6 +987,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.ps2 = pf->ps2;
   a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
   a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
+  a.max_only = pf->step_max_only && !pin_ref ? 1 : 0;
   if (pin_ref) {
     CHECK(pin_upload(pf, pin_ref));
     CHECK(pin_launch(pf, o, false, true));
@@ -988,6 +996,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   if (pin_ref) CHECK(pin_launch(pf, o, false, false));
   CHECK(share_stats(pf));
   pf->t = t;
+  pf->max_only = a.max_only != 0;
   pf->resample_calls = 0;
   pf->marks_pending = false;
   pf->last_obs = o;
@@ -1164,6 +1173,9 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     ra.dev = pf->dev;
     ra.d = d;
     ra.tsum = pf->tsum;
+    ra.ts1 = pf->tsum + pf->n_tiles;
+    ra.ts2 = pf->tsum + 2 * pf->n_tiles;
+    ra.sums_in_pass = pf->max_only ? 1 : 0;
     ra.mk.mark = pf->mark;
     ra.mk.cmark = pf->cmark;
     ra.mk.epoch = ++pf->epoch;
@@ -1311,9 +1323,16 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
 
 extern "C" int gh_pf_run(gh_pf* pf, int n_steps, const gh_obs* obs, int proposal, double thr) {
   if (!pf || n_steps < 0) return set_err(GH_E_INVAL, "gh_pf_run: bad argument");
+  // A step followed by this loop's own maybe_resample! leaves the weight sums
+  // to the fused resample kernel (k_step writes block maxima only; one rank,
+  // fused path only); the last step writes full partials for other readers.
+  const bool fused = pf->ctx->world == 1 && pf->rs_grid > 0 && !pf->cond && pf->n > 0;
   for (int i = 0; i < n_steps; ++i) {
     CHECK(gh_pf_maybe_resample(pf, thr, nullptr, nullptr));
-    CHECK(gh_pf_step(pf, obs ? &obs[i] : nullptr, proposal));
+    pf->step_max_only = fused && i + 1 < n_steps;
+    const int rc = gh_pf_step(pf, obs ? &obs[i] : nullptr, proposal);
+    pf->step_max_only = false;
+    CHECK(rc);
   }
   return GH_OK;
 }

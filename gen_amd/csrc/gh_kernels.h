@@ -69,6 +69,7 @@ struct StepArgs {
   double* logw;
   int64_t n;             // particles on this rank
   int64_t nvb;           // virtual blocks of kBlock particles (= partial count)
+  int max_only;          // write block maxima only (the fused resample sums the weights)
   int64_t lo;            // global id of the first one
   uint64_t seed;
   uint32_t t;            // 1-based step index
@@ -240,6 +241,16 @@ __device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double
   }
 }
 
+// Block maximum only (the fused resample computes the weight sums in its own
+// pass over the log-weights, where it evaluates exp(w - M) anyway).
+__device__ __forceinline__ void block_max_partial(double lw, double (*sm)[4], double* pm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double mw = wave_max(lw);
+  if (lane == 0) sm[0][w] = mw;
+  lds_barrier();
+  if (threadIdx.x == 0) *pm = fmax(fmax(sm[0][0], sm[0][1]), fmax(sm[0][2], sm[0][3]));
+}
+
 // One particle per lane, 64-particle tiles per wave, 4 waves per block, one
 // 256-particle block per workgroup (straight-line code: a persistent
 // grid-stride loop was measured slower — the loop-invariant parameters,
@@ -326,7 +337,8 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   asm volatile("" ::"v"(lw));
   return;
 #endif
-  block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
+  if (a.max_only) block_max_partial(lw, sm, a.pm + vb);
+  else block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
 }
 
 // --------------------------------------------------------------- decision
@@ -820,18 +832,22 @@ struct Resample1Args {
   DevScalars* dev;
   DecideArgs d;
   uint64_t* tsum;          // [grid] published tile totals (bit 63: generation parity)
+  uint64_t* ts1;           // sums_in_pass: [grid] tile sums of e = exp(w - M), e^2 (tagged bits)
+  uint64_t* ts2;
+  int sums_in_pass;        // the step wrote block maxima only: S, S2 from this pass
   MarkArgs mk;             // enabled: systematic marks; else write C
   uint64_t* C;
   uint64_t seed;
   uint32_t t;
 };
 
-// 1024-thread block reductions (16 waves), result broadcast
+// 1024-thread block reductions (16 waves), result broadcast; LDS-only
+// barriers (outstanding global loads/stores are not waited for)
 __device__ __forceinline__ double blk16_max(double v, double* sm) {
   v = wave_max(v);
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   double r = sm[0];
 #pragma unroll
   for (int k = 1; k < 16; ++k) r = fmax(r, sm[k]);
@@ -839,9 +855,9 @@ __device__ __forceinline__ double blk16_max(double v, double* sm) {
 }
 __device__ __forceinline__ double blk16_sum(double v, double* sm) {
   v = wave_sum(v);
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   double r = sm[0];
 #pragma unroll
   for (int k = 1; k < 16; ++k) r += sm[k];
@@ -850,12 +866,12 @@ __device__ __forceinline__ double blk16_sum(double v, double* sm) {
 // two sums in one pass (same per-value order as blk16_sum; sm holds 32)
 __device__ __forceinline__ void blk16_sum2(double* a, double* b, double* sm) {
   const double wa = wave_sum(*a), wb = wave_sum(*b);
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 0) {
     sm[threadIdx.x >> 6] = wa;
     sm[16 + (threadIdx.x >> 6)] = wb;
   }
-  __syncthreads();
+  lds_barrier();
   double ra = sm[0], rb = sm[16];
 #pragma unroll
   for (int k = 1; k < 16; ++k) {
@@ -867,9 +883,9 @@ __device__ __forceinline__ void blk16_sum2(double* a, double* b, double* sm) {
 }
 __device__ __forceinline__ uint64_t blk16_sum_u64(uint64_t v, uint64_t* sm) {
   v = wave_sum_u64(v);
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   uint64_t r = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) r += sm[k];
@@ -879,9 +895,9 @@ __device__ __forceinline__ uint64_t blk16_sum_u64(uint64_t v, uint64_t* sm) {
 __device__ __forceinline__ uint64_t blk16_incl_u64(uint64_t v, uint64_t* sm) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   v = wave_incl_sum_u64(v);
-  __syncthreads();
+  lds_barrier();
   if (lane == 63) sm[w] = v;
-  __syncthreads();
+  lds_barrier();
   for (int k = 0; k < w; ++k) v += sm[k];
   return v;
 }
@@ -913,6 +929,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
 #pragma unroll
   for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
   double M, s1 = 0.0, s2 = 0.0;
+  const bool sums = r.sums_in_pass != 0;  // uniform
   if constexpr (IT <= kRsPart) {  // the partials fit in registers: one round trip
     double pmv[kRsPart], psv[kRsPart], ps2v[kRsPart];
 #pragma unroll
@@ -920,15 +937,15 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
       const int b = threadIdx.x + k * kRsBlock;
       const bool ok = b < r.nb_part;
       pmv[k] = ok ? r.pm[b] : -INFINITY;
-      psv[k] = ok ? r.ps[b] : 0.0;
-      ps2v[k] = ok ? r.ps2[b] : 0.0;
+      psv[k] = ok && !sums ? r.ps[b] : 0.0;
+      ps2v[k] = ok && !sums ? r.ps2[b] : 0.0;
     }
     double m = pmv[0];
 #pragma unroll
     for (int k = 1; k < kRsPart; ++k) m = fmax(m, pmv[k]);
     M = blk16_max(m, smd);
     GH_RS_STAMP(7);
-    if (M > -INFINITY) {
+    if (!sums && M > -INFINITY) {
 #pragma unroll
       for (int k = 0; k < kRsPart; ++k) {
         // pm - M <= 0: the branch-free exp (same values as gh_exp there)
@@ -943,7 +960,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     double m = -INFINITY;
     for (int b = threadIdx.x; b < r.nb_part; b += kRsBlock) m = fmax(m, r.pm[b]);
     M = blk16_max(m, smd);
-    if (M > -INFINITY)
+    if (!sums && M > -INFINITY)
       for (int b = threadIdx.x; b < r.nb_part; b += kRsBlock) {
         const double mb = r.pm[b];
         if (mb > -INFINITY) {
@@ -953,18 +970,22 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
         }
       }
   }
-  blk16_sum2(&s1, &s2, smd);
-  const double S1 = s1, S2 = s2;
+  const bool m_ok = M > -INFINITY && M != INFINITY && M == M;
+  double S1 = 0.0, S2 = 0.0;
   // the resample test alone (ESS = S^2 / S2 < thr, exactly as decide()):
-  // block 0 commits the full decision (logsumexp, log-ML) at its end
+  // block 0 commits the full decision (logsumexp, log-ML) at its end.  With
+  // sums_in_pass the sums come from this pass's own exp(w - M) and the test
+  // follows the grid barrier.
   __shared__ int sfire;
-  if (threadIdx.x == 0) {
-    const bool ok = M > -INFINITY && M != INFINITY && M == M;
-    sfire = ok && ((S1 * S1) / S2 < r.d.thr);
+  __shared__ double sS[2];
+  if (!sums) {
+    blk16_sum2(&s1, &s2, smd);
+    S1 = s1;
+    S2 = s2;
+    if (threadIdx.x == 0) sfire = m_ok && ((S1 * S1) / S2 < r.d.thr);
+    lds_barrier();
   }
-  __syncthreads();
   GH_RS_STAMP(1);
-  const int fire = sfire;
   auto commit = [&]() {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       double st[3] = {M, S1, S2};
@@ -979,48 +1000,72 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
       commit_decision(r.d, dec, r.dev, 0);
     }
   };
-  if (!fire) {  // uniform over the grid: nobody publishes
+  if (sums ? !m_ok : !sfire) {  // uniform over the grid: nobody publishes
     commit();
     return;
   }
   const double Mq = M;
-  // ---- quantise this block's tile (4 consecutive particles per thread)
+  // ---- quantise this block's tile (IT consecutive particles per thread);
+  // sums_in_pass: the same e = exp(w - M) also feed this tile's sums
+  const double qscale = as_f64((uint64_t)(r.shift + 1023) << 52);
   uint64_t q[IT];
   uint64_t tsum = 0;
+  s1 = 0.0;
+  s2 = 0.0;
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
-    q[k] = (i0 + k < r.n) ? quantize_weight_nonpos(lw[k], Mq, r.shift) : 0;
+    const bool in = i0 + k < r.n;
+    const double e = in ? gh_exp_nonpos(lw[k] - Mq) : 0.0;
+    q[k] = in ? (uint64_t)(e * qscale) : 0;  // = quantize_weight_nonpos
     tsum += q[k];
+    if (sums) {
+      const double ee = lw[k] != lw[k] ? lw[k] : e;  // NaN poisons the statistics
+      s1 += ee;
+      s2 += ee * ee;
+    }
   }
   const uint64_t incl = blk16_incl_u64(tsum, smu);
+  if (sums) blk16_sum2(&s1, &s2, smd);
   GH_RS_STAMP(2);
   // ---- grid barrier: each tile total (< 2^62) is published as ONE 8-byte
   // agent-scope store tagged in bit 63 with the generation's parity, and read
   // back with agent-scope loads until every tag matches (the payload is its
-  // own flag: no counter, no fence)
+  // own flag: no counter, no fence).  sums_in_pass: the tile sums (>= 0, so
+  // their sign bit is free) are published and polled the same way.
   const uint64_t kTag = 1ull << 63;
   const uint64_t par = (sgen & 1u) ? kTag : 0ull;
   if (threadIdx.x == kRsBlock - 1) st_sc1(&r.tsum[blockIdx.x], incl | par);
+  if (sums && threadIdx.x == 0) {
+    st_sc1(&r.ts1[blockIdx.x], (as_u64(s1) & ~kTag) | par);
+    st_sc1(&r.ts2[blockIdx.x], (as_u64(s2) & ~kTag) | par);
+  }
   if (threadIdx.x < 64) {  // wave 0 reads every tile total (DPP sums, no block reduction)
     const u32x4 wr = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);  // independent of the totals
     // the grid is at most kRsPoll * 64 blocks (host-checked): each lane polls
     // its kRsPoll tiles together (one round trip per sweep, not per tile)
-    uint64_t v[kRsPoll];
+    // one sweep polls the tile totals and, with sums_in_pass, the tile sums
+    uint64_t v[kRsPoll], v1[kRsPoll], v2[kRsPoll];
     bool ok[kRsPoll];
 #pragma unroll
     for (int k = 0; k < kRsPoll; ++k) {
-      const int b = threadIdx.x + 64 * k;
-      ok[k] = b >= (int)gridDim.x;
-      v[k] = 0;
+      ok[k] = threadIdx.x + 64 * k >= gridDim.x;
+      v[k] = v1[k] = v2[k] = par;
     }
     for (unsigned spins = 0;; ++spins) {  // bounded (~0.5 s): a grid that is not co-resident errors out
 #pragma unroll
       for (int k = 0; k < kRsPoll; ++k)
-        if (!ok[k]) v[k] = ld_sc1(&r.tsum[threadIdx.x + 64 * k]);
+        if (!ok[k]) {
+          const unsigned b = threadIdx.x + 64 * k;
+          v[k] = ld_sc1(&r.tsum[b]);
+          if (sums) {
+            v1[k] = ld_sc1(&r.ts1[b]);
+            v2[k] = ld_sc1(&r.ts2[b]);
+          }
+        }
       bool all_ok = true;
 #pragma unroll
       for (int k = 0; k < kRsPoll; ++k) {
-        ok[k] = ok[k] || (v[k] & kTag) == par;
+        ok[k] = ok[k] || ((v[k] & kTag) == par && (v1[k] & kTag) == par && (v2[k] & kTag) == par);
         all_ok = all_ok && ok[k];
       }
       if (__builtin_amdgcn_ballot_w64(!all_ok) == 0) break;
@@ -1032,17 +1077,29 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     }
     GH_RS_STAMP(3);
     uint64_t before = 0, all = 0;
+    double g1 = 0.0, g2 = 0.0;  // tile order within each lane, then the DPP tree: the same in every block
 #pragma unroll
     for (int k = 0; k < kRsPoll; ++k) {
-      const int b = threadIdx.x + 64 * k;
-      if (b >= (int)gridDim.x) continue;
+      const unsigned b = threadIdx.x + 64 * k;
+      if (b >= gridDim.x) continue;
       const uint64_t x = v[k] & ~kTag;
       all += x;
-      if (b < (int)blockIdx.x) before += x;
+      if (b < blockIdx.x) before += x;
+      g1 += as_f64(v1[k] & ~kTag);
+      g2 += as_f64(v2[k] & ~kTag);
     }
     all = wave_sum_u64(all);
     before = wave_sum_u64(before);
+    if (sums) {
+      g1 = wave_sum(g1);
+      g2 = wave_sum(g2);
+    }
     if (threadIdx.x == 0) {
+      if (sums) {
+        sS[0] = g1;
+        sS[1] = g2;
+        sfire = (g1 * g1) / g2 < r.d.thr;
+      }
       const uint64_t N = (uint64_t)r.d.n_global;
       sd.S = all;
       sd.base = 0;
@@ -1067,6 +1124,14 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     }
   }
   lds_barrier();
+  if (sums) {
+    S1 = sS[0];
+    S2 = sS[1];
+    if (!sfire) {
+      commit();
+      return;
+    }
+  }
   GH_RS_STAMP(4);
   uint64_t run = sbase + incl - tsum;
   if (!MARKS) {

@@ -130,6 +130,34 @@ def test_lgssm_parity(gh_ctx, d, thr):
         assert np.array_equal(st.states(t).T, orc.trajectory(t)), t
 
 
+@pytest.mark.parametrize("model,thr,resampler", [
+    ("lg10", "always", "systematic"), ("lg10", None, "systematic"), ("lg10", "low", "systematic"),
+    ("kit", None, "systematic"), ("lg4", "always", "multinomial")])
+def test_batched_run_parity(gh_ctx, model, thr, resampler):
+    """gh_pf_run (the bench loop): steps followed by the loop's own
+    maybe_resample! write block maxima only and the fused resample computes
+    the weight sums in its pass.  Same filter as the call-by-call oracle, bit
+    for bit; decisions incl. steps that do not resample ("low" threshold)."""
+    m = gen.LinearGaussianSSM.benchmark(10 if model == "lg10" else 4) if model != "kit" else gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(14, np.random.default_rng(6))
+    n = 70001
+    t_thr = {"always": n, None: None, "low": n / 20}[thr]
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=9, resampler=resampler)
+    orc = O.OraclePF(m, n, 9, O.SYSTEMATIC if resampler == "systematic" else O.MULTINOMIAL)
+    orc.init(ys[0])
+    gen.run_particle_filter(st, list(ys[1:]), t_thr)
+    dids = []
+    for t in range(2, len(ys) + 1):
+        dids.append(orc.maybe_resample(t_thr)[0])
+        orc.step(ys[t - 1])
+    _, did = st.ess_history()
+    assert list(did[: len(ys) - 1]) == [bool(x) for x in dids]  # did[s-1]: resampled after step s
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(st.parents, orc.parents())
+    assert_lml_close(st, orc)
+
+
 def random_lgssm(d, dy, seed):
     rng = np.random.default_rng(seed)
     A = 0.5 * np.eye(d) + 0.1 * rng.standard_normal((d, d))
