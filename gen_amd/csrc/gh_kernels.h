@@ -891,6 +891,30 @@ __device__ __forceinline__ uint64_t blk16_sum_u64(uint64_t v, uint64_t* sm) {
   for (int k = 0; k < 16; ++k) r += sm[k];
   return r;
 }
+// inclusive scan of v and the sums of a, b in one LDS round (same per-value
+// orders as blk16_incl_u64 and blk16_sum2)
+__device__ __forceinline__ uint64_t blk16_incl_sum2(uint64_t v, double* a, double* b, uint64_t* smu, double* smd) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_incl_sum_u64(v);
+  const double wa = wave_sum(*a), wb = wave_sum(*b);
+  lds_barrier();
+  if (lane == 63) smu[w] = v;
+  if (lane == 0) {
+    smd[w] = wa;
+    smd[16 + w] = wb;
+  }
+  lds_barrier();
+  for (int k = 0; k < w; ++k) v += smu[k];
+  double ra = smd[0], rb = smd[16];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) {
+    ra += smd[k];
+    rb += smd[16 + k];
+  }
+  *a = ra;
+  *b = rb;
+  return v;
+}
 // inclusive scan over the block's threads
 __device__ __forceinline__ uint64_t blk16_incl_u64(uint64_t v, uint64_t* sm) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1024,8 +1048,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
       s2 += ee * ee;
     }
   }
-  const uint64_t incl = blk16_incl_u64(tsum, smu);
-  if (sums) blk16_sum2(&s1, &s2, smd);
+  const uint64_t incl = sums ? blk16_incl_sum2(tsum, &s1, &s2, smu, smd) : blk16_incl_u64(tsum, smu);
   GH_RS_STAMP(2);
   // ---- grid barrier: each tile total (< 2^62) is published as ONE 8-byte
   // agent-scope store tagged in bit 63 with the generation's parity, and read
