@@ -21,7 +21,6 @@ VARIANTS = {
     "no_bm": ["GH_ABLATE_BOXMULLER"],
     "philox7": ["GH_PHILOX_ROUNDS=7"],
     "syncbar": ["GH_STEP_SYNCBAR"],
-    "tabglobal": ["GH_TAB_GLOBAL"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
