@@ -9,7 +9,7 @@ position_move (when k > 0) and birth_death_move, each an involutive MH step
 """
 from __future__ import annotations
 
-from ctypes import POINTER, byref, c_double, c_int32
+from ctypes import POINTER, byref, c_double, c_int32, c_void_p
 
 import numpy as np
 
@@ -21,30 +21,56 @@ K_MAX = 32
 
 
 class CoalChains:
+    """`n_chains` chains resident in HBM (gh_coal_create/step/read_state):
+    run() continues them without moving their state over PCIe; `state` is
+    read back on demand."""
+
     def __init__(self, events, n_chains: int, seed: int = 0, chain0: int = 0, ctx: Context | None = None):
         self.ctx = ctx or default_context()
         self.events = np.ascontiguousarray(np.sort(np.asarray(events, dtype=np.float64)))
         self.n_chains, self.seed, self.chain0 = int(n_chains), int(seed), int(chain0)
-        self.state = np.zeros((self.n_chains, STATE_W))
         self.accepts = np.zeros((self.n_chains, 3), dtype=np.int32)
         self.iterations = 0
-        self.started = False
         self.kernel_ms = 0.0
+        self._state = None
+        self.h = c_void_p()
+        _lib.check(_lib.load().gh_coal_create(self.ctx.h, self.chain0, self.n_chains, _lib.dptr(self.events),
+                                              self.events.size, self.seed, byref(self.h)))
 
-    def run(self, n_iters: int, k_history: bool = False):
+    def run(self, n_iters: int, k_history: bool = False, accepts: bool = True):
+        """n_iters mcmc_steps (the first call draws the start from the prior
+        first).  `accepts=False` skips the per-call acceptance download."""
         kh = np.zeros((self.n_chains, max(n_iters, 1)), dtype=np.int32) if k_history else None
-        acc = np.zeros((self.n_chains, 3), dtype=np.int32)
+        acc = np.zeros((self.n_chains, 3), dtype=np.int32) if accepts else None
         ms = c_double()
-        _lib.check(_lib.load().gh_coal_run(
-            self.ctx.h, self.chain0, self.n_chains, _lib.dptr(self.events), self.events.size, n_iters,
-            self.iterations, self.seed, 0 if self.started else 1, _lib.dptr(self.state),
-            acc.ctypes.data_as(POINTER(c_int32)), None if kh is None else kh.ctypes.data_as(POINTER(c_int32)),
-            byref(ms)))
-        self.accepts += acc
+        _lib.check(_lib.load().gh_coal_step(
+            self.h, n_iters, None if acc is None else acc.ctypes.data_as(POINTER(c_int32)),
+            None if kh is None else kh.ctypes.data_as(POINTER(c_int32)), byref(ms)))
+        if acc is not None:
+            self.accepts += acc
         self.iterations += n_iters
-        self.started = True
         self.kernel_ms = ms.value
+        self._state = None
         return kh
+
+    @property
+    def state(self) -> np.ndarray:
+        if self._state is None:
+            st = np.zeros((self.n_chains, STATE_W))
+            _lib.check(_lib.load().gh_coal_read_state(self.h, _lib.dptr(st)))
+            self._state = st
+        return self._state
+
+    def close(self):
+        if self.h:
+            _lib.load().gh_coal_destroy(self.h)
+            self.h = c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     @property
     def k(self):

@@ -1979,6 +1979,117 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
   return rc;
 }
 
+struct gh_coal {
+  gh_ctx* ctx = nullptr;
+  double* ev = nullptr;
+  double* st = nullptr;     // [n][2 * kCoalW] (current + proposal rows)
+  int32_t* acc = nullptr;   // [n][3]
+  int E = 0;
+  double T = 0.0;
+  int64_t chain0 = 0, n = 0;
+  uint64_t seed = 0;
+  int iters = 0;
+  bool started = false;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+};
+
+extern "C" int gh_coal_destroy(gh_coal* h) {
+  if (!h) return GH_OK;
+  hipSetDevice(h->ctx->device);
+  hipStreamSynchronize(h->ctx->stream);
+  hipFree(h->ev);
+  hipFree(h->st);
+  hipFree(h->acc);
+  if (h->e0) hipEventDestroy(h->e0);
+  if (h->e1) hipEventDestroy(h->e1);
+  delete h;
+  return GH_OK;
+}
+
+extern "C" int gh_coal_create(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const double* events, int E,
+                              uint64_t seed, gh_coal** out) {
+  if (!ctx || !events || !out || E < 1 || E > kCoalMaxEvents || n_chains < 1 || chain0 < 0)
+    return set_err(GH_E_INVAL, "gh_coal_create: bad argument (events 1..%d, n_chains >= 1)", kCoalMaxEvents);
+  for (int i = 1; i < E; ++i)
+    if (!(events[i] >= events[i - 1])) return set_err(GH_E_INVAL, "gh_coal_create: events must be sorted");
+  if (!(events[E - 1] > 0.0)) return set_err(GH_E_INVAL, "gh_coal_create: the window [0, T] is empty");
+  HIP_TRY(hipSetDevice(ctx->device));
+  gh_coal* h = new gh_coal();
+  h->ctx = ctx;
+  h->E = E;
+  h->T = events[E - 1];
+  h->chain0 = chain0;
+  h->n = n_chains;
+  h->seed = seed;
+  const size_t nc = (size_t)n_chains;
+  if (hipMalloc(&h->ev, sizeof(double) * E) != hipSuccess ||
+      hipMalloc(&h->st, sizeof(double) * 2 * kCoalW * nc) != hipSuccess ||
+      hipMalloc(&h->acc, sizeof(int32_t) * 3 * nc) != hipSuccess || hipEventCreate(&h->e0) != hipSuccess ||
+      hipEventCreate(&h->e1) != hipSuccess) {
+    gh_coal_destroy(h);
+    return set_err(GH_E_NOMEM, "gh_coal_create: device buffers");
+  }
+  if (hipMemcpyAsync(h->ev, events, sizeof(double) * E, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipMemsetAsync(h->st, 0, sizeof(double) * 2 * kCoalW * nc, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess) {
+    gh_coal_destroy(h);
+    return set_err(GH_E_HIP, "gh_coal_create: upload");
+  }
+  *out = h;
+  return GH_OK;
+}
+
+extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* khist, double* kernel_ms) {
+  if (!h || n_iters < 0) return set_err(GH_E_INVAL, "gh_coal_step: bad argument");
+  HIP_TRY(hipSetDevice(h->ctx->device));
+  hipStream_t s = h->ctx->stream;
+  const size_t nc = (size_t)h->n;
+  int32_t* d_kh = nullptr;
+  if (khist && n_iters > 0 && hipMalloc(&d_kh, sizeof(int32_t) * nc * n_iters) != hipSuccess)
+    return set_err(GH_E_NOMEM, "gh_coal_step: k history");
+  CoalArgs a{};
+  a.events = h->ev;
+  a.E = h->E;
+  a.T = h->T;
+  a.chain0 = h->chain0;
+  a.n_chains = h->n;
+  a.seed = h->seed;
+  a.n_iters = n_iters;
+  a.iter0 = h->iters;
+  a.init = h->started ? 0 : 1;
+  a.state = h->st;
+  a.accepts = h->acc;
+  a.khist = d_kh;
+  hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, h->e0, h->e1, 0, a);
+  int rc = GH_OK;
+  if (hipGetLastError() != hipSuccess) rc = set_err(GH_E_HIP, "gh_coal_step: launch");
+  if (!rc && accepts && hipMemcpyAsync(accepts, h->acc, sizeof(int32_t) * 3 * nc, hipMemcpyDeviceToHost, s) != hipSuccess)
+    rc = set_err(GH_E_HIP, "gh_coal_step: accepts");
+  if (!rc && d_kh && hipMemcpyAsync(khist, d_kh, sizeof(int32_t) * nc * n_iters, hipMemcpyDeviceToHost, s) != hipSuccess)
+    rc = set_err(GH_E_HIP, "gh_coal_step: k history");
+  if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = set_err(GH_E_HIP, "gh_coal_step: sync");
+  if (!rc && kernel_ms) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, h->e0, h->e1);
+    *kernel_ms = ms;
+  }
+  hipFree(d_kh);
+  if (!rc) {
+    h->iters += n_iters;
+    h->started = true;
+  }
+  return rc;
+}
+
+extern "C" int gh_coal_read_state(gh_coal* h, double* state) {
+  if (!h || !state) return set_err(GH_E_INVAL, "gh_coal_read_state: null argument");
+  HIP_TRY(hipSetDevice(h->ctx->device));
+  HIP_TRY(hipMemcpy2DAsync(state, sizeof(double) * kCoalW, h->st, sizeof(double) * 2 * kCoalW,
+                           sizeof(double) * kCoalW, (size_t)h->n, hipMemcpyDeviceToHost, h->ctx->stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx->stream));
+  return GH_OK;
+}
+
 // ------------------------------------------------------------ self tests
 extern "C" int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double* oe, double* ol,
                                 double* os, double* od) {

@@ -234,6 +234,18 @@ int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const double* eve
                 int iter0, uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist,
                 double* kernel_ms);
 
+/* Device-resident chains (the same kernel, state kept in HBM between calls:
+   no per-call state upload/download).  gh_coal_step's first call draws the
+   start from the prior (generate) and then runs n_iters iterations; later
+   calls continue.  accepts (nullable) [n_chains][3]: this call's counts;
+   khist as gh_coal_run.  gh_coal_read_state: the [n_chains][68] rows. */
+typedef struct gh_coal gh_coal;
+int gh_coal_create(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const double* events, int E, uint64_t seed,
+                   gh_coal** out);
+int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* khist, double* kernel_ms);
+int gh_coal_read_state(gh_coal* h, double* state);
+int gh_coal_destroy(gh_coal* h);
+
 /* ---- diagnostics ------------------------------------------------------------ */
 const char* gh_last_error(void);
 const char* gh_version(void);
