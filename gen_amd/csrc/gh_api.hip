@@ -1918,10 +1918,12 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   const size_t nc = (size_t)n_chains;
-  double *d_ev = nullptr, *d_st = nullptr;
+  double *d_ev = nullptr, *d_st = nullptr, *d_rows = nullptr;
   int32_t *d_acc = nullptr, *d_kh = nullptr;
-  auto cleanup = [&]() { hipFree(d_ev); hipFree(d_st); hipFree(d_acc); hipFree(d_kh); };
+  auto cleanup = [&]() { hipFree(d_ev); hipFree(d_st); hipFree(d_rows); hipFree(d_acc); hipFree(d_kh); };
+  const unsigned tgrid = (unsigned)((nc * kCoalW + 255) / 256);
   if (hipMalloc(&d_ev, sizeof(double) * E) != hipSuccess || hipMalloc(&d_st, sizeof(double) * 2 * kCoalW * nc) != hipSuccess ||
+      hipMalloc(&d_rows, sizeof(double) * kCoalW * nc) != hipSuccess ||
       hipMalloc(&d_acc, sizeof(int32_t) * 3 * nc) != hipSuccess ||
       (khist && n_iters > 0 && hipMalloc(&d_kh, sizeof(int32_t) * nc * n_iters) != hipSuccess)) {
     cleanup();
@@ -1932,11 +1934,11 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
   do {
     if (hipMemcpyAsync(d_ev, events, sizeof(double) * E, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemsetAsync(d_st, 0, sizeof(double) * 2 * kCoalW * nc, s) != hipSuccess ||
-        (!init && hipMemcpy2DAsync(d_st, sizeof(double) * 2 * kCoalW, state, sizeof(double) * kCoalW,
-                                   sizeof(double) * kCoalW, nc, hipMemcpyHostToDevice, s) != hipSuccess)) {
+        (!init && hipMemcpyAsync(d_rows, state, sizeof(double) * kCoalW * nc, hipMemcpyHostToDevice, s) != hipSuccess)) {
       rc = set_err(GH_E_HIP, "gh_coal_run: upload");
       break;
     }
+    if (!init) hipLaunchKernelGGL(k_coal_rows, dim3(tgrid), dim3(256), 0, s, d_st, (int64_t)nc, d_rows, (int64_t)nc, 1);
     CoalArgs a{};
     a.events = d_ev;
     a.E = E;
@@ -1948,6 +1950,7 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
     a.iter0 = iter0;
     a.init = init ? 1 : 0;
     a.state = d_st;
+    a.ld = (int64_t)nc;
     a.accepts = d_acc;
     a.khist = d_kh;
     if (kernel_ms) {
@@ -1959,8 +1962,8 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
       rc = set_err(GH_E_HIP, "gh_coal_run: launch");
       break;
     }
-    if (hipMemcpy2DAsync(state, sizeof(double) * kCoalW, d_st, sizeof(double) * 2 * kCoalW, sizeof(double) * kCoalW,
-                         nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    hipLaunchKernelGGL(k_coal_rows, dim3(tgrid), dim3(256), 0, s, d_st, (int64_t)nc, d_rows, (int64_t)nc, 0);
+    if (hipMemcpyAsync(state, d_rows, sizeof(double) * kCoalW * nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(accepts, d_acc, sizeof(int32_t) * 3 * nc, hipMemcpyDeviceToHost, s) != hipSuccess ||
         (d_kh && hipMemcpyAsync(khist, d_kh, sizeof(int32_t) * nc * n_iters, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess) {
@@ -2058,6 +2061,7 @@ extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* 
   a.iter0 = h->iters;
   a.init = h->started ? 0 : 1;
   a.state = h->st;
+  a.ld = h->n;
   a.accepts = h->acc;
   a.khist = d_kh;
   hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, h->e0, h->e1, 0, a);
@@ -2084,10 +2088,18 @@ extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* 
 extern "C" int gh_coal_read_state(gh_coal* h, double* state) {
   if (!h || !state) return set_err(GH_E_INVAL, "gh_coal_read_state: null argument");
   HIP_TRY(hipSetDevice(h->ctx->device));
-  HIP_TRY(hipMemcpy2DAsync(state, sizeof(double) * kCoalW, h->st, sizeof(double) * 2 * kCoalW,
-                           sizeof(double) * kCoalW, (size_t)h->n, hipMemcpyDeviceToHost, h->ctx->stream));
-  HIP_TRY(hipStreamSynchronize(h->ctx->stream));
-  return GH_OK;
+  const size_t nc = (size_t)h->n;
+  double* rows = nullptr;
+  if (hipMalloc(&rows, sizeof(double) * kCoalW * nc) != hipSuccess)
+    return set_err(GH_E_NOMEM, "gh_coal_read_state: row buffer");
+  hipLaunchKernelGGL(k_coal_rows, dim3((unsigned)((nc * kCoalW + 255) / 256)), dim3(256), 0, h->ctx->stream, h->st,
+                     h->n, rows, h->n, 0);
+  int rc = GH_OK;
+  if (hipMemcpyAsync(state, rows, sizeof(double) * kCoalW * nc, hipMemcpyDeviceToHost, h->ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(h->ctx->stream) != hipSuccess)
+    rc = set_err(GH_E_HIP, "gh_coal_read_state: download");
+  hipFree(rows);
+  return rc;
 }
 
 // ------------------------------------------------------------ self tests

@@ -33,9 +33,18 @@ struct CoalArgs {
   uint64_t seed;
   int n_iters, iter0;
   int init;              // 1: draw the start from the prior (generate)
-  double* state;         // [n_chains][2][kCoalW]: current row, proposal row
+  double* state;         // SoA [2][kCoalW][ld]: current row fields, then proposal row fields
+  int64_t ld;            // chains per field column (>= n_chains)
   int32_t* accepts;      // [n_chains][3] rate, position, birth/death
   int32_t* khist;        // optional [n_chains][n_iters] k after each iteration
+};
+
+// one chain's row (k, score, cp[32], h[33], pad) in the SoA state: field i
+// of chain c at p[i * ld] — a wave's 64 chains read one field coalesced
+struct CoalRow {
+  double* p;
+  int64_t ld;
+  __device__ __forceinline__ double& operator[](int i) const { return p[(int64_t)i * ld]; }
 };
 
 __device__ __forceinline__ double coal_u(uint64_t seed, uint64_t c, uint32_t step, uint32_t d) {
@@ -55,10 +64,10 @@ __device__ __forceinline__ int coal_upper(const double* ev, int E, double x) {
 }
 
 // score of the state row s (coal.jl:47-62 with poisson_process.jl:34-51)
-__device__ double coal_score(const double* s, const double* ev, int E, double T) {
+__device__ double coal_score(const CoalRow& s, const double* ev, int E, double T) {
   const int k = (int)s[0];
-  const double* cp = s + 2;
-  const double* h = s + 2 + kCoalKMax;
+  const CoalRow cp{s.p + 2 * s.ld, s.ld};
+  const CoalRow h{s.p + (2 + kCoalKMax) * s.ld, s.ld};
   // k ~ poisson(3): k log 3 - 3 - log k!
   double lf = 0.0;
   for (int j = 2; j <= k; ++j) lf += gh_log((double)j);
@@ -95,7 +104,7 @@ __device__ double coal_score(const double* s, const double* ev, int E, double T)
   return lp + (A - B);
 }
 
-__device__ __forceinline__ void coal_copy(const double* src, double* dst) {
+__device__ __forceinline__ void coal_copy(const CoalRow& src, const CoalRow& dst) {
   const int k = (int)src[0];
   dst[0] = src[0];
   for (int i = 0; i < k; ++i) dst[2 + i] = src[2 + i];
@@ -104,7 +113,7 @@ __device__ __forceinline__ void coal_copy(const double* src, double* dst) {
 
 // generate(model, (T,), observations): k, change points and rates from the
 // prior (attempt a uses draws 100 a + ...; a degenerate draw retries)
-__device__ void coal_init(const CoalArgs& a, uint64_t c, double* s) {
+__device__ void coal_init(const CoalArgs& a, uint64_t c, const CoalRow& s) {
   for (int att = 0; att < 64; ++att) {
     const uint32_t d0 = 100u * (uint32_t)att;
     // k ~ poisson(3) by inverse CDF
@@ -150,8 +159,8 @@ __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
   const int64_t cl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (cl >= a.n_chains) return;
   const uint64_t c = (uint64_t)(a.chain0 + cl);
-  double* cur = a.state + cl * 2 * kCoalW;
-  double* prop = cur + kCoalW;
+  const CoalRow cur{a.state + cl, a.ld};
+  const CoalRow prop{a.state + kCoalW * a.ld + cl, a.ld};
   const double T = a.T;
   if (a.init) {
     coal_init(a, c, cur);
@@ -267,6 +276,15 @@ __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
     if (a.khist) a.khist[cl * a.n_iters + it] = (int32_t)cur[0];
   }
   for (int m = 0; m < 3; ++m) a.accepts[cl * 3 + m] = acc[m];
+}
+
+// AoS rows [n][kCoalW] (the host layout) <-> SoA current fields [kCoalW][ld]
+__global__ void k_coal_rows(double* soa, int64_t ld, double* aos, int64_t n, int to_soa) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * kCoalW) return;
+  const int64_t c = i / kCoalW, f = i - c * kCoalW;  // aos index: coalesced on the AoS side
+  if (to_soa) soa[f * ld + c] = aos[i];
+  else aos[i] = soa[f * ld + c];
 }
 
 }  // namespace gh
