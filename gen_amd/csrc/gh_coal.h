@@ -70,7 +70,7 @@ __device__ double coal_score(const CoalRow& s, const double* ev, int E, double T
   const CoalRow h{s.p + (2 + kCoalKMax) * s.ld, s.ld};
   // k ~ poisson(3): k log 3 - 3 - log k!
   double lf = 0.0;
-  for (int j = 2; j <= k; ++j) lf += gh_log((double)j);
+  for (int j = 2; j <= k; ++j) lf += gh_log_unit((double)j);
   double lp = ((double)k * gh_log(3.0) - 3.0) - lf;
   // cp_i ~ min_uniform_continuous(cp_{i-1}, T, k - i + 1)
   double lower = 0.0, l_lower = gh_log(T);
@@ -78,8 +78,8 @@ __device__ double coal_score(const CoalRow& s, const double* ev, int E, double T
     const double x = cp[i - 1];
     if (!(x > lower && x < T)) return -INFINITY;
     const double m = (double)(k - i + 1);
-    const double l_x = gh_log(T - x);
-    lp += ((m - 1.0) * l_x + gh_log(m)) - m * l_lower;
+    const double l_x = gh_log_unit(T - x);
+    lp += ((m - 1.0) * l_x + gh_log_unit(m)) - m * l_lower;
     lower = x;
     l_lower = l_x;
   }
@@ -96,7 +96,7 @@ __device__ double coal_score(const CoalRow& s, const double* ev, int E, double T
   for (int i = 1; i <= k + 1; ++i) {
     const double b_hi = i <= k ? cp[i - 1] : T;
     const int c_hi = coal_upper(ev, E, b_hi);
-    A += (double)(c_hi - c_lo) * gh_log(h[i - 1]);
+    A += (double)(c_hi - c_lo) * gh_log_unit(h[i - 1]);
     B += (b_hi - b_lo) * h[i - 1];
     b_lo = b_hi;
     c_lo = c_hi;

@@ -320,8 +320,8 @@ GH_HD double one_minus_u53(uint32_t a, uint32_t b) {
   return fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0));
 }
 
-// Table-driven log for x in [2^-53, 1] (normal, positive, finite), the
-// Box–Muller radius: x = 2^e m, bin i = top 7 mantissa bits,
+// Table-driven log for positive normal finite x (the Box–Muller radius,
+// x in [2^-53, 1], and the coal score terms): x = 2^e m, bin i = top 7 mantissa bits,
 // bins i >= 53 take m/2 and k = e + 1, so the reduced m lies in
 // [0.70703125, 1.4140625); r = fma(m, invc_i, -1) (|r| <= 2^-8, one rounding),
 // log x = k ln2 + logc_i + log1p(r), log1p(r) = r + r^2 Q(r) with the Taylor

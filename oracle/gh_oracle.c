@@ -1046,15 +1046,15 @@ static double coal_score(const double* s, const double* ev, int E, double T) {
   const double* cp = s + 2;
   const double* h = s + 2 + COAL_KMAX;
   double lf = 0.0;
-  for (int j = 2; j <= k; ++j) lf += orc_log((double)j);
+  for (int j = 2; j <= k; ++j) lf += orc_log_unit((double)j);
   double lp = ((double)k * orc_log(3.0) - 3.0) - lf;
   double lower = 0.0, l_lower = orc_log(T);
   for (int i = 1; i <= k; ++i) {
     double x = cp[i - 1];
     if (!(x > lower && x < T)) return -INFINITY;
     double m = (double)(k - i + 1);
-    double l_x = orc_log(T - x);
-    lp += ((m - 1.0) * l_x + orc_log(m)) - m * l_lower;
+    double l_x = orc_log_unit(T - x);
+    lp += ((m - 1.0) * l_x + orc_log_unit(m)) - m * l_lower;
     lower = x;
     l_lower = l_x;
   }
@@ -1069,7 +1069,7 @@ static double coal_score(const double* s, const double* ev, int E, double T) {
   for (int i = 1; i <= k + 1; ++i) {
     double b_hi = i <= k ? cp[i - 1] : T;
     int c_hi = coal_upper(ev, E, b_hi);
-    A += (double)(c_hi - c_lo) * orc_log(h[i - 1]);
+    A += (double)(c_hi - c_lo) * orc_log_unit(h[i - 1]);
     B += (b_hi - b_lo) * h[i - 1];
     b_lo = b_hi;
     c_lo = c_hi;

@@ -55,6 +55,10 @@ def test_unit_log_within_one_ulp_of_libm():
     ref = np.log(u)
     assert np.all(np.abs(lg - ref) <= np.spacing(np.abs(ref)))
     assert L.orc_log_unit(1.0) == 0.0
+    # any positive normal argument (the coal score's log j, log(T - x), log h)
+    x = np.concatenate([np.exp(rng.uniform(-700, 700, 20000)), np.arange(1.0, 200.0), [2.0**-1022, 1.7e308]])
+    lg = np.array([L.orc_log_unit(v) for v in x])
+    assert np.all(np.abs(lg - np.log(x)) <= np.spacing(np.abs(np.log(x))))
 
 
 def test_trig():
