@@ -1957,7 +1957,7 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
       hipEventCreate(&e0);
       hipEventCreate(&e1);
     }
-    hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, e0, e1, 0, a);
+    hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), sizeof(double) * E, s, e0, e1, 0, a);
     if (hipGetLastError() != hipSuccess) {
       rc = set_err(GH_E_HIP, "gh_coal_run: launch");
       break;
@@ -2064,7 +2064,7 @@ extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* 
   a.ld = h->n;
   a.accepts = h->acc;
   a.khist = d_kh;
-  hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, s, h->e0, h->e1, 0, a);
+  hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), sizeof(double) * h->E, s, h->e0, h->e1, 0, a);
   int rc = GH_OK;
   if (hipGetLastError() != hipSuccess) rc = set_err(GH_E_HIP, "gh_coal_step: launch");
   if (!rc && accepts && hipMemcpyAsync(accepts, h->acc, sizeof(int32_t) * 3 * nc, hipMemcpyDeviceToHost, s) != hipSuccess)

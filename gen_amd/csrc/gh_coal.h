@@ -64,13 +64,13 @@ __device__ __forceinline__ int coal_upper(const double* ev, int E, double x) {
 }
 
 // score of the state row s (coal.jl:47-62 with poisson_process.jl:34-51)
-__device__ double coal_score(const CoalRow& s, const double* ev, int E, double T) {
+__device__ double coal_score(const CoalRow& s, const double* ev, int E, double T, const double* tab) {
   const int k = (int)s[0];
   const CoalRow cp{s.p + 2 * s.ld, s.ld};
   const CoalRow h{s.p + (2 + kCoalKMax) * s.ld, s.ld};
   // k ~ poisson(3): k log 3 - 3 - log k!
   double lf = 0.0;
-  for (int j = 2; j <= k; ++j) lf += gh_log_unit((double)j);
+  for (int j = 2; j <= k; ++j) lf += gh_log_unit((double)j, tab);
   double lp = ((double)k * gh_log(3.0) - 3.0) - lf;
   // cp_i ~ min_uniform_continuous(cp_{i-1}, T, k - i + 1)
   double lower = 0.0, l_lower = gh_log(T);
@@ -78,8 +78,8 @@ __device__ double coal_score(const CoalRow& s, const double* ev, int E, double T
     const double x = cp[i - 1];
     if (!(x > lower && x < T)) return -INFINITY;
     const double m = (double)(k - i + 1);
-    const double l_x = gh_log_unit(T - x);
-    lp += ((m - 1.0) * l_x + gh_log_unit(m)) - m * l_lower;
+    const double l_x = gh_log_unit(T - x, tab);
+    lp += ((m - 1.0) * l_x + gh_log_unit(m, tab)) - m * l_lower;
     lower = x;
     l_lower = l_x;
   }
@@ -96,7 +96,7 @@ __device__ double coal_score(const CoalRow& s, const double* ev, int E, double T
   for (int i = 1; i <= k + 1; ++i) {
     const double b_hi = i <= k ? cp[i - 1] : T;
     const int c_hi = coal_upper(ev, E, b_hi);
-    A += (double)(c_hi - c_lo) * gh_log_unit(h[i - 1]);
+    A += (double)(c_hi - c_lo) * gh_log_unit(h[i - 1], tab);
     B += (b_hi - b_lo) * h[i - 1];
     b_lo = b_hi;
     c_lo = c_hi;
@@ -153,7 +153,9 @@ __device__ void coal_init(const CoalArgs& a, uint64_t c, const CoalRow& s) {
 }
 
 __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
-  __shared__ double ev[kCoalMaxEvents];
+  extern __shared__ double ev[];  // the E event times (dynamic LDS: E doubles)
+  __shared__ double tab[kMathTabDoubles];  // the log table, per-lane reads from LDS
+  load_math_tab(tab);
   for (int i = threadIdx.x; i < a.E; i += blockDim.x) ev[i] = a.events[i];
   __syncthreads();
   const int64_t cl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
   const double T = a.T;
   if (a.init) {
     coal_init(a, c, cur);
-    cur[1] = coal_score(cur, ev, a.E, T);
+    cur[1] = coal_score(cur, ev, a.E, T, tab);
   }
   int acc[3] = {0, 0, 0};
   for (int it = 0; it < a.n_iters; ++it) {
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
       const double nh = lo + (hi - lo) * coal_u(a.seed, c, step, 1);
       coal_copy(cur, prop);
       prop[2 + kCoalKMax + i - 1] = nh;
-      const double sn = coal_score(prop, ev, a.E, T);
+      const double sn = coal_score(prop, ev, a.E, T, tab);
       const double fwd = -gh_log((double)(k + 1)) - gh_log(hi - lo);
       const double bwd = -gh_log((double)(k + 1)) - gh_log(nh * 2.0 - nh / 2.0);
       const double alpha = ((sn - cur[1]) + bwd) - fwd;
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
       const double ncp = lower + (upper - lower) * coal_u(a.seed, c, step, 4);
       coal_copy(cur, prop);
       prop[2 + i - 1] = ncp;
-      const double sn = coal_score(prop, ev, a.E, T);
+      const double sn = coal_score(prop, ev, a.E, T, tab);
       const double fwd = -gh_log((double)k) - gh_log(upper - lower);
       const double bwd = fwd;  // the neighbours bound both proposals
       const double alpha = ((sn - cur[1]) + bwd) - fwd;
@@ -236,7 +238,7 @@ __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
           prop[2 + kCoalKMax + i - 1] = hp;
           prop[2 + kCoalKMax + i] = hn;
           for (int j = i + 2; j <= k + 2; ++j) prop[2 + kCoalKMax + j - 1] = cur[2 + kCoalKMax + j - 2];
-          sn = coal_score(prop, ev, a.E, T);
+          sn = coal_score(prop, ev, a.E, T, tab);
           const double fwd = ((k > 0 ? gh_log(0.5) : 0.0) - gh_log((double)(k + 1))) - gh_log(upper - lower);
           const double bwd = gh_log(0.5) - gh_log((double)(k + 1));
           const double logj = 2.0 * gh_log(hp + hn) - gh_log(h);
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
           for (int j = 1; j < i; ++j) prop[2 + kCoalKMax + j - 1] = cur[2 + kCoalKMax + j - 1];
           prop[2 + kCoalKMax + i - 1] = h;
           for (int j = i + 1; j <= k; ++j) prop[2 + kCoalKMax + j - 1] = cur[2 + kCoalKMax + j];
-          sn = coal_score(prop, ev, a.E, T);
+          sn = coal_score(prop, ev, a.E, T, tab);
           const double fwd = gh_log(0.5) - gh_log((double)k);
           const double bwd = ((k - 1 > 0 ? gh_log(0.5) : 0.0) - gh_log((double)k)) - gh_log(upper - lower);
           const double logj = gh_log(h) - 2.0 * gh_log(hp + hn);
