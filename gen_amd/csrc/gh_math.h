@@ -392,7 +392,9 @@ GH_HD void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1
 }
 
 // two standard normals from one Philox block (words x, y, z)
-GH_HD void normal_pair(u32x4 w, double* z0, double* z1) { box_muller(w.x, w.y, w.z, z0, z1); }
+GH_HD void normal_pair(u32x4 w, double* z0, double* z1, const double* tab = nullptr) {
+  box_muller(w.x, w.y, w.z, z0, z1, tab);
+}
 
 // n standard normals from consecutive blocks draw0, draw0+1, ...: pair p takes
 // words 3p, 3p+1, 3p+2 of the concatenated blocks.

@@ -55,28 +55,45 @@ __device__ __forceinline__ double normal_lpdf(double x, double mu, double sd) {
 // 256..1024-thread block reductions (nw waves), result broadcast
 __device__ __forceinline__ double blkn_max(double v, double* sm, int nw) {
   v = wave_max(v);
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   double r = sm[0];
   for (int k = 1; k < nw; ++k) r = fmax(r, sm[k]);
   return r;
 }
 __device__ __forceinline__ double blkn_sum(double v, double* sm, int nw) {
   v = wave_sum(v);
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   double r = sm[0];
   for (int k = 1; k < nw; ++k) r += sm[k];
   return r;
 }
+// two sums in one LDS round (the same per-value order as blkn_sum; sm holds 32)
+__device__ __forceinline__ void blkn_sum2(double* a, double* b, double* sm, int nw) {
+  const double wa = wave_sum(*a), wb = wave_sum(*b);
+  lds_barrier();
+  if ((threadIdx.x & 63) == 0) {
+    sm[threadIdx.x >> 6] = wa;
+    sm[16 + (threadIdx.x >> 6)] = wb;
+  }
+  lds_barrier();
+  double ra = sm[0], rb = sm[16];
+  for (int k = 1; k < nw; ++k) {
+    ra += sm[k];
+    rb += sm[16 + k];
+  }
+  *a = ra;
+  *b = rb;
+}
 __device__ __forceinline__ uint64_t blkn_incl_u64(uint64_t v, uint64_t* sm, int nw) {
   const int w = threadIdx.x >> 6;
   v = wave_incl_sum_u64(v);
-  __syncthreads();
+  lds_barrier();
   if ((threadIdx.x & 63) == 63) sm[w] = v;
-  __syncthreads();
+  lds_barrier();
   for (int k = 0; k < w; ++k) v += sm[k];
   return v;
 }
@@ -84,7 +101,8 @@ __device__ __forceinline__ uint64_t blkn_incl_u64(uint64_t v, uint64_t* sm, int 
 struct PmmhShared {
   double x[kPmmhMaxInner];
   uint64_t C[kPmmhMaxInner];
-  double smd[16];
+  double tab[kMathTabDoubles];  // Box–Muller log / angle tables
+  double smd[32];
   uint64_t smu[16];
 };
 
@@ -107,24 +125,26 @@ __device__ double pmmh_filter(const PmmhArgs& a, PmmhShared& sh, uint64_t c, uin
   };
   // generate: x_1 ~ normal(0, 5), weight = emission logpdf (pf.jl:23-27)
   double z0, z1;
-  normal_pair(rng_block(a.seed, pid, 1, STREAM_INIT, 0), &z0, &z1);
+  normal_pair(rng_block(a.seed, pid, 1, STREAM_INIT, 0), &z0, &z1, sh.tab);
   double x = 0.0 + 5.0 * z0;
   double lw = obs(a.ys[0], x);
   double log_ml = 0.0;
   for (int t = 2; t <= a.T; ++t) {
     // maybe_resample! (particle_filter.jl:189-213), threshold N/2
     const double M = blkn_max(lw, sh.smd, nw);
-    const double e = lw > -INFINITY ? gh_exp(lw - M) : 0.0;
-    const double S = blkn_sum(e, sh.smd, nw);
-    const double S2 = blkn_sum(e * e, sh.smd, nw);
+    // lw - M <= 0: the branch-free exp (gh_exp's values); the same e gives
+    // the quantised weight (= quantize_weight(lw, M, shift))
+    const double e = lw > -INFINITY ? gh_exp_nonpos(lw - M) : 0.0;
+    double S = e, S2 = e * e;
+    blkn_sum2(&S, &S2, sh.smd, nw);
     double xp = x, base = lw;
     if ((S * S) / S2 < (double)N / 2.0) {
       log_ml += (M + gh_log(S)) - logN;
-      const uint64_t qv = quantize_weight(lw, M, shift);
+      const uint64_t qv = (uint64_t)(e * as_f64((uint64_t)(shift + 1023) << 52));
       const uint64_t incl = blkn_incl_u64(qv, sh.smu, nw);
       sh.C[j] = incl;
       sh.x[j] = x;
-      __syncthreads();
+      lds_barrier();
       const uint64_t Stot = sh.C[N - 1];
       const u32x4 w = rng_block(a.seed, cid, (uint32_t)(t - 1), STREAM_RESAMPLE, 0);
       const uint64_t o = scale_u53(u53_bits(w.x, w.y), Stot);
@@ -138,17 +158,17 @@ __device__ double pmmh_filter(const PmmhArgs& a, PmmhShared& sh, uint64_t c, uin
       }
       xp = sh.x[lo];
       base = 0.0;
-      __syncthreads();
+      lds_barrier();
     }
     // particle_filter_step!: x_t ~ normal(x_mean(x_{t-1}, t), sqrt(var_x))
-    normal_pair(rng_block(a.seed, pid, (uint32_t)t, STREAM_STEP, 0), &z0, &z1);
+    normal_pair(rng_block(a.seed, pid, (uint32_t)t, STREAM_STEP, 0), &z0, &z1, sh.tab);
     const double mean = ((xp / 2.0) + 25.0 * (xp / (1.0 + xp * xp))) + a.ct[t - 1];
     x = mean + sx * z0;
     lw = base + obs(a.ys[t - 1], x);
   }
   // log_ml_estimate (particle_filter.jl:52-55)
   const double M = blkn_max(lw, sh.smd, nw);
-  const double e = lw > -INFINITY ? gh_exp(lw - M) : 0.0;
+  const double e = lw > -INFINITY ? gh_exp_nonpos(lw - M) : 0.0;
   const double S = blkn_sum(e, sh.smd, nw);
   return log_ml + (M + gh_log(S)) - logN;
 }
@@ -157,6 +177,8 @@ __global__ __launch_bounds__(kPmmhMaxInner) void k_pmmh(PmmhArgs a) {
   __shared__ PmmhShared sh;
   const int64_t cl = blockIdx.x;
   if (cl >= a.n_chains) return;
+  load_math_tab(sh.tab);
+  lds_barrier();
   const uint64_t c = (uint64_t)(a.chain0 + cl);
   const double sd_rw = 0x1.6a09e667f3bcdp-1;  // sqrt(0.5)
   double lvx, lvy, lml;
