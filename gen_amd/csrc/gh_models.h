@@ -265,7 +265,7 @@ struct KitModel {
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
     double z0, z1;
-    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1);
+    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1, dr.tab);
     x[0] = p.mu1 + p.s1 * z0;
     return obs(p, o, x[0]);
   }
@@ -273,7 +273,7 @@ struct KitModel {
                                 uint32_t t, int /*proposal*/, const double* xp, double* x,
                                 Draw dr = {STREAM_STEP, 0}) {
     double z0, z1;
-    normal_pair(rng_block(seed, pid, t, dr.stream, dr.base), &z0, &z1);
+    normal_pair(rng_block(seed, pid, t, dr.stream, dr.base), &z0, &z1, dr.tab);
     const double v = xp[0];
     const double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
     x[0] = mean + p.sx * z0;
@@ -313,7 +313,7 @@ struct RegModel {
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
     double z0, z1;
-    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1);
+    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1, dr.tab);
     x[0] = p.mu_s + p.sd_s * z0;
     x[1] = p.mu_i + p.sd_i * z1;
     return loglik(p, o, x);
