@@ -71,3 +71,28 @@ def test_gpu_coal_matches_oracle(gh_ctx):
     ch.run(20)
     ref2 = O.coal_run(EVENTS, 300, 20, seed=11, chain0=7, iter0=30, state=ref[0])
     assert np.array_equal(ch.state, ref2[0])
+
+
+@pytest.mark.gpu
+def test_gpu_coal_run_stateless_matches_oracle(gh_ctx):
+    """gh_coal_run (host rows in and out, transposed to the device's SoA layout
+    at the boundary): generate + 25 iterations, then a continuation from the
+    returned rows, against the oracle."""
+    from ctypes import POINTER, byref, c_double, c_int32
+
+    from gen_amd import _lib
+
+    lib = _lib.load()
+    ev = np.ascontiguousarray(np.sort(EVENTS))
+    n = 257
+    st = np.zeros((n, 68))
+    acc = np.zeros((n, 3), dtype=np.int32)
+    ms = c_double()
+    _lib.check(lib.gh_coal_run(gh_ctx.h, 3, n, _lib.dptr(ev), ev.size, 25, 0, 5, 1, _lib.dptr(st),
+                               acc.ctypes.data_as(POINTER(c_int32)), None, byref(ms)))
+    ref = O.coal_run(EVENTS, n, 25, seed=5, chain0=3)
+    assert np.array_equal(st, ref[0]) and np.array_equal(acc, ref[1])
+    _lib.check(lib.gh_coal_run(gh_ctx.h, 3, n, _lib.dptr(ev), ev.size, 10, 25, 5, 0, _lib.dptr(st),
+                               acc.ctypes.data_as(POINTER(c_int32)), None, byref(ms)))
+    ref2 = O.coal_run(EVENTS, n, 10, seed=5, chain0=3, iter0=25, state=ref[0])
+    assert np.array_equal(st, ref2[0]) and np.array_equal(acc, ref2[1])
