@@ -40,6 +40,17 @@ static int set_err(int code, const char* fmt, ...) {
   return code;
 }
 
+// message for a status the device raised (DevScalars::error)
+static const char* dev_error_msg(int code) {
+  switch (code) {
+    case GH_E_NUMERIC: return "maybe_resample: all log-weights are -Inf or NaN";
+    case GH_E_STATE:
+      return "resample grid barrier timed out: its blocks were not co-resident (the device is running other "
+             "kernels); this filter's state is no longer valid";
+    default: return "error raised on the device";
+  }
+}
+
 #define HIP_TRY(x)                                                                       \
   do {                                                                                   \
     hipError_t e_ = (x);                                                                 \
@@ -1305,7 +1316,10 @@ static int resample_enqueue(gh_pf* pf, double thr) {
 extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
   if (pf->t < 1) return set_err(GH_E_STATE, "maybe_resample before init");
-  if (!(thr > 0.0)) thr = (double)pf->n_global / 2.0;
+  // NaN selects the reference's default N/2 (particle_filter.jl:190); any
+  // other value is the threshold itself: ess < 0 never holds, so a threshold
+  // <= 0 turns resampling off exactly as in maybe_resample! (:194)
+  if (thr != thr) thr = (double)pf->n_global / 2.0;
   CHECK(resample_enqueue(pf, thr));
   // conditional SMC: the distinguished particle's parent is itself (smc.jl:139);
   // the ancestor array is only read if the resample fired
@@ -1314,7 +1328,7 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
     DevScalars h;
     HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
     HIP_TRY(hipStreamSynchronize(pf->s));
-    if (h.error) return set_err(h.error, "maybe_resample: all log-weights are -Inf or NaN");
+    if (h.error) return set_err(h.error, dev_error_msg(h.error));
     if (did) *did = h.fire;
     if (ess) *ess = h.ess;
   }
@@ -1353,7 +1367,7 @@ extern "C" int gh_pf_log_ml_estimate(gh_pf* pf, double* out) {
   std::vector<double> st;
   CHECK(ensure_stats(pf));
   CHECK(read_scalars(pf, &h, &st));
-  if (h.error) return set_err(h.error, "log_ml_estimate: numeric error raised on the device");
+  if (h.error) return set_err(h.error, dev_error_msg(h.error));
   if (flags_live(pf) && (h.pending | h.fire)) {  // all weights are 0: logsumexp(w) - log N = 0
     *out = h.log_ml_est;
     return GH_OK;
@@ -1702,7 +1716,7 @@ static int exchange_states(gh_pf* pf, int32_t* anc_out) {
   HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
   HIP_TRY(hipMemcpyAsync(tot.data(), pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->s));
   HIP_TRY(hipStreamSynchronize(pf->s));
-  if (h.error) return set_err(h.error, "maybe_resample: all log-weights are -Inf or NaN");
+  if (h.error) return set_err(h.error, dev_error_msg(h.error));
   if (!h.fire) return GH_OK;
   uint64_t S = 0;
   for (int r = 0; r < R; ++r) S += tot[r];

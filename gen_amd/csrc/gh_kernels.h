@@ -943,9 +943,13 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   __shared__ int32_t se[(kRsBlock * IT)];
   __shared__ int64_t sfirst;
   __shared__ unsigned sgen;
+  __shared__ int sfail;  // the barrier wait timed out: write nothing
   GH_RS_STAMP(0);
   // barrier generation of this launch: read before this block publishes
-  if (threadIdx.x == 0) sgen = r.dev->bar_gen + 1;
+  if (threadIdx.x == 0) {
+    sgen = r.dev->bar_gen + 1;
+    sfail = 0;
+  }
   // ---- fold the step partials (same order in every block: same result)
   // this tile's log-weights are loaded up front, beside the partials
   const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
@@ -1057,8 +1061,12 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   // their sign bit is free) are published and polled the same way.
   const uint64_t kTag = 1ull << 63;
   const uint64_t par = (sgen & 1u) ? kTag : 0ull;
+  // ts1/ts2 are published on EVERY generation (0 when the sums are not in
+  // this pass), so each of the three words alternates its tag strictly and a
+  // matching tag always means this generation's value: a poller can never
+  // pair a fresh tile total with sums left over from two generations back.
   if (threadIdx.x == kRsBlock - 1) st_sc1(&r.tsum[blockIdx.x], incl | par);
-  if (sums && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     st_sc1(&r.ts1[blockIdx.x], (as_u64(s1) & ~kTag) | par);
     st_sc1(&r.ts2[blockIdx.x], (as_u64(s2) & ~kTag) | par);
   }
@@ -1094,6 +1102,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
       if (__builtin_amdgcn_ballot_w64(!all_ok) == 0) break;
       if (spins == (1u << 22)) {
         r.dev->error = 7;  // GH_E_STATE
+        if (threadIdx.x == 0) sfail = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -1147,6 +1156,10 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     }
   }
   lds_barrier();
+  // Not co-resident (the device runs other kernels, so some blocks of this
+  // grid never started): the totals are partial.  The block leaves without
+  // marks or decision; the error surfaces as GH_E_STATE at the next sync.
+  if (sfail) return;
   if (sums) {
     S1 = sS[0];
     S2 = sS[1];
@@ -1238,6 +1251,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
   const uint64_t par = (sgen & 1u) ? kTag : 0ull;
   if (threadIdx.x == 0) st_sc1(&r.tsum[blockIdx.x], tot | par);
   uint64_t all = 0;
+  unsigned failed = 0;
   for (int b = threadIdx.x; b < (int)gridDim.x; b += kRsBlock) {
     uint64_t v = ld_sc1(&r.tsum[b]);
     unsigned spins = 0;
@@ -1245,13 +1259,15 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
       __builtin_amdgcn_s_sleep(1);
       v = ld_sc1(&r.tsum[b]);
       if (++spins == (1u << 22)) {
-        r.dev->error = 7;
+        r.dev->error = 7;  // GH_E_STATE: not co-resident (see k_resample1)
+        failed = 1;
         break;
       }
     }
     all += v & ~kTag;
   }
   all = blk16_sum_u64(all, smu);
+  if (__syncthreads_or(failed)) return;  // partial totals: publish nothing
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     r.dev->local = all;
     r.dev->bar_gen = sgen;
@@ -1579,9 +1595,9 @@ __global__ void k_selftest_boxmuller(int64_t n, const uint32_t* w, double* out) 
   const uint32_t a = w[3 * i], b = w[3 * i + 1], c = w[3 * i + 2];
   const double u1 = one_minus_u53(a, b);
   out[4 * i] = u1;
-  out[4 * i + 1] = sqrt_radius(-2.0 * gh_log_unit(u1));
+  out[4 * i + 1] = sqrt_radius(-2.0 * gh_log_unit(u1, gh_math_tab_dev));
   double z0, z1;
-  box_muller(a, b, c, &z0, &z1);
+  box_muller(a, b, c, &z0, &z1, gh_math_tab_dev);
   out[4 * i + 2] = z0;
   out[4 * i + 3] = z1;
 }
@@ -1600,7 +1616,7 @@ __global__ void k_selftest_normals(uint64_t seed, int64_t n, uint32_t step, uint
       wd[q] = r == 0 ? w.x : r == 1 ? w.y : r == 2 ? w.z : w.w;
     }
     double a, b;
-    box_muller(wd[0], wd[1], wd[2], &a, &b);
+    box_muller(wd[0], wd[1], wd[2], &a, &b, gh_math_tab_dev);
     out[i * dim + 2 * p] = a;
     if (2 * p + 1 < dim) out[i * dim + 2 * p + 1] = b;
   }

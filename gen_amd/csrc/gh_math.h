@@ -267,12 +267,15 @@ __device__ __forceinline__ void load_math_tab(double* lds) {
     reinterpret_cast<double2*>(lds)[i] = reinterpret_cast<const double2*>(gh_math_tab_dev)[i];
 }
 #endif
+// Device callers always pass a table (a block's LDS copy, or gh_math_tab_dev):
+// a select between an LDS and a constant pointer would be a generic pointer,
+// and its flat loads wait on vmcnt as well (every outstanding global load and
+// store of the wave) instead of lgkmcnt alone.
 GH_HD const double* math_tab(const double* tab) {
-  if (tab) return tab;
 #if defined(__HIP_DEVICE_COMPILE__)
-  return gh_math_tab_dev;
+  return tab;
 #else
-  return gh_math_tab_host;
+  return tab ? tab : gh_math_tab_host;
 #endif
 }
 // both doubles of table entry i (16 bytes) in one load

@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kPmmhMaxInner) void k_pmmh(PmmhArgs a) {
   if (a.init) {
     // generate(model, (), observations): priors normal(0, 2) (example.jl:24-25)
     double z0, z1;
-    normal_pair(rng_block(a.seed, c << 10, 0, STREAM_MH, 0), &z0, &z1);
+    normal_pair(rng_block(a.seed, c << 10, 0, STREAM_MH, 0), &z0, &z1, sh.tab);
     lvx = 0.0 + 2.0 * z0;
     lvy = 0.0 + 2.0 * z1;
     lml = pmmh_filter(a, sh, c, 0, lvx, lvy);
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kPmmhMaxInner) void k_pmmh(PmmhArgs a) {
       const uint32_t u = 1u + 4u * (uint32_t)(a.iter0 + k) + (uint32_t)m;
       const uint64_t cid = ((uint64_t)u << 32) | (c << 10);
       double z0, z1;
-      normal_pair(rng_block(a.seed, cid, 0, STREAM_MH, 0), &z0, &z1);
+      normal_pair(rng_block(a.seed, cid, 0, STREAM_MH, 0), &z0, &z1, sh.tab);
       const u32x4 wa = rng_block(a.seed, cid, 0, STREAM_MH, 1);
       const double logu = gh_log(u53(wa.x, wa.y));
       const bool on_x = (m & 1) == 0;

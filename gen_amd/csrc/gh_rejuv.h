@@ -50,6 +50,9 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
                                                   StepObs o, RejuvArgs a) {
   constexpr int D = Model::kD;
   const typename Model::Params p = p0.rebase(prm);
+  __shared__ double tab[kMathTabDoubles];  // Box–Muller tables (LDS reads)
+  load_math_tab(tab);
+  lds_barrier();
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   unsigned acc = 0;
   if (j < a.n) {
@@ -69,7 +72,8 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
     }
     double ll = Model::loglik(p, o, x);
     for (int m = 0; m < a.n_moves; ++m) {
-      const Draw dr = rejuv_draw(a.move0 + (uint32_t)m);
+      Draw dr = rejuv_draw(a.move0 + (uint32_t)m);
+      dr.tab = tab;
       // the prior proposal's weight increment is the observation log-density
       const double ll2 = INIT ? Model::init(p, o, a.seed, pid, 0, y, dr)
                               : Model::step(p, o, a.seed, pid, a.t, 0, xp, y, dr);

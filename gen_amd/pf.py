@@ -277,7 +277,14 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
                                history_capacity: int = 0, time_kernels: int = 0,
                                ctx: Context | None = None) -> ParticleFilterState:
     """initialize_particle_filter(model, model_args, observations, num_particles)
-    initialize_particle_filter(model, model_args, observations, proposal, proposal_args, num_particles)"""
+    initialize_particle_filter(model, model_args, observations, proposal, proposal_args, num_particles)
+
+    Resampling scheme: Gen's maybe_resample! draws parents multinomially
+    (`Distributions.rand!(Categorical(..))`, particle_filter.jl:200); this
+    engine defaults to SYSTEMATIC resampling (the north-star setting, the
+    lower-variance scheme, and the only one the multi-rank path exchanges).
+    Pass resampler="multinomial" for Gen's distribution of parents; both are
+    unbiased, so log-ML estimates agree in expectation, not draw for draw."""
     if len(args) == 1:
         proposal, num_particles = None, args[0]
     elif len(args) == 3:

@@ -34,7 +34,12 @@
  *    copied at call time, outputs are written into caller-allocated buffers.
  *  - Particle indices are 0-based (Julia's are 1-based).
  *  - A gh_pf is driven by one host thread (as the reference's mutable state is);
- *    distinct handles may run concurrently on distinct streams.
+ *    distinct handles may run concurrently on distinct streams.  The resample
+ *    kernels synchronise their whole grid (sized to the co-resident capacity of
+ *    an idle device, no cooperative launch: it costs ~16 us per step), so they
+ *    assume no other kernel occupies the GPU while they run.  If blocks are
+ *    not co-resident the bounded barrier wait expires, the kernel writes
+ *    nothing and the next synchronising call returns GH_E_STATE.
  *  - Multi-GPU: one process per GPU.  Create the context with
  *    gh_ctx_create_dist(); particles [rank*n/world, (rank+1)*n/world) live on
  *    each rank and every gh_pf_* call is collective over the ranks.
@@ -55,7 +60,7 @@ typedef enum {
   GH_E_NOMEM = 4,
   GH_E_HIP = 5,
   GH_E_RCCL = 6,
-  GH_E_STATE = 7     /* call out of order (e.g. step before init) */
+  GH_E_STATE = 7     /* call out of order (e.g. step before init); resample grid barrier timed out */
 } gh_status;
 
 typedef enum {
@@ -155,7 +160,8 @@ int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles
                const gh_pf_opts* opts, gh_pf** out);
 int gh_pf_destroy(gh_pf* pf);
 int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal);
-/* ess_threshold <= 0 (or NaN) means N/2.  If did_resample/ess are non-NULL the
+/* ess_threshold NaN means the reference's default N/2; any other value is the
+   threshold as given (resample iff ESS < ess_threshold, so <= 0 never resamples).  If did_resample/ess are non-NULL the
    call synchronises and reports them; otherwise the decision stays on the
    device and the call is asynchronous. */
 int gh_pf_maybe_resample(gh_pf* pf, double ess_threshold, int* did_resample, double* ess);

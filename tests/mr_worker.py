@@ -32,7 +32,7 @@ def main():
     p.add_argument("--model", default="lg4")
     p.add_argument("--n", type=int, default=3001)
     p.add_argument("--T", type=int, default=8)
-    p.add_argument("--thr", type=float, default=0.0)
+    p.add_argument("--thr", type=float, default=None, help="ESS threshold (default: N/2)")
     p.add_argument("--seed", type=int, default=9)
     p.add_argument("--transport", default="gloo")
     p.add_argument("--rejuv", type=int, default=0, help="rejuvenation moves after init and every step")
@@ -62,7 +62,7 @@ def main():
         gen.rejuvenate(st, a.rejuv)
     did = []
     for t in range(2, a.T + 1):
-        did.append(gen.maybe_resample(st, a.thr if a.thr > 0 else None))
+        did.append(gen.maybe_resample(st, a.thr))
         gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})
         if a.rejuv:
             gen.rejuvenate(st, a.rejuv)

@@ -158,6 +158,52 @@ def test_batched_run_parity(gh_ctx, model, thr, resampler):
     assert_lml_close(st, orc)
 
 
+@pytest.mark.parametrize("model", ["lg10", "kit"])
+def test_batched_run_chunks_and_thresholds(gh_ctx, model):
+    """Several gh_pf_run calls back to back (the grid barrier of the fused
+    resample crosses generations with and without the in-pass weight sums),
+    each chunk with its own threshold: always (N), the default (None = N/2),
+    and 0, which turns resampling off as `ess < 0` never holds in
+    maybe_resample! (particle_filter.jl:194).  Bit-exact vs the oracle."""
+    m = gen.LinearGaussianSSM.benchmark(10) if model == "lg10" else gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(16, np.random.default_rng(8))
+    n = 70001
+    chunks = [(3, n), (1, 0.0), (4, n), (2, None), (3, 0.0), (2, n)]
+    assert sum(c for c, _ in chunks) == len(ys) - 1
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=12)
+    orc = O.OraclePF(m, n, 12, O.SYSTEMATIC)
+    orc.init(ys[0])
+    t, dids = 2, []
+    for c, thr in chunks:
+        gen.run_particle_filter(st, list(ys[t - 1 : t - 1 + c]), thr)
+        for _ in range(c):
+            dids.append(orc.maybe_resample(thr)[0])
+            orc.step(ys[t - 1])
+            t += 1
+    _, did = st.ess_history()
+    assert list(did[: len(ys) - 1]) == [bool(x) for x in dids]
+    # thr = 0 never fires, thr = N always does
+    k = 0
+    for c, thr in chunks:
+        if thr is not None:
+            assert all(bool(x) == (thr > 0) for x in dids[k : k + c]), (k, thr)
+        k += c
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(st.parents, orc.parents())
+    assert_lml_close(st, orc)
+
+
+def test_zero_threshold_never_resamples(gh_ctx):
+    """maybe_resample(state, 0.0) is `ess < 0`: never true, so no resample, the
+    log-ML estimate accumulates nothing, weights keep growing (as in Gen)."""
+    m = gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(6, np.random.default_rng(2))
+    st, orc = run_both(m, ys, 4001, seed=5, thr=0.0)
+    assert not any(st.ess_history()[1][: len(ys) - 1])
+    assert_lml_close(st, orc)
+
+
 def random_lgssm(d, dy, seed):
     rng = np.random.default_rng(seed)
     A = 0.5 * np.eye(d) + 0.1 * rng.standard_normal((d, d))

@@ -227,8 +227,11 @@ def test_gloo_sharded_oracle_with_product_plan(tmp_path, R):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,R,thr,n", [("lg4", 2, 3001.0, 3001), ("lg4", 3, 0.0, 3001), ("kit", 2, 0.0, 3001),
-                                            ("lg10", 2, 3001.0, 3001), ("lg4", 2, 1e9, 20011), ("kit", 4, 1e9, 4003)])
+# thr: a number is passed through (0.0 never resamples: `ess < 0`); None is the
+# reference's default N/2 (the worker passes no --thr)
+@pytest.mark.parametrize("model,R,thr,n", [("lg4", 2, 3001.0, 3001), ("lg4", 3, None, 3001), ("kit", 2, None, 3001),
+                                            ("kit", 2, 0.0, 3001), ("lg10", 2, 3001.0, 3001),
+                                            ("lg4", 2, 1e9, 20011), ("kit", 4, 1e9, 4003)])
 def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr, n):
     """R ranks share GPU 0 through the gloo host transport; the gathered shards
     equal the single-rank oracle bit for bit (log-ML within 1e-9).  n = 20011
@@ -240,10 +243,10 @@ def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr
     out = str(tmp_path / "g")
     T, seed = 8, 9
     _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
-                  "--thr", str(thr), "--seed", str(seed), "--out", out], R, timeout=400)
+                  *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--out", out], R, timeout=400)
     m = build_model(model)
     _, ys = m.simulate(T, np.random.default_rng(5))
-    ref = O.run_pf(m, ys, n, seed, thr=thr if thr > 0 else None)
+    ref = O.run_pf(m, ys, n, seed, thr=thr)
     parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
     states = np.concatenate([p["states"] for p in parts], axis=0)  # [n, d]
     assert np.array_equal(states.T, ref.state())
