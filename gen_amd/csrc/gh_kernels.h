@@ -270,25 +270,40 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   const typename Model::Params p = p0.rebase(prm);
   __shared__ double sm[3][4];
   __shared__ double logtab[kMathTabDoubles];
-  load_math_tab(logtab);
-  lds_barrier();
-  const Draw dr_init{STREAM_INIT, 0, logtab}, dr_step{STREAM_STEP, 0, logtab};
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t vb = blockIdx.x;
   const int64_t tile = vb * (kBlock / 64) + w;
   const int64_t j = tile * 64 + lane;
-  int pend = 0, use_marks = 0;
+  // The device flags and this slot's range mark + carry are loaded before the
+  // table copy, so one memory round trip covers all three (the marks are
+  // read whenever a resample was enqueued; they are used only if it fired).
+  // (clamped indices, no per-lane branch: a value merged at a divergent join
+  // would be waited for right here)
+  uint64_t mv = 0, cv = 0;
+  int pending = 0, fire = 0;
   if (!INIT && a.resampled) {
-    const int pending = a.dev->pending, fire = a.dev->fire;
-    pend = pending | fire;
-    use_marks = a.mark_mode && fire && !pending;
+    pending = a.dev->pending;
+    fire = a.dev->fire;
+    if (a.mark_mode) {
+      const int64_t last = a.n > 0 ? a.n - 1 : 0;
+      mv = a.mark[j < last ? j : last];
+      cv = a.carry[tile < (last >> 6) ? tile : (last >> 6)];
+    }
   }
+  load_math_tab256(logtab);
+  lds_barrier();
+  // the marks are used from here on (the compiler would otherwise compute
+  // their max where they are loaded, and wait for them there)
+  asm volatile("" : "+v"(mv), "+v"(cv));
+  const int pend = pending | fire;
+  const int use_marks = a.mark_mode && fire && !pending;
+  const Draw dr_init{STREAM_INIT, 0, logtab}, dr_step{STREAM_STEP, 0, logtab};
   double lw = -INFINITY;
   if (tile * 64 < a.n) {  // wave-uniform
     int64_t src = j;
     if (use_marks) {
-      uint64_t v = j < a.n ? a.mark[j] : 0;
-      const uint64_t c = a.carry[tile];
+      uint64_t v = j < a.n ? mv : 0;
+      const uint64_t c = cv;
       v = wave_incl_max_u64(v > c ? v : c);
       src = (int64_t)(uint32_t)v;
       if (a.mark_mode == 2) {  // slots outside [ra, rb) take the received rows in slot order

@@ -263,8 +263,30 @@ __constant__ double gh_math_tab_dev[kMathTabDoubles] = {GH_LOG_TABLE_DATA, GH_TR
 // barrier before the first read.  Per-lane table reads then are ds_read_b128
 // instead of vector-memory loads.
 __device__ __forceinline__ void load_math_tab(double* lds) {
+#if defined(GH_ABLATE_TABLE)  // timing-only variant (with GH_ABLATE_BOXMULLER): no table copy
+  return;
+#endif
   for (int i = threadIdx.x; i < kMathTabDoubles / 2; i += blockDim.x)
     reinterpret_cast<double2*>(lds)[i] = reinterpret_cast<const double2*>(gh_math_tab_dev)[i];
+}
+// The same for a block of exactly 256 threads: both loads of a thread are
+// issued before its first LDS write (one memory round trip, no loop).
+__device__ __forceinline__ void load_math_tab256(double* lds) {
+#if defined(GH_ABLATE_TABLE)
+  return;
+#endif
+  static_assert(kMathTabDoubles / 2 > 256 && kMathTabDoubles / 2 <= 512, "two double2 per thread");
+  const double2* src = reinterpret_cast<const double2*>(gh_math_tab_dev);
+  double2* dst = reinterpret_cast<double2*>(lds);
+  constexpr int n = kMathTabDoubles / 2;
+  // entries [256, n) are written twice with the same value (unconditional
+  // stores: a guarded one would let the compiler sink its load behind the
+  // first wait)
+  const int t = threadIdx.x, t1 = 256 + t % (n - 256);
+  const double2 a = src[t];
+  const double2 b = src[t1];
+  dst[t] = a;
+  dst[t1] = b;
 }
 #endif
 // Device callers always pass a table (a block's LDS copy, or gh_math_tab_dev):

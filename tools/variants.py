@@ -21,6 +21,9 @@ VARIANTS = {
     "no_bm": ["GH_ABLATE_BOXMULLER"],
     "philox7": ["GH_PHILOX_ROUNDS=7"],
     "syncbar": ["GH_STEP_SYNCBAR"],
+    "skel_nomv": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_ABLATE_MATVEC"],
+    "skel_occ8": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_LG10_WAVES=8"],
+    "skel_notab": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_ABLATE_TABLE"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
