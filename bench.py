@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--model", default="lgssm", choices=["lgssm", "kitagawa"],
                    help="lgssm: C2 (the headline); kitagawa: the C4 nonlinear SSM")
     p.add_argument("--resampler", default="systematic")
+    p.add_argument("--proposal", default="default", choices=["default", "optimal"],
+                   help="optimal: the LG-SSM's locally optimal proposal (a custom proposal; not the headline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-history", action="store_true")
@@ -120,11 +122,13 @@ def main():
     T = a.warmup + a.steps + 1
     _, ys = model.simulate(T, np.random.default_rng(2 if a.model == "lgssm" else 3))
     n_global = a.particles * world
+    prop = gen.OptimalProposal if a.proposal == "optimal" else None
+    init_args = (prop, (), n_global) if prop is not None else (n_global,)
     st = gen.initialize_particle_filter(
-        model, (1,), {("chain", 1, "y"): ys[0]}, n_global, seed=42, resampler=a.resampler,
+        model, (1,), {("chain", 1, "y"): ys[0]}, *init_args, seed=42, resampler=a.resampler,
         record_history=not a.no_history, history_capacity=T + 2, time_kernels=0 if a.no_kernel_timing else a.time_every,
     )
-    gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold)
+    gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold, proposal=prop)
     ctx.synchronize()
     st.kernel_time_ms(reset=True)
     ess0, did0 = st.ess_history()
@@ -136,7 +140,7 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    gen.run_particle_filter(st, list(ys[1 + a.warmup : 1 + a.warmup + a.steps]), a.ess_threshold)
+    gen.run_particle_filter(st, list(ys[1 + a.warmup : 1 + a.warmup + a.steps]), a.ess_threshold, proposal=prop)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -155,7 +159,8 @@ def main():
     achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
-    if os.path.exists(pmc) and a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20:  # the profiled config
+    if (os.path.exists(pmc) and a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20
+            and prop is None):  # the profiled config
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
@@ -182,7 +187,8 @@ def main():
         "dtype": "f64",
         "data": f"synthetic (observations simulated from the model, numpy seed {2 if a.model == 'lgssm' else 3})",
         "config": {
-            "workload": (f"C2: {a.d}-dim linear-Gaussian SSM bootstrap PF" if a.model == "lgssm" else
+            "workload": (f"C2: {a.d}-dim linear-Gaussian SSM " + ("optimal-proposal PF" if prop else "bootstrap PF")
+                         if a.model == "lgssm" else
                          "C4: Kitagawa nonlinear SSM bootstrap PF") + f", {a.particles} particles/GPU, "
                         f"systematic resampling at ESS<N/2, record_history={not a.no_history}",
             "particles_global": n_global,
@@ -204,7 +210,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": f"k_step<LGModel<{a.d},3>,false>" if a.model == "lgssm" else "k_step<KitModel,false>",
+            "kernel": (f"k_step<LGOptModel<{a.d}>,false>" if prop else f"k_step<LGModel<{a.d},3>,false>")
+                      if a.model == "lgssm" else "k_step<KitModel,false>",
             "kernel_avg_ms": kms,
             "kernel_launches": kcount,
             "bytes_per_particle_step": bytes_pp,

@@ -296,6 +296,24 @@ static void fwdsub(int d, int m, const double* L, const double* B, double* Y) {
       Y[i * m + c] = s / L[i * d + i];
     }
 }
+// X = L^{-T} B for B (d x m) row-major (backward substitution on L^T)
+static void bwdsub(int d, int m, const double* L, const double* B, double* X) {
+  for (int c = 0; c < m; ++c)
+    for (int i = d - 1; i >= 0; --i) {
+      double s = B[i * m + c];
+      for (int k = i + 1; k < d; ++k) s = fma(-L[k * d + i], X[k * m + c], s);
+      X[i * m + c] = s / L[i * d + i];
+    }
+}
+// C = A B (A: n x k, B: k x m), fma over the inner index ascending
+static void matmul(int n, int k, int m, const double* A, const double* B, double* C) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < m; ++j) {
+      double acc = 0.0;
+      for (int l = 0; l < k; ++l) acc = fma(A[i * k + l], B[l * m + j], acc);
+      C[i * m + j] = acc;
+    }
+}
 static double gauss_cst(int d, const double* L) {
   double acc = 0.0;
   for (int i = 0; i < d; ++i) acc += gh_log(L[i * d + i]);
@@ -310,6 +328,11 @@ struct gh_model {
   double* dparams = nullptr;  // device copy of the derived parameters
   // host copies needed per step
   std::vector<double> LR, c;  // LGSSM: chol(R), offset c
+  // LGSSM locally optimal proposal (LGOptModel): host halves
+  bool lg_opt = false;        // derivable (S, Sigma positive definite, d + dy <= kMaxObs)
+  std::vector<double> LS, Kt, Fb, Wb;       // chol(S), K^T (dy x d), F b, L_S^-1 H b
+  std::vector<double> H, mu0, LS1, Kt1;     // t = 1: H, mu0, chol(S_1), K_1^T
+  double cstS1 = 0.0;
   LGParams lg{};
   int lg_struct = 0;  // LGModel<D, S> structure bits (gh_models.h)
   HMMParams hmm{};
@@ -352,7 +375,7 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     if (chol(d, P0, L0.data())) return fail(GH_E_INVAL, "LGSSM: P0 not positive definite");
     fwdsub(dy, d, m->LR.data(), H, M.data());
     m->c.assign(c, c + dy);
-    // layout: A | b | LQ | M | mu0 | L0
+    // layout: A | b | LQ | M | mu0 | L0 | FA | LSig | WA | LSig1 (below)
     h.insert(h.end(), A, A + d * d);
     h.insert(h.end(), b, b + d);
     h.insert(h.end(), LQ.begin(), LQ.end());
@@ -367,6 +390,59 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     for (int r = 0; m_diag && r < dy; ++r)
       for (int j = 0; j < d; ++j) m_diag = m_diag && (j == r || M[r * d + j] == 0.0);
     m->lg_struct = (lq_diag ? 1 : 0) | (m_diag ? 2 : 0);
+    // locally optimal proposal: S = H Q H^T + R, K^T = S^-1 H Q, F = I - K H,
+    // Sigma = F Q (the same operations as oracle/gh_oracle.c lg_opt_build)
+    std::vector<double> FA(d * d, 0.0), LSig(d * d, 0.0), WA(dy * d, 0.0), LSig1(d * d, 0.0);
+    auto derive = [&](const double* P, std::vector<double>& LSo, std::vector<double>& Kto,
+                      std::vector<double>& Lsigo, std::vector<double>* F_out) -> bool {
+      std::vector<double> HP(dy * d), Sm(dy * dy), Y(dy * d), F(d * d), Sig(d * d);
+      matmul(dy, d, d, H, P, HP.data());
+      for (int r = 0; r < dy; ++r)
+        for (int q = 0; q < dy; ++q) {
+          double acc = R[r * dy + q];
+          for (int j = 0; j < d; ++j) acc = fma(HP[r * d + j], H[q * d + j], acc);
+          Sm[r * dy + q] = acc;
+        }
+      LSo.assign(dy * dy, 0.0);
+      if (chol(dy, Sm.data(), LSo.data())) return false;
+      fwdsub(dy, d, LSo.data(), HP.data(), Y.data());
+      Kto.assign(dy * d, 0.0);
+      bwdsub(dy, d, LSo.data(), Y.data(), Kto.data());
+      for (int i = 0; i < d; ++i)
+        for (int j = 0; j < d; ++j) {
+          double acc = i == j ? 1.0 : 0.0;
+          for (int r = 0; r < dy; ++r) acc = fma(-Kto[r * d + i], H[r * d + j], acc);
+          F[i * d + j] = acc;
+        }
+      matmul(d, d, d, F.data(), P, Sig.data());
+      Lsigo.assign(d * d, 0.0);
+      if (chol(d, Sig.data(), Lsigo.data())) return false;
+      if (F_out) *F_out = F;
+      return true;
+    };
+    std::vector<double> F, LSigv, LSig1v;
+    m->lg_opt = d + dy <= kMaxObs && derive(Q, m->LS, m->Kt, LSigv, &F) && derive(P0, m->LS1, m->Kt1, LSig1v, nullptr);
+    if (m->lg_opt) {
+      matmul(d, d, d, F.data(), A, FA.data());
+      m->Fb.assign(d, 0.0);
+      matmul(d, d, 1, F.data(), b, m->Fb.data());
+      std::vector<double> W(dy * d);
+      fwdsub(dy, d, m->LS.data(), H, W.data());
+      matmul(dy, d, d, W.data(), A, WA.data());
+      m->Wb.assign(dy, 0.0);
+      matmul(dy, d, 1, W.data(), b, m->Wb.data());
+      LSig = LSigv;
+      LSig1 = LSig1v;
+      m->lg.cstS = gauss_cst(dy, m->LS.data());
+      m->cstS1 = gauss_cst(dy, m->LS1.data());
+      m->H.assign(H, H + dy * d);
+      m->mu0.assign(mu0, mu0 + d);
+    }
+    // proposal blocks after the prior's (zeros when not derivable)
+    h.insert(h.end(), FA.begin(), FA.end());
+    h.insert(h.end(), LSig.begin(), LSig.end());
+    h.insert(h.end(), WA.begin(), WA.end());
+    h.insert(h.end(), LSig1.begin(), LSig1.end());
   } else if (desc->family == GH_FAMILY_HMM) {
     const int K = desc->k, V = desc->v;
     if (K < 1 || K > 64 || V < 1) return fail(GH_E_INVAL, "HMM: need 1 <= k <= 64, v >= 1");
@@ -418,7 +494,11 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->lg.LQ = q; q += d * d;
     m->lg.M = q; q += dy * d;
     m->lg.mu0 = q; q += d;
-    m->lg.L0 = q;
+    m->lg.L0 = q; q += d * d;
+    m->lg.FA = q; q += d * d;
+    m->lg.LSig = q; q += d * d;
+    m->lg.WA = q; q += dy * d;
+    m->lg.LSig1 = q;
   } else if (m->family == GH_FAMILY_HMM) {
     const int K = m->k, V = m->v;
     m->hmm.base = m->dparams;
@@ -469,6 +549,50 @@ static int make_obs(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
     o->v[0] = in->values[0];
   }
   return GH_OK;
+}
+
+// The optimal proposal's per-step vectors (LGOptModel): t = 1: o.v[0, d) =
+// mu_1 = mu0 + K_1 (y - c - H mu0), o.ct = log N(y; H mu0 + c, S_1); t >= 2:
+// o.v[0, d) = g_t = F b + K (y - c), o.v[d, d + dy) = L_S^-1 (y - c) - L_S^-1 H b.
+static int make_obs_opt(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
+  CHECK(make_obs(m, t, in, o));
+  if (!o->present) return GH_OK;
+  const int d = m->d, dy = m->dy;
+  double r[kMaxObs];
+  for (int i = 0; i < dy; ++i) r[i] = in->values[i] - m->c[i];
+  if (t == 1) {
+    double e[kMaxObs], u[kMaxObs];
+    for (int q = 0; q < dy; ++q) {
+      double acc = r[q];
+      for (int j = 0; j < d; ++j) acc = fma(-m->H[q * d + j], m->mu0[j], acc);
+      e[q] = acc;
+    }
+    fwdsub(dy, 1, m->LS1.data(), e, u);
+    double quad = 0.0;
+    for (int q = 0; q < dy; ++q) quad = fma(u[q], u[q], quad);
+    o->ct = m->cstS1 - 0.5 * quad;
+    for (int i = 0; i < d; ++i) {
+      double acc = m->mu0[i];
+      for (int q = 0; q < dy; ++q) acc = fma(m->Kt1[q * d + i], e[q], acc);
+      o->v[i] = acc;
+    }
+    return GH_OK;
+  }
+  double ls[kMaxObs];
+  fwdsub(dy, 1, m->LS.data(), r, ls);
+  for (int i = 0; i < d; ++i) {
+    double acc = 0.0;
+    for (int q = 0; q < dy; ++q) acc = fma(m->Kt[q * d + i], r[q], acc);
+    o->v[i] = m->Fb[i] + acc;
+  }
+  for (int q = 0; q < dy; ++q) o->v[d + q] = ls[q] - m->Wb[q];
+  return GH_OK;
+}
+
+static bool proposal_ok(const gh_model* m, int proposal) {
+  if (proposal == GH_PROPOSAL_DEFAULT) return true;
+  if (proposal != GH_PROPOSAL_OPTIMAL) return false;
+  return m->family == GH_FAMILY_HMM || (m->family == GH_FAMILY_LGSSM && m->lg_opt);
 }
 
 // ------------------------------------------------------------ the PF state
@@ -734,6 +858,20 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
                        hipEvent_t e1 = nullptr) {
   if (!init && pf->m->family == GH_FAMILY_REGRESSION)
     return set_err(GH_E_INVAL, "the regression model has no time steps");
+  if (a.proposal == GH_PROPOSAL_OPTIMAL && pf->m->family == GH_FAMILY_LGSSM) {
+    // the LGSSM's locally optimal proposal is its own functor (the default
+    // step kernel stays free of the proposal's code and registers)
+    switch (pf->m->d) {
+#define GH_LGO_CASE(DD) \
+  case DD: launch_step_t<LGOptModel<DD>>(pf, pf->m->lg, o, a, init, e0, e1); break;
+      GH_LGO_CASE(1) GH_LGO_CASE(2) GH_LGO_CASE(3) GH_LGO_CASE(4) GH_LGO_CASE(5) GH_LGO_CASE(6)
+      GH_LGO_CASE(7) GH_LGO_CASE(8) GH_LGO_CASE(10) GH_LGO_CASE(12) GH_LGO_CASE(16)
+#undef GH_LGO_CASE
+      default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", pf->m->d);
+    }
+    HIP_TRY(hipGetLastError());
+    return GH_OK;
+  }
   CHECK(with_model(pf->m, [&](auto model, const auto& p) {
     launch_step_t<decltype(model)>(pf, p, o, a, init, e0, e1);
   }));
@@ -835,8 +973,9 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (!m || !out) return set_err(GH_E_INVAL, "gh_pf_init: null argument");
   if (n_particles < 1 || n_particles > 0x7fffffffLL)
     return set_err(GH_E_INVAL, "gh_pf_init: num_particles must be in 1..2^31-1");
-  if (proposal == GH_PROPOSAL_OPTIMAL && m->family != GH_FAMILY_HMM)
-    return set_err(GH_E_INVAL, "gh_pf_init: the optimal proposal is implemented for HMM only");
+  if (!proposal_ok(m, proposal))
+    return set_err(GH_E_INVAL, "gh_pf_init: proposal %d is not available for this model (the optimal proposal: "
+                               "HMM, and LGSSM with d + dy <= %d)", proposal, kMaxObs);
   gh_ctx* ctx = m->ctx;
   HIP_TRY(hipSetDevice(ctx->device));
   gh_pf* pf = new gh_pf();
@@ -914,8 +1053,12 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     int rc = ensure_capacity(pf, cap0);
     if (rc) return fail(rc);
   }
-  StepObs o;
-  int rc = make_obs(m, 1, obs, &o);
+  StepObs o, o_prior;
+  int rc = make_obs(m, 1, obs, &o_prior);
+  if (!rc) {
+    o = o_prior;
+    if (proposal == GH_PROPOSAL_OPTIMAL && m->family == GH_FAMILY_LGSSM) rc = make_obs_opt(m, 1, obs, &o);
+  }
   if (rc) return fail(rc);
   StepArgs a{};
   a.xout = slot_x(pf, 1);
@@ -944,7 +1087,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   rc = share_stats(pf);
   if (rc) return fail(rc);
   pf->t = 1;
-  pf->last_obs = o;
+  pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
   *out = pf;
   return GH_OK;
 }
@@ -966,14 +1109,17 @@ extern "C" int gh_pf_step_conditional(gh_pf* pf, const gh_obs* obs, const double
 
 static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double* pin_ref) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
-  if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family != GH_FAMILY_HMM)
-    return set_err(GH_E_INVAL, "the optimal proposal is implemented for HMM only");
+  if (!proposal_ok(pf->m, proposal))
+    return set_err(GH_E_INVAL, "proposal %d is not available for this model (the optimal proposal: HMM, and "
+                               "LGSSM with d + dy <= %d)", proposal, kMaxObs);
   if (pf->m->family == GH_FAMILY_REGRESSION)
     return set_err(GH_E_INVAL, "the regression model has no time steps (particle_filter_step needs an Unfold)");
   const int t = pf->t + 1;
   CHECK(grow_for_step(pf, t));
-  StepObs o;
-  CHECK(make_obs(pf->m, t, obs, &o));
+  StepObs o, o_prior;
+  CHECK(make_obs(pf->m, t, obs, &o_prior));
+  o = o_prior;
+  if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family == GH_FAMILY_LGSSM) CHECK(make_obs_opt(pf->m, t, obs, &o));
   StepArgs a{};
   a.xprev = slot_x(pf, t - 1);
   a.ld_prev = pf->n;
@@ -1010,7 +1156,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   pf->max_only = a.max_only != 0;
   pf->resample_calls = 0;
   pf->marks_pending = false;
-  pf->last_obs = o;
+  pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
   pf->rejuv_moves = 0;
   return GH_OK;
 }

@@ -35,7 +35,7 @@ struct Draw {
 // per-step observation, passed by value in the kernel arguments
 struct StepObs {
   double v[kMaxObs];  // LGSSM: L_R^{-1}(y - c); Kitagawa: y; HMM: symbol
-  double ct;          // Kitagawa: 8 cos(1.2 t)
+  double ct;          // Kitagawa: 8 cos(1.2 t); LGSSM optimal proposal at t = 1: the (constant) weight
   int present;
   int sym;            // HMM symbol (integer copy of v[0])
 };
@@ -58,8 +58,15 @@ struct LGParams {
   const double* M;    // dy*d  L_R^{-1} H
   const double* mu0;  // d
   const double* L0;   // d*d lower Cholesky factor of P0
+  // locally optimal proposal (LGOptModel): N(F A x + g_t, Sigma), weight
+  // log N(y; H (A x + b) + c, S) with S = H Q H^T + R, F = I - K H
+  const double* FA;   // d*d F A
+  const double* LSig; // d*d chol(Sigma), Sigma = F Q
+  const double* WA;   // dy*d L_S^{-1} H A
+  const double* LSig1;// d*d chol((I - K_1 H) P0), the t = 1 proposal
   int dy;
   double cstR;        // -0.5 (dy log 2pi + log det R)
+  double cstS;        // -0.5 (dy log 2pi + log det S)
   __device__ LGParams rebase(const double* __restrict__ prm) const {
     LGParams q = *this;
     q.A = rebased(*this, prm, A);
@@ -68,6 +75,10 @@ struct LGParams {
     q.M = rebased(*this, prm, M);
     q.mu0 = rebased(*this, prm, mu0);
     q.L0 = rebased(*this, prm, L0);
+    q.FA = rebased(*this, prm, FA);
+    q.LSig = rebased(*this, prm, LSig);
+    q.WA = rebased(*this, prm, WA);
+    q.LSig1 = rebased(*this, prm, LSig1);
     return q;
   }
 };
@@ -149,6 +160,68 @@ struct LGModel {
       x[i] = acc;
     }
     return obs(p, o, x);
+  }
+};
+
+// ------------------------------------------------ LGSSM, optimal proposal
+// The locally optimal proposal of the linear-Gaussian SSM, a custom proposal
+// in Gen's sense (particle_filter.jl:79-91,139-154 via the
+// SimpleExtendingTraceTranslator, trace_translators.jl:775-802): x_t is drawn
+// from p(x_t | x_{t-1}, y_t) = N(mu, Sigma) and the weight
+//   model weight - proposal score = log p(x_t|x_{t-1}) + log p(y_t|x_t) - log q(x_t)
+// collapses to log p(y_t | x_{t-1}) = log N(y_t; H (A x_{t-1} + b) + c, S),
+// evaluated in that closed form (as the HMM's optimal proposal is).  Host
+// precomputes: S = H Q H^T + R, K = Q H^T S^-1, F = I - K H,
+// Sigma = F Q; per step the vectors g_t = F b + K (y_t - c) (o.v[i], i < d) and
+// v_t = L_S^-1 (y_t - c) - L_S^-1 H b (o.v[d + r]); at t = 1 the proposal mean
+// mu_1 (o.v[i]) and the constant weight log N(y_1; H mu0 + c, H P0 H^T + R)
+// (o.ct).  Without an observation the proposal is the prior (LGModel).
+template <int D>
+struct LGOptModel {
+  static constexpr int kD = D;
+  static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 8 ? 5 : 4);
+  using Params = LGParams;
+  using Prior = LGModel<D, 0>;
+
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return Prior::loglik(p, o, x); }
+
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, int proposal,
+                                double* x, Draw dr = {STREAM_INIT, 0}) {
+    if (!o.present) return Prior::init(p, o, seed, pid, proposal, x, dr);
+    double z[D + 1];
+    normals_n<D>(seed, pid, 1, dr.stream, dr.base, z, dr.tab);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = o.v[i];
+#pragma unroll
+      for (int k = 0; k <= i; ++k) acc = fma(p.LSig1[i * D + k], z[k], acc);
+      x[i] = acc;
+    }
+    return o.ct;
+  }
+
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, uint32_t t,
+                                int proposal, const double* xp, double* x, Draw dr = {STREAM_STEP, 0}) {
+    if (!o.present) return Prior::step(p, o, seed, pid, t, proposal, xp, x, dr);
+    double z[D + 1];
+    normals_n<D>(seed, pid, t, dr.stream, dr.base, z, dr.tab);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = o.v[i];
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc = fma(p.FA[i * D + k], xp[k], acc);
+#pragma unroll
+      for (int k = 0; k <= i; ++k) acc = fma(p.LSig[i * D + k], z[k], acc);
+      x[i] = acc;
+    }
+    double quad = 0.0;
+    for (int r = 0; r < p.dy; ++r) {
+      double u = o.v[D + r];
+#pragma unroll
+      for (int k = 0; k < D; ++k) u = fma(-p.WA[r * D + k], xp[k], u);
+      quad = fma(u, u, quad);
+    }
+    return p.cstS - 0.5 * quad;
   }
 };
 

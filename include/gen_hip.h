@@ -89,8 +89,10 @@ typedef enum { GH_RESAMPLE_SYSTEMATIC = 0, GH_RESAMPLE_MULTINOMIAL = 1 } gh_resa
 
 typedef enum {
   GH_PROPOSAL_DEFAULT = 0, /* the model's internal proposal (prior) */
-  GH_PROPOSAL_OPTIMAL = 1  /* locally optimal proposal (HMM only), the custom proposal
-                              of test/inference/particle_filter.jl:104-127 */
+  GH_PROPOSAL_OPTIMAL = 1  /* locally optimal proposal p(x_t | x_{t-1}, y_t) as a custom
+                              proposal (particle_filter.jl:79-91,139-154): HMM (the proposal
+                              of test/inference/particle_filter.jl:104-127) and LGSSM
+                              (Gaussian, d + dy <= 32); weight log p(y_t | x_{t-1}) */
 } gh_proposal;
 
 typedef struct gh_ctx gh_ctx;

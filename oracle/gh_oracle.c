@@ -272,6 +272,24 @@ static void fwdsub(int d, int m, const double* L, const double* B, double* Y) {
       Y[i * m + c] = s / L[i * d + i];
     }
 }
+/* X = L^{-T} B for B (d x m) row-major */
+static void bwdsub(int d, int m, const double* L, const double* B, double* X) {
+  for (int c = 0; c < m; ++c)
+    for (int i = d - 1; i >= 0; --i) {
+      double s = B[i * m + c];
+      for (int k = i + 1; k < d; ++k) s = fma(-L[k * d + i], X[k * m + c], s);
+      X[i * m + c] = s / L[i * d + i];
+    }
+}
+/* C = A B (n x k times k x m), fma over the inner index ascending */
+static void matmul(int n, int k, int m, const double* A, const double* B, double* C) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < m; ++j) {
+      double acc = 0.0;
+      for (int l = 0; l < k; ++l) acc = fma(A[i * k + l], B[l * m + j], acc);
+      C[i * m + j] = acc;
+    }
+}
 static double gauss_cst(int d, const double* L) {
   double acc = 0.0;
   for (int i = 0; i < d; ++i) acc += orc_log(L[i * d + i]);
@@ -285,6 +303,10 @@ typedef struct {
   /* LGSSM */
   double *A, *b, *LQ, *M, *LR, *c, *mu0, *L0, cstR;
   int lq_diag, m_diag;  /* exact-zero structure: skipped terms */
+  /* locally optimal proposal p(x_t | x_{t-1}, y_t): S = H Q H^T + R,
+     K^T = S^{-1} H Q, F = I - K H, Sigma = F Q; at t = 1 the same with P0 */
+  int opt;
+  double *H, *LS, *Kt, *FA, *Fb, *LSig, *WA, *Wb, *LS1, *Kt1, *LSig1, cstS, cstS1;
   /* HMM */
   double *prior, *T, *E, *logE;
   /* Kitagawa */
@@ -297,6 +319,42 @@ typedef struct {
 static void model_free(model_t* m) {
   free(m->A); free(m->b); free(m->LQ); free(m->M); free(m->LR); free(m->c); free(m->mu0);
   free(m->L0); free(m->prior); free(m->T); free(m->E); free(m->logE);
+  free(m->H); free(m->LS); free(m->Kt); free(m->FA); free(m->Fb); free(m->LSig); free(m->WA); free(m->Wb);
+  free(m->LS1); free(m->Kt1); free(m->LSig1);
+}
+
+/* the optimal proposal's factors for state prior covariance P: chol(S), K^T,
+   chol(Sigma) and (optionally) F; returns 0 when S and Sigma are positive definite */
+static int opt_derive(int d, int dy, const double* H, const double* R, const double* P, double* LS, double* Kt,
+                      double* LSig, double* F_out) {
+  double* HP = malloc(sizeof(double) * dy * d);
+  double* S = malloc(sizeof(double) * dy * dy);
+  double* Y = malloc(sizeof(double) * dy * d);
+  double* F = malloc(sizeof(double) * d * d);
+  double* Sig = malloc(sizeof(double) * d * d);
+  int rc = 0;
+  matmul(dy, d, d, H, P, HP);
+  for (int r = 0; r < dy; ++r)
+    for (int q = 0; q < dy; ++q) {
+      double acc = R[r * dy + q];
+      for (int j = 0; j < d; ++j) acc = fma(HP[r * d + j], H[q * d + j], acc);
+      S[r * dy + q] = acc;
+    }
+  if (chol(dy, S, LS)) { rc = -1; goto out; }
+  fwdsub(dy, d, LS, HP, Y);
+  bwdsub(dy, d, LS, Y, Kt);
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      double acc = i == j ? 1.0 : 0.0;
+      for (int r = 0; r < dy; ++r) acc = fma(-Kt[r * d + i], H[r * d + j], acc);
+      F[i * d + j] = acc;
+    }
+  matmul(d, d, d, F, P, Sig);
+  if (chol(d, Sig, LSig)) { rc = -1; goto out; }
+  if (F_out) memcpy(F_out, F, sizeof(double) * d * d);
+out:
+  free(HP); free(S); free(Y); free(F); free(Sig);
+  return rc;
 }
 
 static int model_build(model_t* m, int family, int d, int dy, int k, int v, const double* p,
@@ -327,6 +385,28 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->m_diag = dy == d;
     for (int r = 0; m->m_diag && r < dy; ++r)
       for (int j = 0; j < d; ++j) if (j != r && m->M[r * d + j] != 0.0) m->m_diag = 0;
+    /* locally optimal proposal (engine: gh_model_create; needs d + dy <= 32) */
+    m->H = malloc(sizeof(double) * dy * d); memcpy(m->H, H, sizeof(double) * dy * d);
+    m->LS = calloc(dy * dy, sizeof(double)); m->Kt = calloc(dy * d, sizeof(double));
+    m->LSig = calloc(d * d, sizeof(double)); m->LS1 = calloc(dy * dy, sizeof(double));
+    m->Kt1 = calloc(dy * d, sizeof(double)); m->LSig1 = calloc(d * d, sizeof(double));
+    m->FA = calloc(d * d, sizeof(double)); m->Fb = calloc(d, sizeof(double));
+    m->WA = calloc(dy * d, sizeof(double)); m->Wb = calloc(dy, sizeof(double));
+    double* F = malloc(sizeof(double) * d * d);
+    m->opt = d + dy <= 32 && opt_derive(d, dy, H, R, Q, m->LS, m->Kt, m->LSig, F) == 0 &&
+             opt_derive(d, dy, H, R, P0, m->LS1, m->Kt1, m->LSig1, NULL) == 0;
+    if (m->opt) {
+      matmul(d, d, d, F, A, m->FA);
+      matmul(d, d, 1, F, b, m->Fb);
+      double* W = malloc(sizeof(double) * dy * d);
+      fwdsub(dy, d, m->LS, H, W);
+      matmul(dy, d, d, W, A, m->WA);
+      matmul(dy, d, 1, W, b, m->Wb);
+      free(W);
+      m->cstS = gauss_cst(dy, m->LS);
+      m->cstS1 = gauss_cst(dy, m->LS1);
+    }
+    free(F);
   } else if (family == ORC_HMM) {
     if (np < (int64_t)k + (int64_t)k * k + (int64_t)v * k) return -1;
     m->d = 1;
@@ -361,6 +441,9 @@ typedef struct {
   int present;
   double bt[64];  /* LGSSM: L_R^{-1}(y - c); Kitagawa: y; HMM: symbol */
   double ct;      /* Kitagawa: 8 cos(1.2 t) */
+  /* LGSSM optimal proposal: t = 1: mean mu1 (g) and constant weight w0;
+     t >= 2: g = F b + K (y - c), vt = L_S^{-1}(y - c) - L_S^{-1} H b */
+  double g[64], vt[64], w0;
 } obs_t;
 
 static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* o) {
@@ -372,6 +455,34 @@ static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* 
     double r[64];
     for (int i = 0; i < m->dy; ++i) r[i] = y[i] - m->c[i];
     fwdsub(m->dy, 1, m->LR, r, o->bt);
+    if (m->opt) {
+      int d = m->d, dy = m->dy;
+      if (t == 1) {
+        double e[64] = {0}, u[64] = {0}, quad = 0.0;
+        for (int q = 0; q < dy; ++q) {
+          double acc = r[q];
+          for (int j = 0; j < d; ++j) acc = fma(-m->H[q * d + j], m->mu0[j], acc);
+          e[q] = acc;
+        }
+        fwdsub(dy, 1, m->LS1, e, u);
+        for (int q = 0; q < dy; ++q) quad = fma(u[q], u[q], quad);
+        o->w0 = m->cstS1 - 0.5 * quad;
+        for (int i = 0; i < d; ++i) {
+          double acc = m->mu0[i];
+          for (int q = 0; q < dy; ++q) acc = fma(m->Kt1[q * d + i], e[q], acc);
+          o->g[i] = acc;
+        }
+      } else {
+        double ls[64];
+        fwdsub(dy, 1, m->LS, r, ls);
+        for (int i = 0; i < d; ++i) {
+          double acc = 0.0;
+          for (int q = 0; q < dy; ++q) acc = fma(m->Kt[q * d + i], r[q], acc);
+          o->g[i] = m->Fb[i] + acc;
+        }
+        for (int q = 0; q < dy; ++q) o->vt[q] = ls[q] - m->Wb[q];
+      }
+    }
   } else if (m->family == ORC_REGRESSION) {
     for (int i = 0; i < m->dy; ++i) o->bt[i] = y[i];
   } else {
@@ -438,6 +549,15 @@ static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const
   if (m->family == ORC_LGSSM) {
     double z[64];
     normals_at(seed, pid, 1, stream, base, m->d, z);
+    if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
+      /* x ~ N(mu1, (I - K1 H) P0); weight log N(y; H mu0 + c, H P0 H^T + R) */
+      for (int i = 0; i < m->d; ++i) {
+        double acc = o->g[i];
+        for (int k = 0; k <= i; ++k) acc = fma(m->LSig1[i * m->d + k], z[k], acc);
+        x[i] = acc;
+      }
+      return o->w0;
+    }
     for (int i = 0; i < m->d; ++i) {
       double acc = m->mu0[i];
       for (int k = 0; k <= i; ++k) acc = fma(m->L0[i * m->d + k], z[k], acc);
@@ -479,10 +599,28 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
     double z[64];
     normals_at(seed, pid, t, stream, base, m->d, z);
     int d = m->d;
+    if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
+      /* x ~ N(F A xp + g, Sigma); weight log p(y | xp) = log N(y; H (A xp + b) + c, S) */
+      for (int i = 0; i < d; ++i) {
+        double acc = o->g[i];
+        for (int k = 0; k < d; ++k) acc = fma(m->FA[i * d + k], xp[k], acc);
+        for (int k = 0; k <= i; ++k) acc = fma(m->LSig[i * d + k], z[k], acc);
+        x[i] = acc;
+      }
+      double quad = 0.0;
+      for (int r = 0; r < m->dy; ++r) {
+        double u = o->vt[r];
+        for (int k = 0; k < d; ++k) u = fma(-m->WA[r * d + k], xp[k], u);
+        quad = fma(u, u, quad);
+      }
+      return m->cstS - 0.5 * quad;
+    }
     for (int i = 0; i < d; ++i) {
       double acc = m->b[i];
       for (int k = 0; k < d; ++k) acc = fma(m->A[i * d + k], xp[k], acc);
-      if (m->lq_diag) acc = fma(m->LQ[i * d + i], z[i], acc);
+      /* the optimal proposal without an observation is the prior in its dense
+         form (the engine's LGOptModel<D> falls back to LGModel<D, 0>) */
+      if (m->lq_diag && proposal != ORC_PROPOSAL_OPTIMAL) acc = fma(m->LQ[i * d + i], z[i], acc);
       else for (int k = 0; k <= i; ++k) acc = fma(m->LQ[i * d + k], z[k], acc);
       x[i] = acc;
     }
@@ -607,7 +745,12 @@ static int init_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
   record(pf);
   return 0;
 }
+static int proposal_ok(const model_t* m, int proposal) {
+  if (proposal == 0) return 1;
+  return proposal == ORC_PROPOSAL_OPTIMAL && (m->family == ORC_HMM || (m->family == ORC_LGSSM && m->opt));
+}
 int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
+  if (!proposal_ok(&pf->m, proposal)) return -1;
   return init_impl(pf, obs, has_obs, proposal, NULL);
 }
 int orc_pf_init_conditional(orc_pf* pf, const double* obs, int has_obs, const double* ref) {
@@ -653,7 +796,7 @@ static int step_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
 }
 
 int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal) {
-  if (pf->cond) return -1;
+  if (pf->cond || !proposal_ok(&pf->m, proposal)) return -1;
   return step_impl(pf, obs, has_obs, proposal, NULL);
 }
 int orc_pf_step_conditional(orc_pf* pf, const double* obs, int has_obs, const double* ref) {

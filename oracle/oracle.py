@@ -144,7 +144,8 @@ class OraclePF:
 
     def init(self, y, proposal=DEFAULT):
         a, has = self._obs(y)
-        lib().orc_pf_init(self.h, _d(a), has, proposal)
+        if lib().orc_pf_init(self.h, _d(a), has, proposal):
+            raise ValueError("oracle: proposal not available for this model")
 
     def step(self, y, proposal=DEFAULT):
         a, has = self._obs(y)

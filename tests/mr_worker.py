@@ -36,6 +36,7 @@ def main():
     p.add_argument("--seed", type=int, default=9)
     p.add_argument("--transport", default="gloo")
     p.add_argument("--rejuv", type=int, default=0, help="rejuvenation moves after init and every step")
+    p.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK)")
     p.add_argument("--out", required=True)
     a = p.parse_args()
 
@@ -52,7 +53,8 @@ def main():
     else:
         uid = [gen.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ctx = gen.Context(device=int(os.environ.get("LOCAL_RANK", "0")), rank=rank, world=world, unique_id=uid[0])
+        dev = a.device if a.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
+        ctx = gen.Context(device=dev, rank=rank, world=world, unique_id=uid[0])
     gen.set_default_context(ctx)
     m = build_model(a.model)
     _, ys = m.simulate(a.T, np.random.default_rng(5))

@@ -1,0 +1,127 @@
+"""The LG-SSM's locally optimal proposal (a custom proposal in Gen's sense,
+src/inference/particle_filter.jl:79-91,139-154 through the
+SimpleExtendingTraceTranslator, src/inference/trace_translators.jl:775-802).
+
+x_t ~ p(x_t | x_{t-1}, y_t) = N(mu, Sigma) and the particle's weight is
+model weight - proposal score = log p(y_t | x_{t-1}) (as for the HMM's
+optimal proposal, test/inference/particle_filter.jl:96-143).
+
+CPU: the oracle's weights against scipy's multivariate normal density and its
+log-ML against the exact Kalman filter (parity with the closed forms, pinned
+independently of the engine).  GPU: states, weights, parents and log-ML of
+the engine equal the oracle's (bit-exact / 1e-9).
+"""
+import numpy as np
+import pytest
+from scipy.stats import multivariate_normal
+
+import gen_amd as gen
+from oracle import oracle as O
+
+
+def dense_model(d, dy, seed):
+    rng = np.random.default_rng(seed)
+    A = 0.6 * np.eye(d) + 0.1 * rng.standard_normal((d, d))
+    B = rng.standard_normal((d, d))
+    C = rng.standard_normal((dy, dy))
+    P = rng.standard_normal((d, d))
+    return gen.LinearGaussianSSM(A, 0.1 * B @ B.T + 0.05 * np.eye(d), rng.standard_normal((dy, d)),
+                                 0.2 * C @ C.T + 0.3 * np.eye(dy), rng.standard_normal(d),
+                                 0.5 * P @ P.T + 0.5 * np.eye(d), b=0.1 * rng.standard_normal(d),
+                                 c=0.1 * rng.standard_normal(dy))
+
+
+def predictive(m, mean_x, cov_x, y):
+    """log N(y; H mean + c, H cov H^T + R)"""
+    return multivariate_normal(m.H @ mean_x + m.c, m.H @ cov_x @ m.H.T + m.R).logpdf(y)
+
+
+@pytest.mark.parametrize("d,dy", [(3, 2), (4, 4), (10, 10)])
+def test_oracle_optimal_weights_are_predictive_densities(d, dy):
+    m = dense_model(d, dy, 3) if d != 10 else gen.LinearGaussianSSM.benchmark(10)
+    _, ys = m.simulate(3, np.random.default_rng(1))
+    n = 64
+    orc = O.OraclePF(m, n, 5)
+    orc.init(ys[0], O.OPTIMAL)
+    # t = 1: every particle carries log p(y_1) under the prior N(mu0, P0)
+    w1 = orc.log_weights()
+    assert np.allclose(w1, predictive(m, m.mu0, m.P0, ys[0]), rtol=1e-12, atol=1e-12)
+    x1 = orc.state()
+    orc.step(ys[1], O.OPTIMAL)  # no resample: the weight increments add to w1
+    inc = orc.log_weights() - w1
+    ref = np.array([predictive(m, m.A @ x1[:, i] + m.b, m.Q, ys[1]) for i in range(n)])
+    assert np.allclose(inc, ref, rtol=1e-11, atol=1e-11)
+
+
+def test_oracle_optimal_proposal_moments():
+    """x_t | x_{t-1}, y_t has the Kalman-update mean and covariance."""
+    m = dense_model(3, 2, 7)
+    _, ys = m.simulate(2, np.random.default_rng(2))
+    n = 200000
+    orc = O.OraclePF(m, n, 9, record_history=False)
+    orc.init(ys[0], O.OPTIMAL)
+    x = orc.state()
+    S = m.H @ m.P0 @ m.H.T + m.R
+    K = m.P0 @ m.H.T @ np.linalg.inv(S)
+    mu = m.mu0 + K @ (ys[0] - m.H @ m.mu0 - m.c)
+    Sig = m.P0 - K @ m.H @ m.P0
+    se = np.sqrt(np.diag(Sig) / n)
+    assert np.all(np.abs(x.mean(axis=1) - mu) < 5 * se)
+    assert np.allclose(np.cov(x), Sig, atol=0.02 * np.max(np.abs(Sig)))
+
+
+def test_oracle_optimal_pf_matches_kalman():
+    """The optimal proposal's PF estimates the exact Kalman log marginal with a
+    much smaller Monte-Carlo error than the bootstrap filter."""
+    m = dense_model(4, 3, 11)
+    _, ys = m.simulate(12, np.random.default_rng(3))
+    exact = m.kalman_log_marginal(ys)
+    err_opt, err_boot = [], []
+    for s in range(3):
+        err_opt.append(O.run_pf(m, ys, 40000, s, proposal=O.OPTIMAL).log_ml_estimate() - exact)
+        err_boot.append(O.run_pf(m, ys, 40000, s).log_ml_estimate() - exact)
+    rms = lambda e: float(np.sqrt(np.mean(np.square(e))))  # noqa: E731
+    assert max(abs(e) for e in err_opt) < 0.05, (err_opt, exact)
+    assert rms(err_opt) < 0.5 * rms(err_boot), (err_opt, err_boot)
+
+
+def test_optimal_proposal_rejected_where_unavailable():
+    m = gen.KitagawaSSM(10.0, 1.0)
+    with pytest.raises(ValueError):
+        O.OraclePF(m, 10, 1).init(np.array([0.3]), O.OPTIMAL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["dense4", "lg10", "dense_3x7"])
+def test_gpu_optimal_proposal_bitexact(gh_ctx, name):
+    m = {"dense4": lambda: dense_model(4, 3, 5), "lg10": lambda: gen.LinearGaussianSSM.benchmark(10),
+         "dense_3x7": lambda: dense_model(3, 7, 6)}[name]()
+    _, ys = m.simulate(9, np.random.default_rng(4))
+    ys = [y if t != 4 else None for t, y in enumerate(ys)]  # one step without an observation
+    n = 9001
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, gen.OptimalProposal, (), n, seed=21)
+    orc = O.OraclePF(m, n, 21)
+    orc.init(ys[0], O.OPTIMAL)
+    for t in range(2, len(ys) + 1):
+        thr = n if t % 3 else None
+        assert gen.maybe_resample(st, thr) == orc.maybe_resample(thr)[0]
+        gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {m.obs_address(t): ys[t - 1]},
+                                 gen.OptimalProposal)
+        orc.step(ys[t - 1], O.OPTIMAL)
+        assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64)), t
+        assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64)), t
+        assert np.array_equal(st.parents, orc.parents()), t
+    a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+    assert abs(a - b) <= 1e-9 * max(1.0, abs(b))
+
+
+@pytest.mark.gpu
+def test_gpu_optimal_proposal_log_ml_near_kalman(gh_ctx):
+    """2^20 particles on the C2 model: the optimal-proposal filter's log-ML is
+    within 0.01 of the exact Kalman value over 30 steps."""
+    m = gen.LinearGaussianSSM.benchmark(10)
+    _, ys = m.simulate(30, np.random.default_rng(8))
+    n = 1 << 20
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, gen.OptimalProposal, (), n, seed=3)
+    gen.run_particle_filter(st, list(ys[1:]), None, proposal=gen.OptimalProposal)
+    assert abs(gen.log_ml_estimate(st) - m.kalman_log_marginal(ys)) < 0.01
