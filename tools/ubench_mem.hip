@@ -136,6 +136,39 @@ __global__ __launch_bounds__(kBlock) void k_gather_wt(Args a) {
   for (int k = 0; k < D; ++k) __hip_atomic_store(&a.y[k * a.ld + j], x[k] + 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&a.logw[j], 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// gather with 16-byte stores: lane pairs swap halves so that each lane holds
+// two consecutive particles of D/2 columns (row_xmask DPP), then dwordx4 stores
+__global__ __launch_bounds__(kBlock) void k_gather_st16(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t j = tile * 64 + lane;
+  uint64_t v = a.mark[j];
+  const uint64_t c = a.carry[tile];
+  v = wave_incl_max_u64(v > c ? v : c);
+  const int64_t src = (int64_t)(uint32_t)v;
+  a.anc[j] = (int32_t)src;
+  double x[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) x[k] = a.x[k * a.ld + src] + 1.0;
+  const bool odd = lane & 1;
+  const int64_t j0 = j & ~1ll;
+#pragma unroll
+  for (int h = 0; h < D / 2; ++h) {
+    // even lane keeps column h and sends column h + D/2; odd lane the reverse
+    const double mine = odd ? x[h] : x[h + D / 2];
+    const uint64_t u = __builtin_bit_cast(uint64_t, mine);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, 0xb1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), 0xb1, 0xf, 0xf, true);
+    const double other = __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+    const int col = odd ? h + D / 2 : h;
+    double2 pr;
+    pr.x = odd ? other : x[h];     // particle j0
+    pr.y = odd ? x[h + D / 2] : other;  // particle j0 + 1
+    *reinterpret_cast<double2*>(&a.y[col * a.ld + j0]) = pr;
+  }
+  a.logw[j] = 1.0;
+}
+
 // a dependent small kernel (the resample's fold: every block reads 4096 doubles)
 __global__ __launch_bounds__(1024) void k_small(const double* p, double* out) {
   double m = -1e300;
@@ -277,6 +310,14 @@ int main() {
          hipLaunchKernelGGL(k_small, dim3(256), dim3(1024), 0, 0, a.logw, (double*)a.tab); }},
       {"small_only", bytes_gather, [](const Args& a, int64_t nvb, int) {
          hipLaunchKernelGGL(k_small, dim3(256), dim3(1024), 0, 0, a.logw, (double*)a.tab); }},
+      {"hist_st16", bytes_gather, [](const Args& a0, int64_t nvb, int) {
+         Args a = a0;
+         a.x = g_hist + (size_t)(g_slot % 16) * D * N;
+         a.y = g_hist + (size_t)((g_slot + 1) % 16) * D * N;
+         ++g_slot;
+         hipLaunchKernelGGL(k_gather_st16, dim3(nvb), dim3(kBlock), 0, 0, a); }},
+      {"st16_same", bytes_gather, [](const Args& a, int64_t nvb, int) {
+         hipLaunchKernelGGL(k_gather_st16, dim3(nvb), dim3(kBlock), 0, 0, a); }},
       {"hist2", bytes_gather, [](const Args& a, int64_t nvb, int) { g_nslots = 2; hist_launch(a, nvb, 0); }},
       {"hist3", bytes_gather, [](const Args& a, int64_t nvb, int) { g_nslots = 3; hist_launch(a, nvb, 0); }},
       {"hist4", bytes_gather, [](const Args& a, int64_t nvb, int) { g_nslots = 4; hist_launch(a, nvb, 0); }},
