@@ -19,7 +19,11 @@ Also reported:
                steps) / its hipEvent-timed average duration on its stream;
                traffic = PMC HBM bytes per launch from profiles/ when present.
   cpu_baseline the CPU oracle (C restatement of Gen's PF, 1 core) on a bounded
-               sample of the same workload, timed on this host.
+               sample of the same workload, timed on this host; its "parity"
+               entry runs the GPU filter and the oracle on the same
+               observations, seed and 2^16 particles and reports the log-ML
+               relative difference (north star: <= 1e-6) and whether the final
+               ancestors agree bit for bit.
 """
 from __future__ import annotations
 
@@ -60,6 +64,28 @@ def parse():
     p.add_argument("--time-every", type=int, default=10,
                    help="time every k-th step kernel with launch events (each timed launch adds queue packets)")
     return p.parse_args()
+
+
+def cpu_parity(model, ys, n, resampler, proposal):
+    """The GPU filter and the CPU restatement of Gen's filter (oracle/) on the
+    same workload, seed and N = n over every observation of the run: their
+    log-ML estimates (the north star's "within 1e-6 relative on fixed RNG
+    seeds") and whether the final ancestors agree bit for bit."""
+    import gen_amd as gen
+    from oracle import oracle as O
+
+    prop = gen.OptimalProposal if proposal == "optimal" else None
+    st = gen.initialize_particle_filter(model, (1,), {("chain", 1, "y"): ys[0]},
+                                        *((prop, (), n) if prop is not None else (n,)), seed=42, resampler=resampler)
+    gen.run_particle_filter(st, list(ys[1:]), None, proposal=prop)
+    gpu = gen.log_ml_estimate(st)
+    gpu_parents = st.parents
+    st.close()
+    orc = O.run_pf(model, ys, n, 42, resampler=O.SYSTEMATIC if resampler == "systematic" else O.MULTINOMIAL,
+                   proposal=O.OPTIMAL if prop is not None else O.DEFAULT, record_history=False)
+    cpu = orc.log_ml_estimate()
+    return {"particles": n, "steps": len(ys), "seed": 42, "log_ml_gpu": gpu, "log_ml_cpu": cpu,
+            "rel": abs(gpu - cpu) / abs(cpu), "parents_bitexact": bool((gpu_parents == orc.parents()).all())}
 
 
 def cpu_baseline(model, ys, budget_s):
@@ -219,6 +245,11 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(model, ys, a.cpu_seconds)
+        # same seed, same observations, N = 2^16: GPU vs the CPU restatement
+        par = cpu_parity(model, ys, 1 << 16, a.resampler, a.proposal)
+        out["cpu_baseline"]["parity"] = par
+        if out["log_ml_error"] is not None:
+            out["log_ml_error"]["vs_cpu_reference_same_seed"] = {"particles": par["particles"], "rel": par["rel"]}
     if rank == 0:
         print(json.dumps(out), flush=True)
     st.close()
