@@ -3,8 +3,9 @@
 Gen's `choicemap((:chain => t => :y, y_t))` (src/choice_map.jl:659-670) maps
 hierarchical addresses to values.  Here an address is a tuple, e.g.
 ("chain", 3, "y") for `:chain => 3 => :y`; `choicemap(((addr), value), ...)`
-builds one.  Only what the hot path consumes is implemented: lookup by the
-address of one time step (the flat `to_array` idea, choice_map.jl:163-169).
+builds one.  Besides lookup by address, `to_array` / `from_array` flatten a
+choice map's values and rebuild one of the same address structure
+(choice_map.jl:163-225).
 """
 from __future__ import annotations
 
@@ -54,6 +55,34 @@ class ChoiceMap:
             if a in out._d:
                 raise ValueError(f"merge: both choice maps have a value at {a}")
             out._d[a] = v
+        return out
+
+    def to_array(self):
+        """to_array(choices, Float64) (choice_map.jl:163-169): every value in
+        address order (the order the choices were added), vectors flattened."""
+        import numpy as np
+
+        parts = [np.atleast_1d(np.asarray(v, dtype=np.float64)).ravel() for v in self._d.values()]
+        return np.concatenate(parts) if parts else np.zeros(0)
+
+    def from_array(self, arr) -> "ChoiceMap":
+        """from_array(proto_choices, arr) (choice_map.jl:190-225): a choice map
+        with this one's addresses and value shapes, values read off arr in
+        to_array's order.  It is an error if arr has the wrong length."""
+        import numpy as np
+
+        arr = np.asarray(arr, dtype=np.float64).ravel()
+        out, pos = ChoiceMap(), 0
+        for a, v in self._d.items():
+            shape = np.shape(v)
+            size = int(np.prod(shape)) if shape else 1
+            if pos + size > arr.size:
+                raise ValueError("from_array: the array is shorter than the prototype's values")
+            chunk = arr[pos:pos + size]
+            out._d[a] = float(chunk[0]) if not shape else chunk.reshape(shape).copy()
+            pos += size
+        if pos != arr.size:
+            raise ValueError("from_array: the array is longer than the prototype's values")
         return out
 
     def __repr__(self):

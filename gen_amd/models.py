@@ -20,6 +20,18 @@ import numpy as np
 from . import _lib
 
 
+def _mvn_logpdf(x, mean, cov) -> float:
+    L = np.linalg.cholesky(cov)
+    z = np.linalg.solve(L, np.asarray(x, dtype=np.float64) - mean)
+    return float(-0.5 * (x.size * np.log(2 * np.pi) + 2.0 * np.log(np.diag(L)).sum() + z @ z))
+
+
+def _normal_logpdf(x, mu, std) -> float:
+    """normal.jl:56-60"""
+    var = std * std
+    return float(-((x - mu) ** 2) / (2.0 * var) - 0.5 * np.log(2.0 * np.pi * var))
+
+
 class Model:
     family: int
     d: int = 1
@@ -130,6 +142,19 @@ class LinearGaussianSSM(Model):
             P = P - K @ self.H @ P
         return float(ll)
 
+    def log_joint(self, xs, ys) -> float:
+        """Score of a trace (Gen's `get_score`): log p(x_1..T, y_1..T) of one
+        latent trajectory xs [T, d] and its observations (None = absent), the
+        sum of the mvnormal logpdfs (mvnormal.jl:12-16) of every choice."""
+        xs = np.atleast_2d(np.asarray(xs, dtype=np.float64))
+        total = 0.0
+        for t, x in enumerate(xs):
+            mean, cov = (self.mu0, self.P0) if t == 0 else (self.A @ xs[t - 1] + self.b, self.Q)
+            total += _mvn_logpdf(x, mean, cov)
+            if ys is not None and ys[t] is not None:
+                total += _mvn_logpdf(np.atleast_1d(ys[t]), self.H @ x + self.c, self.R)
+        return float(total)
+
     @staticmethod
     def benchmark(d: int = 10, seed: int = 1) -> "LinearGaussianSSM":
         """The C2 synthetic model of SURVEY.md §8(d): A = 0.9 I + 0.01 G rescaled to
@@ -164,6 +189,16 @@ class DiscreteHMM(Model):
     def params(self):
         return np.concatenate([self.prior, self.T.ravel(), self.E.ravel()])
 
+    def log_joint(self, zs, xs) -> float:
+        """Score of a trace: log p(z_1..T, x_1..T) (categorical.jl:10-12)."""
+        total = 0.0
+        for t, z in enumerate(np.asarray(zs).ravel().astype(int)):
+            total += np.log(self.prior[z] if t == 0 else self.T[z, prev])
+            if xs is not None and xs[t] is not None:
+                total += np.log(self.E[int(np.asarray(xs[t]).ravel()[0]), z])
+            prev = z
+        return float(total)
+
     def obs_address(self, t: int):
         return ("x_init",) if t == 1 else ("chain", t - 1, "x")
 
@@ -183,6 +218,21 @@ class KitagawaSSM(Model):
 
     def params(self):
         return np.array([self.mu1, self.s1, self.var_x, self.var_y])
+
+    def log_joint(self, xs, ys) -> float:
+        """Score of a trace: log p(x_1..T, y_1..T) (normal.jl:56-60 per choice)."""
+        xs = np.asarray(xs, dtype=np.float64).ravel()
+        total = 0.0
+        for t in range(1, xs.size + 1):
+            x = xs[t - 1]
+            if t == 1:
+                total += _normal_logpdf(x, self.mu1, self.s1)
+            else:
+                v = xs[t - 2]
+                total += _normal_logpdf(x, v / 2 + 25 * v / (1 + v * v) + 8 * np.cos(1.2 * t), np.sqrt(self.var_x))
+            if ys is not None and ys[t - 1] is not None:
+                total += _normal_logpdf(float(np.asarray(ys[t - 1]).ravel()[0]), x * x / 20.0, np.sqrt(self.var_y))
+        return float(total)
 
     def simulate(self, T: int, rng: np.random.Generator):
         xs = np.zeros(T)
@@ -240,6 +290,15 @@ class BayesianLinearRegression(Model):
         if seen != self.dy:
             raise _lib.GenHipError(1, "constrain every y-i (partial observations are not lowered)")
         return ys
+
+    def log_joint(self, x, ys) -> float:
+        """Score of a trace: log p(slope, intercept, y_1..n)."""
+        slope, intercept = np.asarray(x, dtype=np.float64).ravel()[:2]
+        total = _normal_logpdf(slope, self.mu_s, self.sd_s) + _normal_logpdf(intercept, self.mu_i, self.sd_i)
+        if ys is not None:
+            for xi, yi in zip(self.xs, np.asarray(ys, dtype=np.float64).ravel()):
+                total += _normal_logpdf(yi, slope * xi + intercept, self.sigma)
+        return float(total)
 
     def constraints(self, ys):
         return {self.y_address(i + 1): float(y) for i, y in enumerate(ys)}

@@ -165,6 +165,11 @@ class ParticleFilterState:
         ng, nl, lo = c_int64(), c_int64(), c_int64()
         _lib.check(_lib.load().gh_pf_num_particles(handle, byref(ng), byref(nl), byref(lo)))
         self.n_local, self.first = nl.value, lo.value
+        # the observations of every step (host copies) for trace materialisation
+        self.observations: dict[int, np.ndarray | None] = {}
+
+    def _log_obs(self, t: int, arr) -> None:
+        self.observations[t] = None if arr is None else np.array(arr, copy=True)
 
     @property
     def t(self) -> int:
@@ -252,13 +257,70 @@ class ParticleTraces:
     def __getitem__(self, i):
         return _TraceView(self, int(i))
 
+    def step_states(self, t: int) -> np.ndarray:
+        """[n_local, d] latents of step t along every particle's genealogy (cached)."""
+        if t not in self._cache:
+            self._cache[t] = self.state.states(t)
+        return self._cache[t]
+
 
 class _TraceView:
+    """One particle's trace (`get_traces(state)[i]`): the Unfold's latent
+    trajectory along the particle's genealogy plus the observations, with the
+    trace accessors of src/gen_fn_interface.jl (`get_args`, `get_choices`,
+    `get_score`; `trace[addr]` as `getindex`)."""
+
     def __init__(self, traces: ParticleTraces, i: int):
         self.traces, self.i = traces, i
 
     def __getitem__(self, addr):
         return self.traces.column(addr)[self.i]
+
+    def get_args(self) -> tuple:
+        """The model arguments: (T,) for the Unfold models, () for a static model."""
+        st = self.traces.state
+        return () if st.model.static else (st.t,)
+
+    def trajectory(self) -> np.ndarray:
+        """[T, d] latent of every step of this particle's ancestral line."""
+        st = self.traces.state
+        return np.stack([self.traces.step_states(t)[self.i] for t in range(1, st.t + 1)])
+
+    def _obs(self):
+        st = self.traces.state
+        return [st.observations.get(t) for t in range(1, st.t + 1)]
+
+    def get_choices(self) -> ChoiceMap:
+        """get_choices(trace): every latent choice and observation by address."""
+        st = self.traces.state
+        m = st.model
+        cm = ChoiceMap()
+        xs = self.trajectory()
+        if m.static:  # BayesianLinearRegression: :slope, :intercept, "y-i"
+            cm[("slope",)] = float(xs[0, 0])
+            cm[("intercept",)] = float(xs[0, 1])
+            ys = st.observations.get(1)
+            if ys is not None:
+                for i, y in enumerate(np.asarray(ys).ravel()):
+                    cm[m.y_address(i + 1)] = float(y)
+            return cm
+        for t in range(1, st.t + 1):
+            x = xs[t - 1]
+            cm[m.latent_address(t)] = float(x[0]) if x.size == 1 else x.copy()
+            y = st.observations.get(t)
+            if y is not None:
+                y = np.asarray(y).ravel()
+                cm[m.obs_address(t)] = float(y[0]) if y.size == 1 else y.copy()
+        return cm
+
+    def get_score(self) -> float:
+        """get_score(trace) = log p(every choice), evaluated on the host from
+        the materialised trajectory (models.py `log_joint`)."""
+        st = self.traces.state
+        xs = self.trajectory()
+        if st.model.static:
+            return st.model.log_joint(xs[0], st.observations.get(1))
+        return st.model.log_joint(xs if st.model.d > 1 else xs[:, 0], self._obs())
 
 
 # --------------------------------------------------------------- the API
@@ -300,8 +362,9 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
     opts = _opts(resampler, record_history, history_capacity, time_kernels)
     _lib.check(_lib.load().gh_pf_init(mh, byref(obs), _proposal_code(proposal), int(num_particles),
                                       int(seed) & 0xFFFFFFFFFFFFFFFF, byref(opts), byref(h)))
-    del keep
-    return ParticleFilterState(ctx, model, h, int(num_particles))
+    st = ParticleFilterState(ctx, model, h, int(num_particles))
+    st._log_obs(1, keep)
+    return st
 
 
 def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: tuple, observations,
@@ -313,7 +376,7 @@ def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: 
         raise _lib.GenHipError(1, "the length argument changes: its argdiff must be UnknownChange()")
     obs, keep = _step_obs(state.model, t, observations)
     _lib.check(_lib.load().gh_pf_step(state.h, byref(obs), _proposal_code(proposal)))
-    del keep
+    state._log_obs(t, keep)
 
 
 def maybe_resample(state: ParticleFilterState, ess_threshold: float | None = None, verbose: bool = False) -> bool:
@@ -348,6 +411,8 @@ def run_particle_filter(state: ParticleFilterState, observations_per_step, ess_t
             arr[i] = _lib.Obs(_lib.dptr(a), a.size, 1)
     thr = state.num_particles / 2 if ess_threshold is None else float(ess_threshold)
     _lib.check(_lib.load().gh_pf_run(state.h, len(observations_per_step), arr, _proposal_code(proposal), thr))
+    for i, v in enumerate(observations_per_step):
+        state._log_obs(t0 + 1 + i, None if v is None else model.obs_values(v))
     del keep, t0
 
 
@@ -412,8 +477,9 @@ def initialize_conditional_particle_filter(model: Model, model_args: tuple, obse
     opts = _opts("multinomial", record_history, history_capacity, 0)
     _lib.check(_lib.load().gh_pf_init_conditional(mh, byref(obs), int(num_particles), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                                   byref(opts), _lib.dptr(ref), byref(h)))
-    del keep
-    return ParticleFilterState(ctx, model, h, int(num_particles))
+    st = ParticleFilterState(ctx, model, h, int(num_particles))
+    st._log_obs(1, keep)
+    return st
 
 
 def conditional_particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: tuple, observations,
@@ -426,7 +492,7 @@ def conditional_particle_filter_step(state: ParticleFilterState, new_args: tuple
     obs, keep = _step_obs(state.model, t, observations)
     ref = _ref_state(state.model, reference_xt)
     _lib.check(_lib.load().gh_pf_step_conditional(state.h, byref(obs), _lib.dptr(ref)))
-    del keep
+    state._log_obs(t, keep)
 
 
 def conditional_smc(model: Model, observations_per_step, num_particles: int, reference, seed: int = 0,
