@@ -639,9 +639,15 @@ struct gh_pf {
   int32_t* xanc = nullptr;        // [send_cap] local ancestors of the sent rows
   int64_t send_cap = 0;
   int64_t* gparent = nullptr;     // [n] global parent ids of the last exchange
-  hipStream_t aux = nullptr;      // multi-rank: side stream for the plan's D2H read
+  hipStream_t aux = nullptr;      // multi-rank: side stream (the plan's D2H read, the row exchange)
   hipEvent_t ev_tot = nullptr;    // multi-rank: totals all-gathered
+  hipEvent_t ev_plan = nullptr;   //   fire flag + totals landed in h_plan
+  hipEvent_t ev_rb = nullptr;     //   k_rank_b packed the rows
+  hipEvent_t ev_x = nullptr;      //   rows exchanged
   uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]]
+  bool plan_pending = false;      // k_rank_b enqueued; the host has not read the totals yet
+  bool rem_fire = false;          // the resample fired (read by finish_plan)
+  int64_t rem_ra = 0, rem_rb = 0; // local slots [0, ra) and [rb, n) take received rows
   int mark_mode = 1;              // 1: one-rank marks; 2: marks + received rows
   // rejuvenation (gh_pf_rejuvenate): the current step's observation and the
   // MH moves already applied at this step (their draw windows)
@@ -764,6 +770,7 @@ static void pf_free(gh_pf* pf) {
   if (!pf) return;
   hipSetDevice(pf->ctx->device);
   hipStreamSynchronize(pf->s);
+  if (pf->aux) hipStreamSynchronize(pf->aux);
   for (auto c : pf->chunks) hipFree(c);
   for (auto e : pf->ev) hipEventDestroy(e);
   hipFree(pf->logw); hipFree(pf->C); hipFree(pf->mark); hipFree(pf->cmark); hipFree(pf->bsum); hipFree(pf->pm); hipFree(pf->ps);
@@ -773,6 +780,9 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->acc_count); hipFree(pf->pin);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
+  if (pf->ev_plan) hipEventDestroy(pf->ev_plan);
+  if (pf->ev_rb) hipEventDestroy(pf->ev_rb);
+  if (pf->ev_x) hipEventDestroy(pf->ev_x);
   if (pf->h_plan) hipHostFree(pf->h_plan);
   if (!pf->opts.record_history) {
     for (auto p : pf->xs) hipFree(p);
@@ -791,8 +801,8 @@ template <class Model>
 static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const StepObs& o,
                           const StepArgs& a0, bool init, hipEvent_t e0, hipEvent_t e1) {
   StepArgs a = a0;
-  a.nvb = pf->nb_step;
-  const dim3 grid((unsigned)pf->nb_step), block(kBlock);
+  a.nvb = (a.n + kBlock - 1) / kBlock;
+  const dim3 grid((unsigned)(a.part == 2 ? a.nvb : pf->nb_step)), block(kBlock);
   // the timed launch records its events at the kernel's own start and end
   if (init)
     hipExtLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, e0, e1, 0, (const double*)pf->m->dparams,
@@ -802,10 +812,10 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
                           p, o, a);
 }
 
-// fold the step kernel's block partials into the rank's (M, S, S2)
-static void launch_fold(gh_pf* pf, const StepArgs& a, bool init) {
-  hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_step,
-                     a.stats_out, pf->dev, init ? 0 : 1, 0.0, pf->n_global);
+// fold the step kernel's block partials (nb of them) into the rank's (M, S, S2)
+static void launch_fold(gh_pf* pf, const StepArgs& a, bool init, int64_t nb) {
+  hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)nb, a.stats_out, pf->dev,
+                     init ? 0 : 1, 0.0, pf->n_global);
 }
 
 // one rank: make stats_all current (the fold is otherwise done by k_resample1)
@@ -879,6 +889,53 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
   return GH_OK;
 }
 
+static int finish_plan(gh_pf* pf);
+
+// Multi-rank, after the step kernel: when the step followed a resample it was
+// enqueued before the host read the plan (part 1); now the plan is read, the
+// rows exchanged and the tiles holding slots that take received rows run
+// again (part 2).  Then the fold of the block partials.
+static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init) {
+  if (a.part == 1) {
+    CHECK(finish_plan(pf));
+    if (pf->rem_fire) {
+      // tiles [0, tA) and [tB, nb) hold the slots [0, ra) and [rb, n)
+      const int64_t n = pf->n, nb = pf->nb_step, ra = pf->rem_ra, rb = pf->rem_rb;
+      int64_t tA = (ra + kBlock - 1) / kBlock;
+      int64_t tB = rb < n ? rb / kBlock : nb;
+      if (tB <= tA) {  // the ranges meet: one launch over every tile
+        tA = nb;
+        tB = nb;
+      }
+      if (tA > 0) {
+        StepArgs b = a;
+        b.part = 2;
+        b.n = std::min<int64_t>(n, tA * kBlock);
+        CHECK(launch_step(pf, o, b, init));
+      }
+      if (tB < nb) {  // every per-slot pointer advanced to tile tB
+        const int64_t off = tB * kBlock;
+        StepArgs b = a;
+        b.part = 2;
+        b.j0 = off;
+        b.n = n - off;
+        b.lo = a.lo + off;
+        b.anc = a.anc + off;
+        b.mark = a.mark + off;
+        b.carry = a.carry + off / 64;
+        b.xout = a.xout + off;
+        b.logw = a.logw + off;
+        b.pm = a.pm + tB;
+        b.ps = a.ps + tB;
+        b.ps2 = a.ps2 + tB;
+        CHECK(launch_step(pf, o, b, init));
+      }
+    }
+  }
+  launch_fold(pf, a, init, pf->nb_step);
+  return GH_OK;
+}
+
 // the step kernel (timed alone when opts.time_kernels).  Multi-rank: the
 // fold follows at once (its triple is all-gathered every step); one rank: the
 // next maybe_resample! folds inside k_resample1, other readers fold on demand.
@@ -888,7 +945,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   const int every = pf->opts.time_kernels;
   if (every <= 0 || (a.t - 1) % (uint32_t)every != 0) {
     CHECK(launch_step(pf, o, a, init));
-    if (pf->ctx->world > 1) launch_fold(pf, a, init);
+    if (pf->ctx->world > 1) CHECK(finish_split(pf, o, a, init));
     HIP_TRY(hipGetLastError());
     return GH_OK;
   }
@@ -902,7 +959,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   hipEvent_t e0 = pf->ev[pf->ev_used], e1 = pf->ev[pf->ev_used + 1];
   pf->ev_used += 2;
   CHECK(launch_step(pf, o, a, init, e0, e1));
-  if (pf->ctx->world > 1) launch_fold(pf, a, init);
+  if (pf->ctx->world > 1) CHECK(finish_split(pf, o, a, init));
   HIP_TRY(hipGetLastError());
   return GH_OK;
 }
@@ -1022,6 +1079,9 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     ALLOC(pf->gparent, sizeof(int64_t) * n);
     if (hipStreamCreateWithFlags(&pf->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&pf->ev_tot, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&pf->ev_plan, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&pf->ev_rb, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&pf->ev_x, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&pf->h_plan, sizeof(uint64_t) * (ctx->world + 1), hipHostMallocDefault) != hipSuccess)
       return fail(set_err(GH_E_NOMEM, "multi-rank plan buffers"));
   }
@@ -1145,6 +1205,8 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
   a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
   a.max_only = pf->step_max_only && !pin_ref ? 1 : 0;
+  // multi-rank after a resample: the local half now, the rest once the rows arrive
+  a.part = pf->plan_pending && a.mark_mode == 2 ? 1 : 0;
   if (pin_ref) {
     CHECK(pin_upload(pf, pin_ref));
     CHECK(pin_launch(pf, o, false, true));
@@ -1163,7 +1225,10 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
 
 // Expand pending systematic marks into the ancestor array of step t+1 (for
 // genealogy reads before the next step, or a second resample).
+static int finish_plan(gh_pf* pf);
+
 static int materialize_marks(gh_pf* pf) {
+  CHECK(finish_plan(pf));
   if (!pf->marks_pending) return GH_OK;
   int32_t* anc_target = anc_for_step(pf, pf->t + 1);
   hipLaunchKernelGGL(k_sys_ancestors, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
@@ -1179,6 +1244,7 @@ static int exchange_states(gh_pf* pf, int32_t* anc_out);
 
 static void sys_plan(int64_t N, int R, int q, const uint64_t* totals, uint64_t o, int64_t* send_lo,
                      int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi);
+static int64_t sys_count_host(uint64_t X, uint64_t N, uint64_t S, uint64_t o);
 
 static void launch_rank_b(gh_pf* pf, const RankBArgs& rb) {
   switch (pf->rs_it) {
@@ -1190,18 +1256,22 @@ static void launch_rank_b(gh_pf* pf, const RankBArgs& rb) {
 
 // Multi-rank systematic resample: decision + quantise + rank
 // total (k_rank_a), all-gather of the totals, marks + outgoing rows
-// (k_rank_b).  The host reads the totals on a side stream while k_rank_b
-// runs, derives the row counts (gh_sys_plan's arithmetic) and posts the
-// grouped send/recv; the next step kernel reads own-slot ancestors from the
-// marks and the other slots from the received rows.
+// (k_rank_b).  Nothing here waits for the device: the fire flag and the
+// totals are copied to pinned memory on the side stream, and finish_plan
+// (called by the next step after it has enqueued the local half of its work)
+// reads them, derives the row counts (gh_sys_plan's arithmetic) and posts
+// the grouped send/recv on the side stream.
 static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   gh_ctx* c = pf->ctx;
   const int R = c->world, q = c->rank;
   const int D = pf->D;
   if (pf->send_cap < 1) {
-    const int64_t cap = pf->n / 4 + 1024;
+    // every row this rank could send: its particles may cover every other
+    // rank's slots (all the weight on this rank), so the worst case is sized
+    // once and the packing never has to be redone
+    const int64_t cap = std::max<int64_t>(pf->n_global - pf->n, 1);
     if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess)
-      return set_err(GH_E_NOMEM, "send rows");
+      return set_err(GH_E_NOMEM, "send rows (%lld)", (long long)cap);
     pf->send_cap = cap;
   }
   RankAArgs ra{};
@@ -1244,41 +1314,52 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.rows_cap = pf->send_cap;
   launch_rank_b(pf, rb);
   HIP_TRY(hipGetLastError());
-  // the counts: decision + totals on the host, overlapping k_rank_b
+  HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
+  // the decision and the totals, read on the side stream while k_rank_b runs
   HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_tot, 0));
   HIP_TRY(hipMemcpyAsync(pf->h_plan, &pf->dev->fire, sizeof(int), hipMemcpyDeviceToHost, pf->aux));
   HIP_TRY(hipMemcpyAsync(pf->h_plan + 1, pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->aux));
-  HIP_TRY(hipStreamSynchronize(pf->aux));
-  int fire = 0;
-  memcpy(&fire, pf->h_plan, sizeof(int));
+  HIP_TRY(hipEventRecord(pf->ev_plan, pf->aux));
   pf->mark_mode = 2;
   pf->marks_pending = true;  // harmless when it did not fire: k_step gates on the device flag
+  pf->plan_pending = true;
+  pf->rem_fire = false;
+  return GH_OK;
+}
+
+// The host half of rank_resample: wait for the fire flag and the totals, post
+// the row exchange on the side stream and make the filter's stream wait for
+// it (work already enqueued on the filter's stream — the local half of the
+// next step — runs meanwhile).  Sets the received-row slot ranges.
+static int finish_plan(gh_pf* pf) {
+  if (!pf->plan_pending) return GH_OK;
+  pf->plan_pending = false;
+  gh_ctx* c = pf->ctx;
+  const int R = c->world, q = c->rank;
+  const int D = pf->D;
+  const int t = pf->t;
+  HIP_TRY(hipEventSynchronize(pf->ev_plan));
+  int fire = 0;
+  memcpy(&fire, pf->h_plan, sizeof(int));
   if (!fire) return GH_OK;
   const uint64_t* tot = pf->h_plan + 1;
-  uint64_t S = 0;
-  for (int r = 0; r < R; ++r) S += tot[r];
+  uint64_t S = 0, base = 0;
+  for (int r = 0; r < R; ++r) {
+    if (r < q) base += tot[r];
+    S += tot[r];
+  }
   if (S == 0) return GH_OK;  // the device raised GH_E_NUMERIC
+  pf->rem_fire = true;
   const u32x4 w = rng_block(pf->seed, ~0ull, (uint32_t)t, STREAM_RESAMPLE, 0);
   const uint64_t o = scale_u53(u53_bits(w.x, w.y), S);
+  // this rank's own slots covered by other ranks: [0, ra) and [rb, n) (as k_rank_b)
+  const uint64_t N = (uint64_t)pf->n_global;
+  const int64_t own_lo = pf->lo, own_hi = pf->lo + pf->n;
+  auto clamp_own = [&](int64_t v) { return v < own_lo ? own_lo : (v > own_hi ? own_hi : v); };
+  pf->rem_ra = clamp_own(sys_count_host(base, N, S, o)) - own_lo;
+  pf->rem_rb = clamp_own(sys_count_host(base + tot[q], N, S, o)) - own_lo;
   std::vector<int64_t> slo(R), shi(R), rlo(R), rhi(R);
   sys_plan(pf->n_global, R, q, tot, o, slo.data(), shi.data(), rlo.data(), rhi.data());
-  int64_t n_send = 0;
-  for (int r = 0; r < R; ++r)
-    if (r != q) n_send += shi[r] - slo[r];
-  if (n_send > pf->send_cap) {  // rows did not fit: grow and pack again
-    HIP_TRY(hipStreamSynchronize(pf->s));
-    hipFree(pf->rows_send);
-    pf->rows_send = nullptr;
-    pf->send_cap = 0;
-    const int64_t cap = n_send + n_send / 4 + 1024;
-    if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess)
-      return set_err(GH_E_NOMEM, "send rows");
-    pf->send_cap = cap;
-    rb.rows = pf->rows_send;
-    rb.rows_cap = cap;
-    launch_rank_b(pf, rb);
-    HIP_TRY(hipGetLastError());
-  }
   std::vector<CommMsg> sends, recvs;
   const size_t row_bytes = sizeof(double) * (D + 1);
   int64_t soff = 0, roff = 0;
@@ -1290,7 +1371,12 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
     soff += ls > 0 ? ls : 0;
     roff += lr > 0 ? lr : 0;
   }
-  CHECK(comm_exchange(c, sends, recvs, pf->s));
+  if (soff > pf->send_cap) return set_err(GH_E_STATE, "internal: %lld send rows > capacity", (long long)soff);
+  if (sends.empty() && recvs.empty()) return GH_OK;
+  HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_rb, 0));
+  CHECK(comm_exchange(c, sends, recvs, pf->aux));
+  HIP_TRY(hipEventRecord(pf->ev_x, pf->aux));
+  HIP_TRY(hipStreamWaitEvent(pf->s, pf->ev_x, 0));
   return GH_OK;
 }
 

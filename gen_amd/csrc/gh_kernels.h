@@ -79,6 +79,15 @@ struct StepArgs {
   double* ps;            //                 sum e
   double* ps2;           //                 sum e^2
   double* stats_out;     // where the rank's (M, S, S2) goes
+  // multi-rank split of a step after a resample: part 1 runs
+  // every tile before the received rows exist (its results for slots [0, ra)
+  // and [rb, n) are discarded), part 2 runs again the tiles holding such
+  // slots, once the rows are in, and overwrites them (the draws are
+  // counter-based and a resample resets the weights, so the tiles' other
+  // slots get the same values again).  A part-2 launch over a later tile range
+  // gets every per-slot pointer advanced by j0 slots (j0 = 0 otherwise).
+  int part;              // host only: 0 one launch; 1, 2 the halves of a split step
+  int64_t j0;            // slot offset of this launch (the received-row index only)
 };
 
 // ------------------------------------------------------------ reductions
@@ -307,9 +316,9 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
       v = wave_incl_max_u64(v > c ? v : c);
       src = (int64_t)(uint32_t)v;
       if (a.mark_mode == 2) {  // slots outside [ra, rb) take the received rows in slot order
-        const int64_t ra = a.dev->ra, rb = a.dev->rb;
-        if (j < ra) src = -1 - j;
-        else if (j >= rb) src = -1 - (ra + (j - rb));
+        const int64_t ra = a.dev->ra, rb = a.dev->rb, js = a.j0 + j;
+        if (js < ra) src = -1 - js;
+        else if (js >= rb) src = -1 - (ra + (js - rb));
       }
       if (j < a.n) a.anc[j] = (int32_t)src;  // genealogy record
     }
@@ -906,6 +915,14 @@ __device__ __forceinline__ uint64_t blk16_sum_u64(uint64_t v, uint64_t* sm) {
   for (int k = 0; k < 16; ++k) r += sm[k];
   return r;
 }
+// sum of the first w of the 16 wave totals: all 16 read at once (no serial
+// LDS round trips), the rest masked
+__device__ __forceinline__ uint64_t blk16_excl(const uint64_t* sm, int w) {
+  uint64_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 15; ++k) r += k < w ? sm[k] : 0ull;
+  return r;
+}
 // inclusive scan of v and the sums of a, b in one LDS round (same per-value
 // orders as blk16_incl_u64 and blk16_sum2)
 __device__ __forceinline__ uint64_t blk16_incl_sum2(uint64_t v, double* a, double* b, uint64_t* smu, double* smd) {
@@ -919,7 +936,7 @@ __device__ __forceinline__ uint64_t blk16_incl_sum2(uint64_t v, double* a, doubl
     smd[16 + w] = wb;
   }
   lds_barrier();
-  for (int k = 0; k < w; ++k) v += smu[k];
+  v += blk16_excl(smu, w);
   double ra = smd[0], rb = smd[16];
 #pragma unroll
   for (int k = 1; k < 16; ++k) {
@@ -937,8 +954,7 @@ __device__ __forceinline__ uint64_t blk16_incl_u64(uint64_t v, uint64_t* sm) {
   lds_barrier();
   if (lane == 63) sm[w] = v;
   lds_barrier();
-  for (int k = 0; k < w; ++k) v += sm[k];
-  return v;
+  return v + blk16_excl(sm, w);
 }
 
 #if defined(GH_RS_STAMPS)  // timing-only variant: per-block phase clocks
@@ -973,29 +989,48 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
   double M, s1 = 0.0, s2 = 0.0;
   const bool sums = r.sums_in_pass != 0;  // uniform
-  if constexpr (IT <= kRsPart) {  // the partials fit in registers: one round trip
-    double pmv[kRsPart], psv[kRsPart], ps2v[kRsPart];
+  // KP partials per thread stay in registers (one round trip for the maxima;
+  // the sums of small tiles ride along, larger tiles load them once M is known)
+  constexpr int KP = IT > kRsPart ? IT : kRsPart;
+  constexpr bool kSumsEarly = IT <= kRsPart;
+  if (IT <= 8 && r.nb_part <= KP * kRsBlock) {  // uniform; always true at IT <= kRsPart (host-checked)
+    double pmv[KP], psv[kSumsEarly ? KP : 1], ps2v[kSumsEarly ? KP : 1];
 #pragma unroll
-    for (int k = 0; k < kRsPart; ++k) {
+    for (int k = 0; k < KP; ++k) {
       const int b = threadIdx.x + k * kRsBlock;
       const bool ok = b < r.nb_part;
       pmv[k] = ok ? r.pm[b] : -INFINITY;
-      psv[k] = ok && !sums ? r.ps[b] : 0.0;
-      ps2v[k] = ok && !sums ? r.ps2[b] : 0.0;
+      if constexpr (kSumsEarly) {
+        psv[k] = ok && !sums ? r.ps[b] : 0.0;
+        ps2v[k] = ok && !sums ? r.ps2[b] : 0.0;
+      }
     }
     double m = pmv[0];
 #pragma unroll
-    for (int k = 1; k < kRsPart; ++k) m = fmax(m, pmv[k]);
+    for (int k = 1; k < KP; ++k) m = fmax(m, pmv[k]);
     M = blk16_max(m, smd);
     GH_RS_STAMP(7);
     if (!sums && M > -INFINITY) {
+      double a1[KP], a2[KP];
 #pragma unroll
-      for (int k = 0; k < kRsPart; ++k) {
+      for (int k = 0; k < KP; ++k) {
+        const int b = threadIdx.x + k * kRsBlock;
+        const bool ok = b < r.nb_part;
+        if constexpr (kSumsEarly) {
+          a1[k] = psv[k];
+          a2[k] = ps2v[k];
+        } else {
+          a1[k] = ok ? r.ps[b] : 0.0;
+          a2[k] = ok ? r.ps2[b] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
         // pm - M <= 0: the branch-free exp (same values as gh_exp there)
         const double f = gh_exp_nonpos(pmv[k] - M);
         if (pmv[k] > -INFINITY) {
-          s1 += psv[k] * f;
-          s2 += ps2v[k] * (f * f);
+          s1 += a1[k] * f;
+          s2 += a2[k] * (f * f);
         }
       }
     }

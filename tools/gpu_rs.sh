@@ -1,8 +1,12 @@
 #!/bin/bash
+# resample phase clocks (GH_RS_STAMPS variant) for the C2 and C4 sizes
 set -e
 mkdir -p gpurun_out/rs
 export TMPDIR=/tmp
-timeout -k 10 120 python tools/rs_stamps.py > gpurun_out/rs/stamps.txt 2>&1
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/rs/pytest_gpu.log 2>&1
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/rs/bench.json 2> gpurun_out/rs/bench.err
-GH_PROF_STEPS=20 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/rs/trace -o run --output-format csv -- python3 tools/profile_run.py > gpurun_out/rs/trace.log 2>&1
+timeout -k 10 120 python tools/rs_stamps.py lg10 20 > gpurun_out/rs/stamps_lg10.txt 2>&1
+timeout -k 10 120 python tools/rs_stamps.py kit 21 > gpurun_out/rs/stamps_kit.txt 2>&1
+if [ "$1" = "full" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/rs/pytest_gpu.log 2>&1
+  timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/rs/bench.json 2> gpurun_out/rs/bench.err
+  timeout -k 10 300 python bench.py --no-cpu-baseline --model kitagawa --particles 2097152 > gpurun_out/rs/bench_kit.json 2> gpurun_out/rs/bench_kit.err
+fi

@@ -1,6 +1,7 @@
 """Per-phase clocks of k_resample1 (variant build with GH_RS_STAMPS).
 
-python tools/rs_stamps.py   (on the GPU box, after `python tools/variants.py build rs_stamps`)
+python tools/rs_stamps.py [lg10|kit] [log2 N]   (on the GPU box, after
+`python tools/variants.py build rs_stamps`)
 """
 import ctypes
 import os
@@ -16,16 +17,20 @@ from gen_amd import _lib  # noqa: E402
 
 ctx = gen.Context(device=0)
 gen.set_default_context(ctx)
-m = gen.LinearGaussianSSM.benchmark(10)
+name = sys.argv[1] if len(sys.argv) > 1 else "lg10"
+n = 1 << (int(sys.argv[2]) if len(sys.argv) > 2 else 20)
+m = gen.LinearGaussianSSM.benchmark(10) if name == "lg10" else gen.KitagawaSSM(10.0, 1.0)
 _, ys = m.simulate(12, np.random.default_rng(2))
-st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, 1 << 20, seed=42, record_history=False)
+st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=42, record_history=False)
 gen.run_particle_filter(st, list(ys[1:10]))
 ctx.synchronize()
 lib = _lib.load()
 buf = (ctypes.c_uint64 * (1024 * 8))()
 lib.gh_debug_rs_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 _lib.check(lib.gh_debug_rs_stamps(buf, 1024 * 8))
-a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[:256, :8].astype(np.int64)
+grid = -(-n // (1024 * (4 if n <= 1 << 20 else 8)))
+print(f"{name} n={n} grid={grid}")
+a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[:grid, :8].astype(np.int64)
 t0 = a[:, 0].min()
 rel = (a - t0) * 0.01  # wall_clock64 ticks at 100 MHz -> us
 names = {0: "start", 7: "max", 1: "decided", 2: "quantised", 3: "barrier", 4: "offsets", 5: "marks", 6: "end"}
