@@ -723,7 +723,7 @@ static int ensure_capacity(gh_pf* pf, int steps) {
   if (steps <= pf->cap) return GH_OK;
   int nc = pf->cap ? pf->cap : 16;
   while (nc < steps) nc *= 2;
-  const size_t xbytes = sizeof(double) * (size_t)pf->D * (size_t)pf->n;
+  const size_t xbytes = sizeof(double) * (size_t)slot_doubles(pf->n, pf->D);
   const size_t abytes = sizeof(int32_t) * (size_t)(pf->n ? pf->n : 1);
   if (pf->opts.record_history) {
     // allocate the new slots as one chunk (no hipMalloc per step)
@@ -923,7 +923,7 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
         b.anc = a.anc + off;
         b.mark = a.mark + off;
         b.carry = a.carry + off / 64;
-        b.xout = a.xout + off;
+        b.xout = a.xout + tix(off, pf->D);  // off is a whole number of tiles
         b.logw = a.logw + off;
         b.pm = a.pm + tB;
         b.ps = a.ps + tB;
@@ -979,7 +979,6 @@ static int pin_launch(gh_pf* pf, const StepObs& o, bool init, bool pre) {
   a.dev = pf->dev;
   a.resampled = flags_live(pf);
   a.x = slot_x(pf, init ? 1 : pf->t + 1);
-  a.ld = pf->n;
   a.logw = pf->logw;
   a.n = pf->n;
   a.pm = pf->pm;
@@ -1088,7 +1087,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (!pf->opts.record_history) {
     for (int i = 0; i < 2; ++i) {
       double* x = nullptr;
-      ALLOC(x, sizeof(double) * pf->D * n);
+      ALLOC(x, sizeof(double) * slot_doubles(n, pf->D));
       pf->xs.push_back(x);
     }
     int32_t* a = nullptr;
@@ -1122,7 +1121,6 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (rc) return fail(rc);
   StepArgs a{};
   a.xout = slot_x(pf, 1);
-  a.ld_out = pf->n;
   a.logw = pf->logw;
   a.n = pf->n;
   a.lo = pf->lo;
@@ -1134,7 +1132,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   a.ps = pf->ps;
   a.ps2 = pf->ps2;
   a.stats_out = ctx->world == 1 ? pf->stats_all : pf->dev->stats;
-  a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
+  a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   rc = timed_step(pf, o, a, true);
   if (rc) return fail(rc);
   if (pin_ref) {
@@ -1182,7 +1180,6 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family == GH_FAMILY_LGSSM) CHECK(make_obs_opt(pf->m, t, obs, &o));
   StepArgs a{};
   a.xprev = slot_x(pf, t - 1);
-  a.ld_prev = pf->n;
   a.anc = anc_for_step(pf, t);
   a.mark = pf->mark;
   a.carry = pf->cmark;
@@ -1191,7 +1188,6 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.remote = pf->rows_recv;
   a.ld_remote = pf->D + 1;
   a.xout = slot_x(pf, t);
-  a.ld_out = pf->n;
   a.logw = pf->logw;
   a.n = pf->n;
   a.lo = pf->lo;
@@ -1203,7 +1199,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.ps = pf->ps;
   a.ps2 = pf->ps2;
   a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
-  a.buf = (int64_t)pf->D * pf->n * 8 < (1LL << 32) ? 1 : 0;
+  a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   a.max_only = pf->step_max_only && !pin_ref ? 1 : 0;
   // multi-rank after a resample: the local half now, the rest once the rows arrive
   a.part = pf->plan_pending && a.mark_mode == 2 ? 1 : 0;
@@ -1308,7 +1304,6 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.mk.n_groups = (pf->n + 63) / 64;
   rb.mk.enabled = 1;
   rb.xprev = slot_x(pf, t);
-  rb.ldx = pf->n;
   rb.D = D;
   rb.rows = pf->rows_send;
   rb.rows_cap = pf->send_cap;
@@ -1677,7 +1672,6 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   ta.anc_pending = (pf->ctx->world == 1 && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
   ta.live = flags_live(pf);
   ta.n = n;
-  ta.ld = n;
   ta.t_target = t;
   ta.t_cur = T;
   ta.D = pf->D;
@@ -1699,10 +1693,8 @@ extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {
     CHECK(read_scalars(pf, &h, nullptr));
     if (flags_live(pf) && (h.pending | h.fire))
       return set_err(GH_E_STATE, "multi-rank: states of a pending resample are materialised by the next step");
-    CHECK(d2h(pf, out, slot_x(pf, pf->t), sizeof(double) * pf->D * pf->n));
-    return GH_OK;
   }
-  return gh_pf_get_trajectory(pf, pf->t, out);
+  return gh_pf_get_trajectory(pf, pf->t, out);  // untiles the slot into [D][n]
 }
 
 extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
@@ -1773,14 +1765,12 @@ extern "C" int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted) {
     RejuvArgs a{};
     if (t >= 2) {
       a.xprev = slot_x(pf, t - 1);
-      a.ld_prev = pf->n;
       a.anc = anc_for_step(pf, t);
       a.res = pf->res_hist + t;
       a.remote = pf->rows_recv;
       a.ld_remote = pf->D + 1;
     }
     a.x = slot_x(pf, t);
-    a.ld = pf->n;
     a.n = pf->n;
     a.lo = pf->lo;
     a.seed = pf->seed;
@@ -2004,7 +1994,7 @@ static int exchange_states(gh_pf* pf, int32_t* anc_out) {
   }
   if (n_send > 0)
     hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((n_send + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s,
-                       pf->xanc, n_send, slot_x(pf, t), pf->n, D, pf->lo, pf->rows_send);
+                       pf->xanc, n_send, slot_x(pf, t), D, pf->lo, pf->rows_send);
   int64_t roff = 0;
   for (int r = 0; r < R; ++r) {
     const int64_t len = rhi[r] - rlo[r];

@@ -22,6 +22,21 @@ constexpr int kBlock = 256;
 constexpr int kScanItems = 4;                    // items per thread in the CDF kernels
 constexpr int kScanTile = kBlock * kScanItems;   // particles per CDF block
 
+// Wave-tiled state slots: the states of one step are stored in
+// 64-particle tiles, [ceil(n/64)][D][64] fp64 — component k of particle i at
+// tix(i, D) + k * kTileP.  A wave's 64 particles read and write 512 contiguous
+// bytes per component and a tile's D components are one contiguous run (the
+// column-major [D][n] layout put a particle's D components n·8 bytes apart —
+// 8 MiB at 2^20 — and its gather+store skeleton ran 12 % slower through HBM,
+// tools/ubench_layout.hip).
+constexpr int kTileP = 64;
+__host__ __device__ __forceinline__ int64_t tix(int64_t i, int D) {
+  return (i >> 6) * (int64_t)(kTileP * D) + (i & 63);
+}
+__host__ __device__ __forceinline__ int64_t slot_doubles(int64_t n, int D) {
+  return ((n + kTileP - 1) / kTileP) * (int64_t)(kTileP * D);
+}
+
 // Device-resident state of one particle filter (one rank).
 struct DevScalars {
   double stats[3];     // this rank's (max, sum exp(w-max), sum exp(w-max)^2)
@@ -52,8 +67,7 @@ struct DevScalars {
 };
 
 struct StepArgs {
-  const double* xprev;   // [D][ld_prev] states of the previous step
-  int64_t ld_prev;
+  const double* xprev;   // wave-tiled states of the previous step (tix)
   int32_t* anc;          // ancestors for this step (read when a resample is pending;
                          // written here when they come from the systematic marks)
   const uint64_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode)
@@ -64,8 +78,7 @@ struct StepArgs {
   int buf;               // state slots < 4 GiB: address them by buffer descriptors
   const double* remote;  // multi-rank: rows received from other ranks, row r at
   int64_t ld_remote;     // remote[r * ld_remote] = (x_0 .. x_{D-1}, global id)
-  double* xout;          // [D][ld_out]
-  int64_t ld_out;
+  double* xout;          // wave-tiled states of this step (tix)
   double* logw;
   int64_t n;             // particles on this rank
   int64_t nvb;           // virtual blocks of kBlock particles (= partial count)
@@ -333,13 +346,13 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
         // defined on divergent paths make the register allocator spill)
         if (a.buf && a.mark_mode != 2) {  // local rows, slots < 4 GiB: buffer loads
           const __amdgpu_buffer_rsrc_t rp = gh_rsrc(a.xprev);
+          const uint32_t vo = ((uint32_t)src >> 6) * (uint32_t)(kTileP * D * 8) + ((uint32_t)src & 63u) * 8u;
 #pragma unroll
-          for (int k = 0; k < D; ++k)
-            xp[k] = buf_ld_f64(rp, (uint32_t)src * 8u, (uint32_t)k * (uint32_t)a.ld_prev * 8u);
-        } else {  // general: a local column (stride ld_prev) or a received row (stride 1)
+          for (int k = 0; k < D; ++k) xp[k] = buf_ld_f64(rp, vo, (uint32_t)(k * kTileP * 8));
+        } else {  // general: a local tile column (stride kTileP) or a received row (stride 1)
           const bool loc = src >= 0;
-          const double* q = loc ? a.xprev + src : a.remote + (-1 - src) * a.ld_remote;
-          const int64_t st = loc ? a.ld_prev : 1;
+          const double* q = loc ? a.xprev + tix(src, D) : a.remote + (-1 - src) * a.ld_remote;
+          const int64_t st = loc ? kTileP : 1;
 #pragma unroll
           for (int k = 0; k < D; ++k) xp[k] = q[k * st];
         }
@@ -348,11 +361,13 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
       }
       if (a.buf) {
         const __amdgpu_buffer_rsrc_t ro = gh_rsrc(a.xout);
+        const uint32_t vo = (uint32_t)tile * (uint32_t)(kTileP * D * 8) + (uint32_t)lane * 8u;
 #pragma unroll
-        for (int k = 0; k < D; ++k) buf_st_f64(x[k], ro, (uint32_t)j * 8u, (uint32_t)k * (uint32_t)a.ld_out * 8u);
+        for (int k = 0; k < D; ++k) buf_st_f64(x[k], ro, vo, (uint32_t)(k * kTileP * 8));
       } else {
+        double* q = a.xout + tix(j, D);
 #pragma unroll
-        for (int k = 0; k < D; ++k) a.xout[k * a.ld_out + j] = x[k];
+        for (int k = 0; k < D; ++k) q[k * kTileP] = x[k];
       }
       a.logw[j] = lw;
     }
@@ -1344,8 +1359,7 @@ struct RankBArgs {
   uint64_t seed;
   uint32_t t;
   MarkArgs mk;            // marks / carries in this rank's local slot space
-  const double* xprev;    // [D][ldx] states of the current step
-  int64_t ldx;
+  const double* xprev;    // wave-tiled states of the current step (tix)
   int D;
   double* rows;           // send rows [(D+1)] per slot
   int64_t rows_cap;
@@ -1451,7 +1465,8 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
       const int64_t row = ssoff[dst] + (sl - sseg_lo[dst]);
       if (row < r.rows_cap) {
         double* rw = r.rows + row * (r.D + 1);
-        for (int c = 0; c < r.D; ++c) rw[c] = r.xprev[c * r.ldx + i];
+        const double* xi = r.xprev + tix(i, r.D);
+        for (int c = 0; c < r.D; ++c) rw[c] = xi[c * kTileP];
         rw[r.D] = __longlong_as_double(r.lo + i);
       }
     }
@@ -1563,12 +1578,13 @@ __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs g, con
 // ------------------------------------------------- multi-rank exchange
 // Rows sent to other ranks: row j = (x[:, anc[j]], global id of anc[j]).
 __global__ __launch_bounds__(kBlock) void k_pack_rows(const int32_t* anc, int64_t rows, const double* x,
-                                                      int64_t ldx, int D, int64_t lo, double* out) {
+                                                      int D, int64_t lo, double* out) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= rows) return;
   const int32_t a = anc[j];
   double* r = out + j * (D + 1);
-  for (int k = 0; k < D; ++k) r[k] = x[k * ldx + a];
+  const double* xa = x + tix(a, D);
+  for (int k = 0; k < D; ++k) r[k] = xa[k * kTileP];
   r[D] = __longlong_as_double(lo + a);
 }
 
@@ -1599,7 +1615,7 @@ struct TrajArgs {
   const int32_t* const* ancs; // device array of per-step ancestor arrays (index t-1)
   const int32_t* res_before;  // res_before[t]: a resample preceded step t
   const int32_t* anc_pending; // ancestors of a resample pending after the last step
-  int64_t n, ld;
+  int64_t n;
   int t_target, t_cur, D;
   int live;                   // the device resample flags are current
   double* out;                // [D][n]
@@ -1612,8 +1628,8 @@ __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevScalars* d
   if (a.live && (dev->pending | dev->fire) && a.anc_pending) idx = a.anc_pending[idx];
   for (int s = a.t_cur; s > a.t_target; --s)
     if (a.res_before[s]) idx = a.ancs[s - 1][idx];
-  const double* x = a.xs[a.t_target - 1];
-  for (int k = 0; k < a.D; ++k) a.out[k * a.n + j] = x[k * a.ld + idx];
+  const double* x = a.xs[a.t_target - 1] + tix(idx, a.D);
+  for (int k = 0; k < a.D; ++k) a.out[k * a.n + j] = x[k * kTileP];
 }
 
 // sample_unweighted: prepare max / equal-weight flag from the current stats

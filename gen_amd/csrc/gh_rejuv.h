@@ -29,14 +29,12 @@ __device__ __host__ __forceinline__ Draw rejuv_draw(uint32_t w) {
 }
 
 struct RejuvArgs {
-  const double* xprev;    // [D][ld_prev] states of step t-1 (t >= 2)
-  int64_t ld_prev;
+  const double* xprev;    // wave-tiled states of step t-1 (t >= 2)
   const int32_t* anc;     // ancestors consumed by step t (valid when *res)
   const int32_t* res;     // res_hist + t: a resample preceded step t
   const double* remote;   // multi-rank rows received by the last exchange
   int64_t ld_remote;
-  double* x;              // [D][ld] states of step t, rewritten in place
-  int64_t ld;
+  double* x;              // wave-tiled states of step t, rewritten in place
   int64_t n, lo;
   uint64_t seed;
   uint32_t t;
@@ -59,12 +57,12 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
     const uint64_t pid = (uint64_t)(a.lo + j);
     double x[D], xp[D], y[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = a.x[k * a.ld + j];
+    for (int k = 0; k < D; ++k) x[k] = a.x[tix(j, D) + k * kTileP];
     if (!INIT) {
       const int64_t src = *a.res ? (int64_t)a.anc[j] : j;
       if (src >= 0) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) xp[k] = a.xprev[k * a.ld_prev + src];
+        for (int k = 0; k < D; ++k) xp[k] = a.xprev[tix(src, D) + k * kTileP];
       } else {
 #pragma unroll
         for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
@@ -87,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
       }
     }
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.x[k * a.ld + j] = x[k];
+    for (int k = 0; k < D; ++k) a.x[tix(j, D) + k * kTileP] = x[k];
   }
   const uint64_t tot = wave_sum_u64((uint64_t)acc);
   if ((threadIdx.x & 63) == 0 && tot) atomicAdd(a.accepted, (unsigned long long)tot);

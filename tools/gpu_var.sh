@@ -1,10 +1,8 @@
 #!/bin/bash
-# Timing variants (tools/variants.py run) after the GPU parity tests, then the
-# resample phase clocks.  Variants: pass names as arguments.
+# Interleaved A/B of timing-only variants on one box (C2): tools/gpu_var.sh v1 v2 ...
 set -e
-mkdir -p gpurun_out
+mkdir -p gpurun_out/var
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-timeout -k 10 900 python tools/variants.py run "$@" > gpurun_out/variants.log 2>&1
-timeout -k 10 900 python tools/variants.py run "$@" >> gpurun_out/variants.log 2>&1
-if [ -f gen_amd/variants/rs_stamps.so ]; then timeout -k 10 120 python tools/rs_stamps.py > gpurun_out/rs_stamps.txt 2>&1; fi
+for i in 1 2 3; do
+  timeout -k 10 300 python tools/variants.py run "$@" >> gpurun_out/var/c2.log 2>&1
+done
