@@ -24,6 +24,8 @@ VARIANTS = {
     "skel_nomv": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_ABLATE_MATVEC"],
     "skel_occ8": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_LG10_WAVES=8"],
     "skel_notab": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_ABLATE_TABLE"],
+    "early": ["GH_EARLY_PHILOX"],
+    "early_occ6": ["GH_EARLY_PHILOX", "GH_LG10_WAVES=6"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
