@@ -923,7 +923,7 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
         b.anc = a.anc + off;
         b.mark = a.mark + off;
         b.carry = a.carry + off / 64;
-        b.xout = a.xout + tix(off, pf->D);  // off is a whole number of tiles
+        b.xout = a.xout + tbase(off, pf->D);  // off is a whole number of tiles
         b.logw = a.logw + off;
         b.pm = a.pm + tB;
         b.ps = a.ps + tB;

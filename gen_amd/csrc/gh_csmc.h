@@ -25,7 +25,7 @@ struct PinArgs {
   double* w0;             // scratch: its new log weight
   const DevScalars* dev;  // resample flags (read when `resampled`)
   int resampled;          // a maybe_resample! was enqueued since the last step
-  double* x;              // wave-tiled states of this step (tix)
+  double* x;              // wave-tiled states of this step (xidx)
   double* logw;
   int64_t n;
   double* pm;             // block-0 partial of the step kernel
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(kBlock) void k_pin_post(PinArgs a, int D) {
   const int64_t j = threadIdx.x;
   double lw = j < a.n ? a.logw[j] : -INFINITY;
   if (j == 0) {
-    for (int k = 0; k < D; ++k) a.x[k * kTileP] = a.ref[k];  // particle 0: tix(0, D) = 0
+    for (int k = 0; k < D; ++k) a.x[xidx(0, k, D)] = a.ref[k];  // particle 0
     lw = *a.w0;
     a.logw[0] = lw;
   }

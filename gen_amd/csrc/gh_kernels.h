@@ -23,15 +23,19 @@ constexpr int kScanItems = 4;                    // items per thread in the CDF 
 constexpr int kScanTile = kBlock * kScanItems;   // particles per CDF block
 
 // Wave-tiled state slots: the states of one step are stored in
-// 64-particle tiles, [ceil(n/64)][D][64] fp64 — component k of particle i at
-// tix(i, D) + k * kTileP.  A wave's 64 particles read and write 512 contiguous
-// bytes per component and a tile's D components are one contiguous run (the
-// column-major [D][n] layout put a particle's D components n·8 bytes apart —
-// 8 MiB at 2^20 — and its gather+store skeleton ran 12 % slower through HBM,
-// tools/ubench_layout.hip).
+// 64-particle tiles, a tile's D components one contiguous run of 64·D
+// doubles: component pairs (2c, 2c+1) interleaved per particle, [D/2][64][2],
+// then for odd D the last component as a plain [64] column — component k of
+// particle i at xidx(i, k, D).  A lane reads or writes a component pair as one
+// 16-byte word (a wave: 1 KiB contiguous).  (The column-major [D][n] layout
+// put a particle's D components n·8 bytes apart — 8 MiB at 2^20 — and its
+// gather+store skeleton ran 14 % slower through HBM; 8-byte words per
+// component 3 % slower: tools/ubench_layout.hip.)
 constexpr int kTileP = 64;
-__host__ __device__ __forceinline__ int64_t tix(int64_t i, int D) {
-  return (i >> 6) * (int64_t)(kTileP * D) + (i & 63);
+__host__ __device__ __forceinline__ int64_t tbase(int64_t i, int D) { return (i >> 6) * (int64_t)(kTileP * D); }
+__host__ __device__ __forceinline__ int64_t xidx(int64_t i, int k, int D) {
+  const int l = (int)(i & 63);
+  return tbase(i, D) + (k < (D & ~1) ? (k >> 1) * (2 * kTileP) + 2 * l + (k & 1) : (D - 1) * kTileP + l);
 }
 __host__ __device__ __forceinline__ int64_t slot_doubles(int64_t n, int D) {
   return ((n + kTileP - 1) / kTileP) * (int64_t)(kTileP * D);
@@ -67,7 +71,7 @@ struct DevScalars {
 };
 
 struct StepArgs {
-  const double* xprev;   // wave-tiled states of the previous step (tix)
+  const double* xprev;   // wave-tiled states of the previous step (xidx)
   int32_t* anc;          // ancestors for this step (read when a resample is pending;
                          // written here when they come from the systematic marks)
   const uint64_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode)
@@ -78,7 +82,7 @@ struct StepArgs {
   int buf;               // state slots < 4 GiB: address them by buffer descriptors
   const double* remote;  // multi-rank: rows received from other ranks, row r at
   int64_t ld_remote;     // remote[r * ld_remote] = (x_0 .. x_{D-1}, global id)
-  double* xout;          // wave-tiled states of this step (tix)
+  double* xout;          // wave-tiled states of this step (xidx)
   double* logw;
   int64_t n;             // particles on this rank
   int64_t nvb;           // virtual blocks of kBlock particles (= partial count)
@@ -223,6 +227,18 @@ __device__ __forceinline__ double buf_ld_f64(__amdgpu_buffer_rsrc_t r, uint32_t 
 __device__ __forceinline__ void buf_st_f64(double v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gh_v2u, v), r, (int)voff, (int)soff, 0);
 }
+typedef unsigned int gh_v4u __attribute__((ext_vector_type(4)));
+// a component pair (16 bytes) of the wave-tiled slots
+__device__ __forceinline__ void buf_ld_f64x2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double* out) {
+  const gh_v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+  out[0] = __builtin_bit_cast(double, ((uint64_t)v.y << 32) | v.x);
+  out[1] = __builtin_bit_cast(double, ((uint64_t)v.w << 32) | v.z);
+}
+__device__ __forceinline__ void buf_st_f64x2(const double* in, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const uint64_t a = __builtin_bit_cast(uint64_t, in[0]), b = __builtin_bit_cast(uint64_t, in[1]);
+  const gh_v4u v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)voff, (int)soff, 0);
+}
 
 // ---------------------------------------------------------------- k_step
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
@@ -344,30 +360,30 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
         if (pend && !use_marks) src = a.anc[j];
         // one load sequence per uniform case (no per-lane branch: values
         // defined on divergent paths make the register allocator spill)
-        if (a.buf && a.mark_mode != 2) {  // local rows, slots < 4 GiB: buffer loads
+        if (a.buf && a.mark_mode != 2) {  // local rows, slots < 4 GiB: 16-byte buffer loads of component pairs
           const __amdgpu_buffer_rsrc_t rp = gh_rsrc(a.xprev);
-          const uint32_t vo = ((uint32_t)src >> 6) * (uint32_t)(kTileP * D * 8) + ((uint32_t)src & 63u) * 8u;
+          const uint32_t tb = ((uint32_t)src >> 6) * (uint32_t)(kTileP * D * 8), l = (uint32_t)src & 63u;
 #pragma unroll
-          for (int k = 0; k < D; ++k) xp[k] = buf_ld_f64(rp, vo, (uint32_t)(k * kTileP * 8));
-        } else {  // general: a local tile column (stride kTileP) or a received row (stride 1)
+          for (int c = 0; c < D / 2; ++c) buf_ld_f64x2(rp, tb + l * 16u, (uint32_t)(c * kTileP * 16), &xp[2 * c]);
+          if (D & 1) xp[D - 1] = buf_ld_f64(rp, tb + l * 8u, (uint32_t)((D - 1) * kTileP * 8));
+        } else {  // general: a local tile (xidx) or a received row (stride 1)
           const bool loc = src >= 0;
-          const double* q = loc ? a.xprev + tix(src, D) : a.remote + (-1 - src) * a.ld_remote;
-          const int64_t st = loc ? kTileP : 1;
 #pragma unroll
-          for (int k = 0; k < D; ++k) xp[k] = q[k * st];
+          for (int k = 0; k < D; ++k)
+            xp[k] = loc ? a.xprev[xidx(src, k, D)] : a.remote[(-1 - src) * a.ld_remote + k];
         }
         const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x, dr_step);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
       }
       if (a.buf) {
         const __amdgpu_buffer_rsrc_t ro = gh_rsrc(a.xout);
-        const uint32_t vo = (uint32_t)tile * (uint32_t)(kTileP * D * 8) + (uint32_t)lane * 8u;
+        const uint32_t tb = (uint32_t)tile * (uint32_t)(kTileP * D * 8);
 #pragma unroll
-        for (int k = 0; k < D; ++k) buf_st_f64(x[k], ro, vo, (uint32_t)(k * kTileP * 8));
+        for (int c = 0; c < D / 2; ++c) buf_st_f64x2(&x[2 * c], ro, tb + (uint32_t)lane * 16u, (uint32_t)(c * kTileP * 16));
+        if (D & 1) buf_st_f64(x[D - 1], ro, tb + (uint32_t)lane * 8u, (uint32_t)((D - 1) * kTileP * 8));
       } else {
-        double* q = a.xout + tix(j, D);
 #pragma unroll
-        for (int k = 0; k < D; ++k) q[k * kTileP] = x[k];
+        for (int k = 0; k < D; ++k) a.xout[xidx(j, k, D)] = x[k];
       }
       a.logw[j] = lw;
     }
@@ -1359,7 +1375,7 @@ struct RankBArgs {
   uint64_t seed;
   uint32_t t;
   MarkArgs mk;            // marks / carries in this rank's local slot space
-  const double* xprev;    // wave-tiled states of the current step (tix)
+  const double* xprev;    // wave-tiled states of the current step (xidx)
   int D;
   double* rows;           // send rows [(D+1)] per slot
   int64_t rows_cap;
@@ -1465,8 +1481,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
       const int64_t row = ssoff[dst] + (sl - sseg_lo[dst]);
       if (row < r.rows_cap) {
         double* rw = r.rows + row * (r.D + 1);
-        const double* xi = r.xprev + tix(i, r.D);
-        for (int c = 0; c < r.D; ++c) rw[c] = xi[c * kTileP];
+        for (int c = 0; c < r.D; ++c) rw[c] = r.xprev[xidx(i, c, r.D)];
         rw[r.D] = __longlong_as_double(r.lo + i);
       }
     }
@@ -1583,8 +1598,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_rows(const int32_t* anc, int64_
   if (j >= rows) return;
   const int32_t a = anc[j];
   double* r = out + j * (D + 1);
-  const double* xa = x + tix(a, D);
-  for (int k = 0; k < D; ++k) r[k] = xa[k * kTileP];
+  for (int k = 0; k < D; ++k) r[k] = x[xidx(a, k, D)];
   r[D] = __longlong_as_double(lo + a);
 }
 
@@ -1628,8 +1642,8 @@ __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevScalars* d
   if (a.live && (dev->pending | dev->fire) && a.anc_pending) idx = a.anc_pending[idx];
   for (int s = a.t_cur; s > a.t_target; --s)
     if (a.res_before[s]) idx = a.ancs[s - 1][idx];
-  const double* x = a.xs[a.t_target - 1] + tix(idx, a.D);
-  for (int k = 0; k < a.D; ++k) a.out[k * a.n + j] = x[k * kTileP];
+  const double* x = a.xs[a.t_target - 1];
+  for (int k = 0; k < a.D; ++k) a.out[k * a.n + j] = x[xidx(idx, k, a.D)];
 }
 
 // sample_unweighted: prepare max / equal-weight flag from the current stats

@@ -57,12 +57,12 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
     const uint64_t pid = (uint64_t)(a.lo + j);
     double x[D], xp[D], y[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) x[k] = a.x[tix(j, D) + k * kTileP];
+    for (int k = 0; k < D; ++k) x[k] = a.x[xidx(j, k, D)];
     if (!INIT) {
       const int64_t src = *a.res ? (int64_t)a.anc[j] : j;
       if (src >= 0) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) xp[k] = a.xprev[tix(src, D) + k * kTileP];
+        for (int k = 0; k < D; ++k) xp[k] = a.xprev[xidx(src, k, D)];
       } else {
 #pragma unroll
         for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
       }
     }
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.x[tix(j, D) + k * kTileP] = x[k];
+    for (int k = 0; k < D; ++k) a.x[xidx(j, k, D)] = x[k];
   }
   const uint64_t tot = wave_sum_u64((uint64_t)acc);
   if ((threadIdx.x & 63) == 0 && tot) atomicAdd(a.accepted, (unsigned long long)tot);

@@ -50,6 +50,38 @@ struct Args {
 };
 
 // index of component k of particle i
+// pair-interleaved 64-particle tiles: components (2c, 2c+1) of a particle are
+// one 16-byte word, [N/64][D/2][64][2]
+__device__ __forceinline__ int64_t at_pair(int64_t i, int c) { return (i >> 6) * (64 * D) + c * 128 + (i & 63) * 2; }
+
+template <bool GATHER>
+__global__ __launch_bounds__(kBlock) void k_pair(Args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t j = tile * 64 + lane;
+  int64_t src = j;
+  if (GATHER) {
+    uint64_t v = a.mark[j];
+    const uint64_t c = a.carry[tile];
+    v = wave_incl_max_u64(v > c ? v : c);
+    src = (int64_t)(uint32_t)v;
+    a.anc[j] = (int32_t)src;
+  }
+  double2 x[D / 2];
+#pragma unroll
+  for (int c = 0; c < D / 2; ++c) x[c] = *reinterpret_cast<const double2*>(&a.x[at_pair(src, c)]);
+#pragma unroll
+  for (int c = 0; c < D / 2; ++c) {
+    double2 y = x[c];
+    y.x += 1.0;
+    y.y += 1.0;
+    *reinterpret_cast<double2*>(&a.y[at_pair(j, c)]) = y;
+  }
+  a.logw[j] = 1.0;
+}
+template <bool GATHER>
+static void launch_pair(Args a);
+
 template <int L, int P>
 __device__ __forceinline__ int64_t at(int64_t i, int k) {
   if (L == 0) return (int64_t)k * (N + P) + i;                       // SoA, padded pitch
@@ -100,6 +132,14 @@ static void launch(Args a) {
   hipLaunchKernelGGL((k_skel<L, P, GATHER, MODE>), dim3(N / kBlock), dim3(kBlock), 0, 0, a);
 }
 
+template <bool GATHER>
+static void launch_pair(Args a) {
+  a.x = g_hist + (size_t)(g_slot % kSlots) * g_slot_pitch;
+  a.y = g_hist + (size_t)((g_slot + 1) % kSlots) * g_slot_pitch;
+  ++g_slot;
+  hipLaunchKernelGGL((k_pair<GATHER>), dim3(N / kBlock), dim3(kBlock), 0, 0, a);
+}
+
 int main() {
   std::vector<uint64_t> mark(N, 0), carry(N / 64, 0);
   {  // a systematic-resampling pattern: ancestors drawn from skewed weights
@@ -142,26 +182,16 @@ int main() {
     void (*f)(Args);
   } vs[] = {
       {"soa_p0", bytes, launch<0, 0, true, 0>},
-      {"soa_p64", bytes, launch<0, 64, true, 0>},
       {"soa_p512", bytes, launch<0, 512, true, 0>},
-      {"soa_p4160", bytes, launch<0, 4160, true, 0>},
-      {"soa_p8000", bytes, launch<0, 8000, true, 0>},
       {"tile_64", bytes, launch<64, 0, true, 0>},
+      {"pair_64", bytes, launch_pair<true>},
+      {"pair_copy", (double)N * (16.0 * D + 8.0), launch_pair<false>},
       {"tile_256", bytes, launch<256, 0, true, 0>},
-      {"tile_1024", bytes, launch<1024, 0, true, 0>},
       {"tile_32", bytes, launch<32, 0, true, 0>},
       {"tile_128", bytes, launch<128, 0, true, 0>},
-      {"tile_64p16", bytes, launch<64, 16, true, 0>},
-      {"tile_64p64", bytes, launch<64, 64, true, 0>},
-      {"tile_64p256", bytes, launch<64, 256, true, 0>},
       {"copy_p0", (double)N * (16.0 * D + 8.0), launch<0, 0, false, 0>},
-      {"copy_p512", (double)N * (16.0 * D + 8.0), launch<0, 512, false, 0>},
       {"copy_t256", (double)N * (16.0 * D + 8.0), launch<256, 0, false, 0>},
       {"copy_t64", (double)N * (16.0 * D + 8.0), launch<64, 0, false, 0>},
-      {"rd_p0", (double)N * (8.0 * D + 8.0), launch<0, 0, false, 1>},
-      {"wr_p0", (double)N * (8.0 * D + 8.0), launch<0, 0, false, 2>},
-      {"rd_t256", (double)N * (8.0 * D + 8.0), launch<256, 0, false, 1>},
-      {"wr_t256", (double)N * (8.0 * D + 8.0), launch<256, 0, false, 2>},
       {"rd_t64", (double)N * (8.0 * D + 8.0), launch<64, 0, false, 1>},
       {"wr_t64", (double)N * (8.0 * D + 8.0), launch<64, 0, false, 2>},
   };
