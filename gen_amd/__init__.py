@@ -10,6 +10,7 @@ from .models import BayesianLinearRegression, DiscreteHMM, KitagawaSSM, LinearGa
 from .pf import (
     Context,
     NoChange,
+    GaussianProposal,
     OptimalProposal,
     conditional_particle_filter_step,
     conditional_smc,
@@ -37,7 +38,7 @@ from ._lib import GenHipError
 
 __all__ = [
     "ChoiceMap", "EmptyChoiceMap", "choicemap", "BayesianLinearRegression", "DiscreteHMM", "KitagawaSSM", "LinearGaussianSSM", "Model",
-    "Context", "NoChange", "OptimalProposal", "ParticleFilterState", "UnknownChange", "default_context",
+    "Context", "GaussianProposal", "NoChange", "OptimalProposal", "ParticleFilterState", "UnknownChange", "default_context",
     "get_log_weights", "get_traces", "importance_resampling", "importance_sampling",
     "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",
     "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",

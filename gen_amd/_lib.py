@@ -25,7 +25,7 @@ STATUS = {
 
 FAMILY_LGSSM, FAMILY_HMM, FAMILY_KITAGAWA, FAMILY_REGRESSION = 1, 2, 3, 4
 RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = 0, 1
-PROPOSAL_DEFAULT, PROPOSAL_OPTIMAL = 0, 1
+PROPOSAL_DEFAULT, PROPOSAL_OPTIMAL, PROPOSAL_GAUSSIAN = 0, 1, 2
 
 
 class GenHipError(RuntimeError):
@@ -80,6 +80,9 @@ SIGNATURES = {
     "gh_pf_init": (c_int, [c_void_p, POINTER(Obs), c_int, c_int64, c_uint64, POINTER(PFOpts), POINTER(c_void_p)]),
     "gh_pf_destroy": (c_int, [c_void_p]),
     "gh_pf_step": (c_int, [c_void_p, POINTER(Obs), c_int]),
+    "gh_pf_init_q": (c_int, [c_void_p, POINTER(Obs), c_int, POINTER(c_double), c_int, c_int64, c_uint64,
+                             POINTER(PFOpts), POINTER(c_void_p)]),
+    "gh_pf_step_q": (c_int, [c_void_p, POINTER(Obs), c_int, POINTER(c_double), c_int]),
     "gh_pf_maybe_resample": (c_int, [c_void_p, c_double, POINTER(c_int), POINTER(c_double)]),
     "gh_pf_run": (c_int, [c_void_p, c_int, POINTER(Obs), c_int, c_double]),
     "gh_pf_log_ml_estimate": (c_int, [c_void_p, POINTER(c_double)]),

@@ -461,6 +461,10 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->kit.sx = sqrt(p[2]);
     m->kit.inv2vy = 1.0 / (2.0 * p[3]);
     m->kit.csty = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * p[3]);
+    m->kit.inv2vx = 1.0 / (2.0 * p[2]);
+    m->kit.cstx = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * p[2]);
+    m->kit.inv2v1 = 1.0 / (2.0 * (p[1] * p[1]));
+    m->kit.cst1 = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
     h.push_back(0.0);
   } else if (desc->family == GH_FAMILY_REGRESSION) {
     const int n = desc->dy;
@@ -551,6 +555,19 @@ static int make_obs(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
   return GH_OK;
 }
 
+// The Gaussian custom proposal's arguments (KitGaussModel): o.v[1..4] =
+// (alpha, beta, gamma, sigma_q), o.v[5] = 1/(2 sigma_q^2), o.v[6] =
+// -0.5 log(2 pi sigma_q^2).
+static int make_obs_gauss(const gh_model* m, int t, const gh_obs* in, const double* q, StepObs* o) {
+  CHECK(make_obs(m, t, in, o));
+  if (!(q[3] > 0.0)) return set_err(GH_E_INVAL, "Gaussian proposal: sigma_q must be > 0");
+  const double v = q[3] * q[3];
+  for (int i = 0; i < 4; ++i) o->v[1 + i] = q[i];
+  o->v[5] = 1.0 / (2.0 * v);
+  o->v[6] = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * v);
+  return GH_OK;
+}
+
 // The optimal proposal's per-step vectors (LGOptModel): t = 1: o.v[0, d) =
 // mu_1 = mu0 + K_1 (y - c - H mu0), o.ct = log N(y; H mu0 + c, S_1); t >= 2:
 // o.v[0, d) = g_t = F b + K (y - c), o.v[d, d + dy) = L_S^-1 (y - c) - L_S^-1 H b.
@@ -591,6 +608,7 @@ static int make_obs_opt(const gh_model* m, int t, const gh_obs* in, StepObs* o) 
 
 static bool proposal_ok(const gh_model* m, int proposal) {
   if (proposal == GH_PROPOSAL_DEFAULT) return true;
+  if (proposal == GH_PROPOSAL_GAUSSIAN) return m->family == GH_FAMILY_KITAGAWA;
   if (proposal != GH_PROPOSAL_OPTIMAL) return false;
   return m->family == GH_FAMILY_HMM || (m->family == GH_FAMILY_LGSSM && m->lg_opt);
 }
@@ -654,6 +672,9 @@ struct gh_pf {
   StepObs last_obs{};
   uint32_t rejuv_moves = 0;
   unsigned long long* acc_count = nullptr;
+  // the Gaussian custom proposal's last arguments (alpha, beta, gamma, sigma_q)
+  double qargs[4] = {0, 0, 0, 0};
+  bool has_q = false;
   // conditional SMC (gh_csmc.h): particle 0 is pinned to a given trajectory
   bool cond = false;
   double* pin = nullptr;          // [D] this step's distinguished state, [D] its new log weight
@@ -868,6 +889,11 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
                        hipEvent_t e1 = nullptr) {
   if (!init && pf->m->family == GH_FAMILY_REGRESSION)
     return set_err(GH_E_INVAL, "the regression model has no time steps");
+  if (a.proposal == GH_PROPOSAL_GAUSSIAN) {  // Kitagawa only (proposal_ok); its own functor
+    launch_step_t<KitGaussModel>(pf, pf->m->kit, o, a, init, e0, e1);
+    HIP_TRY(hipGetLastError());
+    return GH_OK;
+  }
   if (a.proposal == GH_PROPOSAL_OPTIMAL && pf->m->family == GH_FAMILY_LGSSM) {
     // the LGSSM's locally optimal proposal is its own functor (the default
     // step kernel stays free of the proposal's code and registers)
@@ -1007,11 +1033,30 @@ static int pin_upload(gh_pf* pf, const double* ref) {
 }
 
 static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles, uint64_t seed,
-                        const gh_pf_opts* opts, const double* pin_ref, gh_pf** out);
+                        const gh_pf_opts* opts, const double* pin_ref, gh_pf** out,
+                        const double* qargs = nullptr, int nq = 0);
 
 extern "C" int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles,
                           uint64_t seed, const gh_pf_opts* opts, gh_pf** out) {
   return pf_init_impl(m, obs, proposal, n_particles, seed, opts, nullptr, out);
+}
+
+extern "C" int gh_pf_init_q(gh_model* m, const gh_obs* obs, int proposal, const double* proposal_args,
+                            int n_proposal_args, int64_t n_particles, uint64_t seed, const gh_pf_opts* opts,
+                            gh_pf** out) {
+  return pf_init_impl(m, obs, proposal, n_particles, seed, opts, nullptr, out, proposal_args, n_proposal_args);
+}
+
+// the stored arguments of the Gaussian custom proposal (4: alpha, beta, gamma, sigma_q)
+static int set_qargs(double* dst, bool* has, int proposal, const double* q, int nq) {
+  if (!q || nq == 0) return proposal == GH_PROPOSAL_GAUSSIAN && !*has
+                              ? set_err(GH_E_INVAL, "the Gaussian proposal needs (alpha, beta, gamma, sigma_q)")
+                              : GH_OK;
+  if (nq != 4 || !(q[3] > 0.0))
+    return set_err(GH_E_INVAL, "Gaussian proposal arguments: (alpha, beta, gamma, sigma_q > 0)");
+  for (int i = 0; i < 4; ++i) dst[i] = q[i];
+  *has = true;
+  return GH_OK;
 }
 
 extern "C" int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_particles, uint64_t seed,
@@ -1025,13 +1070,17 @@ extern "C" int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_
 }
 
 static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles, uint64_t seed,
-                        const gh_pf_opts* opts, const double* pin_ref, gh_pf** out) {
+                        const gh_pf_opts* opts, const double* pin_ref, gh_pf** out, const double* qargs, int nq) {
   if (!m || !out) return set_err(GH_E_INVAL, "gh_pf_init: null argument");
+  double q0[4] = {0, 0, 0, 0};
+  bool has_q = false;
+  CHECK(set_qargs(q0, &has_q, proposal, qargs, nq));
   if (n_particles < 1 || n_particles > 0x7fffffffLL)
     return set_err(GH_E_INVAL, "gh_pf_init: num_particles must be in 1..2^31-1");
   if (!proposal_ok(m, proposal))
     return set_err(GH_E_INVAL, "gh_pf_init: proposal %d is not available for this model (the optimal proposal: "
-                               "HMM, and LGSSM with d + dy <= %d)", proposal, kMaxObs);
+                               "HMM, and LGSSM with d + dy <= %d; the Gaussian proposal: the nonlinear SSM)",
+                   proposal, kMaxObs);
   gh_ctx* ctx = m->ctx;
   HIP_TRY(hipSetDevice(ctx->device));
   gh_pf* pf = new gh_pf();
@@ -1039,6 +1088,8 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->ctx = ctx;
   pf->s = ctx->stream;
   pf->D = m->d;
+  for (int i = 0; i < 4; ++i) pf->qargs[i] = q0[i];
+  pf->has_q = has_q;
   if (opts) pf->opts = *opts;
   else gh_pf_opts_default(&pf->opts);
   if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC && pf->opts.resampler != GH_RESAMPLE_MULTINOMIAL) {
@@ -1117,6 +1168,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (!rc) {
     o = o_prior;
     if (proposal == GH_PROPOSAL_OPTIMAL && m->family == GH_FAMILY_LGSSM) rc = make_obs_opt(m, 1, obs, &o);
+    if (proposal == GH_PROPOSAL_GAUSSIAN) rc = make_obs_gauss(m, 1, obs, pf->qargs, &o);
   }
   if (rc) return fail(rc);
   StepArgs a{};
@@ -1156,6 +1208,15 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
 
 extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   if (pf && pf->cond) return set_err(GH_E_STATE, "a conditional filter steps with gh_pf_step_conditional");
+  if (pf) CHECK(set_qargs(pf->qargs, &pf->has_q, proposal, nullptr, 0));
+  return pf_step_impl(pf, obs, proposal, nullptr);
+}
+
+extern "C" int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const double* proposal_args,
+                            int n_proposal_args) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
+  if (pf->cond) return set_err(GH_E_STATE, "a conditional filter steps with gh_pf_step_conditional");
+  CHECK(set_qargs(pf->qargs, &pf->has_q, proposal, proposal_args, n_proposal_args));
   return pf_step_impl(pf, obs, proposal, nullptr);
 }
 
@@ -1178,6 +1239,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   CHECK(make_obs(pf->m, t, obs, &o_prior));
   o = o_prior;
   if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family == GH_FAMILY_LGSSM) CHECK(make_obs_opt(pf->m, t, obs, &o));
+  if (proposal == GH_PROPOSAL_GAUSSIAN) CHECK(make_obs_gauss(pf->m, t, obs, pf->qargs, &o));
   StepArgs a{};
   a.xprev = slot_x(pf, t - 1);
   a.anc = anc_for_step(pf, t);

@@ -325,6 +325,8 @@ struct KitParams {
   double sx;        // sqrt(var_x)
   double inv2vy;    // 1 / (2 var_y)
   double csty;      // -0.5 log(2 pi var_y)
+  double inv2vx, cstx;  // the prior densities (Gaussian custom proposal's weight): 1/(2 var_x), -0.5 log(2 pi var_x)
+  double inv2v1, cst1;  //   and at t = 1: 1/(2 s1^2), -0.5 log(2 pi s1^2)
   __device__ KitParams rebase(const double* __restrict__) const { return *this; }
 };
 
@@ -355,6 +357,52 @@ struct KitModel {
     const double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
     x[0] = mean + p.sx * z0;
     return obs(p, o, x[0]);
+  }
+};
+
+// ------------------------------------- nonlinear SSM, Gaussian custom proposal
+// A user-parameterised custom proposal in Gen's sense (particle_filter.jl:
+// 79-91,139-154 via the SimpleExtendingTraceTranslator, trace_translators.jl:
+// 775-802): x_t ~ q = normal(mu_q, sigma_q), mu_q = alpha m + beta y_t + gamma
+// with m the prior mean (m = mu1 at t = 1; beta y_t only when y_t is
+// observed); the weight is model weight - proposal score =
+// log p(x_t | x_{t-1}) + log p(y_t | x_t) - log q(x_t).  (alpha, beta, gamma,
+// sigma_q) are the step's proposal arguments, passed with 1/(2 sigma_q^2) and
+// -0.5 log(2 pi sigma_q^2) in o.v[1..6] (gh_pf_step_q).  alpha = 1, beta =
+// gamma = 0, sigma_q = sqrt(var_x) is the bootstrap proposal.
+struct KitGaussModel {
+  static constexpr int kD = 1;
+  static constexpr int kMinWaves = 8;
+  using Params = KitParams;
+  __device__ static double lpn(double x, double mu, double inv2, double cst) {
+    const double d = x - mu;
+    return -(d * d) * inv2 + cst;
+  }
+  __device__ static double propose(const Params& p, const StepObs& o, double mean, double inv2p, double cstp,
+                                   double z, double* x) {
+    double mq = o.v[1] * mean;
+    if (o.present) mq = mq + o.v[2] * o.v[0];
+    mq = mq + o.v[3];
+    x[0] = mq + o.v[4] * z;
+    double w = lpn(x[0], mean, inv2p, cstp);
+    if (o.present) w = w + KitModel::obs(p, o, x[0]);
+    return w - lpn(x[0], mq, o.v[5], o.v[6]);
+  }
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return KitModel::obs(p, o, x[0]); }
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
+    double z0, z1;
+    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1, dr.tab);
+    return propose(p, o, p.mu1, p.inv2v1, p.cst1, z0, x);
+  }
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
+                                uint32_t t, int /*proposal*/, const double* xp, double* x,
+                                Draw dr = {STREAM_STEP, 0}) {
+    double z0, z1;
+    normal_pair(rng_block(seed, pid, t, dr.stream, dr.base), &z0, &z1, dr.tab);
+    const double v = xp[0];
+    const double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
+    return propose(p, o, mean, p.inv2vx, p.cstx, z0, x);
   }
 };
 

@@ -45,6 +45,24 @@ class OptimalProposal:
     (test/inference/particle_filter.jl:104-127)."""
 
 
+class GaussianProposal:
+    """A user-parameterised custom proposal for the nonlinear SSM (a proposal
+    generative function in Gen's sense, particle_filter.jl:79-91,139-154):
+    x_t ~ normal(alpha * m + beta * y_t + gamma, sigma_q), m the model's prior
+    mean of x_t; proposal_args = (alpha, beta, gamma, sigma_q).  The weight is
+    log p(x_t | x_{t-1}) + log p(y_t | x_t) - log q(x_t)
+    (trace_translators.jl:775-802)."""
+
+
+def _qargs(proposal, proposal_args):
+    if not (proposal is GaussianProposal or isinstance(proposal, GaussianProposal)):
+        return None, 0
+    a = np.ascontiguousarray(proposal_args, dtype=np.float64)
+    if a.size != 4:
+        raise _lib.GenHipError(1, "GaussianProposal takes proposal_args = (alpha, beta, gamma, sigma_q)")
+    return a, 4
+
+
 # ------------------------------------------------------------------ context
 class Context:
     """One GPU (and, for multi-GPU, one rank of an RCCL communicator)."""
@@ -150,6 +168,8 @@ def _proposal_code(proposal) -> int:
         return _lib.PROPOSAL_DEFAULT
     if proposal is OptimalProposal or isinstance(proposal, OptimalProposal) or proposal == "optimal":
         return _lib.PROPOSAL_OPTIMAL
+    if proposal is GaussianProposal or isinstance(proposal, GaussianProposal):
+        return _lib.PROPOSAL_GAUSSIAN
     raise _lib.GenHipError(1, f"unsupported proposal {proposal!r}: the engine lowers the model's default "
                               "proposal and the locally optimal proposal")
 
@@ -347,10 +367,11 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
     lower-variance scheme, and the only one the multi-rank path exchanges).
     Pass resampler="multinomial" for Gen's distribution of parents; both are
     unbiased, so log-ML estimates agree in expectation, not draw for draw."""
+    proposal_args = ()
     if len(args) == 1:
         proposal, num_particles = None, args[0]
     elif len(args) == 3:
-        proposal, _, num_particles = args
+        proposal, proposal_args, num_particles = args
     else:
         raise TypeError("expected (num_particles) or (proposal, proposal_args, num_particles)")
     if not model.static and tuple(model_args)[:1] not in ((1,), ()):
@@ -360,8 +381,10 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
     obs, keep = _step_obs(model, 1, observations)
     h = c_void_p()
     opts = _opts(resampler, record_history, history_capacity, time_kernels)
-    _lib.check(_lib.load().gh_pf_init(mh, byref(obs), _proposal_code(proposal), int(num_particles),
-                                      int(seed) & 0xFFFFFFFFFFFFFFFF, byref(opts), byref(h)))
+    qa, nq = _qargs(proposal, proposal_args)
+    _lib.check(_lib.load().gh_pf_init_q(mh, byref(obs), _proposal_code(proposal),
+                                        _lib.dptr(qa) if qa is not None else None, nq, int(num_particles),
+                                        int(seed) & 0xFFFFFFFFFFFFFFFF, byref(opts), byref(h)))
     st = ParticleFilterState(ctx, model, h, int(num_particles))
     st._log_obs(1, keep)
     return st
@@ -375,7 +398,9 @@ def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: 
     if argdiffs and not isinstance(argdiffs[0], UnknownChange):
         raise _lib.GenHipError(1, "the length argument changes: its argdiff must be UnknownChange()")
     obs, keep = _step_obs(state.model, t, observations)
-    _lib.check(_lib.load().gh_pf_step(state.h, byref(obs), _proposal_code(proposal)))
+    qa, nq = _qargs(proposal, proposal_args)
+    _lib.check(_lib.load().gh_pf_step_q(state.h, byref(obs), _proposal_code(proposal),
+                                        _lib.dptr(qa) if qa is not None else None, nq))
     state._log_obs(t, keep)
 
 
@@ -395,10 +420,18 @@ def maybe_resample_async(state: ParticleFilterState, ess_threshold: float | None
 
 
 def run_particle_filter(state: ParticleFilterState, observations_per_step, ess_threshold: float | None = None,
-                        proposal=None) -> None:
+                        proposal=None, proposal_args: tuple | None = None) -> None:
     """The reference caller loop {maybe_resample!; particle_filter_step!} over
-    the given per-step observations (arrays or None), enqueued without host sync."""
+    the given per-step observations (arrays or None), enqueued without host sync.
+    A proposal with arguments uses proposal_args, or the last ones given."""
     model = state.model
+    if proposal_args is not None and len(observations_per_step) > 0:
+        qa, nq = _qargs(proposal, proposal_args)
+        if qa is not None:  # store them (the library keeps the last arguments)
+            maybe_resample_async(state, ess_threshold)
+            particle_filter_step(state, (state.t + 1,), (UnknownChange(),), observations_per_step[0], proposal,
+                                 proposal_args)
+            observations_per_step = list(observations_per_step)[1:]
     t0 = state.t
     keep = []
     arr = (_lib.Obs * max(1, len(observations_per_step)))()

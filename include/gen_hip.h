@@ -89,10 +89,16 @@ typedef enum { GH_RESAMPLE_SYSTEMATIC = 0, GH_RESAMPLE_MULTINOMIAL = 1 } gh_resa
 
 typedef enum {
   GH_PROPOSAL_DEFAULT = 0, /* the model's internal proposal (prior) */
-  GH_PROPOSAL_OPTIMAL = 1  /* locally optimal proposal p(x_t | x_{t-1}, y_t) as a custom
+  GH_PROPOSAL_OPTIMAL = 1, /* locally optimal proposal p(x_t | x_{t-1}, y_t) as a custom
                               proposal (particle_filter.jl:79-91,139-154): HMM (the proposal
                               of test/inference/particle_filter.jl:104-127) and LGSSM
                               (Gaussian, d + dy <= 32); weight log p(y_t | x_{t-1}) */
+  GH_PROPOSAL_GAUSSIAN = 2 /* user-parameterised custom proposal of the nonlinear SSM
+                              (particle_filter.jl:79-91,139-154 via trace_translators.jl:
+                              775-802): x_t ~ normal(alpha m + beta y_t + gamma, sigma_q),
+                              m the prior mean; proposal_args = (alpha, beta, gamma, sigma_q)
+                              through gh_pf_init_q / gh_pf_step_q; weight log p(x_t|x_{t-1})
+                              + log p(y_t|x_t) - log q(x_t) */
 } gh_proposal;
 
 typedef struct gh_ctx gh_ctx;
@@ -162,6 +168,14 @@ int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles
                const gh_pf_opts* opts, gh_pf** out);
 int gh_pf_destroy(gh_pf* pf);
 int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal);
+/* initialize_particle_filter(model, args, obs, proposal, proposal_args, N) and
+   particle_filter_step!(state, args, argdiffs, obs, proposal, proposal_args)
+   (particle_filter.jl:79-91, 139-154) for proposals with arguments
+   (GH_PROPOSAL_GAUSSIAN: 4 doubles).  The arguments are kept: gh_pf_step and
+   gh_pf_run reuse the last ones given. */
+int gh_pf_init_q(gh_model* m, const gh_obs* obs, int proposal, const double* proposal_args, int n_proposal_args,
+                 int64_t n_particles, uint64_t seed, const gh_pf_opts* opts, gh_pf** out);
+int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const double* proposal_args, int n_proposal_args);
 /* ess_threshold NaN means the reference's default N/2; any other value is the
    threshold as given (resample iff ESS < ess_threshold, so <= 0 never resamples).  If did_resample/ess are non-NULL the
    call synchronises and reports them; otherwise the decision stays on the

@@ -309,8 +309,11 @@ typedef struct {
   double *H, *LS, *Kt, *FA, *Fb, *LSig, *WA, *Wb, *LS1, *Kt1, *LSig1, cstS, cstS1;
   /* HMM */
   double *prior, *T, *E, *logE;
-  /* Kitagawa */
-  double mu1, s1, sx, inv2vy, csty;
+  /* Kitagawa; the prior densities for the Gaussian custom proposal's weight,
+     and that proposal's arguments (alpha, beta, gamma, sigma_q) with
+     1/(2 sigma_q^2), -0.5 log(2 pi sigma_q^2) */
+  double mu1, s1, sx, inv2vy, csty, inv2vx, cstx, inv2v1, cst1;
+  double qa[6];
   /* regression (quickstart.jl:3-9): priors, 1/(2 sigma^2), -0.5 log(2 pi sigma^2), xs */
   double mu_s, sd_s, mu_i, sd_i, inv2v, cst;
   double xs[32];
@@ -422,6 +425,10 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->sx = sqrt(p[2]);
     m->inv2vy = 1.0 / (2.0 * p[3]);
     m->csty = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * p[3]);
+    m->inv2vx = 1.0 / (2.0 * p[2]);
+    m->cstx = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * p[2]);
+    m->inv2v1 = 1.0 / (2.0 * (p[1] * p[1]));
+    m->cst1 = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
   } else if (family == ORC_REGRESSION) {
     if (dy < 1 || dy > 32 || np < 5 + (int64_t)dy) return -1;
     m->d = 2;
@@ -537,6 +544,29 @@ static double reg_loglik(const model_t* m, const obs_t* o, const double* x) {
 
 /* draws come from (stream, base + j): the filter uses (S_INIT / S_STEP, 0),
    rejuvenation moves (S_MH, 16 * move) */
+/* Gaussian custom proposal of the nonlinear SSM (particle_filter.jl:79-91,
+   139-154 via trace_translators.jl:775-802): x ~ q = normal(mu_q, sigma_q),
+   mu_q = alpha * m + beta * y + gamma with m the prior mean (beta * y only
+   when y is observed); weight = log p(x | prior) + log p(y | x) - log q(x)
+   (gen_amd/csrc/gh_models.h KitGaussModel, same operation order). */
+static double kit_lpn(double x, double mu, double inv2, double cst) {
+  double d = x - mu;
+  return -(d * d) * inv2 + cst;
+}
+static double kit_gauss(const model_t* m, const obs_t* o, double mean, double inv2p, double cstp, double z,
+                        double* x) {
+  double mq = m->qa[0] * mean;
+  if (o->present) mq = mq + m->qa[1] * o->bt[0];
+  mq = mq + m->qa[2];
+  x[0] = mq + m->qa[3] * z;
+  double w = kit_lpn(x[0], mean, inv2p, cstp);
+  if (o->present) {
+    double diff = o->bt[0] - x[0] * x[0] / 20.0;
+    w = w + (-(diff * diff) * m->inv2vy + m->csty);
+  }
+  return w - kit_lpn(x[0], mq, m->qa[4], m->qa[5]);
+}
+
 static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
                             int proposal, double* x, uint32_t stream, uint32_t base) {
   if (m->family == ORC_REGRESSION) {
@@ -567,6 +597,7 @@ static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const
   } else if (m->family == ORC_KITAGAWA) {
     double z[2];
     normals_at(seed, pid, 1, stream, base, 1, z);
+    if (proposal == ORC_PROPOSAL_GAUSSIAN) return kit_gauss(m, o, m->mu1, m->inv2v1, m->cst1, z[0], x);
     x[0] = m->mu1 + m->s1 * z[0];
     if (!o->present) return 0.0;
     double diff = o->bt[0] - x[0] * x[0] / 20.0;
@@ -630,6 +661,7 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
     normals_at(seed, pid, t, stream, base, 1, z);
     double v = xp[0];
     double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o->ct;
+    if (proposal == ORC_PROPOSAL_GAUSSIAN) return kit_gauss(m, o, mean, m->inv2vx, m->cstx, z[0], x);
     x[0] = mean + m->sx * z[0];
     if (!o->present) return 0.0;
     double diff = o->bt[0] - x[0] * x[0] / 20.0;
@@ -747,7 +779,16 @@ static int init_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
 }
 static int proposal_ok(const model_t* m, int proposal) {
   if (proposal == 0) return 1;
+  if (proposal == ORC_PROPOSAL_GAUSSIAN) return m->family == ORC_KITAGAWA && m->qa[3] > 0.0;
   return proposal == ORC_PROPOSAL_OPTIMAL && (m->family == ORC_HMM || (m->family == ORC_LGSSM && m->opt));
+}
+int orc_pf_set_proposal_args(orc_pf* pf, const double* args, int n) {
+  if (n != 4 || !(args[3] > 0.0)) return -1;
+  double v = args[3] * args[3];
+  pf->m.qa[0] = args[0]; pf->m.qa[1] = args[1]; pf->m.qa[2] = args[2]; pf->m.qa[3] = args[3];
+  pf->m.qa[4] = 1.0 / (2.0 * v);
+  pf->m.qa[5] = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * v);
+  return 0;
 }
 int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal) {
   if (!proposal_ok(&pf->m, proposal)) return -1;

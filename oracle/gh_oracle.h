@@ -39,7 +39,7 @@ extern "C" {
 
 enum { ORC_LGSSM = 1, ORC_HMM = 2, ORC_KITAGAWA = 3, ORC_REGRESSION = 4 };
 enum { ORC_SYSTEMATIC = 0, ORC_MULTINOMIAL = 1 };
-enum { ORC_PROPOSAL_DEFAULT = 0, ORC_PROPOSAL_OPTIMAL = 1 };
+enum { ORC_PROPOSAL_DEFAULT = 0, ORC_PROPOSAL_OPTIMAL = 1, ORC_PROPOSAL_GAUSSIAN = 2 };
 
 typedef struct orc_pf orc_pf;
 
@@ -61,6 +61,9 @@ orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* par
 void orc_pf_destroy(orc_pf* pf);
 int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal);
 int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal);
+/* arguments of the Gaussian custom proposal (alpha, beta, gamma, sigma_q), used
+   by init / step with ORC_PROPOSAL_GAUSSIAN (nonlinear SSM) until changed */
+int orc_pf_set_proposal_args(orc_pf* pf, const double* args, int n);
 /* single-rank maybe_resample!: returns 1/0, or -1 on numeric error */
 int orc_pf_maybe_resample(orc_pf* pf, double ess_threshold, double* ess_out);
 /* rejuvenation: n_moves mh(trace, select(x_t)) moves per particle (src/inference/mh.jl:14-26);

@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 LGSSM, HMM, KITAGAWA, REGRESSION = 1, 2, 3, 4
 SYSTEMATIC, MULTINOMIAL = 0, 1
-DEFAULT, OPTIMAL = 0, 1
+DEFAULT, OPTIMAL, GAUSSIAN = 0, 1, 2
 
 _lib = None
 
@@ -51,6 +51,7 @@ def lib():
             "orc_pf_destroy": (None, [V]),
             "orc_pf_init": (I, [V, D, I, I]),
             "orc_pf_step": (I, [V, D, I, I]),
+            "orc_pf_set_proposal_args": (I, [V, D, I]),
             "orc_pf_maybe_resample": (I, [V, c_double, D]),
             "orc_pf_rejuvenate": (I, [V, I, POINTER(c_int64)]),
             "orc_pf_init_conditional": (I, [V, D, I, D]),
@@ -141,6 +142,12 @@ class OraclePF:
             return None, 0
         a = np.ascontiguousarray(np.atleast_1d(np.asarray(y, dtype=np.float64)))
         return a, 1
+
+    def set_proposal_args(self, args):
+        """(alpha, beta, gamma, sigma_q) of the GAUSSIAN proposal (nonlinear SSM)"""
+        a = np.ascontiguousarray(args, dtype=np.float64)
+        if lib().orc_pf_set_proposal_args(self.h, _d(a), a.size):
+            raise ValueError("oracle: proposal arguments (alpha, beta, gamma, sigma_q > 0)")
 
     def init(self, y, proposal=DEFAULT):
         a, has = self._obs(y)
