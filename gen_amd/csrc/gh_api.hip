@@ -818,6 +818,14 @@ extern "C" int gh_pf_destroy(gh_pf* pf) {
 }
 
 // ----------------------------------------------------------- kernel launch
+// Kernel-timing events: no system-scope fence when an event is recorded.  The
+// default event writes back and invalidates the caches at the kernel's end,
+// so a timed step kernel pushed the ~80 MB of states it had just written out
+// of L2 / Infinity Cache synchronously and the run lost 25-60 us per timed
+// launch (C2, measured); the timestamps are read after a stream
+// synchronisation, which acquires anyway.
+constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
+
 template <class Model>
 static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const StepObs& o,
                           const StepArgs& a0, bool init, hipEvent_t e0, hipEvent_t e1) {
@@ -978,7 +986,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   if (pf->ev_used + 2 > pf->ev.size()) {
     for (int i = 0; i < 64; ++i) {
       hipEvent_t e;
-      HIP_TRY(hipEventCreate(&e));
+      HIP_TRY(hipEventCreateWithFlags(&e, kTimingEventFlags));
       pf->ev.push_back(e);
     }
   }
@@ -2172,8 +2180,8 @@ extern "C" int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_
     a.hist = d_hist;
     a.init = init ? 1 : 0;
     if (kernel_ms) {
-      hipEventCreate(&e0);
-      hipEventCreate(&e1);
+      hipEventCreateWithFlags(&e0, kTimingEventFlags);
+      hipEventCreateWithFlags(&e1, kTimingEventFlags);
     }
     hipExtLaunchKernelGGL(k_pmmh, dim3((unsigned)n_chains), dim3((unsigned)n_inner), 0, s, e0, e1, 0, a);
     if (hipGetLastError() != hipSuccess) {
@@ -2252,8 +2260,8 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
     a.accepts = d_acc;
     a.khist = d_kh;
     if (kernel_ms) {
-      hipEventCreate(&e0);
-      hipEventCreate(&e1);
+      hipEventCreateWithFlags(&e0, kTimingEventFlags);
+      hipEventCreateWithFlags(&e1, kTimingEventFlags);
     }
     hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), sizeof(double) * E, s, e0, e1, 0, a);
     if (hipGetLastError() != hipSuccess) {
@@ -2325,8 +2333,8 @@ extern "C" int gh_coal_create(gh_ctx* ctx, int64_t chain0, int64_t n_chains, con
   const size_t nc = (size_t)n_chains;
   if (hipMalloc(&h->ev, sizeof(double) * E) != hipSuccess ||
       hipMalloc(&h->st, sizeof(double) * 2 * kCoalW * nc) != hipSuccess ||
-      hipMalloc(&h->acc, sizeof(int32_t) * 3 * nc) != hipSuccess || hipEventCreate(&h->e0) != hipSuccess ||
-      hipEventCreate(&h->e1) != hipSuccess) {
+      hipMalloc(&h->acc, sizeof(int32_t) * 3 * nc) != hipSuccess || hipEventCreateWithFlags(&h->e0, kTimingEventFlags) != hipSuccess ||
+      hipEventCreateWithFlags(&h->e1, kTimingEventFlags) != hipSuccess) {
     gh_coal_destroy(h);
     return set_err(GH_E_NOMEM, "gh_coal_create: device buffers");
   }
