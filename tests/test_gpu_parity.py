@@ -194,6 +194,31 @@ def test_batched_run_chunks_and_thresholds(gh_ctx, model):
     assert_lml_close(st, orc)
 
 
+def test_timed_launches_change_nothing(gh_ctx):
+    """The bench's kernel timing (start/stop events on the step kernel's own
+    launch, created without the system-scope fence) must not change the
+    filter: with every 3rd step launch timed the run equals an untimed run bit
+    for bit, and the timer reports the expected number of launches with a
+    positive average duration."""
+    m = gen.LinearGaussianSSM.benchmark(10)
+    _, ys = m.simulate(12, np.random.default_rng(13))
+    n = 70001
+    out = []
+    for every in (0, 3):
+        st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=21, time_kernels=every)
+        st.kernel_time_ms(reset=True)  # drop the init launch
+        gen.run_particle_filter(st, list(ys[1:]), None)
+        ms, count = st.kernel_time_ms()
+        out.append((gen.get_log_weights(st), st.states(), st.parents, gen.log_ml_estimate(st), ms, count))
+        st.close()
+    (w0, x0, p0, l0, _, c0), (w1, x1, p1, l1, ms1, c1) = out
+    assert c0 == 0 and c1 == sum(1 for t in range(2, len(ys) + 1) if (t - 1) % 3 == 0)
+    assert ms1 > 0.0
+    assert np.array_equal(w0.view(np.uint64), w1.view(np.uint64))
+    assert np.array_equal(x0.view(np.uint64), x1.view(np.uint64))
+    assert np.array_equal(p0, p1) and l0 == l1
+
+
 def test_zero_threshold_never_resamples(gh_ctx):
     """maybe_resample(state, 0.0) is `ess < 0`: never true, so no resample, the
     log-ML estimate accumulates nothing, weights keep growing (as in Gen)."""
