@@ -116,6 +116,44 @@ def test_normal_logpdf_golden():
         assert got == pytest.approx(row["logpdf"], rel=1e-15, abs=1e-15)
 
 
+def test_unfold_update_regenerate_kats():
+    """The Unfold update / regenerate weights and scores of the reference's
+    known-answer tests (test/modeling_library/unfold.jl:116-481, kernel
+    x ~ normal(alpha x_prev + beta, 1), unfold.jl:5-8), recomposed from the
+    oracle's normal logpdf exactly as the reference states them.  The PF step's
+    weight (update extending the chain, constrained new choices) is the
+    `update_extend_change` shape: new-step logpdf plus the re-scored changes."""
+    g = gold("unfold_kats.json")
+    a = g["args"]
+    lp = O.lib().orc_normal_logpdf
+    xi, al, be, x1, x2 = a["x_init"], a["alpha"], a["beta"], a["x1"], a["x2"]
+    an, s = 0.5, 1.0
+    want = g["cases"]
+    got = {
+        "update_extend_change": (
+            lp(x1, xi * an + be, s) + lp(1.3, x1 * an + be, s) + lp(1.4, 1.3 * an + be, s),
+            lp(1.4, 1.3 * an + be, s) + lp(1.3, x1 * an + be, s) - lp(x2, x1 * al + be, s)
+            + lp(x1, xi * an + be, s) - lp(x1, xi * al + be, s)),
+        "update_shrink_change": (
+            lp(1.3, xi * an + be, s),
+            lp(1.3, xi * an + be, s) - lp(x1, xi * al + be, s) - lp(x2, x1 * al + be, s)),
+        "update_nochange": (lp(x1, xi * al + be, s) + lp(x2, x1 * al + be, s), 0.0),
+        "update_change_x2": (
+            lp(x1, xi * al + be, s) + lp(3.3, x1 * al + be, s),
+            lp(3.3, x1 * al + be, s) - lp(x2, x1 * al + be, s)),
+        "update_params": (
+            lp(x1, xi * an + be, s) + lp(x2, x1 * an + be, s),
+            lp(x1, xi * an + be, s) - lp(x1, xi * al + be, s) + lp(x2, x1 * an + be, s) - lp(x2, x1 * al + be, s)),
+        "regenerate_init": (
+            lp(x1, -0.1 * al + be, s) + lp(x2, x1 * al + be, s),
+            lp(x1, -0.1 * al + be, s) - lp(x1, xi * al + be, s)),
+    }
+    assert set(got) == set(want)
+    for k, (score, weight) in got.items():
+        assert score == pytest.approx(want[k]["score"], rel=1e-13, abs=1e-13), k
+        assert weight == pytest.approx(want[k]["weight"], rel=1e-12, abs=1e-12), k
+
+
 def hmm_forward(prior, E, T, obs):
     ml = 1.0
     alpha = np.asarray(prior)
