@@ -187,9 +187,13 @@ def main():
     bytes_pp = 16 * d + 16 + 4.0 * n_res / max(1, a.steps)
     achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
-    if (os.path.exists(pmc) and a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20
-            and prop is None):  # the profiled config
+    # PMC HBM bytes per step-kernel launch of the profiled configs (tools/pmc_json.py)
+    pmc = None
+    if a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20 and prop is None:
+        pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    elif a.model == "kitagawa" and a.particles == 1 << 21:
+        pmc = os.path.join(ROOT, "profiles", "pmc_k_step_kitagawa.json")
+    if pmc is not None and os.path.exists(pmc):
         try:
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
