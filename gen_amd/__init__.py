@@ -30,6 +30,8 @@ from .pf import (
     maybe_resample_async,
     particle_filter_step,
     rejuvenate,
+    ObservationBatch,
+    prepare_observations,
     run_particle_filter,
     sample_unweighted_traces,
     set_default_context,
@@ -43,5 +45,5 @@ __all__ = [
     "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",
     "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
     "conditional_particle_filter_step", "conditional_smc", "get_particle", "initialize_conditional_particle_filter",
-    "particle_gibbs", "GenHipError",
+    "particle_gibbs", "GenHipError", "ObservationBatch", "prepare_observations",
 ]

@@ -419,34 +419,47 @@ def maybe_resample_async(state: ParticleFilterState, ess_threshold: float | None
     _lib.check(_lib.load().gh_pf_maybe_resample(state.h, thr, None, None))
 
 
+class ObservationBatch:
+    """The gh_obs array of several consecutive steps, built once (the host-side
+    marshalling of run_particle_filter, done ahead of a timed loop)."""
+
+    def __init__(self, model: Model, observations_per_step):
+        self.values = [None if v is None else model.obs_values(v) for v in observations_per_step]
+        self.arr = (_lib.Obs * max(1, len(self.values)))()
+        for i, a in enumerate(self.values):
+            self.arr[i] = _lib.Obs(None, 0, 0) if a is None else _lib.Obs(_lib.dptr(a), a.size, 1)
+
+    def __len__(self):
+        return len(self.values)
+
+
+def prepare_observations(model: Model, observations_per_step) -> ObservationBatch:
+    return ObservationBatch(model, observations_per_step)
+
+
 def run_particle_filter(state: ParticleFilterState, observations_per_step, ess_threshold: float | None = None,
                         proposal=None, proposal_args: tuple | None = None) -> None:
     """The reference caller loop {maybe_resample!; particle_filter_step!} over
-    the given per-step observations (arrays or None), enqueued without host sync.
-    A proposal with arguments uses proposal_args, or the last ones given."""
+    the given per-step observations (arrays or None, or an ObservationBatch of
+    them), enqueued without host sync.  A proposal with arguments uses
+    proposal_args, or the last ones given."""
     model = state.model
-    if proposal_args is not None and len(observations_per_step) > 0:
-        qa, nq = _qargs(proposal, proposal_args)
-        if qa is not None:  # store them (the library keeps the last arguments)
-            maybe_resample_async(state, ess_threshold)
-            particle_filter_step(state, (state.t + 1,), (UnknownChange(),), observations_per_step[0], proposal,
-                                 proposal_args)
-            observations_per_step = list(observations_per_step)[1:]
+    if isinstance(observations_per_step, ObservationBatch):
+        batch = observations_per_step
+    else:
+        if proposal_args is not None and len(observations_per_step) > 0:
+            qa, nq = _qargs(proposal, proposal_args)
+            if qa is not None:  # store them (the library keeps the last arguments)
+                maybe_resample_async(state, ess_threshold)
+                particle_filter_step(state, (state.t + 1,), (UnknownChange(),), observations_per_step[0], proposal,
+                                     proposal_args)
+                observations_per_step = list(observations_per_step)[1:]
+        batch = ObservationBatch(model, observations_per_step)
     t0 = state.t
-    keep = []
-    arr = (_lib.Obs * max(1, len(observations_per_step)))()
-    for i, v in enumerate(observations_per_step):
-        if v is None:
-            arr[i] = _lib.Obs(None, 0, 0)
-        else:
-            a = model.obs_values(v)
-            keep.append(a)
-            arr[i] = _lib.Obs(_lib.dptr(a), a.size, 1)
     thr = state.num_particles / 2 if ess_threshold is None else float(ess_threshold)
-    _lib.check(_lib.load().gh_pf_run(state.h, len(observations_per_step), arr, _proposal_code(proposal), thr))
-    for i, v in enumerate(observations_per_step):
-        state._log_obs(t0 + 1 + i, None if v is None else model.obs_values(v))
-    del keep, t0
+    _lib.check(_lib.load().gh_pf_run(state.h, len(batch), batch.arr, _proposal_code(proposal), thr))
+    for i, a in enumerate(batch.values):
+        state._log_obs(t0 + 1 + i, a)
 
 
 def log_ml_estimate(state: ParticleFilterState) -> float:
