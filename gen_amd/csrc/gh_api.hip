@@ -1455,6 +1455,8 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   d.stats_all = pf->stats_all;
   d.R = R;
   d.n_global = pf->n_global;
+  d.log_n = gh_log((double)pf->n_global);
+  d.inv_n = 1.0 / (double)pf->n_global;
   d.thr = thr;
   d.ess_hist = pf->ess_hist;
   d.res_hist = pf->res_hist;

@@ -404,6 +404,8 @@ struct DecideArgs {
   const double* stats_all;  // [3*R]
   int R;
   int64_t n_global;
+  double log_n;      // gh_log(n_global), evaluated on the host (same function, same bits)
+  double inv_n;      // 1 / n_global (division estimate, corrected exactly)
   double thr;
   double* ess_hist;  // indexed by step
   int32_t* res_hist; // res_hist[t+1]: a resample precedes step t+1
@@ -454,7 +456,7 @@ __device__ __forceinline__ void commit_decision(const DecideArgs& d, const Decis
   dev->ess = r.ess;
   dev->fire = r.fire;
   if (r.err) dev->error = r.err;
-  if (r.fire) dev->log_ml_est += r.L - gh_log((double)d.n_global);
+  if (r.fire) dev->log_ml_est += r.L - d.log_n;
   if (d.ess_hist) d.ess_hist[d.t] = r.ess;
   if (d.res_hist) d.res_hist[d.t + 1] = pending | r.fire;
 }
@@ -684,6 +686,17 @@ __device__ __forceinline__ uint64_t udiv_n(uint64_t num, uint64_t N, double invN
   return q;
 }
 
+// 1 / x for the slot-count estimates (x >= 1): the hardware reciprocal and two
+// Newton steps (within 2 ulp; sys_count's exactness argument allows far more)
+// instead of the ~30-instruction IEEE division on the resample's serial path.
+__device__ __forceinline__ double recip_est(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+
 // systematic target of global slot j: floor((j S + o) / N)
 __device__ __forceinline__ uint64_t sys_target(const DevScalars* dev, uint64_t N, uint64_t j) {
   return j * dev->Qs + udiv_n(j * dev->Rs + dev->o, N, dev->invN);
@@ -702,9 +715,10 @@ __device__ __forceinline__ int64_t sys_count_exact(const DevScalars* dev, uint64
 }
 
 // The same count from v = (X N - o) / S in floating point: count = ceil(v)
-// clamped to [0, N].  The computed v is within 5 N 2^-53 (< 2^-19 for
-// N < 2^31) of the exact quotient, so ceil is exact whenever v is more than
-// 2^-16 away from an integer; otherwise (probability ~2^-15) count exactly.
+// clamped to [0, N].  With 1/S within 2 ulp (recip_est) the computed v is
+// within 7 N 2^-53 (< 2^-19 for N < 2^31) of the exact quotient, so ceil is
+// exact whenever v is more than 2^-16 away from an integer; otherwise
+// (probability ~2^-15) count exactly.
 __device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, uint64_t X) {
   if (X == 0) return 0;
   if (X >= dev->S) return (int64_t)N;
@@ -713,7 +727,9 @@ __device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, 
   const double fr = v - fl;
   if (fr > 0x1p-16 && fr < 1.0 - 0x1p-16) {
     const double j = fl + 1.0;
-    return j <= 0.0 ? 0 : (j >= (double)N ? (int64_t)N : (int64_t)j);
+    if (j <= 0.0) return 0;
+    if (j >= (double)N) return (int64_t)N;
+    return N < (1ull << 31) ? (int64_t)(int32_t)j : (int64_t)j;  // v_cvt_i32_f64 when it fits
   }
   return sys_count_exact(dev, N, X);
 }
@@ -988,6 +1004,82 @@ __device__ __forceinline__ uint64_t blk16_incl_u64(uint64_t v, uint64_t* sm) {
   return v + blk16_excl(sm, w);
 }
 
+// The resample kernel's block scan, with the cross-wave work done once: the
+// 16 wave totals are scanned by wave 0 (one DPP scan over lanes 0..15) and
+// each wave reads its one exclusive offset, instead of every wave summing 16
+// LDS values under a mask; with `sums`, thread 0 alone adds the 16 wave sums
+// of a and b (the block totals it publishes; same order as blk16_sum2).
+// smu: 32 u64 (totals, offsets), smd: 32 doubles.  Inclusive scan returned;
+// *a, *b hold the block sums in thread 0 only.
+template <bool SUMS>
+__device__ __forceinline__ uint64_t blk16_scan(uint64_t v, double* a, double* b, uint64_t* smu, double* smd) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_incl_sum_u64(v);
+  double wa = 0.0, wb = 0.0;
+  if (SUMS) {
+    wa = wave_sum(*a);
+    wb = wave_sum(*b);
+  }
+  lds_barrier();
+  if (lane == 63) smu[w] = v;
+  if (SUMS && lane == 0) {
+    smd[w] = wa;
+    smd[16 + w] = wb;
+  }
+  lds_barrier();
+  if (w == 0) {
+    const uint64_t t = lane < 16 ? smu[lane] : 0ull;
+    const uint64_t inc = wave_incl_sum_u64(t);
+    if (lane < 16) smu[16 + lane] = inc - t;
+    if (SUMS && lane == 0) {
+      double ra = smd[0], rb = smd[16];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) {
+        ra += smd[k];
+        rb += smd[16 + k];
+      }
+      *a = ra;
+      *b = rb;
+    }
+  }
+  lds_barrier();
+  return v + smu[16 + w];
+}
+
+// block max (16 waves): wave 0 folds the 16 wave maxima, every thread reads one
+// LDS value (fmax is exact in any order)
+__device__ __forceinline__ double blk16_max1(double v, double* sm) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max(v);
+  lds_barrier();
+  if (lane == 0) sm[w] = v;
+  lds_barrier();
+  if (w == 0) {
+    double r = lane < 16 ? sm[lane] : -INFINITY;
+    r = wave_max(r);
+    if (lane == 0) sm[16] = r;
+  }
+  lds_barrier();
+  return sm[16];
+}
+
+// (uint64)x for 0 <= x <= 2^52 in three instructions: floor, then the integer
+// read off the mantissa of floor(x) + 2^52 (exact below 2^53); the generic
+// f64 -> u64 conversion is a dozen
+__device__ __forceinline__ uint64_t f64_to_u52(double x) {
+  return as_u64(floor(x) + 0x1p52) - 0x4330000000000000ull;
+}
+
+// timing-only variants (results wrong): GH_RS_EXIT=k leaves k_resample1 after
+// phase k (0 start, 1 fold, 2 quantise + scan, 3 grid barrier), to price the
+// phases including the launch
+#if defined(GH_RS_EXIT)
+#define GH_RS_EXIT_AT(k) \
+  if (GH_RS_EXIT == (k)) return;
+#else
+#define GH_RS_EXIT_AT(k)
+#endif
+
 #if defined(GH_RS_STAMPS)  // timing-only variant: per-block phase clocks
 __device__ uint64_t g_rs_stamps[1024 * 8];
 #define GH_RS_STAMP(k) \
@@ -999,18 +1091,21 @@ __device__ uint64_t g_rs_stamps[1024 * 8];
 template <bool MARKS, int IT>
 __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   __shared__ double smd[32];
-  __shared__ uint64_t smu[16];
+  __shared__ uint64_t smu[32];
   __shared__ DevScalars sd;
   __shared__ uint64_t sbase;
   __shared__ int32_t se[(kRsBlock * IT)];
   __shared__ int64_t sfirst;
   __shared__ unsigned sgen;
   __shared__ int sfail;  // the barrier wait timed out: write nothing
+  __shared__ int smany;  // a particle of the tile covers more than two 64-slot group starts
   GH_RS_STAMP(0);
+  GH_RS_EXIT_AT(0);
   // barrier generation of this launch: read before this block publishes
   if (threadIdx.x == 0) {
     sgen = r.dev->bar_gen + 1;
     sfail = 0;
+    smany = 0;
   }
   // ---- fold the step partials (same order in every block: same result)
   // this tile's log-weights are loaded up front, beside the partials
@@ -1039,8 +1134,9 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     double m = pmv[0];
 #pragma unroll
     for (int k = 1; k < KP; ++k) m = fmax(m, pmv[k]);
-    M = blk16_max(m, smd);
+    M = blk16_max1(m, smd);
     GH_RS_STAMP(7);
+    GH_RS_EXIT_AT(1);
     if (!sums && M > -INFINITY) {
       double a1[KP], a2[KP];
 #pragma unroll
@@ -1125,7 +1221,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   for (int k = 0; k < IT; ++k) {
     const bool in = i0 + k < r.n;
     const double e = in ? gh_exp_nonpos(lw[k] - Mq) : 0.0;
-    q[k] = in ? (uint64_t)(e * qscale) : 0;  // = quantize_weight_nonpos
+    q[k] = e == e ? f64_to_u52(e * qscale) : 0;  // = quantize_weight_nonpos (e * 2^shift <= 2^52)
     tsum += q[k];
     if (sums) {
       const double ee = lw[k] != lw[k] ? lw[k] : e;  // NaN poisons the statistics
@@ -1133,8 +1229,9 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
       s2 += ee * ee;
     }
   }
-  const uint64_t incl = sums ? blk16_incl_sum2(tsum, &s1, &s2, smu, smd) : blk16_incl_u64(tsum, smu);
+  const uint64_t incl = sums ? blk16_scan<true>(tsum, &s1, &s2, smu, smd) : blk16_scan<false>(tsum, &s1, &s2, smu, smd);
   GH_RS_STAMP(2);
+  GH_RS_EXIT_AT(2);
   // ---- grid barrier: each tile total (< 2^62) is published as ONE 8-byte
   // agent-scope store tagged in bit 63 with the generation's parity, and read
   // back with agent-scope loads until every tag matches (the payload is its
@@ -1218,10 +1315,10 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
       sd.base = 0;
       sd.local = all;
       sd.o = scale_u53(u53_bits(wr.x, wr.y), all);
-      sd.invN = 1.0 / (double)N;
+      sd.invN = r.d.inv_n;
       sd.Qs = udiv_n(all, N, sd.invN);
       sd.Rs = all - sd.Qs * N;
-      sd.invS = 1.0 / (double)all;
+      sd.invS = recip_est((double)all);
       sbase = before;
       if (blockIdx.x == 0) {
         r.dev->bar_gen = sgen;  // every block has published, so has read the old value
@@ -1241,6 +1338,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   // grid never started): the totals are partial.  The block leaves without
   // marks or decision; the error surfaces as GH_E_STATE at the next sync.
   if (sfail) return;
+  GH_RS_EXIT_AT(3);
   if (sums) {
     S1 = sS[0];
     S2 = sS[1];
@@ -1263,28 +1361,44 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   const uint64_t N = (uint64_t)r.mk.n_global;
   int64_t s_i = sys_count(&sd, N, run);
   if (threadIdx.x == 0) sfirst = s_i;
+  // particle i owns the slots [s_i, e_i): a tagged mark at s_i, and the carry
+  // of every 64-slot group that starts inside the range; a lane writes up to
+  // two carries itself, a longer range (a particle with > 64 offspring) makes
+  // the block write its whole span's carries by the search below
+  bool many = false;
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     run += q[k];
     const int64_t e_i = (i0 + k < r.n && q[k]) ? sys_count(&sd, N, run) : s_i;
     se[threadIdx.x * IT + k] = (int32_t)e_i;
-    if (e_i > s_i) r.mk.mark[s_i] = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
+    const uint64_t tagged = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
+    if (e_i > s_i) r.mk.mark[s_i] = tagged;
+    const int64_t g0 = (s_i + 63) >> 6, g1 = (e_i + 63) >> 6;  // groups g with 64 g in [s_i, e_i)
+    if (g1 - g0 <= 2) {
+      if (g1 > g0) r.mk.cmark[g0] = tagged;
+      if (g1 > g0 + 1) r.mk.cmark[g0 + 1] = tagged;
+    } else {
+      many = true;
+    }
     s_i = e_i;
   }
-  lds_barrier();  // se[] only; the mark stores need not have landed
+  if (many) smany = 1;
+  lds_barrier();  // se[] and smany; the mark and carry stores need not have landed
   GH_RS_STAMP(5);
-  // 64-slot groups starting inside this tile's slot span get their carry
-  const int64_t s_lo = sfirst, s_hi = se[(kRsBlock * IT) - 1];
-  const int64_t pbase = (int64_t)blockIdx.x * (kRsBlock * IT);
-  for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
-    const int32_t slot = (int32_t)(g * 64);
-    int lo = 0, hi = (kRsBlock * IT) - 1;  // first particle p with se[p] > slot
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (se[mid] > slot) hi = mid;
-      else lo = mid + 1;
+  if (smany) {
+    // 64-slot groups starting inside this tile's slot span get their carry
+    const int64_t s_lo = sfirst, s_hi = se[(kRsBlock * IT) - 1];
+    const int64_t pbase = (int64_t)blockIdx.x * (kRsBlock * IT);
+    for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
+      const int32_t slot = (int32_t)(g * 64);
+      int lo = 0, hi = (kRsBlock * IT) - 1;  // first particle p with se[p] > slot
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (se[mid] > slot) hi = mid;
+        else lo = mid + 1;
+      }
+      r.mk.cmark[g] = (r.mk.epoch << 32) | (uint64_t)(pbase + lo);
     }
-    r.mk.cmark[g] = (r.mk.epoch << 32) | (uint64_t)(pbase + lo);
   }
   commit();
   GH_RS_STAMP(6);

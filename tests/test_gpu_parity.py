@@ -296,21 +296,34 @@ def test_hmm_large_n_converges(gh_ctx):
 
 # --------------------------------------------------------- full C2 size
 def test_lgssm_full_size_against_kalman(gh_ctx):
-    """C2: d=10, N=2^20, T=100.  The exact Kalman log-ML bounds the PF estimate
-    (PF log-ML is consistent; its bias/variance at this N is O(1e-1))."""
+    """C2: d=10, N=2^20, T=100, 8 seeds.  log Z-hat is asymptotically normal
+    with mean log Z - var/2 (Z-hat is unbiased): the bias-corrected mean is
+    within 4 of its standard errors of the exact Kalman log-ML, the spread is
+    the Monte-Carlo one (sd ~0.3 at this N; the CPU test pins 2^17), and every
+    seed is within 5 sd of 0.3."""
     k = gold("kalman.json")["lg10"]
     d = k["d"]
     m = gen.LinearGaussianSSM(np.array(k["A"]), 0.1 * np.eye(d), np.eye(d), 0.5 * np.eye(d), np.zeros(d), np.eye(d))
     ys = np.array(k["ys"])
     n = 1 << 20
-    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=42, history_capacity=128)
-    gen.run_particle_filter(st, list(ys[1:]))
-    est = gen.log_ml_estimate(st)
-    assert abs(est - k["log_ml"]) < 3.0, (est, k["log_ml"])
-    ess, did = st.ess_history()
-    assert did.any()
-    par = st.parents
-    assert np.all(np.diff(par) >= 0) and par[0] >= 0 and par[-1] < n
+    ests = []
+    for seed in range(42, 50):
+        st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=seed, history_capacity=128)
+        gen.run_particle_filter(st, list(ys[1:]))
+        ests.append(gen.log_ml_estimate(st))
+        if seed == 42:
+            ess, did = st.ess_history()
+            assert did.any()
+            par = st.parents
+            assert np.all(np.diff(par) >= 0) and par[0] >= 0 and par[-1] < n
+        st.close()
+    ests = np.array(ests)
+    print("log-ML over seeds", ests, "exact", k["log_ml"], "sd", ests.std(ddof=1))
+    var = ests.var(ddof=1)
+    se = np.sqrt(var / ests.size + var**2 / (2 * (ests.size - 1)))
+    assert np.sqrt(var) < 0.6, ests
+    assert abs(ests.mean() + var / 2 - k["log_ml"]) < 4 * se, (ests, k["log_ml"])
+    assert np.all(np.abs(ests - k["log_ml"]) < 1.5), (ests, k["log_ml"])
 
 
 def test_lgssm_full_size_first_steps_bitexact(gh_ctx):

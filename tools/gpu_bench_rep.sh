@@ -1,6 +1,7 @@
 #!/bin/bash
 # Repeat bench.py variants on one box (A/B without box-to-box noise):
 #   tools/gpu_bench_rep.sh OUT REPS "args A" "args B" ...
+# a variant "lib.so|args" runs bench.py with GEN_HIP_LIB=lib.so (another build);
 # writes OUT/<i>_<rep>.json and a summary OUT/summary.txt (us per step).
 set -e
 OUT=$1; REPS=$2; shift 2
@@ -10,7 +11,9 @@ for rep in $(seq 1 "$REPS"); do
   i=0
   for args in "$@"; do
     i=$((i+1))
-    timeout -k 10 200 python bench.py --no-cpu-baseline $args > "$OUT/${i}_${rep}.json" 2> "$OUT/${i}_${rep}.err"
+    lib=""
+    if [[ "$args" == *"|"* ]]; then lib="${args%%|*}"; args="${args#*|}"; fi
+    GEN_HIP_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline $args > "$OUT/${i}_${rep}.json" 2> "$OUT/${i}_${rep}.err"
   done
 done
 python - "$OUT" "$REPS" "$@" > "$OUT/summary.txt" <<'EOF'

@@ -11,7 +11,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["GEN_HIP_LIB"] = os.path.join(ROOT, "gen_amd", "variants", "rs_stamps.so")
+os.environ.setdefault("GEN_HIP_LIB", os.path.join(ROOT, "gen_amd", "variants", "rs_stamps.so"))
 import gen_amd as gen  # noqa: E402
 from gen_amd import _lib  # noqa: E402
 
