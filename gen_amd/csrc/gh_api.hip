@@ -2213,6 +2213,26 @@ extern "C" int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_
 }
 
 // ------------------------------------------------------------------ coal
+// The model constants of k_coal (gh_coal.h) and the bucket table of event-scan
+// start indices (any table is exact: coal_count corrects its start).
+static void coal_consts(const double* events, int E, CoalArgs* a, std::vector<int32_t>* bucket) {
+  a->E = E;
+  a->T = events[E - 1];
+  a->bscale = (double)kCoalBuckets / a->T;
+  a->kb = gh_log(3.0) - gh_log(a->T);
+  a->ktheta = gh_log(kCoalRate);
+  a->lhalf = gh_log(0.5);
+  bucket->assign(kCoalBuckets, 0);
+  int j = 0;
+  for (int b = 0; b < kCoalBuckets; ++b) {
+    const double lo = (double)b / a->bscale;
+    while (j < E && events[j] < lo) ++j;
+    (*bucket)[b] = j;
+  }
+}
+
+static size_t coal_lds_bytes(int E) { return sizeof(double) * (size_t)E + sizeof(int32_t) * kCoalBuckets; }
+
 extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const double* events, int E, int n_iters,
                            int iter0, uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist,
                            double* kernel_ms) {
@@ -2227,10 +2247,14 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
   hipStream_t s = ctx->stream;
   const size_t nc = (size_t)n_chains;
   double *d_ev = nullptr, *d_st = nullptr, *d_rows = nullptr;
-  int32_t *d_acc = nullptr, *d_kh = nullptr;
-  auto cleanup = [&]() { hipFree(d_ev); hipFree(d_st); hipFree(d_rows); hipFree(d_acc); hipFree(d_kh); };
+  int32_t *d_acc = nullptr, *d_kh = nullptr, *d_bk = nullptr;
+  auto cleanup = [&]() { hipFree(d_ev); hipFree(d_st); hipFree(d_rows); hipFree(d_acc); hipFree(d_kh); hipFree(d_bk); };
   const unsigned tgrid = (unsigned)((nc * kCoalW + 255) / 256);
-  if (hipMalloc(&d_ev, sizeof(double) * E) != hipSuccess || hipMalloc(&d_st, sizeof(double) * 2 * kCoalW * nc) != hipSuccess ||
+  CoalArgs a{};
+  std::vector<int32_t> bucket;
+  coal_consts(events, E, &a, &bucket);
+  if (hipMalloc(&d_ev, sizeof(double) * E) != hipSuccess || hipMalloc(&d_st, sizeof(double) * kCoalW * nc) != hipSuccess ||
+      hipMalloc(&d_bk, sizeof(int32_t) * kCoalBuckets) != hipSuccess ||
       hipMalloc(&d_rows, sizeof(double) * kCoalW * nc) != hipSuccess ||
       hipMalloc(&d_acc, sizeof(int32_t) * 3 * nc) != hipSuccess ||
       (khist && n_iters > 0 && hipMalloc(&d_kh, sizeof(int32_t) * nc * n_iters) != hipSuccess)) {
@@ -2241,16 +2265,15 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
   hipEvent_t e0 = nullptr, e1 = nullptr;
   do {
     if (hipMemcpyAsync(d_ev, events, sizeof(double) * E, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemsetAsync(d_st, 0, sizeof(double) * 2 * kCoalW * nc, s) != hipSuccess ||
+        hipMemcpyAsync(d_bk, bucket.data(), sizeof(int32_t) * kCoalBuckets, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(d_st, 0, sizeof(double) * kCoalW * nc, s) != hipSuccess ||
         (!init && hipMemcpyAsync(d_rows, state, sizeof(double) * kCoalW * nc, hipMemcpyHostToDevice, s) != hipSuccess)) {
       rc = set_err(GH_E_HIP, "gh_coal_run: upload");
       break;
     }
     if (!init) hipLaunchKernelGGL(k_coal_rows, dim3(tgrid), dim3(256), 0, s, d_st, (int64_t)nc, d_rows, (int64_t)nc, 1);
-    CoalArgs a{};
     a.events = d_ev;
-    a.E = E;
-    a.T = events[E - 1];
+    a.bucket = d_bk;
     a.chain0 = chain0;
     a.n_chains = n_chains;
     a.seed = seed;
@@ -2265,7 +2288,8 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
       hipEventCreateWithFlags(&e0, kTimingEventFlags);
       hipEventCreateWithFlags(&e1, kTimingEventFlags);
     }
-    hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), sizeof(double) * E, s, e0, e1, 0, a);
+    hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + kCoalBlock - 1) / kCoalBlock)), dim3(kCoalBlock),
+                          coal_lds_bytes(E), s, e0, e1, 0, a);
     if (hipGetLastError() != hipSuccess) {
       rc = set_err(GH_E_HIP, "gh_coal_run: launch");
       break;
@@ -2293,8 +2317,10 @@ extern "C" int gh_coal_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const 
 struct gh_coal {
   gh_ctx* ctx = nullptr;
   double* ev = nullptr;
-  double* st = nullptr;     // [n][2 * kCoalW] (current + proposal rows)
+  double* st = nullptr;     // SoA [kCoalW][n] rows
   int32_t* acc = nullptr;   // [n][3]
+  int32_t* bk = nullptr;    // bucket table of the event scan
+  CoalArgs consts{};        // model constants (coal_consts)
   int E = 0;
   double T = 0.0;
   int64_t chain0 = 0, n = 0;
@@ -2311,6 +2337,7 @@ extern "C" int gh_coal_destroy(gh_coal* h) {
   hipFree(h->ev);
   hipFree(h->st);
   hipFree(h->acc);
+  hipFree(h->bk);
   if (h->e0) hipEventDestroy(h->e0);
   if (h->e1) hipEventDestroy(h->e1);
   delete h;
@@ -2333,15 +2360,19 @@ extern "C" int gh_coal_create(gh_ctx* ctx, int64_t chain0, int64_t n_chains, con
   h->n = n_chains;
   h->seed = seed;
   const size_t nc = (size_t)n_chains;
+  std::vector<int32_t> bucket;
+  coal_consts(events, E, &h->consts, &bucket);
   if (hipMalloc(&h->ev, sizeof(double) * E) != hipSuccess ||
-      hipMalloc(&h->st, sizeof(double) * 2 * kCoalW * nc) != hipSuccess ||
+      hipMalloc(&h->st, sizeof(double) * kCoalW * nc) != hipSuccess ||
+      hipMalloc(&h->bk, sizeof(int32_t) * kCoalBuckets) != hipSuccess ||
       hipMalloc(&h->acc, sizeof(int32_t) * 3 * nc) != hipSuccess || hipEventCreateWithFlags(&h->e0, kTimingEventFlags) != hipSuccess ||
       hipEventCreateWithFlags(&h->e1, kTimingEventFlags) != hipSuccess) {
     gh_coal_destroy(h);
     return set_err(GH_E_NOMEM, "gh_coal_create: device buffers");
   }
   if (hipMemcpyAsync(h->ev, events, sizeof(double) * E, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
-      hipMemsetAsync(h->st, 0, sizeof(double) * 2 * kCoalW * nc, ctx->stream) != hipSuccess ||
+      hipMemcpyAsync(h->bk, bucket.data(), sizeof(int32_t) * kCoalBuckets, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipMemsetAsync(h->st, 0, sizeof(double) * kCoalW * nc, ctx->stream) != hipSuccess ||
       hipStreamSynchronize(ctx->stream) != hipSuccess) {
     gh_coal_destroy(h);
     return set_err(GH_E_HIP, "gh_coal_create: upload");
@@ -2358,10 +2389,9 @@ extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* 
   int32_t* d_kh = nullptr;
   if (khist && n_iters > 0 && hipMalloc(&d_kh, sizeof(int32_t) * nc * n_iters) != hipSuccess)
     return set_err(GH_E_NOMEM, "gh_coal_step: k history");
-  CoalArgs a{};
+  CoalArgs a = h->consts;
   a.events = h->ev;
-  a.E = h->E;
-  a.T = h->T;
+  a.bucket = h->bk;
   a.chain0 = h->chain0;
   a.n_chains = h->n;
   a.seed = h->seed;
@@ -2372,7 +2402,8 @@ extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* 
   a.ld = h->n;
   a.accepts = h->acc;
   a.khist = d_kh;
-  hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + 255) / 256)), dim3(256), sizeof(double) * h->E, s, h->e0, h->e1, 0, a);
+  hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + kCoalBlock - 1) / kCoalBlock)), dim3(kCoalBlock),
+                        coal_lds_bytes(h->E), s, h->e0, h->e1, 0, a);
   int rc = GH_OK;
   if (hipGetLastError() != hipSuccess) rc = set_err(GH_E_HIP, "gh_coal_step: launch");
   if (!rc && accepts && hipMemcpyAsync(accepts, h->acc, sizeof(int32_t) * 3 * nc, hipMemcpyDeviceToHost, s) != hipSuccess)

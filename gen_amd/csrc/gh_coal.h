@@ -3,18 +3,33 @@
 //
 // Reference: examples/coal/coal.jl:47-62 (model), :18-33 (min_uniform_continuous),
 // examples/coal/poisson_process.jl:9-67 (piecewise Poisson process), and the
-// three moves of mcmc_step (coal.jl:329-336): rate_move (:126-150),
-// position_move (:156-184), birth_death_move (:190-318), each an involutive
+// three moves of mcmc_step (coal.jl:329-336): rate_move (:103-134),
+// position_move (:140-167), birth_death_move (:173-318), each an involutive
 // MH step (src/inference/mh.jl:85-98 over trace_translators.jl:848-876:
 // log_weight = new score - old score + bwd score - fwd score + log|J|).
 // The Jacobian of the birth map (h, u) -> (h_prev, h_next) is taken in closed
 // form, |J| = (h_prev + h_next)^2 / h (Green 1995), where the reference
 // differentiates the transform with ForwardDiff (trace_translators.jl:534-589).
 //
-// One thread per chain.  A chain's state lives in HBM as one row of
-// kCoalW doubles (k, score, change points, rates); the 190 event times live
-// in LDS.  The full specification (score order, draw indices) is DESIGN.md
-// §7c and is restated by oracle/gh_oracle.c (orc_coal_run).
+// The score, written for the state (k, cp[1..k], h[1..k+1]) with b_0 = 0,
+// b_{k+1} = T, c_i = #events in segment i and len_i = b_i - b_{i-1}:
+//   poisson(3) + the k sequential min_uniform_continuous terms + gamma priors
+//   + piecewise Poisson process
+//   = k (log 3 - log T) - 3 + sum_i [-log(theta) - h_i / theta]
+//     + sum_i [c_i log h_i - len_i h_i]
+// (the order-statistic densities telescope to log k! - k log T, and log k!
+// cancels against the Poisson prior's; tests/test_coal_pins.py checks this
+// against the reference's formulas term by term).  Each move changes one or
+// two segments, so it is scored by its difference alone: a rate move touches
+// segment i, a position move segments i and i+1, a birth / death the segment
+// split or merged — no copy of the state, no full re-score.
+//
+// One thread per chain; a chain's change points and rates live in LDS for the
+// whole launch ([field][lane] per wave: conflict-free for any per-lane
+// index), k and the score in registers; HBM is read once and written once per
+// launch.  Event counts come from the sorted event times in LDS through a
+// bucket table (start index) and a short scan.  The oracle
+// (oracle/gh_oracle.c, orc_coal_run) restates the same arithmetic.
 #pragma once
 #include "gh_kernels.h"
 
@@ -22,29 +37,58 @@ namespace gh {
 
 constexpr int kCoalKMax = 32;
 constexpr int kCoalW = 2 + kCoalKMax + (kCoalKMax + 1) + 1;  // 68: k, score, cp[32], h[33], pad
+constexpr int kCoalF = kCoalKMax + (kCoalKMax + 1);          // 65 LDS fields per chain: cp[32], h[33]
 constexpr int kCoalMaxEvents = 4096;
-constexpr double kCoalTheta = 1.0 / 200.0;  // gamma(1, 1/200) rate prior (coal.jl:56-58)
+constexpr int kCoalBlock = 128;                              // two waves: 2 blocks (66.5 KB state each) per CU
+constexpr int kCoalBuckets = 256;                            // event-count start table
+constexpr double kCoalRate = 200.0;                          // gamma(1, 1/200) rate prior: 1 / theta (coal.jl:56-58)
 
 struct CoalArgs {
   const double* events;  // sorted event times
+  const int32_t* bucket; // [kCoalBuckets] start index of the event scan per bucket of [0, T]
   int E;
   double T;              // observation window [0, T]
+  double bscale;         // kCoalBuckets / T
+  double kb;             // log 3 - log T: the score per change point
+  double ktheta;         // -log(theta): the gamma prior's constant per rate
+  double lhalf;          // log 0.5 (the is_birth bernoulli)
   int64_t chain0, n_chains;
   uint64_t seed;
   int n_iters, iter0;
   int init;              // 1: draw the start from the prior (generate)
-  double* state;         // SoA [2][kCoalW][ld]: current row fields, then proposal row fields
+  double* state;         // SoA [kCoalW][ld] rows (k, score, cp[32], h[33], pad); unused fields 0
   int64_t ld;            // chains per field column (>= n_chains)
   int32_t* accepts;      // [n_chains][3] rate, position, birth/death
   int32_t* khist;        // optional [n_chains][n_iters] k after each iteration
 };
 
-// one chain's row (k, score, cp[32], h[33], pad) in the SoA state: field i
-// of chain c at p[i * ld] — a wave's 64 chains read one field coalesced
-struct CoalRow {
-  double* p;
-  int64_t ld;
-  __device__ __forceinline__ double& operator[](int i) const { return p[(int64_t)i * ld]; }
+// the two uniforms of Philox block b of an iteration: u53(x, y), u53(z, w);
+// 1 - u as the exact one_minus_u53 of the same words
+struct CoalU {
+  uint32_t x, y, z, w;
+};
+__device__ __forceinline__ CoalU coal_block(uint64_t seed, uint64_t c, uint32_t step, uint32_t b) {
+  const u32x4 r = rng_block(seed, c, step, STREAM_MH, b);
+  return CoalU{r.x, r.y, r.z, r.w};
+}
+
+// #events <= y: start from the bucket before y's (a lower bound of the
+// count whatever the rounding of y * bscale), scan forward, and step back if
+// the start overshot — exact for any table.
+__device__ __forceinline__ int coal_count(const double* ev, const int32_t* bk, int E, double bscale, double y) {
+  int bi = (int)(y * bscale);
+  bi = bi < 1 ? 0 : (bi > kCoalBuckets ? kCoalBuckets - 1 : bi - 1);
+  int j = bk[bi];
+  while (j < E && ev[j] <= y) ++j;
+  while (j > 0 && ev[j - 1] > y) --j;
+  return j;
+}
+
+// one chain's LDS fields: cp[i - 1] at f(i - 1), h[i - 1] at f(kCoalKMax + i - 1)
+struct CoalLds {
+  double* p;  // wave base + lane
+  __device__ __forceinline__ double& cp(int i) const { return p[(i - 1) * 64]; }              // i = 1..k
+  __device__ __forceinline__ double& h(int i) const { return p[(kCoalKMax + i - 1) * 64]; }  // i = 1..k+1
 };
 
 __device__ __forceinline__ double coal_u(uint64_t seed, uint64_t c, uint32_t step, uint32_t d) {
@@ -52,74 +96,19 @@ __device__ __forceinline__ double coal_u(uint64_t seed, uint64_t c, uint32_t ste
   return u53(w.x, w.y);
 }
 
-// number of events <= x (events sorted, in LDS)
-__device__ __forceinline__ int coal_upper(const double* ev, int E, double x) {
-  int lo = 0, hi = E;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (ev[mid] <= x) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// score of the state row s (coal.jl:47-62 with poisson_process.jl:34-51)
-__device__ double coal_score(const CoalRow& s, const double* ev, int E, double T, const double* tab) {
-  const int k = (int)s[0];
-  const CoalRow cp{s.p + 2 * s.ld, s.ld};
-  const CoalRow h{s.p + (2 + kCoalKMax) * s.ld, s.ld};
-  // k ~ poisson(3): k log 3 - 3 - log k!
-  double lf = 0.0;
-  for (int j = 2; j <= k; ++j) lf += gh_log_unit((double)j, tab);
-  double lp = ((double)k * gh_log(3.0) - 3.0) - lf;
-  // cp_i ~ min_uniform_continuous(cp_{i-1}, T, k - i + 1)
-  double lower = 0.0, l_lower = gh_log(T);
-  for (int i = 1; i <= k; ++i) {
-    const double x = cp[i - 1];
-    if (!(x > lower && x < T)) return -INFINITY;
-    const double m = (double)(k - i + 1);
-    const double l_x = gh_log_unit(T - x, tab);
-    lp += ((m - 1.0) * l_x + gh_log_unit(m, tab)) - m * l_lower;
-    lower = x;
-    l_lower = l_x;
-  }
-  // h_i ~ gamma(1, theta): -log theta - x / theta
-  const double l_theta = gh_log(kCoalTheta);
-  for (int i = 1; i <= k + 1; ++i) {
-    const double x = h[i - 1];
-    if (!(x > 0.0)) return -INFINITY;
-    lp += -l_theta - x / kCoalTheta;
-  }
-  // events ~ piecewise_poisson_process([0, cp..., T], h)
-  double A = 0.0, B = 0.0, b_lo = 0.0;
-  int c_lo = 0;
-  for (int i = 1; i <= k + 1; ++i) {
-    const double b_hi = i <= k ? cp[i - 1] : T;
-    const int c_hi = coal_upper(ev, E, b_hi);
-    A += (double)(c_hi - c_lo) * gh_log_unit(h[i - 1], tab);
-    B += (b_hi - b_lo) * h[i - 1];
-    b_lo = b_hi;
-    c_lo = c_hi;
-  }
-  return lp + (A - B);
-}
-
-__device__ __forceinline__ void coal_copy(const CoalRow& src, const CoalRow& dst) {
-  const int k = (int)src[0];
-  dst[0] = src[0];
-  for (int i = 0; i < k; ++i) dst[2 + i] = src[2 + i];
-  for (int i = 0; i <= k; ++i) dst[2 + kCoalKMax + i] = src[2 + kCoalKMax + i];
-}
-
 // generate(model, (T,), observations): k, change points and rates from the
-// prior (attempt a uses draws 100 a + ...; a degenerate draw retries)
-__device__ void coal_init(const CoalArgs& a, uint64_t c, const CoalRow& s) {
-  for (int att = 0; att < 64; ++att) {
+// prior (attempt a uses draws 100 a + ...; a degenerate draw retries), then
+// the score from scratch.  Returns k.
+__device__ int coal_init(const CoalArgs& a, uint64_t c, const CoalLds& s, const double* ev, const int32_t* bk,
+                         const double* tab, double* score) {
+  int k = 0;
+  bool done = false;
+  for (int att = 0; att < 64 && !done; ++att) {
     const uint32_t d0 = 100u * (uint32_t)att;
     // k ~ poisson(3) by inverse CDF
     const double u = coal_u(a.seed, c, 0, d0);
     double p = gh_exp(-3.0), cum = p;
-    int k = 0;
+    k = 0;
     while (u >= cum && k < 200) {
       ++k;
       p = p * (3.0 / (double)k);
@@ -134,153 +123,211 @@ __device__ void coal_init(const CoalArgs& a, uint64_t c, const CoalRow& s) {
       const double m = (double)(k - i + 1);
       const double x = a.T - (a.T - lower) * gh_exp(gh_log(1.0 - q) / m);
       if (!(x > lower && x < a.T)) ok = false;
-      s[2 + i - 1] = x;
+      s.cp(i) = x;
       lower = x;
     }
     for (int i = 1; i <= k + 1; ++i) {
       // gamma(1, theta) = exponential: -theta log(1 - q)
       const double q = coal_u(a.seed, c, 0, d0 + 40u + (uint32_t)i);
-      const double x = -kCoalTheta * gh_log(1.0 - q);
+      const double x = -gh_log(1.0 - q) / kCoalRate;
       if (!(x > 0.0)) ok = false;
-      s[2 + kCoalKMax + i - 1] = x;
+      s.h(i) = x;
     }
-    if (!ok) continue;
-    s[0] = (double)k;
-    return;
+    done = ok;
   }
-  s[0] = 0.0;  // unreachable in practice: k = 0 with a mean rate
-  s[2 + kCoalKMax] = (double)a.E / a.T;
+  if (!done) {  // unreachable in practice: k = 0 with the mean rate
+    k = 0;
+    s.h(1) = (double)a.E / a.T;
+  }
+  for (int i = k + 1; i <= kCoalKMax; ++i) s.cp(i) = 0.0;
+  for (int i = k + 2; i <= kCoalKMax + 1; ++i) s.h(i) = 0.0;
+  // the score (the decomposition of the header), segment by segment
+  double sc = (double)k * a.kb - 3.0;
+  int n_lo = 0;
+  double b_lo = 0.0;
+  for (int i = 1; i <= k + 1; ++i) {
+    const double b_hi = i <= k ? s.cp(i) : a.T;
+    const int n_hi = i <= k ? coal_count(ev, bk, a.E, a.bscale, b_hi) : a.E;
+    const double h = s.h(i);
+    sc += a.ktheta - h * kCoalRate;
+    sc += (double)(n_hi - n_lo) * gh_log_unit(h, tab) - (b_hi - b_lo) * h;
+    n_lo = n_hi;
+    b_lo = b_hi;
+  }
+  *score = sc;
+  return k;
 }
 
-__global__ __launch_bounds__(256) void k_coal(CoalArgs a) {
-  extern __shared__ double ev[];  // the E event times (dynamic LDS: E doubles)
-  __shared__ double tab[kMathTabDoubles];  // the log table, per-lane reads from LDS
-  load_math_tab(tab);
-  for (int i = threadIdx.x; i < a.E; i += blockDim.x) ev[i] = a.events[i];
+__global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
+  __shared__ double st[kCoalBlock / 64][kCoalF * 64];  // per wave: [field][lane]
+  __shared__ double tab[kMathTabDoubles / 3];          // the log bins (gh_log_unit)
+  extern __shared__ double dyn[];                      // E event times, then the bucket table
+  double* ev = dyn;
+  int32_t* bk = reinterpret_cast<int32_t*>(dyn + a.E);
+  for (int i = threadIdx.x; i < kMathTabDoubles / 3; i += kCoalBlock) tab[i] = gh_math_tab_dev[i];
+  for (int i = threadIdx.x; i < a.E; i += kCoalBlock) ev[i] = a.events[i];
+  for (int i = threadIdx.x; i < kCoalBuckets; i += kCoalBlock) bk[i] = a.bucket[i];
   __syncthreads();
-  const int64_t cl = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (cl >= a.n_chains) return;
+  const int64_t cl = (int64_t)blockIdx.x * kCoalBlock + threadIdx.x;
+  if (cl >= a.n_chains) return;  // no block barrier below
+  const int lane = threadIdx.x & 63;
+  const CoalLds s{&st[threadIdx.x >> 6][lane]};
   const uint64_t c = (uint64_t)(a.chain0 + cl);
-  const CoalRow cur{a.state + cl, a.ld};
-  const CoalRow prop{a.state + kCoalW * a.ld + cl, a.ld};
   const double T = a.T;
+  const double* g = a.state + cl;  // field f at g[f * ld]
+  int k;
+  double score;
   if (a.init) {
-    coal_init(a, c, cur);
-    cur[1] = coal_score(cur, ev, a.E, T, tab);
+    k = coal_init(a, c, s, ev, bk, tab, &score);
+  } else {
+    k = (int)g[0];
+    score = g[a.ld];
+#pragma unroll 5
+    for (int f = 0; f < kCoalF; ++f) s.p[f * 64] = g[(2 + f) * a.ld];
   }
   int acc[3] = {0, 0, 0};
   for (int it = 0; it < a.n_iters; ++it) {
     const uint32_t step = (uint32_t)(a.iter0 + it + 1);
-    // ---- rate move (coal.jl:126-150)
+    const CoalU B0 = coal_block(a.seed, c, step, 0);
+    const CoalU B1 = coal_block(a.seed, c, step, 1);
+    // ---- rate move (coal.jl:103-134): segment i's rate h -> nh ~ U(h/2, 2h)
     {
-      const int k = (int)cur[0];
-      const double ui = coal_u(a.seed, c, step, 0);
-      const int i = (int)(ui * (double)(k + 1)) + 1;  // uniform_discrete(1, k+1)
-      const double h = cur[2 + kCoalKMax + i - 1];
-      const double lo = h / 2.0, hi = h * 2.0;
-      const double nh = lo + (hi - lo) * coal_u(a.seed, c, step, 1);
-      coal_copy(cur, prop);
-      prop[2 + kCoalKMax + i - 1] = nh;
-      const double sn = coal_score(prop, ev, a.E, T, tab);
-      const double fwd = -gh_log((double)(k + 1)) - gh_log(hi - lo);
-      const double bwd = -gh_log((double)(k + 1)) - gh_log(nh * 2.0 - nh / 2.0);
-      const double alpha = ((sn - cur[1]) + bwd) - fwd;
-      if (gh_log(coal_u(a.seed, c, step, 2)) < alpha) {
-        cur[2 + kCoalKMax + i - 1] = nh;
-        cur[1] = sn;
+      const int i = (int)(u53(B0.x, B0.y) * (double)(k + 1)) + 1;  // uniform_discrete(1, k+1)
+      const double h = s.h(i);
+      const double lo = h * 0.5, hi = h * 2.0;
+      const double nh = lo + (hi - lo) * u53(B0.z, B0.w);
+      const double b_lo = i == 1 ? 0.0 : s.cp(i - 1);
+      const double b_hi = i == k + 1 ? T : s.cp(i);
+      const int n_lo = i == 1 ? 0 : coal_count(ev, bk, a.E, a.bscale, b_lo);
+      const int n_hi = i == k + 1 ? a.E : coal_count(ev, bk, a.E, a.bscale, b_hi);
+      const double dh = nh - h;
+      const double delta =
+          ((double)(n_hi - n_lo) * (gh_log_unit(nh, tab) - gh_log_unit(h, tab)) - (b_hi - b_lo) * dh) - dh * kCoalRate;
+      // fwd - bwd: the uniform_discrete terms cancel; the new_rate densities
+      const double alpha = delta + (gh_log_unit(hi - lo, tab) - gh_log_unit(nh * 2.0 - nh * 0.5, tab));
+      if (gh_log_unit(one_minus_u53(B1.x, B1.y), tab) < alpha) {
+        s.h(i) = nh;
+        score += delta;
         acc[0] += 1;
       }
     }
-    // ---- position move (coal.jl:156-184), if k > 0
-    if ((int)cur[0] > 0) {
-      const int k = (int)cur[0];
-      const int i = (int)(coal_u(a.seed, c, step, 3) * (double)k) + 1;  // uniform_discrete(1, k)
-      const double lower = i == 1 ? 0.0 : cur[2 + i - 2];
-      const double upper = i == k ? T : cur[2 + i];
-      const double ncp = lower + (upper - lower) * coal_u(a.seed, c, step, 4);
-      coal_copy(cur, prop);
-      prop[2 + i - 1] = ncp;
-      const double sn = coal_score(prop, ev, a.E, T, tab);
-      const double fwd = -gh_log((double)k) - gh_log(upper - lower);
-      const double bwd = fwd;  // the neighbours bound both proposals
-      const double alpha = ((sn - cur[1]) + bwd) - fwd;
-      if (gh_log(coal_u(a.seed, c, step, 5)) < alpha) {
-        cur[2 + i - 1] = ncp;
-        cur[1] = sn;
+    // ---- position move (coal.jl:140-167), if k > 0: cp_i -> U(cp_{i-1}, cp_{i+1})
+    if (k > 0) {
+      const CoalU B2 = coal_block(a.seed, c, step, 2);
+      const int i = (int)(u53(B1.z, B1.w) * (double)k) + 1;  // uniform_discrete(1, k)
+      const double lower = i == 1 ? 0.0 : s.cp(i - 1);
+      const double upper = i == k ? T : s.cp(i + 1);
+      const double x = s.cp(i);
+      const double nx = lower + (upper - lower) * u53(B2.x, B2.y);
+      double alpha = -INFINITY, delta = 0.0;
+      if (nx > lower && nx < upper) {
+        const double hi_ = s.h(i), hn = s.h(i + 1);
+        const int dc = coal_count(ev, bk, a.E, a.bscale, nx) - coal_count(ev, bk, a.E, a.bscale, x);
+        delta = (double)dc * (gh_log_unit(hi_, tab) - gh_log_unit(hn, tab)) - (nx - x) * (hi_ - hn);
+        alpha = delta;  // the neighbours bound both proposals: fwd == bwd
+      }
+      if (gh_log_unit(one_minus_u53(B2.z, B2.w), tab) < alpha) {
+        s.cp(i) = nx;
+        score += delta;
         acc[1] += 1;
       }
     }
-    // ---- birth / death move (coal.jl:190-318)
+    // ---- birth / death move (coal.jl:173-318)
     {
-      const int k = (int)cur[0];
-      const bool birth = k == 0 || coal_u(a.seed, c, step, 6) < 0.5;
-      double alpha = -INFINITY, sn = -INFINITY;
+      const CoalU B3 = coal_block(a.seed, c, step, 3);
+      const CoalU B4 = coal_block(a.seed, c, step, 4);
+      const bool birth = k == 0 || u53(B3.x, B3.y) < 0.5;
+      double alpha = -INFINITY, delta = 0.0;
+      int i = 0;
+      double x = 0.0, hp = 0.0, hn = 0.0, h = 0.0;
       if (birth) {
-        const int i = (int)(coal_u(a.seed, c, step, 7) * (double)(k + 1)) + 1;  // CHOSEN
-        const double lower = i == 1 ? 0.0 : cur[2 + i - 2];
-        const double upper = i == k + 1 ? T : cur[2 + i - 1];
-        const double ncp = lower + (upper - lower) * coal_u(a.seed, c, step, 8);
-        const double uu = coal_u(a.seed, c, step, 9);
-        const double d_prev = ncp - lower, d_next = upper - ncp;
+        i = (int)(u53(B3.z, B3.w) * (double)(k + 1)) + 1;  // CHOSEN: segment to split
+        const double lower = i == 1 ? 0.0 : s.cp(i - 1);
+        const double upper = i == k + 1 ? T : s.cp(i);
+        x = lower + (upper - lower) * u53(B4.x, B4.y);
+        const double uu = u53(B4.z, B4.w);
+        const double d_prev = x - lower, d_next = upper - x;
         if (k < kCoalKMax && d_prev > 0.0 && d_next > 0.0 && uu > 0.0) {
-          // new_rates (coal.jl:222-235)
-          const double h = cur[2 + kCoalKMax + i - 1];
+          // new_rates (coal.jl:211-223)
+          h = s.h(i);
           const double d_total = d_prev + d_next;
-          const double lr = gh_log(1.0 - uu) - gh_log(uu);
-          const double hp = gh_exp(gh_log(h) - (d_next / d_total) * lr);
-          const double hn = gh_exp(gh_log(h) + (d_prev / d_total) * lr);
-          // birth(k, i) (coal.jl:273-297): insert cp at i, rates (hp, hn) at (i, i+1)
-          prop[0] = (double)(k + 1);
-          for (int j = 1; j < i; ++j) prop[2 + j - 1] = cur[2 + j - 1];
-          prop[2 + i - 1] = ncp;
-          for (int j = i + 1; j <= k + 1; ++j) prop[2 + j - 1] = cur[2 + j - 2];
-          for (int j = 1; j < i; ++j) prop[2 + kCoalKMax + j - 1] = cur[2 + kCoalKMax + j - 1];
-          prop[2 + kCoalKMax + i - 1] = hp;
-          prop[2 + kCoalKMax + i] = hn;
-          for (int j = i + 2; j <= k + 2; ++j) prop[2 + kCoalKMax + j - 1] = cur[2 + kCoalKMax + j - 2];
-          sn = coal_score(prop, ev, a.E, T, tab);
-          const double fwd = ((k > 0 ? gh_log(0.5) : 0.0) - gh_log((double)(k + 1))) - gh_log(upper - lower);
-          const double bwd = gh_log(0.5) - gh_log((double)(k + 1));
-          const double logj = 2.0 * gh_log(hp + hn) - gh_log(h);
-          alpha = (((sn - cur[1]) + bwd) - fwd) + logj;
+          const double lh = gh_log_unit(h, tab);
+          const double lr = gh_log_unit(one_minus_u53(B4.z, B4.w), tab) - gh_log_unit(uu, tab);
+          hp = gh_exp(lh - (d_next / d_total) * lr);
+          hn = gh_exp(lh + (d_prev / d_total) * lr);
+          const int n_lo = i == 1 ? 0 : coal_count(ev, bk, a.E, a.bscale, lower);
+          const int n_hi = i == k + 1 ? a.E : coal_count(ev, bk, a.E, a.bscale, upper);
+          const int n_x = coal_count(ev, bk, a.E, a.bscale, x);
+          const double lhp = gh_log_unit(hp, tab), lhn = gh_log_unit(hn, tab);
+          delta = ((a.kb + a.ktheta) - ((hp + hn) - h) * kCoalRate) +
+                  (((double)(n_x - n_lo) * lhp + (double)(n_hi - n_x) * lhn) - (double)(n_hi - n_lo) * lh) -
+                  ((d_prev * hp + d_next * hn) - (upper - lower) * h);
+          const double fwd = ((k > 0 ? a.lhalf : 0.0) - gh_log_unit((double)(k + 1), tab)) -
+                             gh_log_unit(upper - lower, tab);
+          const double bwd = a.lhalf - gh_log_unit((double)(k + 1), tab);
+          const double logj = 2.0 * gh_log_unit(hp + hn, tab) - lh;
+          alpha = ((delta + bwd) - fwd) + logj;
         }
       } else {
-        const int i = (int)(coal_u(a.seed, c, step, 7) * (double)k) + 1;  // CHOSEN
-        const double cpd = cur[2 + i - 1];
-        const double lower = i == 1 ? 0.0 : cur[2 + i - 2];
-        const double upper = i == k ? T : cur[2 + i];
-        const double d_prev = cpd - lower, d_next = upper - cpd;
+        i = (int)(u53(B3.z, B3.w) * (double)k) + 1;  // CHOSEN: change point to delete
+        x = s.cp(i);
+        const double lower = i == 1 ? 0.0 : s.cp(i - 1);
+        const double upper = i == k ? T : s.cp(i + 1);
+        const double d_prev = x - lower, d_next = upper - x;
         if (d_prev > 0.0 && d_next > 0.0) {
-          // new_rates_inverse (coal.jl:237-250)
-          const double hp = cur[2 + kCoalKMax + i - 1], hn = cur[2 + kCoalKMax + i];
+          // new_rates_inverse (coal.jl:225-238)
+          hp = s.h(i);
+          hn = s.h(i + 1);
           const double d_total = d_prev + d_next;
-          const double h = gh_exp((d_prev / d_total) * gh_log(hp) + (d_next / d_total) * gh_log(hn));
-          // death(k, i) (coal.jl:299-318): remove cp i, rate h at i
-          prop[0] = (double)(k - 1);
-          for (int j = 1; j < i; ++j) prop[2 + j - 1] = cur[2 + j - 1];
-          for (int j = i; j <= k - 1; ++j) prop[2 + j - 1] = cur[2 + j];
-          for (int j = 1; j < i; ++j) prop[2 + kCoalKMax + j - 1] = cur[2 + kCoalKMax + j - 1];
-          prop[2 + kCoalKMax + i - 1] = h;
-          for (int j = i + 1; j <= k; ++j) prop[2 + kCoalKMax + j - 1] = cur[2 + kCoalKMax + j];
-          sn = coal_score(prop, ev, a.E, T, tab);
-          const double fwd = gh_log(0.5) - gh_log((double)k);
-          const double bwd = ((k - 1 > 0 ? gh_log(0.5) : 0.0) - gh_log((double)k)) - gh_log(upper - lower);
-          const double logj = gh_log(h) - 2.0 * gh_log(hp + hn);
-          alpha = (((sn - cur[1]) + bwd) - fwd) + logj;
+          const double lhp = gh_log_unit(hp, tab), lhn = gh_log_unit(hn, tab);
+          h = gh_exp((d_prev / d_total) * lhp + (d_next / d_total) * lhn);
+          const double lh = gh_log_unit(h, tab);
+          const int n_lo = i == 1 ? 0 : coal_count(ev, bk, a.E, a.bscale, lower);
+          const int n_hi = i == k ? a.E : coal_count(ev, bk, a.E, a.bscale, upper);
+          const int n_x = coal_count(ev, bk, a.E, a.bscale, x);
+          delta = (-(a.kb + a.ktheta) - (h - (hp + hn)) * kCoalRate) +
+                  ((double)(n_hi - n_lo) * lh - ((double)(n_x - n_lo) * lhp + (double)(n_hi - n_x) * lhn)) -
+                  ((upper - lower) * h - (d_prev * hp + d_next * hn));
+          const double fwd = a.lhalf - gh_log_unit((double)k, tab);
+          const double bwd = ((k - 1 > 0 ? a.lhalf : 0.0) - gh_log_unit((double)k, tab)) -
+                             gh_log_unit(upper - lower, tab);
+          const double logj = lh - 2.0 * gh_log_unit(hp + hn, tab);
+          alpha = ((delta + bwd) - fwd) + logj;
         }
       }
-      if (gh_log(coal_u(a.seed, c, step, 10)) < alpha) {
-        coal_copy(prop, cur);
-        cur[1] = sn;
+      const CoalU B5 = coal_block(a.seed, c, step, 5);
+      if (gh_log_unit(one_minus_u53(B5.x, B5.y), tab) < alpha) {
+        if (birth) {  // birth(k, i) (coal.jl:260-283): insert cp at i, rates (hp, hn) at (i, i+1)
+          for (int j = k; j >= i; --j) s.cp(j + 1) = s.cp(j);
+          s.cp(i) = x;
+          for (int j = k + 1; j >= i + 1; --j) s.h(j + 1) = s.h(j);
+          s.h(i) = hp;
+          s.h(i + 1) = hn;
+          k += 1;
+        } else {  // death(k, i) (coal.jl:285-305): remove cp i, rate h at i
+          for (int j = i; j <= k - 1; ++j) s.cp(j) = s.cp(j + 1);
+          s.cp(k) = 0.0;
+          s.h(i) = h;
+          for (int j = i + 1; j <= k; ++j) s.h(j) = s.h(j + 1);
+          s.h(k + 1) = 0.0;
+          k -= 1;
+        }
+        score += delta;
         acc[2] += 1;
       }
     }
-    if (a.khist) a.khist[cl * a.n_iters + it] = (int32_t)cur[0];
+    if (a.khist) a.khist[cl * a.n_iters + it] = (int32_t)k;
   }
+  double* gw = a.state + cl;
+  gw[0] = (double)k;
+  gw[a.ld] = score;
+#pragma unroll 5
+  for (int f = 0; f < kCoalF; ++f) gw[(2 + f) * a.ld] = s.p[f * 64];
+  gw[(kCoalW - 1) * a.ld] = 0.0;
   for (int m = 0; m < 3; ++m) a.accepts[cl * 3 + m] = acc[m];
 }
 
-// AoS rows [n][kCoalW] (the host layout) <-> SoA current fields [kCoalW][ld]
+// AoS rows [n][kCoalW] (the host layout) <-> SoA fields [kCoalW][ld]
 __global__ void k_coal_rows(double* soa, int64_t ld, double* aos, int64_t n, int to_soa) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n * kCoalW) return;

@@ -1083,9 +1083,22 @@ int orc_importance_sampling(int family, int d, int dy, int k, int v, const doubl
 
 /* ----------------------------------------------------------------- PMMH */
 /* Particle-marginal MH over the Kitagawa model (examples/pmmh/example.jl:
-   20-79 with the ParticleFilterCombinator of examples/pmmh/pf.jl:14-73 and
-   mh.jl:14-62).  Random-number layout and move order: gen_amd/csrc/gh_pmmh.h
-   (DESIGN.md §9). */
+   20-79).  The likelihood term is the ParticleFilterCombinator of
+   examples/pmmh/pf.jl:14-73: generate/update/regenerate of the :hmm call run a
+   particle filter (initialize_particle_filter, then {maybe_resample!;
+   particle_filter_step!} for t = 2..T, pf.jl:40-56, with maybe_resample! at
+   ESS < N/2 and systematic integer resampling as everywhere here) over the
+   model of example.jl:5-22 / model.jl:9-13 (x_1 ~ normal(0, 5); x_t ~
+   normal(x_mean(x_{t-1}, t), sqrt(var_x)); y_t ~ normal(x_t^2 / 20,
+   sqrt(var_y))) and return its log_ml_estimate as the weight
+   (pf.jl:58-73).  do_inference (example.jl:64-79): each iteration applies
+   mh(select(:var_x)), mh(select(:var_y)) — regenerate from the normal(0, 2)
+   prior, weight = new log-ML - old (mh.jl:14-28) — and the random walks
+   mh(tr, var_x_proposal) / var_y_proposal, normal(cur, sqrt(0.5)), weight =
+   prior ratio + log-ML ratio, alpha = weight - fwd + bwd (mh.jl:41-62).
+   Randomness: move counter u (0 = generate, 1 + 4 iter + m), particle id
+   (u << 32) | (chain << 10) | p.  tests/test_pmmh.py checks
+   the inner estimate against the PF oracle (run_pf) on the same model. */
 static double pmmh_filter(uint64_t seed, uint64_t c, uint32_t u, double lvx, double lvy, int N,
                           const double* ys, const double* ct, int T, double* x, double* lw, double* xp,
                           uint64_t* C) {
@@ -1142,6 +1155,20 @@ static double pmmh_filter(uint64_t seed, uint64_t c, uint32_t u, double lvx, dou
   for (int p = 0; p < N; ++p) M = fmax(M, lw[p]);
   for (int p = 0; p < N; ++p) S += lw[p] > -INFINITY ? orc_exp(lw[p] - M) : 0.0;
   return log_ml + (M + orc_log(S)) - logN;
+}
+
+double orc_pmmh_loglik(uint64_t seed, uint64_t chain, uint32_t u, double lvx, double lvy, int n_inner,
+                       const double* ys, int T) {
+  if (n_inner < 1 || n_inner > 1024 || T < 1) return NAN;
+  double* x = malloc(sizeof(double) * n_inner);
+  double* lw = malloc(sizeof(double) * n_inner);
+  double* xp = malloc(sizeof(double) * n_inner);
+  uint64_t* C = malloc(sizeof(uint64_t) * n_inner);
+  double* ct = malloc(sizeof(double) * T);
+  for (int t = 1; t <= T; ++t) ct[t - 1] = 8.0 * orc_cos(1.2 * (double)t);
+  double ml = pmmh_filter(seed, chain, u, lvx, lvy, n_inner, ys, ct, T, x, lw, xp, C);
+  free(x); free(lw); free(xp); free(C); free(ct);
+  return ml;
 }
 
 int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T, int n_iters,
@@ -1206,74 +1233,101 @@ int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys
 }
 
 /* ------------------------------------------------------------------ coal */
-/* Reversible-jump MH on the coal change-point model (config C3): a plain
-   restatement of gen_amd/csrc/gh_coal.h (which cites examples/coal/coal.jl
-   and poisson_process.jl line by line); spec DESIGN.md §7c. */
+/* Reversible-jump MH on the coal change-point model (config C3), following
+   examples/coal/coal.jl: the model (:47-62) with k ~ poisson(3) change points
+   placed by min_uniform_continuous (:18-33), gamma(1, 1/200) rates and the
+   piecewise Poisson process of poisson_process.jl:32-51 over the events;
+   mcmc_step (:329-336) = rate_move (:103-134), position_move (:140-167) when
+   k > 0, birth_death_move (:173-318), each metropolis_hastings with an
+   involution (src/inference/mh.jl:85-98; weight = new score - old score +
+   bwd score - fwd score + log|J|, trace_translators.jl:848-876), the birth
+   Jacobian in closed form |J| = (h_prev + h_next)^2 / h (coal.jl:211-238's
+   new_rates differentiated; the reference uses ForwardDiff).
+
+   Score of (k, cp[1..k], h[1..k+1]), b_0 = 0, b_{k+1} = T, c_i the events in
+   segment i = (b_{i-1}, b_i] (segment 1 also holds the event at 0):
+     logpdf(poisson(3), k) + sum_i logpdf(min_uniform_continuous(cp_{i-1}, T,
+     k - i + 1), cp_i) + sum_i logpdf(gamma(1, 1/200), h_i)
+     + logpdf(piecewise_poisson_process(b, h), events)
+   = k (log 3 - log T) - 3 + sum_i [log 200 - 200 h_i] + sum_i [c_i log h_i - len_i h_i]
+   (the order statistics telescope to log k! - k log T; log k! cancels the
+   Poisson's).  Moves are scored by their difference (one or two segments).
+   tests/test_coal_pins.py checks the score against the reference formulas
+   term by term (scipy Poisson / gamma, the min_uniform density, the
+   piecewise process) and every move's acceptance ratio against an
+   independent Python involution with a finite-difference Jacobian.
+   Random numbers: iteration s of chain c uses Philox blocks b = 0..5 of
+   (seed, c, s, S_MH, b), two 53-bit uniforms per block; the
+   GPU kernel gen_amd/csrc/gh_coal.h computes the same arithmetic. */
 #define COAL_KMAX 32
 #define COAL_W 68
-#define COAL_THETA (1.0 / 200.0)
+#define COAL_RATE 200.0
+#define COAL_BUCKETS 256
 
 static double coal_u(uint64_t seed, uint64_t c, uint32_t step, uint32_t d) {
   uint32_t w[4];
   rng(seed, c, step, S_MH, d, w);
   return unif53(w[0], w[1]);
 }
+static double one_minus53(uint32_t a, uint32_t b) {
+  uint32_t hi = a >> 11, lo = ((a << 21) & 0xFC000000u) | (b >> 6);
+  return fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0));
+}
 
-static int coal_upper(const double* ev, int E, double x) {
+/* #events <= x (events sorted) */
+static int coal_count(const double* ev, int E, double x) {
   int lo = 0, hi = E;
   while (lo < hi) { int mid = (lo + hi) >> 1; if (ev[mid] <= x) lo = mid + 1; else hi = mid; }
   return lo;
 }
 
-static double coal_score(const double* s, const double* ev, int E, double T) {
-  int k = (int)s[0];
-  const double* cp = s + 2;
-  const double* h = s + 2 + COAL_KMAX;
-  double lf = 0.0;
-  for (int j = 2; j <= k; ++j) lf += orc_log_unit((double)j);
-  double lp = ((double)k * orc_log(3.0) - 3.0) - lf;
-  double lower = 0.0, l_lower = orc_log(T);
-  for (int i = 1; i <= k; ++i) {
-    double x = cp[i - 1];
-    if (!(x > lower && x < T)) return -INFINITY;
-    double m = (double)(k - i + 1);
-    double l_x = orc_log_unit(T - x);
-    lp += ((m - 1.0) * l_x + orc_log_unit(m)) - m * l_lower;
-    lower = x;
-    l_lower = l_x;
+typedef struct { double T, kb, ktheta, lhalf; const double* ev; int E; } coal_m;
+static coal_m coal_model(const double* ev, int E) {
+  coal_m m;
+  m.T = ev[E - 1];
+  m.kb = orc_log(3.0) - orc_log(m.T);
+  m.ktheta = orc_log(COAL_RATE);
+  m.lhalf = orc_log(0.5);
+  m.ev = ev;
+  m.E = E;
+  return m;
+}
+
+/* the score of a row (k, score, cp[32], h[33], pad) from scratch */
+static double coal_score(const coal_m* M, const double* row) {
+  int k = (int)row[0];
+  const double* cp = row + 2;
+  const double* h = row + 2 + COAL_KMAX;
+  double lower = 0.0;
+  for (int i = 0; i < k; ++i) {
+    if (!(cp[i] > lower && cp[i] < M->T)) return -INFINITY;
+    lower = cp[i];
   }
-  double l_theta = orc_log(COAL_THETA);
+  for (int i = 0; i <= k; ++i)
+    if (!(h[i] > 0.0)) return -INFINITY;
+  double sc = (double)k * M->kb - 3.0;
+  int n_lo = 0;
+  double b_lo = 0.0;
   for (int i = 1; i <= k + 1; ++i) {
-    double x = h[i - 1];
-    if (!(x > 0.0)) return -INFINITY;
-    lp += -l_theta - x / COAL_THETA;
-  }
-  double A = 0.0, B = 0.0, b_lo = 0.0;
-  int c_lo = 0;
-  for (int i = 1; i <= k + 1; ++i) {
-    double b_hi = i <= k ? cp[i - 1] : T;
-    int c_hi = coal_upper(ev, E, b_hi);
-    A += (double)(c_hi - c_lo) * orc_log_unit(h[i - 1]);
-    B += (b_hi - b_lo) * h[i - 1];
+    double b_hi = i <= k ? cp[i - 1] : M->T;
+    int n_hi = i <= k ? coal_count(M->ev, M->E, b_hi) : M->E;
+    double hh = h[i - 1];
+    sc += M->ktheta - hh * COAL_RATE;
+    sc += (double)(n_hi - n_lo) * orc_log_unit(hh) - (b_hi - b_lo) * hh;
+    n_lo = n_hi;
     b_lo = b_hi;
-    c_lo = c_hi;
   }
-  return lp + (A - B);
+  return sc;
 }
 
-static void coal_copy(const double* src, double* dst) {
-  int k = (int)src[0];
-  dst[0] = src[0];
-  for (int i = 0; i < k; ++i) dst[2 + i] = src[2 + i];
-  for (int i = 0; i <= k; ++i) dst[2 + COAL_KMAX + i] = src[2 + COAL_KMAX + i];
-}
-
-static void coal_init(uint64_t seed, uint64_t c, double T, int E, double* s) {
-  for (int att = 0; att < 64; ++att) {
+static int coal_init(uint64_t seed, uint64_t c, const coal_m* M, double* s) {
+  double T = M->T;
+  int k = 0, done = 0;
+  for (int att = 0; att < 64 && !done; ++att) {
     uint32_t d0 = 100u * (uint32_t)att;
     double u = coal_u(seed, c, 0, d0);
     double p = orc_exp(-3.0), cum = p;
-    int k = 0;
+    k = 0;
     while (u >= cum && k < 200) { ++k; p = p * (3.0 / (double)k); cum += p; }
     if (k > COAL_KMAX) continue;
     int ok = 1;
@@ -1288,117 +1342,180 @@ static void coal_init(uint64_t seed, uint64_t c, double T, int E, double* s) {
     }
     for (int i = 1; i <= k + 1; ++i) {
       double q = coal_u(seed, c, 0, d0 + 40u + (uint32_t)i);
-      double x = -COAL_THETA * orc_log(1.0 - q);
+      double x = -orc_log(1.0 - q) / COAL_RATE;
       if (!(x > 0.0)) ok = 0;
       s[2 + COAL_KMAX + i - 1] = x;
     }
-    if (!ok) continue;
-    s[0] = (double)k;
-    return;
+    done = ok;
   }
-  s[0] = 0.0;
-  s[2 + COAL_KMAX] = (double)E / T;
+  if (!done) { k = 0; s[2 + COAL_KMAX] = (double)M->E / T; }
+  for (int i = k + 1; i <= COAL_KMAX; ++i) s[2 + i - 1] = 0.0;
+  for (int i = k + 2; i <= COAL_KMAX + 1; ++i) s[2 + COAL_KMAX + i - 1] = 0.0;
+  s[0] = (double)k;
+  s[COAL_W - 1] = 0.0;
+  s[1] = coal_score(M, s);
+  return k;
+}
+
+enum { COAL_RATE_MOVE = 0, COAL_POSITION = 1, COAL_BIRTH = 2, COAL_DEATH = 3 };
+
+/* One move's proposal on row s with its uniforms u[] (rate: segment, new rate;
+   position: change point, new position; birth: segment, position, u, and
+   u1m = 1 - u exactly; death: change point).  Writes the proposed row to out
+   (score updated by the difference) and returns alpha (-inf: invalid). */
+static double coal_propose(const coal_m* M, const double* s, int move, const double* u, double u1m, double* out) {
+  const double T = M->T;
+  const double* cp = s + 2;
+  const double* h = s + 2 + COAL_KMAX;
+  int k = (int)s[0];
+  memcpy(out, s, sizeof(double) * COAL_W);
+  double* ocp = out + 2;
+  double* oh = out + 2 + COAL_KMAX;
+  if (move == COAL_RATE_MOVE) {
+    int i = (int)(u[0] * (double)(k + 1)) + 1;
+    double hh = h[i - 1];
+    double lo = hh * 0.5, hi = hh * 2.0;
+    double nh = lo + (hi - lo) * u[1];
+    double b_lo = i == 1 ? 0.0 : cp[i - 2];
+    double b_hi = i == k + 1 ? T : cp[i - 1];
+    int n_lo = i == 1 ? 0 : coal_count(M->ev, M->E, b_lo);
+    int n_hi = i == k + 1 ? M->E : coal_count(M->ev, M->E, b_hi);
+    double dh = nh - hh;
+    double delta = ((double)(n_hi - n_lo) * (orc_log_unit(nh) - orc_log_unit(hh)) - (b_hi - b_lo) * dh) - dh * COAL_RATE;
+    oh[i - 1] = nh;
+    out[1] = s[1] + delta;
+    return delta + (orc_log_unit(hi - lo) - orc_log_unit(nh * 2.0 - nh * 0.5));
+  }
+  if (move == COAL_POSITION) {
+    if (k < 1) return -INFINITY;
+    int i = (int)(u[0] * (double)k) + 1;
+    double lower = i == 1 ? 0.0 : cp[i - 2];
+    double upper = i == k ? T : cp[i];
+    double x = cp[i - 1];
+    double nx = lower + (upper - lower) * u[1];
+    if (!(nx > lower && nx < upper)) return -INFINITY;
+    double hi_ = h[i - 1], hn = h[i];
+    int dc = coal_count(M->ev, M->E, nx) - coal_count(M->ev, M->E, x);
+    double delta = (double)dc * (orc_log_unit(hi_) - orc_log_unit(hn)) - (nx - x) * (hi_ - hn);
+    ocp[i - 1] = nx;
+    out[1] = s[1] + delta;
+    return delta;
+  }
+  if (move == COAL_BIRTH) {
+    int i = (int)(u[0] * (double)(k + 1)) + 1;
+    double lower = i == 1 ? 0.0 : cp[i - 2];
+    double upper = i == k + 1 ? T : cp[i - 1];
+    double x = lower + (upper - lower) * u[1];
+    double uu = u[2];
+    double d_prev = x - lower, d_next = upper - x;
+    if (!(k < COAL_KMAX && d_prev > 0.0 && d_next > 0.0 && uu > 0.0)) return -INFINITY;
+    double hh = h[i - 1];
+    double d_total = d_prev + d_next;
+    double lh = orc_log_unit(hh);
+    double lr = orc_log_unit(u1m) - orc_log_unit(uu);
+    double hp = orc_exp(lh - (d_next / d_total) * lr);
+    double hn = orc_exp(lh + (d_prev / d_total) * lr);
+    int n_lo = i == 1 ? 0 : coal_count(M->ev, M->E, lower);
+    int n_hi = i == k + 1 ? M->E : coal_count(M->ev, M->E, upper);
+    int n_x = coal_count(M->ev, M->E, x);
+    double lhp = orc_log_unit(hp), lhn = orc_log_unit(hn);
+    double delta = ((M->kb + M->ktheta) - ((hp + hn) - hh) * COAL_RATE) +
+                   (((double)(n_x - n_lo) * lhp + (double)(n_hi - n_x) * lhn) - (double)(n_hi - n_lo) * lh) -
+                   ((d_prev * hp + d_next * hn) - (upper - lower) * hh);
+    double fwd = ((k > 0 ? M->lhalf : 0.0) - orc_log_unit((double)(k + 1))) - orc_log_unit(upper - lower);
+    double bwd = M->lhalf - orc_log_unit((double)(k + 1));
+    double logj = 2.0 * orc_log_unit(hp + hn) - lh;
+    /* birth(k, i) (coal.jl:260-283): insert cp at i, rates (hp, hn) at (i, i + 1) */
+    for (int j = k; j >= i; --j) ocp[j] = cp[j - 1];
+    ocp[i - 1] = x;
+    for (int j = k + 1; j >= i + 1; --j) oh[j] = h[j - 1];
+    oh[i - 1] = hp;
+    oh[i] = hn;
+    out[0] = (double)(k + 1);
+    out[1] = s[1] + delta;
+    return ((delta + bwd) - fwd) + logj;
+  }
+  /* death */
+  if (k < 1) return -INFINITY;
+  int i = (int)(u[0] * (double)k) + 1;
+  double x = cp[i - 1];
+  double lower = i == 1 ? 0.0 : cp[i - 2];
+  double upper = i == k ? T : cp[i];
+  double d_prev = x - lower, d_next = upper - x;
+  if (!(d_prev > 0.0 && d_next > 0.0)) return -INFINITY;
+  double hp = h[i - 1], hn = h[i];
+  double d_total = d_prev + d_next;
+  double lhp = orc_log_unit(hp), lhn = orc_log_unit(hn);
+  double hh = orc_exp((d_prev / d_total) * lhp + (d_next / d_total) * lhn);
+  double lh = orc_log_unit(hh);
+  int n_lo = i == 1 ? 0 : coal_count(M->ev, M->E, lower);
+  int n_hi = i == k ? M->E : coal_count(M->ev, M->E, upper);
+  int n_x = coal_count(M->ev, M->E, x);
+  double delta = (-(M->kb + M->ktheta) - (hh - (hp + hn)) * COAL_RATE) +
+                 ((double)(n_hi - n_lo) * lh - ((double)(n_x - n_lo) * lhp + (double)(n_hi - n_x) * lhn)) -
+                 ((upper - lower) * hh - (d_prev * hp + d_next * hn));
+  double fwd = M->lhalf - orc_log_unit((double)k);
+  double bwd = ((k - 1 > 0 ? M->lhalf : 0.0) - orc_log_unit((double)k)) - orc_log_unit(upper - lower);
+  double logj = lh - 2.0 * orc_log_unit(hp + hn);
+  /* death(k, i) (coal.jl:285-305): remove cp i, rate h at i */
+  for (int j = i; j <= k - 1; ++j) ocp[j - 1] = cp[j];
+  ocp[k - 1] = 0.0;
+  oh[i - 1] = hh;
+  for (int j = i + 1; j <= k; ++j) oh[j - 1] = h[j];
+  oh[k] = 0.0;
+  out[0] = (double)(k - 1);
+  out[1] = s[1] + delta;
+  return ((delta + bwd) - fwd) + logj;
+}
+
+double orc_coal_score(const double* row, const double* ev, int E) {
+  coal_m M = coal_model(ev, E);
+  return coal_score(&M, row);
+}
+
+double orc_coal_propose(const double* row, const double* ev, int E, int move, const double* u, double* out) {
+  coal_m M = coal_model(ev, E);
+  return coal_propose(&M, row, move, u, 1.0 - u[2], out);
 }
 
 int orc_coal_run(int64_t chain0, int64_t n_chains, const double* ev, int E, int n_iters, int iter0,
                  uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist) {
   if (E < 1) return 1;
-  double T = ev[E - 1];
+  coal_m M = coal_model(ev, E);
   double prop[COAL_W];
   for (int64_t cl = 0; cl < n_chains; ++cl) {
     uint64_t c = (uint64_t)(chain0 + cl);
     double* cur = state + cl * COAL_W;
     if (init) {
       memset(cur, 0, sizeof(double) * COAL_W);
-      coal_init(seed, c, T, E, cur);
-      cur[1] = coal_score(cur, ev, E, T);
+      coal_init(seed, c, &M, cur);
     }
     int acc[3] = {0, 0, 0};
     for (int it = 0; it < n_iters; ++it) {
       uint32_t step = (uint32_t)(iter0 + it + 1);
-      { /* rate move */
-        int k = (int)cur[0];
-        int i = (int)(coal_u(seed, c, step, 0) * (double)(k + 1)) + 1;
-        double h = cur[2 + COAL_KMAX + i - 1];
-        double lo = h / 2.0, hi = h * 2.0;
-        double nh = lo + (hi - lo) * coal_u(seed, c, step, 1);
-        coal_copy(cur, prop);
-        prop[2 + COAL_KMAX + i - 1] = nh;
-        double sn = coal_score(prop, ev, E, T);
-        double fwd = -orc_log((double)(k + 1)) - orc_log(hi - lo);
-        double bwd = -orc_log((double)(k + 1)) - orc_log(nh * 2.0 - nh / 2.0);
-        double alpha = ((sn - cur[1]) + bwd) - fwd;
-        if (orc_log(coal_u(seed, c, step, 2)) < alpha) { cur[2 + COAL_KMAX + i - 1] = nh; cur[1] = sn; acc[0]++; }
+      uint32_t B[6][4];
+      for (uint32_t b = 0; b < 6; ++b) rng(seed, c, step, S_MH, b, B[b]);
+      double u[3];
+      /* rate move */
+      u[0] = unif53(B[0][0], B[0][1]);
+      u[1] = unif53(B[0][2], B[0][3]);
+      double alpha = coal_propose(&M, cur, COAL_RATE_MOVE, u, 0.0, prop);
+      if (orc_log_unit(one_minus53(B[1][0], B[1][1])) < alpha) { memcpy(cur, prop, sizeof prop); acc[0]++; }
+      /* position move, if k > 0 */
+      if ((int)cur[0] > 0) {
+        u[0] = unif53(B[1][2], B[1][3]);
+        u[1] = unif53(B[2][0], B[2][1]);
+        alpha = coal_propose(&M, cur, COAL_POSITION, u, 0.0, prop);
+        if (orc_log_unit(one_minus53(B[2][2], B[2][3])) < alpha) { memcpy(cur, prop, sizeof prop); acc[1]++; }
       }
-      if ((int)cur[0] > 0) { /* position move */
-        int k = (int)cur[0];
-        int i = (int)(coal_u(seed, c, step, 3) * (double)k) + 1;
-        double lower = i == 1 ? 0.0 : cur[2 + i - 2];
-        double upper = i == k ? T : cur[2 + i];
-        double ncp = lower + (upper - lower) * coal_u(seed, c, step, 4);
-        coal_copy(cur, prop);
-        prop[2 + i - 1] = ncp;
-        double sn = coal_score(prop, ev, E, T);
-        double fwd = -orc_log((double)k) - orc_log(upper - lower), bwd = fwd;
-        double alpha = ((sn - cur[1]) + bwd) - fwd;
-        if (orc_log(coal_u(seed, c, step, 5)) < alpha) { cur[2 + i - 1] = ncp; cur[1] = sn; acc[1]++; }
-      }
-      { /* birth / death move */
-        int k = (int)cur[0];
-        int birth = k == 0 || coal_u(seed, c, step, 6) < 0.5;
-        double alpha = -INFINITY, sn = -INFINITY;
-        if (birth) {
-          int i = (int)(coal_u(seed, c, step, 7) * (double)(k + 1)) + 1;
-          double lower = i == 1 ? 0.0 : cur[2 + i - 2];
-          double upper = i == k + 1 ? T : cur[2 + i - 1];
-          double ncp = lower + (upper - lower) * coal_u(seed, c, step, 8);
-          double uu = coal_u(seed, c, step, 9);
-          double d_prev = ncp - lower, d_next = upper - ncp;
-          if (k < COAL_KMAX && d_prev > 0.0 && d_next > 0.0 && uu > 0.0) {
-            double h = cur[2 + COAL_KMAX + i - 1];
-            double d_total = d_prev + d_next;
-            double lr = orc_log(1.0 - uu) - orc_log(uu);
-            double hp = orc_exp(orc_log(h) - (d_next / d_total) * lr);
-            double hn = orc_exp(orc_log(h) + (d_prev / d_total) * lr);
-            prop[0] = (double)(k + 1);
-            for (int j = 1; j < i; ++j) prop[2 + j - 1] = cur[2 + j - 1];
-            prop[2 + i - 1] = ncp;
-            for (int j = i + 1; j <= k + 1; ++j) prop[2 + j - 1] = cur[2 + j - 2];
-            for (int j = 1; j < i; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j - 1];
-            prop[2 + COAL_KMAX + i - 1] = hp;
-            prop[2 + COAL_KMAX + i] = hn;
-            for (int j = i + 2; j <= k + 2; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j - 2];
-            sn = coal_score(prop, ev, E, T);
-            double fwd = ((k > 0 ? orc_log(0.5) : 0.0) - orc_log((double)(k + 1))) - orc_log(upper - lower);
-            double bwd = orc_log(0.5) - orc_log((double)(k + 1));
-            double logj = 2.0 * orc_log(hp + hn) - orc_log(h);
-            alpha = (((sn - cur[1]) + bwd) - fwd) + logj;
-          }
-        } else {
-          int i = (int)(coal_u(seed, c, step, 7) * (double)k) + 1;
-          double cpd = cur[2 + i - 1];
-          double lower = i == 1 ? 0.0 : cur[2 + i - 2];
-          double upper = i == k ? T : cur[2 + i];
-          double d_prev = cpd - lower, d_next = upper - cpd;
-          if (d_prev > 0.0 && d_next > 0.0) {
-            double hp = cur[2 + COAL_KMAX + i - 1], hn = cur[2 + COAL_KMAX + i];
-            double d_total = d_prev + d_next;
-            double h = orc_exp((d_prev / d_total) * orc_log(hp) + (d_next / d_total) * orc_log(hn));
-            prop[0] = (double)(k - 1);
-            for (int j = 1; j < i; ++j) prop[2 + j - 1] = cur[2 + j - 1];
-            for (int j = i; j <= k - 1; ++j) prop[2 + j - 1] = cur[2 + j];
-            for (int j = 1; j < i; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j - 1];
-            prop[2 + COAL_KMAX + i - 1] = h;
-            for (int j = i + 1; j <= k; ++j) prop[2 + COAL_KMAX + j - 1] = cur[2 + COAL_KMAX + j];
-            sn = coal_score(prop, ev, E, T);
-            double fwd = orc_log(0.5) - orc_log((double)k);
-            double bwd = ((k - 1 > 0 ? orc_log(0.5) : 0.0) - orc_log((double)k)) - orc_log(upper - lower);
-            double logj = orc_log(h) - 2.0 * orc_log(hp + hn);
-            alpha = (((sn - cur[1]) + bwd) - fwd) + logj;
-          }
-        }
-        if (orc_log(coal_u(seed, c, step, 10)) < alpha) { coal_copy(prop, cur); cur[1] = sn; acc[2]++; }
-      }
+      /* birth / death move */
+      int k = (int)cur[0];
+      int birth = k == 0 || unif53(B[3][0], B[3][1]) < 0.5;
+      u[0] = unif53(B[3][2], B[3][3]);
+      u[1] = unif53(B[4][0], B[4][1]);
+      u[2] = unif53(B[4][2], B[4][3]);
+      alpha = coal_propose(&M, cur, birth ? COAL_BIRTH : COAL_DEATH, u, one_minus53(B[4][2], B[4][3]), prop);
+      if (orc_log_unit(one_minus53(B[5][0], B[5][1])) < alpha) { memcpy(cur, prop, sizeof prop); acc[2]++; }
       if (khist) khist[cl * n_iters + it] = (int32_t)cur[0];
     }
     for (int m = 0; m < 3; ++m) accepts[cl * 3 + m] = acc[m];

@@ -102,16 +102,25 @@ int orc_importance_sampling(int family, int d, int dy, int k, int v, const doubl
                             double* lml);
 
 /* particle-marginal MH (config C5): chains [chain0, chain0 + n_chains) of the
-   Kitagawa PMMH of examples/pmmh/example.jl; see gen_amd/csrc/gh_pmmh.h */
+   Kitagawa PMMH of examples/pmmh/example.jl:20-79 over pf.jl:14-73 */
 int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T, int n_iters,
                  int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml, int32_t* accepts,
                  double* hist);
 
-/* reversible-jump MH on the coal change-point model (config C3): chains
-   [chain0, chain0 + n_chains); state rows of 68 doubles (k, score, cp[32],
-   h[33], pad); see gen_amd/csrc/gh_coal.h */
+/* reversible-jump MH on the coal change-point model (config C3,
+   examples/coal/coal.jl:47-62, :103-336): chains [chain0, chain0 + n_chains);
+   state rows of 68 doubles (k, score, cp[32], h[33], pad; unused fields 0) */
 int orc_coal_run(int64_t chain0, int64_t n_chains, const double* events, int E, int n_iters, int iter0,
                  uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist);
+/* the score of a row from scratch, and one move's proposal (move 0 rate, 1
+   position, 2 birth, 3 death) from explicit uniforms u[3]: returns the MH
+   log acceptance ratio, writes the proposed row (tests/test_coal_pins.py) */
+double orc_coal_score(const double* row, const double* events, int E);
+double orc_coal_propose(const double* row, const double* events, int E, int move, const double* u, double* out);
+/* the inner particle filter of the PMMH (its log-ML estimate) for chain c and
+   move counter u at parameters (log var_x, log var_y) */
+double orc_pmmh_loglik(uint64_t seed, uint64_t chain, uint32_t u, double lvx, double lvy, int n_inner,
+                       const double* ys, int T);
 
 /* static weight helpers used by the golden-vector tests */
 double orc_normal_logpdf(double x, double mu, double std);

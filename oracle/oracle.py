@@ -71,6 +71,9 @@ def lib():
             "orc_normal_logpdf": (c_double, [c_double, c_double, c_double]),
             "orc_pmmh_run": (I, [I64, I64, I, D, I, I, I, U64, I, D, D, D, POINTER(ctypes.c_int32), D]),
             "orc_coal_run": (I, [I64, I64, D, I, I, I, U64, I, D, POINTER(ctypes.c_int32), POINTER(ctypes.c_int32)]),
+            "orc_coal_score": (c_double, [D, D, I]),
+            "orc_coal_propose": (c_double, [D, D, I, I, D, D]),
+            "orc_pmmh_loglik": (c_double, [U64, U64, U32, c_double, c_double, I, D, I]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -328,3 +331,29 @@ def coal_run(events, n_chains, n_iters, seed, chain0=0, iter0=0, state=None, khi
     if rc:
         raise ValueError("oracle coal failed")
     return st, acc, kh
+
+
+def coal_score(row, events):
+    """The oracle's score of one 68-double coal row (k, score, cp[32], h[33], pad)."""
+    r = np.ascontiguousarray(row, dtype=np.float64)
+    ev = np.ascontiguousarray(events, dtype=np.float64)
+    return lib().orc_coal_score(_d(r), _d(ev), ev.size)
+
+
+COAL_MOVES = {"rate": 0, "position": 1, "birth": 2, "death": 3}
+
+
+def coal_propose(row, events, move, u):
+    """One coal move from explicit uniforms u (3): (alpha, proposed row)."""
+    r = np.ascontiguousarray(row, dtype=np.float64)
+    ev = np.ascontiguousarray(events, dtype=np.float64)
+    uu = np.ascontiguousarray(np.resize(np.asarray(u, dtype=np.float64), 3))
+    out = np.zeros(COAL_W)
+    a = lib().orc_coal_propose(_d(r), _d(ev), ev.size, COAL_MOVES[move], _d(uu), _d(out))
+    return a, out
+
+
+def pmmh_loglik(ys, lvx, lvy, n_inner, seed, chain, u=0):
+    """The PMMH inner particle filter's log-ML estimate (orc_pmmh_loglik)."""
+    y = np.ascontiguousarray(np.asarray(ys, dtype=np.float64))
+    return lib().orc_pmmh_loglik(seed, chain, u, lvx, lvy, n_inner, _d(y), y.size)

@@ -23,6 +23,30 @@ def data(T=25, seed=3):
     return ys
 
 
+@pytest.mark.parametrize("lvx,lvy", [(np.log(4.0), 0.0), (1.0, 0.3), (1.6, -0.3)])
+def test_oracle_pmmh_inner_filter_is_the_particle_filter(lvx, lvy):
+    """The likelihood term of the PMMH (the ParticleFilterCombinator's
+    log_ml_estimate, examples/pmmh/pf.jl:40-56) is the particle filter of
+    src/inference/particle_filter.jl on the model of example.jl:5-22: its
+    estimates over 300 chains (independent random streams) have the mean and
+    spread of the PF oracle's (O.run_pf, KitagawaSSM(exp(lvx), exp(lvy), 0, 5),
+    N = 256, 300 seeds), and the average of the Z estimates (Z-hat is
+    unbiased) agrees with a 2^16-particle estimate."""
+    ys = data(T=25)
+    m = KitagawaSSM(float(np.exp(lvx)), float(np.exp(lvy)), 0.0, 5.0)
+    n = 300
+    a = np.array([O.pmmh_loglik(ys, lvx, lvy, 256, seed=3, chain=c) for c in range(n)])
+    b = np.array([O.run_pf(m, ys, 256, s, record_history=False).log_ml_estimate() for s in range(n)])
+    se = np.sqrt(a.var(ddof=1) / n + b.var(ddof=1) / n)
+    assert abs(a.mean() - b.mean()) < 4 * se, (a.mean(), b.mean(), se)
+    assert 0.7 < a.var(ddof=1) / b.var(ddof=1) < 1.4
+    big = np.mean([O.run_pf(m, ys, 1 << 16, s, record_history=False).log_ml_estimate() for s in range(2)])
+    for x in (a, b):
+        log_mean_z = x.max() + np.log(np.mean(np.exp(x - x.max())))
+        assert abs(log_mean_z - big) < 0.5, (log_mean_z, big)
+        assert x.mean() < big  # log Z-hat is biased low
+
+
 def test_oracle_pmmh_deterministic_and_continues():
     ys = data()
     a = O.pmmh_run(ys, 3, 64, 4, seed=11, chain0=2)

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--chains", type=int, default=1 << 20)
-    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--cpu-chains", type=int, default=64)
     a = p.parse_args()
     import gen_amd as gen
