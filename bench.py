@@ -17,19 +17,28 @@ Also reported:
   roofline     achieved HBM GB/s of the dominant kernel (k_step) from its
                algorithmic bytes (16d+16 per particle-step, +4 on resample
                steps) / its hipEvent-timed average duration on its stream;
-               traffic = PMC HBM bytes per launch from profiles/ when present.
-  cpu_baseline the CPU oracle (C restatement of Gen's PF, 1 core) on a bounded
-               sample of the same workload, timed on this host; its "parity"
-               entry runs the GPU filter and the oracle on the same
+               traffic = PMC HBM bytes per launch from profiles/ when present;
+               step_frac = the same bytes per whole step / ms_per_step / peak.
+  cpu_baseline the CPU oracle (C restatement of Gen's PF) on a bounded sample
+               of the same workload, timed on this host on every core
+               (OpenMP build) with the one-core figure beside it (median of
+               5 repetitions each, CPU model and thread count stated); its
+               "parity" entry runs the GPU filter and the oracle on the same
                observations, seed and 2^16 particles and reports the log-ML
                relative difference (north star: <= 1e-6) and whether the final
                ancestors agree bit for bit.
+  secondary    (one GPU, rank 0) the other GPU configurations of BASELINE.json
+               measured in the same run, each with its own CPU baseline:
+               C4 the nonlinear SSM at 2^21 particles per GPU (the 8-GPU
+               scaling config's shard), C3 coal RJMCMC 2^20 chains x 1000
+               steps, C5 PMMH 2^16 chains x 256 inner particles.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -41,7 +50,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
@@ -54,7 +63,8 @@ def parse():
     p.add_argument("--proposal", default="default", choices=["default", "optimal"],
                    help="optimal: the LG-SSM's locally optimal proposal (a custom proposal; not the headline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=1.5, help="seconds per CPU repetition (5 per baseline)")
+    p.add_argument("--no-secondary", action="store_true", help="skip the C3 / C4 / C5 measurements")
     p.add_argument("--no-history", action="store_true")
     p.add_argument("--ess-threshold", type=float, default=None, help="default N/2 (the reference's default)")
     p.add_argument("--no-kernel-timing", action="store_true", help="no hipEvents around the step kernel")
@@ -63,8 +73,81 @@ def parse():
                         "(ranks may share a GPU; a correctness rehearsal, not a benchmark)")
     p.add_argument("--time-every", type=int, default=None,
                    help="time every k-th step kernel with launch events (default: steps // 2, i.e. two timed "
-                        "launches in the timed region; each timed launch costs the run 25-60 us, measured)")
-    return p.parse_args()
+                        "launches in the timed region)")
+    return p.parse_args(argv)
+
+
+# ------------------------------------------------------------ CPU baselines
+def host_info():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff}
+
+
+def median_rate(fn, reps=5):
+    """fn() -> (units, seconds); the median rate over reps repetitions."""
+    rates = []
+    for _ in range(reps):
+        u, dt = fn()
+        rates.append(u / dt)
+    return statistics.median(rates), rates
+
+
+def cpu_pair(make_sample, unit, sample_desc, reps=5):
+    """The oracle on every host core (OpenMP build) and on one core, median of
+    `reps` repetitions each: the all-cores value is the reported baseline."""
+    from oracle import oracle as O
+
+    out = {}
+    for omp in (True, False):
+        O.set_openmp(omp)
+        threads = O.num_threads()
+        med, rates = median_rate(make_sample(threads), reps)
+        out[omp] = {"value": med, "cores": threads, "repetitions": [round(r, 1) for r in rates]}
+    O.set_openmp(False)
+    return {
+        "value": out[True]["value"],
+        "unit": unit,
+        "cores": out[True]["cores"],
+        "kind": "port",
+        "sample": sample_desc + " (oracle/gh_oracle.c, the C restatement of Gen's algorithm — not Gen.jl: no "
+                                "Julia on the box; OpenMP build, median of 5)",
+        "single_core": {"value": out[False]["value"], "cores": 1, "repetitions": out[False]["repetitions"]},
+        "repetitions": out[True]["repetitions"],
+        "host": host_info(),
+    }
+
+
+def pf_cpu_baseline(model, ys, budget_s):
+    """The oracle's PF on a bounded sample of the same workload: N = 2^14
+    particles per thread, as many {maybe_resample!; step} as fit in budget_s."""
+    from oracle import oracle as O
+
+    def make(threads):
+        n = (1 << 14) * max(1, threads)
+
+        def sample():
+            pf = O.OraclePF(model, n, 42, record_history=False)
+            pf.init(ys[0])
+            t0 = time.perf_counter()
+            steps, i = 0, 1
+            while time.perf_counter() - t0 < budget_s:
+                pf.maybe_resample()
+                pf.step(ys[i % len(ys)])
+                i += 1
+                steps += 1
+            return n * steps, time.perf_counter() - t0
+        return sample
+
+    name = f"LG-SSM d={model.d}" if hasattr(model, "A") else "Kitagawa SSM"
+    return cpu_pair(make, "particle-steps/s", f"{name}, N = 2^14 per thread, {budget_s:.1f} s per repetition")
 
 
 def cpu_parity(model, ys, n, resampler, proposal):
@@ -89,35 +172,194 @@ def cpu_parity(model, ys, n, resampler, proposal):
             "rel": abs(gpu - cpu) / abs(cpu), "parents_bitexact": bool((gpu_parents == orc.parents()).all())}
 
 
-def cpu_baseline(model, ys, budget_s):
-    """The oracle (scalar C, 1 core) on N = 2^14 particles, as many steps of
-    the same workload as fit in ~budget_s seconds."""
-    from oracle import oracle as O
+def pmc_profile(name):
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return None
 
-    n = 1 << 14
-    pf = O.OraclePF(model, n, 42, record_history=False)
+
+# --------------------------------------------------------------- PF runs
+def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn):
+    """One filter: init, warm-up steps, then the timed region over K steps
+    (barrier + device sync on both sides, max over ranks)."""
+    T = a.warmup + a.steps + 1
+    seed_data = 2 if isinstance(model, gen.LinearGaussianSSM) else 3
+    _, ys = model.simulate(T, np.random.default_rng(seed_data))
+    n_global = particles * world
+    prop = gen.OptimalProposal if a.proposal == "optimal" and isinstance(model, gen.LinearGaussianSSM) else None
+    init_args = (prop, (), n_global) if prop is not None else (n_global,)
+    st = gen.initialize_particle_filter(
+        model, (1,), {("chain", 1, "y"): ys[0]}, *init_args, seed=42, resampler=a.resampler,
+        record_history=not a.no_history, history_capacity=T + 2, time_kernels=0 if a.no_kernel_timing else a.time_every,
+        ctx=ctx,
+    )
+    gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold, proposal=prop)
+    ctx.synchronize()
+    st.kernel_time_ms(reset=True)
+    # the observations of the timed steps, marshalled into the C ABI's gh_obs
+    # array before the clock starts (inputs ready, as the workload's data)
+    batch = gen.prepare_observations(model, list(ys[1 + a.warmup : 1 + a.warmup + a.steps]))
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
     t0 = time.perf_counter()
-    pf.init(ys[0])
-    steps = 0
-    i = 1
-    while time.perf_counter() - t0 < budget_s:
-        pf.maybe_resample()
-        pf.step(ys[i % len(ys)])
-        i += 1
-        steps += 1
+    gen.run_particle_filter(st, batch, a.ess_threshold, proposal=prop)
+    barrier()
     dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kms, kcount = st.kernel_time_ms()
+    ess, did = st.ess_history()
+    n_res = int(did[a.warmup : a.warmup + a.steps].sum())  # resamples ahead of the timed steps
+    lml = gen.log_ml_estimate(st)
+    bytes_pp = bytes_fn(n_res)
+    achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+    st.close()
     return {
-        "value": n * (steps + 1) / dt,
-        "unit": "particle-steps/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"oracle/gh_oracle.c (C restatement of Gen's PF, not Gen.jl: no Julia on the box), "
-                  f"LG-SSM d={model.d}, N={n}, {steps + 1} steps incl. init, {dt:.1f} s",
+        "ys": ys, "dt": dt, "n_global": n_global, "n_res": n_res, "lml": lml, "prop": prop,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": kernel_name,
+            "kernel_avg_ms": kms,
+            "kernel_launches": kcount,
+            "bytes_per_particle_step": bytes_pp,
+            # the whole step (every kernel and gap) against the same bytes
+            "step_frac": bytes_pp * particles / (dt / a.steps) / 1e9 / HBM_PEAK_GBS,
+        },
     }
 
 
-def main():
-    a = parse()
+# ------------------------------------------------------------ secondaries
+def secondary_c4(gen, ctx, a):
+    """C4: the nonlinear (Kitagawa) SSM at 2^21 particles — one GPU's shard of
+    the 16M-particle 8-GPU configuration (BASELINE.json configs[3])."""
+    model = gen.KitagawaSSM(10.0, 1.0)  # examples/pmmh/run.jl:69 (var_x = 10, var_y = 1)
+    n = 1 << 21
+    r = pf_run(gen, ctx, None, 1, a, model, n, "k_step<KitModel,false>",
+               lambda n_res: 16 * 1 + 16 + 4.0 * n_res / max(1, a.steps))
+    pmc = pmc_profile("pmc_k_step_kitagawa.json")
+    r["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
+    out = {
+        "metric": "particle-steps/sec, nonlinear SSM (C4 shard)",
+        "value": n * a.steps / r["dt"],
+        "unit": "particle-steps/s",
+        "ms_per_step": r["dt"] * 1e3 / a.steps,
+        "steps": a.steps,
+        "config": {"workload": "C4: Kitagawa SSM bootstrap PF, 2097152 particles (one GPU's shard of 16M), "
+                               f"systematic resampling at ESS<N/2, record_history={not a.no_history}",
+                   "resample_steps_timed": r["n_res"], "log_ml": r["lml"]},
+        "roofline": r["roofline"],
+    }
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = pf_cpu_baseline(model, r["ys"], a.cpu_seconds)
+    return out
+
+
+def secondary_c3(gen, ctx, a):
+    """C3: coal change-point RJMCMC, 2^20 independent chains x 1000 mcmc_steps
+    (BASELINE.json configs[2])."""
+    from gen_amd.coal import CoalChains
+    from oracle import oracle as O
+
+    ev = np.array(json.load(open(os.path.join(ROOT, "tests", "golden", "coal_events.json")))["events"])
+    chains, steps = 1 << 20, 1000
+    ch = CoalChains(ev, chains, seed=42, ctx=ctx)
+    ch.run(0, accepts=False)  # generate (the start from the prior), untimed
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    ch.run(steps, accepts=False)  # chains resident on the device: the timed call moves no state
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    ks = np.bincount(ch.k, minlength=10)[:10] / chains
+    kms = ch.kernel_ms
+    ch.close()
+    pmc = pmc_profile("pmc_k_coal.json")
+    out = {
+        "metric": "coal RJMCMC chain-steps/s (C3)",
+        "value": chains * steps / dt,
+        "unit": "chain-steps/s",
+        "config": {"workload": "C3: examples/coal RJMCMC (rate, position, birth/death moves), 190 events",
+                   "chains": chains, "steps": steps},
+        "kernel_ms": kms,
+        "k_posterior": [round(float(x), 4) for x in ks],
+        "roofline": {"bound": "valu", "kernel": "k_coal",
+                     "hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                     "valu_frac": pmc.get("valu_frac") if pmc else None,
+                     "source": pmc.get("source") if pmc else None,
+                     "note": "state in LDS for the launch: HBM = one read + one write of the 544-byte rows"},
+    }
+    if not a.no_cpu_baseline:
+        def make(threads):
+            nc = 512 * max(1, threads)
+
+            def sample():
+                t = time.perf_counter()
+                O.coal_run(ev, nc, 200, seed=42)
+                return nc * 200, time.perf_counter() - t
+            return sample
+        out["cpu_baseline"] = cpu_pair(make, "chain-steps/s", "orc_coal_run, 512 chains per thread x 200 steps")
+    return out
+
+
+def secondary_c5(gen, ctx, a):
+    """C5: PMMH, 2^16 outer chains x 256 inner particles, T = 100
+    (BASELINE.json configs[4]; one GPU's share is replicas only)."""
+    from gen_amd.pmmh import PMMHChains
+    from oracle import oracle as O
+
+    T, chains, inner, iters = 100, 1 << 16, 256, 2
+    _, ys = gen.KitagawaSSM(4.0, 1.0, 0.0, 5.0).simulate(T, np.random.default_rng(3))
+    ch = PMMHChains(ys, chains, inner, seed=42, ctx=ctx)
+    ch.run(0)  # generate: the start from the prior, one filter per chain (untimed)
+    t0 = time.perf_counter()
+    ch.run(iters)
+    dt = time.perf_counter() - t0
+    units = chains * iters * 4 * T * inner
+    pmc = pmc_profile("pmc_k_pmmh.json")
+    out = {
+        "metric": "PMMH inner particle-steps/s (C5)",
+        "value": units / dt,
+        "unit": "particle-steps/s",
+        "config": {"workload": "C5: examples/pmmh PMMH (4 MH moves per iteration, each an inner PF of T=100)",
+                   "chains": chains, "inner": inner, "T": T, "iterations": iters},
+        "kernel_ms": ch.kernel_ms,
+        "accept_rate": [round(float(x), 4) for x in ch.accepts.sum(axis=0) / (chains * iters)],
+        "roofline": {"bound": "valu", "kernel": "k_pmmh",
+                     "valu_frac": pmc.get("valu_frac") if pmc else None,
+                     "hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch") if pmc else None,
+                     "source": pmc.get("source") if pmc else None},
+    }
+    if not a.no_cpu_baseline:
+        def make(threads):
+            nc = 4 * max(1, threads)
+
+            def sample():
+                t = time.perf_counter()
+                O.pmmh_run(ys, nc, inner, 1, seed=42)  # generate + 1 iteration = 5 filters per chain
+                return nc * 5 * T * inner, time.perf_counter() - t
+            return sample
+        out["cpu_baseline"] = cpu_pair(make, "particle-steps/s", "orc_pmmh_run, 4 chains per thread x (generate + 1 iteration)")
+    return out
+
+
+# ------------------------------------------------------------------- main
+def main(argv=None):
+    a = parse(argv)
     if a.time_every is None:
         a.time_every = max(1, a.steps // 2)
     import gen_amd as gen
@@ -146,63 +388,23 @@ def main():
 
     if a.model == "lgssm":
         model = gen.LinearGaussianSSM.benchmark(a.d)
+        d = a.d
+        kname = f"k_step<LGOptModel<{a.d}>,false>" if a.proposal == "optimal" else f"k_step<LGModel<{a.d},3>,false>"
     else:
         model = gen.KitagawaSSM(10.0, 1.0)  # examples/pmmh/run.jl:69 (var_x = 10, var_y = 1)
-    T = a.warmup + a.steps + 1
-    _, ys = model.simulate(T, np.random.default_rng(2 if a.model == "lgssm" else 3))
-    n_global = a.particles * world
-    prop = gen.OptimalProposal if a.proposal == "optimal" else None
-    init_args = (prop, (), n_global) if prop is not None else (n_global,)
-    st = gen.initialize_particle_filter(
-        model, (1,), {("chain", 1, "y"): ys[0]}, *init_args, seed=42, resampler=a.resampler,
-        record_history=not a.no_history, history_capacity=T + 2, time_kernels=0 if a.no_kernel_timing else a.time_every,
-    )
-    gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold, proposal=prop)
-    ctx.synchronize()
-    st.kernel_time_ms(reset=True)
-    ess0, did0 = st.ess_history()
-
-    def barrier():
-        ctx.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    # the observations of the timed steps, marshalled into the C ABI's gh_obs
-    # array before the clock starts (inputs ready, as the workload's data)
-    batch = gen.prepare_observations(model, list(ys[1 + a.warmup : 1 + a.warmup + a.steps]))
-    barrier()
-    t0 = time.perf_counter()
-    gen.run_particle_filter(st, batch, a.ess_threshold, proposal=prop)
-    barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    kms, kcount = st.kernel_time_ms()
-    ess, did = st.ess_history()
-    n_res = int(did[a.warmup : a.warmup + a.steps].sum())  # resamples ahead of the timed steps
-    lml = gen.log_ml_estimate(st)
-
-    d = a.d if a.model == "lgssm" else 1
-    bytes_pp = 16 * d + 16 + 4.0 * n_res / max(1, a.steps)
-    achieved = bytes_pp * st.n_local / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
-    traffic = None
+        d = 1
+        kname = "k_step<KitModel,false>"
+    r = pf_run(gen, ctx, dist, world, a, model, a.particles, kname,
+               lambda n_res: 16 * d + 16 + 4.0 * n_res / max(1, a.steps))
     # PMC HBM bytes per step-kernel launch of the profiled configs (tools/pmc_json.py)
     pmc = None
-    if a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20 and prop is None:
-        pmc = os.path.join(ROOT, "profiles", "pmc_k_step.json")
+    if a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20 and r["prop"] is None:
+        pmc = pmc_profile("pmc_k_step.json")
     elif a.model == "kitagawa" and a.particles == 1 << 21:
-        pmc = os.path.join(ROOT, "profiles", "pmc_k_step_kitagawa.json")
-    if pmc is not None and os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+        pmc = pmc_profile("pmc_k_step_kitagawa.json")
+    r["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
 
-    value = n_global * a.steps / dt
+    ys, n_global, lml = r["ys"], r["n_global"], r["lml"]
     log_ml_error = None
     if a.model == "lgssm":
         exact = model.kalman_log_marginal(ys[: 1 + a.warmup + a.steps])
@@ -211,19 +413,19 @@ def main():
     out = {
         "metric": ("particle-steps/sec (whole node) + log-ML error vs CPU ref, 1M-particle SSM" if a.model == "lgssm"
                    else "particle-steps/sec (whole node), nonlinear SSM (C4)"),
-        "value": value,
+        "value": n_global * a.steps / r["dt"],
         "unit": "particle-steps/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": dt * 1e3 / a.steps,
+        "ms_per_step": r["dt"] * 1e3 / a.steps,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": f"synthetic (observations simulated from the model, numpy seed {2 if a.model == 'lgssm' else 3})",
         "config": {
-            "workload": (f"C2: {a.d}-dim linear-Gaussian SSM " + ("optimal-proposal PF" if prop else "bootstrap PF")
+            "workload": (f"C2: {a.d}-dim linear-Gaussian SSM " + ("optimal-proposal PF" if r["prop"] else "bootstrap PF")
                          if a.model == "lgssm" else
                          "C4: Kitagawa nonlinear SSM bootstrap PF") + f", {a.particles} particles/GPU, "
                         f"systematic resampling at ESS<N/2, record_history={not a.no_history}",
@@ -231,7 +433,7 @@ def main():
             "d": d,
             "resampler": a.resampler,
             "parallelism": f"particle-dp{world}",
-            "resample_steps_timed": n_res,
+            "resample_steps_timed": r["n_res"],
             "log_ml": lml,
         },
         # log-ML error against the exact answer of the CPU reference's target
@@ -239,32 +441,20 @@ def main():
         # Monte-Carlo error at this N dominates it; parity with the CPU
         # restatement of Gen's filter at equal seeds is 1e-9 (tests/).
         "log_ml_error": log_ml_error,
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "kernel": (f"k_step<LGOptModel<{a.d}>,false>" if prop else f"k_step<LGModel<{a.d},3>,false>")
-                      if a.model == "lgssm" else "k_step<KitModel,false>",
-            "kernel_avg_ms": kms,
-            "kernel_launches": kcount,
-            "bytes_per_particle_step": bytes_pp,
-            # the whole step (every kernel and gap) against the same bytes
-            "step_frac": bytes_pp * n_global / world / (dt / a.steps) / 1e9 / HBM_PEAK_GBS,
-        },
+        "roofline": r["roofline"],
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(model, ys, a.cpu_seconds)
+        out["cpu_baseline"] = pf_cpu_baseline(model, ys, a.cpu_seconds)
         # same seed, same observations, N = 2^16: GPU vs the CPU restatement
         par = cpu_parity(model, ys, 1 << 16, a.resampler, a.proposal)
         out["cpu_baseline"]["parity"] = par
         if out["log_ml_error"] is not None:
             out["log_ml_error"]["vs_cpu_reference_same_seed"] = {"particles": par["particles"], "rel": par["rel"]}
+    if rank == 0 and world == 1 and not a.no_secondary and a.model == "lgssm":
+        out["secondary"] = {"C4": secondary_c4(gen, ctx, a), "C3": secondary_c3(gen, ctx, a),
+                            "C5": secondary_c5(gen, ctx, a)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    st.close()
     if dist is not None:
         dist.barrier()
     ctx.close()

@@ -5,7 +5,7 @@ C ABI in include/gen_hip.h).  This package is its Python host mirror of Gen's
 inference API (src/inference/particle_filter.jl, importance.jl); see
 DESIGN.md.  Importing it does not touch the GPU; the first call does.
 """
-from .choicemap import ChoiceMap, EmptyChoiceMap, choicemap
+from .choicemap import ChoiceMap, EmptyChoiceMap, Selection, choicemap, select
 from .models import BayesianLinearRegression, DiscreteHMM, KitagawaSSM, LinearGaussianSSM, Model
 from .pf import (
     Context,
@@ -28,6 +28,8 @@ from .pf import (
     log_ml_estimate,
     maybe_resample,
     maybe_resample_async,
+    metropolis_hastings,
+    mh,
     particle_filter_step,
     rejuvenate,
     ObservationBatch,
@@ -45,5 +47,6 @@ __all__ = [
     "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",
     "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
     "conditional_particle_filter_step", "conditional_smc", "get_particle", "initialize_conditional_particle_filter",
-    "particle_gibbs", "GenHipError", "ObservationBatch", "prepare_observations",
+    "particle_gibbs", "GenHipError", "ObservationBatch", "prepare_observations", "Selection", "select",
+    "metropolis_hastings", "mh",
 ]

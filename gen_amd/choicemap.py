@@ -97,3 +97,28 @@ def choicemap(*pairs) -> ChoiceMap:
 
 
 EmptyChoiceMap = ChoiceMap
+
+
+class Selection:
+    """A set of addresses (src/address.jl:54,352 `select(addrs...)`), with the
+    same tuple convention as ChoiceMap: select("slope") names :slope,
+    select(("chain", 3, "x")) names :chain => 3 => :x."""
+
+    def __init__(self, addrs=()):
+        self.addrs = frozenset(_norm(a) for a in addrs)
+
+    def __contains__(self, addr):
+        return _norm(addr) in self.addrs
+
+    def __iter__(self):
+        return iter(self.addrs)
+
+    def __len__(self):
+        return len(self.addrs)
+
+    def __repr__(self):
+        return f"select({', '.join(map(repr, sorted(self.addrs, key=repr)))})"
+
+
+def select(*addrs) -> Selection:
+    return Selection(addrs)

@@ -1821,9 +1821,22 @@ static int launch_rejuv(gh_pf* pf, const RejuvArgs& a, bool init) {
 // are rewritten in place; the parent states are those step t consumed: the
 // previous slot through the step's ancestors, or rows received from other
 // ranks (still resident until the next exchange).
+// latent addresses of the current step a selection may name (bit i = address i)
+static uint32_t latent_addresses(const gh_model* m) { return m->family == GH_FAMILY_REGRESSION ? 3u : 1u; }
+
 extern "C" int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
+  return gh_pf_mh_select(pf, latent_addresses(pf->m), n_moves, accepted);
+}
+
+extern "C" int gh_pf_mh_select(gh_pf* pf, uint32_t selection, int n_moves, int64_t* accepted) {
+  if (!pf) return set_err(GH_E_INVAL, "null pf");
   if (n_moves < 0) return set_err(GH_E_INVAL, "gh_pf_rejuvenate: n_moves < 0");
+  if (selection == 0 || (selection & ~latent_addresses(pf->m)) != 0)
+    return set_err(GH_E_INVAL, "gh_pf_mh_select: selection 0x%x names no latent address of this step (valid: 0x%x)",
+                   selection, latent_addresses(pf->m));
+  if (pf->m->family == GH_FAMILY_REGRESSION && pf->t != 1)
+    return set_err(GH_E_STATE, "gh_pf_mh_select: the regression is a static model (t = 1)");
   if (pf->resample_calls > 0)
     return set_err(GH_E_STATE, "gh_pf_rejuvenate: call after a step and before maybe_resample");
   if (pf->cond) return set_err(GH_E_STATE, "gh_pf_rejuvenate: the distinguished particle of a conditional filter is fixed");
@@ -1848,6 +1861,7 @@ extern "C" int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted) {
     a.seed = pf->seed;
     a.t = (uint32_t)t;
     a.move0 = pf->rejuv_moves;
+    a.select = selection;
     a.n_moves = n_moves;
     a.accepted = pf->acc_count;
     CHECK(launch_rejuv(pf, a, t == 1));

@@ -443,6 +443,19 @@ struct RegModel {
     x[1] = p.mu_i + p.sd_i * z1;
     return loglik(p, o, x);
   }
+  // regenerate the selected addresses from their prior (bit 0 :slope, bit 1
+  // :intercept; the same draws as init), keep the others: the proposal of
+  // mh(trace, select(...)) (src/inference/mh.jl:14-28).  The returned value is
+  // the new log-likelihood: the selected choices' prior scores cancel in the
+  // regenerate weight, the unselected roots' do not change.
+  __device__ static double init_select(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, uint32_t sel,
+                                       const double* xc, double* x, Draw dr = {STREAM_INIT, 0}) {
+    double z0, z1;
+    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1, dr.tab);
+    x[0] = (sel & 1u) ? p.mu_s + p.sd_s * z0 : xc[0];
+    x[1] = (sel & 2u) ? p.mu_i + p.sd_i * z1 : xc[1];
+    return loglik(p, o, x);
+  }
   // no time structure: the host refuses particle_filter_step for this family
   __device__ static double step(const Params&, const StepObs&, uint64_t, uint64_t, uint32_t, int,
                                 const double* xp, double* x, Draw = {STREAM_STEP, 0}) {

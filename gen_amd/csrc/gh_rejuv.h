@@ -9,7 +9,12 @@
 // current latent x_t from its prior given x_{t-1} gives
 //     weight = log p(y_t | x'_t) - log p(y_t | x_t)
 // because the transition density cancels between the new score and the
-// proposal.  At t = 1 the prior is the initial-state distribution.
+// proposal.  At t = 1 the prior is the initial-state distribution.  A static
+// model with several latent addresses (the regression's :slope, :intercept)
+// regenerates the selected ones only (mh(trace, select(:slope)),
+// examples/regression/quickstart.jl:17-22): weight = the log-likelihood
+// difference again (the selected choices' prior scores cancel, the
+// unselected roots' are unchanged).
 //
 // One particle per lane; the current state and its parent's state live in
 // registers for all moves.  Move w (counted from the step) draws its proposal
@@ -17,6 +22,8 @@
 // and its acceptance uniform from the last draw of that window;
 // the first 4096 moves use the MH stream itself.
 #pragma once
+#include <type_traits>
+
 #include "gh_kernels.h"
 
 namespace gh {
@@ -39,6 +46,7 @@ struct RejuvArgs {
   uint64_t seed;
   uint32_t t;
   uint32_t move0;         // moves already applied at this step
+  uint32_t select;        // selected latent addresses of the step (the regression: bit 0 :slope, bit 1 :intercept)
   int n_moves;
   unsigned long long* accepted;  // accepted moves (summed over particles)
 };
@@ -73,8 +81,11 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
       Draw dr = rejuv_draw(a.move0 + (uint32_t)m);
       dr.tab = tab;
       // the prior proposal's weight increment is the observation log-density
-      const double ll2 = INIT ? Model::init(p, o, a.seed, pid, 0, y, dr)
-                              : Model::step(p, o, a.seed, pid, a.t, 0, xp, y, dr);
+      double ll2;
+      if constexpr (INIT && std::is_same<Model, RegModel>::value)
+        ll2 = Model::init_select(p, o, a.seed, pid, a.select, x, y, dr);
+      else
+        ll2 = INIT ? Model::init(p, o, a.seed, pid, 0, y, dr) : Model::step(p, o, a.seed, pid, a.t, 0, xp, y, dr);
       const u32x4 w = rng_block(a.seed, pid, a.t, dr.stream, dr.base + kRejuvDraws - 1);
       const double logu = gh_log(u53(w.x, w.y));
       if (logu < ll2 - ll) {

@@ -498,6 +498,36 @@ def rejuvenate(state: ParticleFilterState, n_moves: int = 1) -> int:
     return int(acc.value)
 
 
+def metropolis_hastings(state: ParticleFilterState, selection, n_moves: int = 1) -> int:
+    """``metropolis_hastings(trace, selection)`` (src/inference/mh.jl:14-28; alias
+    ``mh``) applied to every particle's trace: regenerate the selected choices
+    from their prior and accept with log(rand()) < the regenerate weight.  The
+    selection names latent addresses of the current step — the regression's
+    "slope" / "intercept" (examples/regression/quickstart.jl:17-22), or the
+    Unfold models' latent of the last step — and the particles' log weights
+    are unchanged.  Returns the accepted moves over this rank's particles."""
+    from .choicemap import Selection, select as _select
+
+    sel = selection if isinstance(selection, Selection) else _select(*selection)
+    m = state.model
+    if m.static:
+        names = {("slope",): 1, ("intercept",): 2}
+    else:
+        names = {tuple(m.latent_address(state.t)): 1}
+    mask = 0
+    for a in sel:
+        if a not in names:
+            raise _lib.GenHipError(1, f"selection names {a}: only {sorted(names)} (the current step's latent "
+                                      "addresses) are lowered")
+        mask |= names[a]
+    acc = c_int64()
+    _lib.check(_lib.load().gh_pf_mh_select(state.h, mask, int(n_moves), byref(acc)))
+    return int(acc.value)
+
+
+mh = metropolis_hastings
+
+
 # ------------------------------------------------------ conditional SMC
 def _ref_state(model: Model, x) -> np.ndarray:
     a = np.ascontiguousarray(np.atleast_1d(np.asarray(x, dtype=np.float64)).ravel())

@@ -17,6 +17,8 @@
  *   gh_pf_sample_unweighted sample_unweighted_traces     src/inference/particle_filter.jl:62-70
  *   gh_pf_rejuvenate        mh(trace, select(x_t)) on    src/inference/mh.jl:14-26 (applied per
  *                           every particle               particle, as callers of the PF do)
+ *   gh_pf_mh_select         mh(trace, selection) on      src/inference/mh.jl:14-28,
+ *                           every particle               examples/regression/quickstart.jl:17-22
  *   gh_pf_init_conditional /
  *   gh_pf_step_conditional  conditional_smc              examples/pmmh/smc.jl:100-151
  *   gh_is_run               importance_sampling          src/inference/importance.jl:20-52
@@ -203,6 +205,15 @@ int gh_pf_sample_unweighted(gh_pf* pf, int64_t n_samples, uint64_t seed, int64_t
    *accepted (optional, synchronises) = accepted moves summed over the local
    particles. */
 int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted);
+/* metropolis_hastings(trace, selection) on every particle (src/inference/mh.jl:14-28,
+   the selection form): regenerate the selected latent addresses of the current
+   step from their prior, accept with log(rand()) < the regenerate weight.
+   selection is a bit mask over the step's latent addresses: the Unfold families
+   have one (bit 0: :chain => t => :x, the same move as gh_pf_rejuvenate); the
+   regression has two (bit 0 :slope, bit 1 :intercept; quickstart.jl:17-22's
+   mh(trace, select(:slope)) / mh(trace, select(:intercept))).  The moves share
+   gh_pf_rejuvenate's draw windows and per-step move counter. */
+int gh_pf_mh_select(gh_pf* pf, uint32_t selection, int n_moves, int64_t* accepted);
 /* Conditional SMC (examples/pmmh/smc.jl:100-151, the particle-Gibbs sweep):
    particle 0 is the distinguished particle, pinned to ref_x1 at init and to
    ref_xt at each step, its parent always itself, its weight the observation

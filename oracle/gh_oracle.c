@@ -13,6 +13,22 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* The same source built with -fopenmp (liboracle_omp.so) runs the
+   per-particle / per-chain loops on every host core: used only for the
+   all-cores CPU baseline of bench.py.  Every parallel loop computes values
+   that depend on its own index alone; reductions stay serial in index order,
+   so both builds give identical results. */
+int orc_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
 
 /* ------------------------------------------------------------------ bits */
 static double f64_of(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
@@ -758,8 +774,9 @@ static int init_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
   obs_t o;
   obs_build(&pf->m, 1, obs, has_obs, &o);
   int D = pf->m.d;
-  double x[64];
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < pf->n; ++i) {
+    double x[64];
     pf->logw[i] = particle_init(&pf->m, pf->seed, (uint64_t)(pf->lo + i), &o, proposal, x, S_INIT, 0);
     for (int k = 0; k < D; ++k) pf->x[(size_t)k * pf->n + i] = x[k];
     pf->anc[i] = pf->lo + i;
@@ -809,8 +826,9 @@ static int step_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
   double* src = pf->pending ? pf->anc_state : pf->x;
   memcpy(pf->xprev, src, sizeof(double) * D * n);
   const double w0_old = n > 0 ? pf->logw[0] : 0.0;
-  double xp[64], x[64];
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; ++i) {
+    double xp[64], x[64];
     for (int k = 0; k < D; ++k) xp[k] = pf->xprev[(size_t)k * n + i];
     double inc = particle_step(&pf->m, pf->seed, (uint64_t)(pf->lo + i), t, &o, proposal, xp, x, S_STEP, 0);
     for (int k = 0; k < D; ++k) pf->x[(size_t)k * n + i] = x[k];
@@ -863,6 +881,18 @@ static double model_loglik(const model_t* m, const obs_t* o, const double* x) {
    log(u) < weight.  Move w of the step uses stream S_MH + 16 (w / 4096), draws
    [16 (w mod 4096), +8) for the proposal and draw 16 (w mod 4096) + 15 for u. */
 int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted) {
+  return orc_pf_mh_select(pf, pf->m.family == ORC_REGRESSION ? 3u : 1u, n_moves, accepted);
+}
+
+/* mh(trace, selection) on every particle (src/inference/mh.jl:14-28): the
+   regression regenerates the selected ones of :slope (bit 0) / :intercept
+   (bit 1) with the same draws as a full regeneration, weight = the
+   log-likelihood difference (quickstart.jl:17-22); the Unfold families have
+   one latent address per step (the rejuvenation move above). */
+int orc_pf_mh_select(orc_pf* pf, uint32_t mask, int n_moves, int64_t* accepted) {
+  const uint32_t all = pf->m.family == ORC_REGRESSION ? 3u : 1u;
+  if (mask == 0 || (mask & ~all)) return -1;
+  if (pf->m.family == ORC_REGRESSION && pf->t != 1) return -1;
   if (pf->cond || pf->pending || pf->t < 1 || n_moves < 0 || (uint64_t)pf->moves + (uint64_t)n_moves > (1u << 24)) return -1;
   const int D = pf->m.d;
   const int64_t n = pf->n;
@@ -878,8 +908,13 @@ int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted) {
     for (int m = 0; m < n_moves; ++m) {
       const uint32_t mv = pf->moves + (uint32_t)m;
       const uint32_t stream = (uint32_t)S_MH + ((mv >> 12) << 4), base = (mv & 4095u) * 16u;
-      const double ll2 = t == 1 ? particle_init(&pf->m, pf->seed, pid, &pf->obs, 0, y, stream, base)
-                                : particle_step(&pf->m, pf->seed, pid, t, &pf->obs, 0, xp, y, stream, base);
+      double ll2 = t == 1 ? particle_init(&pf->m, pf->seed, pid, &pf->obs, 0, y, stream, base)
+                          : particle_step(&pf->m, pf->seed, pid, t, &pf->obs, 0, xp, y, stream, base);
+      if (pf->m.family == ORC_REGRESSION && mask != all) {
+        if (!(mask & 1u)) y[0] = x[0];
+        if (!(mask & 2u)) y[1] = x[1];
+        ll2 = reg_loglik(&pf->m, &pf->obs, y);
+      }
       uint32_t w[4];
       rng(pf->seed, pid, t, stream, base + 15u, w);
       const double logu = orc_log(unif53(w[0], w[1]));
@@ -906,12 +941,14 @@ void orc_pf_local_stats(orc_pf* pf, double out[3]) {
   }
   double S = 0.0, S2 = 0.0;
   if (M > -INFINITY) {
+    double* e = malloc(sizeof(double) * (pf->n ? pf->n : 1));
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < pf->n; ++i) e[i] = orc_exp((pf->pending ? 0.0 : pf->logw[i]) - M);
     for (int64_t i = 0; i < pf->n; ++i) {
-      double w = pf->pending ? 0.0 : pf->logw[i];
-      double e = orc_exp(w - M);
-      S += e;
-      S2 += e * e;
+      S += e[i];
+      S2 += e[i] * e[i];
     }
+    free(e);
   }
   out[0] = M; out[1] = S; out[2] = S2;
 }
@@ -939,6 +976,7 @@ int orc_combine_stats(const double* st, int R, int64_t n_global, double thr, dou
 uint64_t orc_pf_local_qtotal(orc_pf* pf, double M) {
   int sh = qshift((uint64_t)pf->n_global);
   uint64_t s = 0;
+#pragma omp parallel for schedule(static) reduction(+ : s)
   for (int64_t i = 0; i < pf->n; ++i) s += quantize(pf->pending ? 0.0 : pf->logw[i], M, sh);
   return s;
 }
@@ -963,9 +1001,11 @@ int64_t orc_pf_resample_emit(orc_pf* pf, double M, const uint64_t* totals, int R
   uint64_t mine = totals[rank];
   /* inclusive local CDF */
   uint64_t* C = malloc(sizeof(uint64_t) * (pf->n ? pf->n : 1));
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < pf->n; ++i) C[i] = quantize(pf->pending ? 0.0 : pf->logw[i], M, sh);
   uint64_t acc = 0;
   for (int64_t i = 0; i < pf->n; ++i) {
-    acc += quantize(pf->pending ? 0.0 : pf->logw[i], M, sh);
+    acc += C[i];
     C[i] = acc;
   }
   const double* xs = pf->pending ? pf->anc_state : pf->x;
@@ -977,6 +1017,22 @@ int64_t orc_pf_resample_emit(orc_pf* pf, double M, const uint64_t* totals, int R
   }
   int D = pf->m.d;
   int64_t cnt = 0;
+  if (R == 1) {  /* one shard: every slot is this rank's, slot j is emitted j-th */
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < pf->n_global; ++j) {
+      uint64_t lt = slot_target(pf, S, j, o);
+      int64_t lo = 0, hi = pf->n - 1;
+      while (lo < hi) {
+        int64_t mid = lo + (hi - lo) / 2;
+        if (C[mid] > lt) hi = mid; else lo = mid + 1;
+      }
+      slot_out[j] = j;
+      anc_out[j] = pf->pending ? pf->anc[lo] : pf->lo + lo;
+      for (int k = 0; k < D; ++k) state_out[j * D + k] = xs[(size_t)k * pf->n + lo];
+    }
+    free(C);
+    return pf->n_global;
+  }
   for (int64_t j = 0; j < pf->n_global; ++j) {
     uint64_t tg = slot_target(pf, S, j, o);
     if (tg < base || tg >= base + mine) continue;
@@ -1175,13 +1231,16 @@ int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys
                  int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml, int32_t* accepts,
                  double* hist) {
   if (n_inner < 1 || n_inner > 1024 || T < 1) return 1;
+  double* ct = malloc(sizeof(double) * T);
+  for (int t = 1; t <= T; ++t) ct[t - 1] = 8.0 * orc_cos(1.2 * (double)t);
+  const double sd_rw = 0x1.6a09e667f3bcdp-1;
+#pragma omp parallel
+  {
   double* x = malloc(sizeof(double) * n_inner);
   double* lw = malloc(sizeof(double) * n_inner);
   double* xp = malloc(sizeof(double) * n_inner);
   uint64_t* C = malloc(sizeof(uint64_t) * n_inner);
-  double* ct = malloc(sizeof(double) * T);
-  for (int t = 1; t <= T; ++t) ct[t - 1] = 8.0 * orc_cos(1.2 * (double)t);
-  const double sd_rw = 0x1.6a09e667f3bcdp-1;
+#pragma omp for schedule(dynamic, 1)
   for (int64_t cl = 0; cl < n_chains; ++cl) {
     uint64_t c = (uint64_t)(chain0 + cl);
     double vx, vy, ml;
@@ -1228,7 +1287,9 @@ int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys
     lvx[cl] = vx; lvy[cl] = vy; lml[cl] = ml;
     for (int m = 0; m < 4; ++m) accepts[cl * 4 + m] = acc[m];
   }
-  free(x); free(lw); free(xp); free(C); free(ct);
+  free(x); free(lw); free(xp); free(C);
+  }
+  free(ct);
   return 0;
 }
 
@@ -1482,8 +1543,9 @@ int orc_coal_run(int64_t chain0, int64_t n_chains, const double* ev, int E, int 
                  uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist) {
   if (E < 1) return 1;
   coal_m M = coal_model(ev, E);
-  double prop[COAL_W];
+#pragma omp parallel for schedule(dynamic, 4)
   for (int64_t cl = 0; cl < n_chains; ++cl) {
+    double prop[COAL_W];
     uint64_t c = (uint64_t)(chain0 + cl);
     double* cur = state + cl * COAL_W;
     if (init) {

@@ -69,6 +69,9 @@ int orc_pf_maybe_resample(orc_pf* pf, double ess_threshold, double* ess_out);
 /* rejuvenation: n_moves mh(trace, select(x_t)) moves per particle (src/inference/mh.jl:14-26);
    -1 if a resample is pending */
 int orc_pf_rejuvenate(orc_pf* pf, int n_moves, int64_t* accepted);
+/* mh(trace, selection) on every particle: mask over the step's latent addresses
+   (the regression: bit 0 :slope, bit 1 :intercept; the Unfold families: bit 0) */
+int orc_pf_mh_select(orc_pf* pf, uint32_t mask, int n_moves, int64_t* accepted);
 /* conditional SMC (examples/pmmh/smc.jl:100-151): particle 0 pinned to ref
    (multinomial resampler, one shard); a conditional filter steps only with
    orc_pf_step_conditional.  -1 on misuse */
@@ -121,6 +124,10 @@ double orc_coal_propose(const double* row, const double* events, int E, int move
    move counter u at parameters (log var_x, log var_y) */
 double orc_pmmh_loglik(uint64_t seed, uint64_t chain, uint32_t u, double lvx, double lvy, int n_inner,
                        const double* ys, int T);
+
+/* host threads the loops use: 1, or the OpenMP team size of liboracle_omp.so
+   (the all-cores CPU baseline) */
+int orc_num_threads(void);
 
 /* static weight helpers used by the golden-vector tests */
 double orc_normal_logpdf(double x, double mu, double std);

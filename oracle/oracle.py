@@ -16,26 +16,50 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
+OMP_PATH = os.path.join(HERE, "liboracle_omp.so")  # the same oracle on every host core (CPU baseline only)
 
 LGSSM, HMM, KITAGAWA, REGRESSION = 1, 2, 3, 4
 SYSTEMATIC, MULTINOMIAL = 0, 1
 DEFAULT, OPTIMAL, GAUSSIAN = 0, 1, 2
 
 _lib = None
+_libs = {}
+_use_omp = False
 
 
-def build(force: bool = False) -> str:
+def build(force: bool = False, target: str = "liboracle.so") -> str:
     src = os.path.join(HERE, "gh_oracle.c")
-    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
-        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "liboracle.so"], check=True)
-    return LIB_PATH
+    path = os.path.join(HERE, target)
+    if force or not os.path.exists(path) or os.path.getmtime(path) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", HERE] + (["-B"] if force else []) + [target], check=True)
+    return path
+
+
+def set_openmp(on: bool) -> None:
+    """Route the module's calls (and OraclePFs created afterwards) to the
+    OpenMP build (all host cores) or back to the scalar build."""
+    global _lib, _use_omp
+    _use_omp = bool(on)
+    _lib = None
+
+
+def num_threads() -> int:
+    return lib().orc_num_threads()
 
 
 def lib():
     global _lib
     if _lib is None:
-        build()
-        L = ctypes.CDLL(LIB_PATH)
+        target = "liboracle_omp.so" if _use_omp else "liboracle.so"
+        if target not in _libs:
+            _libs[target] = _load(build(target=target))
+        _lib = _libs[target]
+    return _lib
+
+
+def _load(path):
+    if True:
+        L = ctypes.CDLL(path)
         D, I, I64, U64, U32, V = POINTER(c_double), c_int, c_int64, c_uint64, c_uint32, c_void_p
         sig = {
             "orc_philox4x32_10": (None, [POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
@@ -54,6 +78,7 @@ def lib():
             "orc_pf_set_proposal_args": (I, [V, D, I]),
             "orc_pf_maybe_resample": (I, [V, c_double, D]),
             "orc_pf_rejuvenate": (I, [V, I, POINTER(c_int64)]),
+            "orc_pf_mh_select": (I, [V, U32, I, POINTER(c_int64)]),
             "orc_pf_init_conditional": (I, [V, D, I, D]),
             "orc_pf_step_conditional": (I, [V, D, I, D]),
             "orc_pf_log_ml_estimate": (c_double, [V]),
@@ -75,12 +100,12 @@ def lib():
             "orc_coal_propose": (c_double, [D, D, I, I, D, D]),
             "orc_pmmh_loglik": (c_double, [U64, U64, U32, c_double, c_double, I, D, I]),
         }
+        sig["orc_num_threads"] = (I, [])
         for name, (res, args) in sig.items():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        _lib = L
-    return _lib
+    return L
 
 
 def _d(a):
@@ -123,12 +148,13 @@ class OraclePF:
 
     def __init__(self, model, n_global, seed, resampler=SYSTEMATIC, lo=0, n_local=None, record_history=True):
         fam, d, dy, k, v, p = model_args(model)
+        self.L = lib()
         self._p = p
         self.d = d if fam in (LGSSM, REGRESSION) else 1
         self.n_global = n_global
         self.lo = lo
         self.n = n_global if n_local is None else n_local
-        self.h = lib().orc_pf_create(fam, d, dy, k, v, _d(p), p.size, n_global, lo, self.n, seed, resampler,
+        self.h = self.L.orc_pf_create(fam, d, dy, k, v, _d(p), p.size, n_global, lo, self.n, seed, resampler,
                                      int(record_history))
         if not self.h:
             raise ValueError("oracle: bad model parameters")
@@ -136,7 +162,7 @@ class OraclePF:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orc_pf_destroy(self.h)
+            self.L.orc_pf_destroy(self.h)
             self.h = None
 
     @staticmethod
@@ -149,35 +175,35 @@ class OraclePF:
     def set_proposal_args(self, args):
         """(alpha, beta, gamma, sigma_q) of the GAUSSIAN proposal (nonlinear SSM)"""
         a = np.ascontiguousarray(args, dtype=np.float64)
-        if lib().orc_pf_set_proposal_args(self.h, _d(a), a.size):
+        if self.L.orc_pf_set_proposal_args(self.h, _d(a), a.size):
             raise ValueError("oracle: proposal arguments (alpha, beta, gamma, sigma_q > 0)")
 
     def init(self, y, proposal=DEFAULT):
         a, has = self._obs(y)
-        if lib().orc_pf_init(self.h, _d(a), has, proposal):
+        if self.L.orc_pf_init(self.h, _d(a), has, proposal):
             raise ValueError("oracle: proposal not available for this model")
 
     def step(self, y, proposal=DEFAULT):
         a, has = self._obs(y)
-        if lib().orc_pf_step(self.h, _d(a), has, proposal):
+        if self.L.orc_pf_step(self.h, _d(a), has, proposal):
             raise ValueError("oracle: this filter does not take plain steps")
 
     def init_conditional(self, y, ref):
         a, has = self._obs(y)
         r = np.ascontiguousarray(np.atleast_1d(np.asarray(ref, dtype=np.float64)))
-        if lib().orc_pf_init_conditional(self.h, _d(a), has, _d(r)):
+        if self.L.orc_pf_init_conditional(self.h, _d(a), has, _d(r)):
             raise ValueError("oracle: conditional SMC needs the multinomial resampler on one shard")
 
     def step_conditional(self, y, ref):
         a, has = self._obs(y)
         r = np.ascontiguousarray(np.atleast_1d(np.asarray(ref, dtype=np.float64)))
-        if lib().orc_pf_step_conditional(self.h, _d(a), has, _d(r)):
+        if self.L.orc_pf_step_conditional(self.h, _d(a), has, _d(r)):
             raise ValueError("oracle: not a conditional filter")
 
     def maybe_resample(self, thr=None):
         thr = self.n_global / 2 if thr is None else thr
         ess = c_double()
-        r = lib().orc_pf_maybe_resample(self.h, thr, ctypes.byref(ess))
+        r = self.L.orc_pf_maybe_resample(self.h, thr, ctypes.byref(ess))
         if r < 0:
             raise FloatingPointError("oracle: all log-weights are -Inf/NaN")
         return bool(r), ess.value
@@ -185,40 +211,47 @@ class OraclePF:
     def rejuvenate(self, n_moves):
         """n_moves mh(trace, select(x_t)) moves on every particle; returns accepted moves."""
         acc = c_int64()
-        if lib().orc_pf_rejuvenate(self.h, n_moves, ctypes.byref(acc)):
+        if self.L.orc_pf_rejuvenate(self.h, n_moves, ctypes.byref(acc)):
             raise RuntimeError("oracle: rejuvenate after a resample / too many moves")
         return acc.value
 
+    def mh_select(self, mask, n_moves=1):
+        """mh(trace, selection) on every particle (mask over the step's latent addresses)."""
+        acc = c_int64()
+        if self.L.orc_pf_mh_select(self.h, int(mask), n_moves, ctypes.byref(acc)):
+            raise RuntimeError("oracle: bad selection / mh after a resample")
+        return acc.value
+
     def log_ml_estimate(self):
-        return lib().orc_pf_log_ml_estimate(self.h)
+        return self.L.orc_pf_log_ml_estimate(self.h)
 
     def log_weights(self):
         o = np.empty(self.n)
-        lib().orc_pf_get_log_weights(self.h, _d(o))
+        self.L.orc_pf_get_log_weights(self.h, _d(o))
         return o
 
     def state(self):
         o = np.empty((self.d, self.n))
-        lib().orc_pf_get_state(self.h, _d(o))
+        self.L.orc_pf_get_state(self.h, _d(o))
         return o
 
     def parents(self):
         o = np.empty(self.n, dtype=np.int64)
-        lib().orc_pf_get_parents(self.h, o.ctypes.data_as(POINTER(c_int64)))
+        self.L.orc_pf_get_parents(self.h, o.ctypes.data_as(POINTER(c_int64)))
         return o
 
     def history(self, t):
         x = np.empty((self.d, self.n))
         anc = np.empty(self.n, dtype=np.int32)
         res = c_int()
-        rc = lib().orc_pf_get_history(self.h, t, _d(x), anc.ctypes.data_as(POINTER(c_int32)), ctypes.byref(res))
+        rc = self.L.orc_pf_get_history(self.h, t, _d(x), anc.ctypes.data_as(POINTER(c_int32)), ctypes.byref(res))
         if rc:
             raise ValueError("no history")
         return x, (anc if res.value else None)
 
     def trajectory(self, t):
         """latent of step t along the genealogy of the current particles (single rank)."""
-        T = lib().orc_pf_num_steps(self.h)
+        T = self.L.orc_pf_num_steps(self.h)
         idx = np.arange(self.n)
         for s in range(T, t, -1):
             _, anc = self.history(s)
@@ -230,11 +263,11 @@ class OraclePF:
     # distributed building blocks
     def local_stats(self):
         o = np.empty(3)
-        lib().orc_pf_local_stats(self.h, _d(o))
+        self.L.orc_pf_local_stats(self.h, _d(o))
         return o
 
     def qtotal(self, M):
-        return lib().orc_pf_local_qtotal(self.h, M)
+        return self.L.orc_pf_local_qtotal(self.h, M)
 
     def emit(self, M, totals, rank):
         tot = np.ascontiguousarray(totals, dtype=np.uint64)
@@ -242,7 +275,7 @@ class OraclePF:
         slots = np.empty(n, dtype=np.int64)
         ancs = np.empty(n, dtype=np.int64)
         st = np.empty(n * self.d)
-        c = lib().orc_pf_resample_emit(self.h, M, tot.ctypes.data_as(POINTER(c_uint64)), tot.size, rank,
+        c = self.L.orc_pf_resample_emit(self.h, M, tot.ctypes.data_as(POINTER(c_uint64)), tot.size, rank,
                                        slots.ctypes.data_as(POINTER(c_int64)), ancs.ctypes.data_as(POINTER(c_int64)),
                                        _d(st))
         return slots[:c].copy(), ancs[:c].copy(), st[: c * self.d].reshape(c, self.d).copy()
@@ -251,7 +284,7 @@ class OraclePF:
         slots = np.ascontiguousarray(slots, dtype=np.int64)
         ancs = np.ascontiguousarray(ancs, dtype=np.int64)
         states = np.ascontiguousarray(states, dtype=np.float64)
-        lib().orc_pf_resample_apply(self.h, L, slots.size, slots.ctypes.data_as(POINTER(c_int64)),
+        self.L.orc_pf_resample_apply(self.h, L, slots.size, slots.ctypes.data_as(POINTER(c_int64)),
                                     ancs.ctypes.data_as(POINTER(c_int64)), _d(states))
 
 

@@ -92,3 +92,52 @@ def test_gpu_regression_rejuvenation_bitexact(gh_ctx):
     assert gen.rejuvenate(st, 4090) + gen.rejuvenate(st, 10) == orc.rejuvenate(4090) + orc.rejuvenate(10)
     assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
     assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+
+
+# ------------------------------------------------ mh(trace, select(...))
+def test_oracle_single_address_mh_reaches_posterior():
+    """The quickstart's inference loop (examples/regression/quickstart.jl:17-22):
+    each iteration mh(trace, select(:slope)) then mh(trace, select(:intercept)),
+    one independent chain per particle.  The chains' states reproduce the
+    conjugate posterior; a move leaves the unselected address untouched."""
+    m, ys = _c1()
+    n = 1024
+    orc = O.OraclePF(m, n, 21)
+    orc.init(ys)
+    x0 = orc.state().copy()
+    orc.mh_select(1, 1)
+    x1 = orc.state()
+    assert np.array_equal(x1[1], x0[1]) and not np.array_equal(x1[0], x0[0])
+    orc.mh_select(2, 1)
+    assert np.array_equal(orc.state()[0], x1[0])
+    for _ in range(2000):  # prior proposals on a correlated posterior: ~1000 sweeps to mix
+        orc.mh_select(1, 1)
+        orc.mh_select(2, 1)
+    x = orc.state().T
+    mean, cov = m.posterior(ys)
+    sd = np.sqrt(np.diag(cov))
+    assert np.all(np.abs(x.mean(0) - mean) < 0.15 * sd), (x.mean(0), mean)  # MC error ~ sd / 32
+    assert np.allclose(np.sqrt(np.diag(np.cov(x.T))), sd, rtol=0.1)
+    with pytest.raises(RuntimeError):
+        orc.mh_select(4, 1)
+
+
+@pytest.mark.gpu
+def test_gpu_single_address_mh_bitexact(gh_ctx):
+    m, ys = _c1()
+    n = 3001
+    st = gen.initialize_particle_filter(m, (m.xs,), m.constraints(ys), n, seed=17)
+    orc = O.OraclePF(m, n, 17)
+    orc.init(ys)
+    for sel, mask in [(("slope",), 1), (("intercept",), 2), (("slope", "intercept"), 3), (("slope",), 1)]:
+        assert gen.mh(st, gen.select(*sel), 3) == orc.mh_select(mask, 3)
+        assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    with pytest.raises(gen.GenHipError):
+        gen.mh(st, gen.select("noise"))
+    # the quickstart loop: slope, intercept alternately, 2000 iterations
+    for _ in range(2000):
+        gen.mh(st, gen.select("slope"))
+        gen.mh(st, gen.select("intercept"))
+    x = st.states()
+    mean, cov = m.posterior(ys)
+    assert np.all(np.abs(x.mean(0) - mean) < 0.12 * np.sqrt(np.diag(cov)))

@@ -8,7 +8,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.argv = [sys.argv[0], "--steps", os.environ.get("GH_PROF_STEPS", "20"), "--warmup", "5", "--no-cpu-baseline"] + sys.argv[1:]
+sys.argv = [sys.argv[0], "--steps", os.environ.get("GH_PROF_STEPS", "20"), "--warmup", "5", "--no-cpu-baseline", "--no-secondary"] + sys.argv[1:]
 import bench  # noqa: E402
 
 bench.main()
