@@ -6,6 +6,7 @@ kernels spell every fused multiply-add as fma() and must not get extra ones.
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
@@ -16,9 +17,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgen_hip.so")
 SOURCES = [os.path.join(CSRC, "gh_api.hip")]
-HEADERS = [os.path.join(CSRC, f) for f in ("gh_math.h", "gh_models.h", "gh_kernels.h")] + [
-    os.path.join(ROOT, "include", "gen_hip.h")
-]
+HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "gen_hip.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GH_OFFLOAD_ARCH", "gfx950")

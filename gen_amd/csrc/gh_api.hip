@@ -22,6 +22,7 @@
 #include "gh_kernels.h"
 #include "gh_pmmh.h"
 #include "gh_coal.h"
+#include "gh_scores.h"
 #include "gh_rejuv.h"
 #include "gh_csmc.h"
 
@@ -384,6 +385,8 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     h.insert(h.end(), L0.begin(), L0.end());
     m->lg.dy = dy;
     m->lg.cstR = gauss_cst(dy, m->LR.data());
+    m->lg.cstQ = gauss_cst(d, LQ.data());
+    m->lg.cst0 = gauss_cst(d, L0.data());
     bool lq_diag = true, m_diag = dy == d;
     for (int i = 0; i < d; ++i)
       for (int j = 0; j < i; ++j) lq_diag = lq_diag && LQ[i * d + j] == 0.0;
@@ -480,6 +483,10 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     const double var = p[4] * p[4];
     m->reg.inv2v = 1.0 / (2.0 * var);
     m->reg.cst = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * var);
+    m->reg.inv2s = 1.0 / (2.0 * (p[1] * p[1]));
+    m->reg.csts = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
+    m->reg.inv2i = 1.0 / (2.0 * (p[3] * p[3]));
+    m->reg.csti = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (p[3] * p[3]));
     m->reg.n = n;
     for (int i = 0; i < n; ++i) m->reg.xs[i] = p[5 + i];
     h.push_back(0.0);
@@ -670,6 +677,7 @@ struct gh_pf {
   // rejuvenation (gh_pf_rejuvenate): the current step's observation and the
   // MH moves already applied at this step (their draw windows)
   StepObs last_obs{};
+  std::vector<StepObs> obs_hist;  // every step's observation (prior form), index t-1: trace scores
   uint32_t rejuv_moves = 0;
   unsigned long long* acc_count = nullptr;
   // the Gaussian custom proposal's last arguments (alpha, beta, gamma, sigma_q)
@@ -1206,6 +1214,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (rc) return fail(rc);
   pf->t = 1;
   pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
+  pf->obs_hist.assign(1, o_prior);
   *out = pf;
   return GH_OK;
 }
@@ -1285,6 +1294,8 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   pf->resample_calls = 0;
   pf->marks_pending = false;
   pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
+  if ((int)pf->obs_hist.size() < t) pf->obs_hist.resize(t);
+  pf->obs_hist[t - 1] = o_prior;
   pf->rejuv_moves = 0;
   return GH_OK;
 }
@@ -1756,6 +1767,77 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   hipFree(dxs);
   hipFree(dancs);
   return GH_OK;
+}
+
+// Trace score columns (gh_scores.h): per particle and step the latent's and
+// the observation's score, and the trace's total (get_score).
+extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
+  if (!pf || !total) return set_err(GH_E_INVAL, "null argument");
+  CHECK(materialize_marks(pf));
+  const int T = pf->t;
+  if (T < 1) return set_err(GH_E_STATE, "gh_pf_get_scores before init");
+  if (!pf->opts.record_history && T > 1) return set_err(GH_E_STATE, "gh_pf_get_scores needs record_history");
+  if (pf->ctx->world > 1 && T > 1)
+    return set_err(GH_E_STATE, "multi-rank: the genealogy before the current step is not materialised");
+  if ((int)pf->obs_hist.size() < T) return set_err(GH_E_STATE, "internal: observation history");
+  const int64_t n = pf->n;
+  if (n == 0) return GH_OK;
+  double *dtot = nullptr, *dper = nullptr;
+  const double** dxs = nullptr;
+  const int32_t** dancs = nullptr;
+  StepObs* dobs = nullptr;
+  auto cleanup = [&]() { hipFree(dtot); hipFree(dper); hipFree(dxs); hipFree(dancs); hipFree(dobs); };
+  std::vector<const double*> hx(T);
+  std::vector<const int32_t*> ha(T);
+  for (int s = 1; s <= T; ++s) {
+    hx[s - 1] = slot_x(pf, s);
+    ha[s - 1] = anc_for_step(pf, s);
+  }
+  if (hipMalloc(&dtot, sizeof(double) * n) != hipSuccess ||
+      hipMalloc(&dper, sizeof(double) * 2 * (size_t)T * n) != hipSuccess ||
+      hipMalloc(&dxs, sizeof(double*) * T) != hipSuccess || hipMalloc(&dancs, sizeof(int32_t*) * T) != hipSuccess ||
+      hipMalloc(&dobs, sizeof(StepObs) * T) != hipSuccess) {
+    cleanup();
+    return set_err(GH_E_NOMEM, "gh_pf_get_scores: %d steps x %lld particles", T, (long long)n);
+  }
+  int rc = GH_OK;
+  do {
+    if (hipMemcpyAsync(dxs, hx.data(), sizeof(double*) * T, hipMemcpyHostToDevice, pf->s) != hipSuccess ||
+        hipMemcpyAsync(dancs, ha.data(), sizeof(int32_t*) * T, hipMemcpyHostToDevice, pf->s) != hipSuccess ||
+        hipMemcpyAsync(dobs, pf->obs_hist.data(), sizeof(StepObs) * T, hipMemcpyHostToDevice, pf->s) != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_pf_get_scores: upload");
+      break;
+    }
+    ScoreArgs sa{};
+    sa.xs = dxs;
+    sa.ancs = dancs;
+    sa.res_before = pf->res_hist;
+    sa.anc_pending = (pf->ctx->world == 1 && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
+    sa.live = flags_live(pf);
+    sa.obs = dobs;
+    sa.n = n;
+    sa.T = T;
+    sa.per_step = dper;
+    sa.total = dtot;
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    // the model's own densities, whatever proposal made the particles
+    rc = with_model(pf->m, [&](auto model, const auto& p) {
+      hipLaunchKernelGGL(k_scores<decltype(model)>, grid, dim3(kBlock), 0, pf->s, (const double*)pf->m->dparams, p, sa,
+                         (const DevScalars*)pf->dev);
+    });
+    if (rc) break;
+    if (hipGetLastError() != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_pf_get_scores: launch");
+      break;
+    }
+    if (hipMemcpyAsync(total, dtot, sizeof(double) * n, hipMemcpyDeviceToHost, pf->s) != hipSuccess ||
+        (per_step && hipMemcpyAsync(per_step, dper, sizeof(double) * 2 * (size_t)T * n, hipMemcpyDeviceToHost, pf->s) !=
+                         hipSuccess) ||
+        hipStreamSynchronize(pf->s) != hipSuccess)
+      rc = set_err(GH_E_HIP, "gh_pf_get_scores: download");
+  } while (0);
+  cleanup();
+  return rc;
 }
 
 extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {

@@ -67,6 +67,7 @@ struct LGParams {
   int dy;
   double cstR;        // -0.5 (dy log 2pi + log det R)
   double cstS;        // -0.5 (dy log 2pi + log det S)
+  double cstQ, cst0;  // the same for Q and P0 (trace scores, gh_pf_get_scores)
   __device__ LGParams rebase(const double* __restrict__ prm) const {
     LGParams q = *this;
     q.A = rebased(*this, prm, A);
@@ -122,6 +123,37 @@ struct LGModel {
   }
 
   __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return obs(p, o, x); }
+
+  // the trace's choice scores of step t (Gen's per-choice score fields,
+  // static_ir/trace.jl:91-129): *lat = logpdf(mvnormal(A x_prev + b, Q), x)
+  // (t = 1: mvnormal(mu0, P0)) by forward substitution with the Cholesky factor
+  // (mvnormal.jl:12-16), *ob = logpdf(mvnormal(H x + c, R), y) (0 if unobserved)
+  __device__ static void score(const Params& p, const StepObs& o, uint32_t t, const double* xp, const double* x,
+                               double* lat, double* ob) {
+    const double* L = t == 1 ? p.L0 : p.LQ;
+    double u[D];
+    double quad = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double mean;
+      if (t == 1) {
+        mean = p.mu0[i];
+      } else {
+        mean = p.b[i];
+#pragma unroll
+        for (int k = 0; k < D; ++k) mean = fma(p.A[i * D + k], xp[k], mean);
+      }
+      double r = x[i] - mean;
+      if (t == 1 || !(S & 1)) {
+#pragma unroll
+        for (int k = 0; k < i; ++k) r = fma(-L[i * D + k], u[k], r);
+      }
+      u[i] = r / L[i * D + i];
+      quad = fma(u[i], u[i], quad);
+    }
+    *lat = (t == 1 ? p.cst0 : p.cstQ) - 0.5 * quad;
+    *ob = obs(p, o, x);
+  }
 
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
@@ -286,6 +318,13 @@ struct HMMModel {
   __device__ static double loglik(const Params& p, const StepObs& o, const double* x) {
     return o.present ? p.logE[o.sym * p.k + (int)x[0]] : 0.0;
   }
+  // categorical.jl:10-12: log prior[z] (t = 1) or log T[z | z_prev]; the emission
+  __device__ static void score(const Params& p, const StepObs& o, uint32_t t, const double* xp, const double* x,
+                               double* lat, double* ob) {
+    const int z = (int)x[0];
+    *lat = gh_log(t == 1 ? p.prior[z] : p.T[z * p.k + (int)xp[0]]);
+    *ob = loglik(p, o, x);
+  }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int proposal, double* x, Draw dr = {STREAM_INIT, 0}) {
     const u32x4 w = rng_block(seed, pid, 1, dr.stream, dr.base);
@@ -341,6 +380,20 @@ struct KitModel {
     return -(diff * diff) * p.inv2vy + p.csty;
   }
   __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return obs(p, o, x[0]); }
+  // normal.jl:56-60 for x_t | x_{t-1} (t = 1: normal(mu1, s1)) and y_t | x_t
+  __device__ static void score(const Params& p, const StepObs& o, uint32_t t, const double* xp, const double* x,
+                               double* lat, double* ob) {
+    double mean = p.mu1, inv2 = p.inv2v1, cst = p.cst1;
+    if (t > 1) {
+      const double v = xp[0];
+      mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
+      inv2 = p.inv2vx;
+      cst = p.cstx;
+    }
+    const double d = x[0] - mean;
+    *lat = -(d * d) * inv2 + cst;
+    *ob = obs(p, o, x[0]);
+  }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
     double z0, z1;
@@ -416,6 +469,7 @@ struct RegParams {
   double mu_s, sd_s, mu_i, sd_i;
   double inv2v;  // 1 / (2 sigma^2)
   double cst;    // -0.5 log(2 pi sigma^2)
+  double inv2s, csts, inv2i, csti;  // the same for the slope and intercept priors
   int n;
   double xs[kMaxObs];
   __device__ RegParams rebase(const double* __restrict__) const { return *this; }
@@ -442,6 +496,13 @@ struct RegModel {
     x[0] = p.mu_s + p.sd_s * z0;
     x[1] = p.mu_i + p.sd_i * z1;
     return loglik(p, o, x);
+  }
+  // :slope and :intercept scores (normal.jl:56-60) and the y's
+  __device__ static void score(const Params& p, const StepObs& o, uint32_t, const double*, const double* x,
+                               double* lat, double* ob) {
+    const double ds = x[0] - p.mu_s, di = x[1] - p.mu_i;
+    *lat = (-(ds * ds) * p.inv2s + p.csts) + (-(di * di) * p.inv2i + p.csti);
+    *ob = loglik(p, o, x);
   }
   // regenerate the selected addresses from their prior (bit 0 :slope, bit 1
   // :intercept; the same draws as init), keep the others: the proposal of

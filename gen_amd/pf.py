@@ -266,6 +266,11 @@ class ParticleTraces:
         raise KeyError(addr)
 
     def column(self, addr) -> np.ndarray:
+        if self.state.model.static:  # the regression: :slope, :intercept are the two latent components
+            comp = {("slope",): 0, ("intercept",): 1}.get(tuple(addr))
+            if comp is None:
+                raise KeyError(addr)
+            return self.step_states(1)[:, comp]
         t, kind = self._step_of(tuple(addr))
         if kind == "obs":
             raise KeyError(f"{addr} is an observation; it is constrained to the same value in every trace")
@@ -282,6 +287,20 @@ class ParticleTraces:
         if t not in self._cache:
             self._cache[t] = self.state.states(t)
         return self._cache[t]
+
+    def scores(self, per_step: bool = False):
+        """The traces' score columns, computed on the device from the history
+        (gh_pf_get_scores): get_score of every trace [n_local], and with
+        per_step the [t, 2, n_local] scores of each step's latent and
+        observation choices."""
+        key = "_scores_ps" if per_step else "_scores"
+        if key not in self._cache:
+            st = self.state
+            tot = np.empty(st.n_local)
+            ps = np.empty((st.t, 2, st.n_local)) if per_step else None
+            _lib.check(_lib.load().gh_pf_get_scores(st.h, _lib.dptr(tot), _lib.dptr(ps) if ps is not None else None))
+            self._cache[key] = (tot, ps) if per_step else tot
+        return self._cache[key]
 
 
 class _TraceView:
@@ -334,13 +353,47 @@ class _TraceView:
         return cm
 
     def get_score(self) -> float:
-        """get_score(trace) = log p(every choice), evaluated on the host from
-        the materialised trajectory (models.py `log_joint`)."""
+        """get_score(trace) = log p(every choice): the device score column
+        (gh_pf_get_scores) of this particle."""
+        return float(self.traces.scores()[self.i])
+
+    def project(self, selection) -> float:
+        """project(trace, selection) (src/static_ir/project.jl:8-28): the sum
+        of the selected choices' scores, from the device score columns (the
+        regression's :slope / :intercept scores separately on the host)."""
+        from .choicemap import Selection, select as _select
+
+        sel = selection if isinstance(selection, Selection) else _select(*selection)
         st = self.traces.state
-        xs = self.trajectory()
-        if st.model.static:
-            return st.model.log_joint(xs[0], st.observations.get(1))
-        return st.model.log_joint(xs if st.model.d > 1 else xs[:, 0], self._obs())
+        m = st.model
+        _, ps = self.traces.scores(per_step=True)
+        total = 0.0
+        for a in sel:
+            a = tuple(a)
+            if m.static:
+                x = self.trajectory()[0]
+                if a == ("slope",):
+                    total += _normal_lp(x[0], m.mu_s, m.sd_s)
+                elif a == ("intercept",):
+                    total += _normal_lp(x[1], m.mu_i, m.sd_i)
+                elif len(a) == 1 and isinstance(a[0], str) and a[0].startswith("y-"):
+                    i = int(a[0][2:]) - 1
+                    ys = st.observations.get(1)
+                    if ys is not None:
+                        total += _normal_lp(float(ys[i]), x[0] * m.xs[i] + x[1], m.sigma)
+                continue
+            for t in range(1, st.t + 1):
+                if a == tuple(m.latent_address(t)):
+                    total += ps[t - 1, 0, self.i]
+                elif a == tuple(m.obs_address(t)):
+                    total += ps[t - 1, 1, self.i]
+        return float(total)
+
+
+def _normal_lp(x, mu, sd) -> float:
+    """normal.jl:56-60"""
+    v = sd * sd
+    return float(-((x - mu) ** 2) / (2.0 * v) - 0.5 * np.log(2.0 * np.pi * v))
 
 
 # --------------------------------------------------------------- the API

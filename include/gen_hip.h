@@ -14,6 +14,7 @@
  *   gh_pf_get_states /
  *   gh_pf_get_trajectory    get_traces (SoA columns)     src/inference/particle_filter.jl:31-34
  *   gh_pf_get_parents       ParticleFilterState.parents  src/inference/particle_filter.jl:23
+ *   gh_pf_get_scores        get_score / per-choice scores src/static_ir/trace.jl:91-129
  *   gh_pf_sample_unweighted sample_unweighted_traces     src/inference/particle_filter.jl:62-70
  *   gh_pf_rejuvenate        mh(trace, select(x_t)) on    src/inference/mh.jl:14-26 (applied per
  *                           every particle               particle, as callers of the PF do)
@@ -196,6 +197,13 @@ int gh_pf_get_parents(gh_pf* pf, int64_t* host_out /* n_local, global ids */);
 /* latent of step t (1-based) of the current particles' traces: follows the
    genealogy back from the current step (record_history required) */
 int gh_pf_get_trajectory(gh_pf* pf, int t, double* host_out /* [d][n_local] */);
+/* The score columns of the current particles' traces (the per-choice score
+   fields of static_ir/trace.jl:91-129): total[i] = get_score(trace i), and
+   (nullable) per_step[t-1][0][i] / per_step[t-1][1][i] = the scores of the
+   latent :chain => t => :x and the observation :chain => t => :y (0 when not
+   observed) — the model's densities, whatever proposal made the particles.
+   Computed on the device from the history (record_history, one rank). */
+int gh_pf_get_scores(gh_pf* pf, double* total /* [n_local] */, double* per_step /* [t][2][n_local] */);
 int gh_pf_sample_unweighted(gh_pf* pf, int64_t n_samples, uint64_t seed, int64_t* host_idx);
 /* Rejuvenation: n_moves MH moves on every particle, each regenerating the
    current latent x_t from its prior given x_{t-1} (x_1 from the initial

@@ -317,7 +317,7 @@ static double gauss_cst(int d, const double* L) {
 typedef struct {
   int family, d, dy, k, v;
   /* LGSSM */
-  double *A, *b, *LQ, *M, *LR, *c, *mu0, *L0, cstR;
+  double *A, *b, *LQ, *M, *LR, *c, *mu0, *L0, cstR, cstQ, cst0;
   int lq_diag, m_diag;  /* exact-zero structure: skipped terms */
   /* locally optimal proposal p(x_t | x_{t-1}, y_t): S = H Q H^T + R,
      K^T = S^{-1} H Q, F = I - K H, Sigma = F Q; at t = 1 the same with P0 */
@@ -331,7 +331,7 @@ typedef struct {
   double mu1, s1, sx, inv2vy, csty, inv2vx, cstx, inv2v1, cst1;
   double qa[6];
   /* regression (quickstart.jl:3-9): priors, 1/(2 sigma^2), -0.5 log(2 pi sigma^2), xs */
-  double mu_s, sd_s, mu_i, sd_i, inv2v, cst;
+  double mu_s, sd_s, mu_i, sd_i, inv2v, cst, inv2s, csts, inv2i, csti;
   double xs[32];
 } model_t;
 
@@ -398,6 +398,8 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->L0 = malloc(sizeof(double) * d * d);
     if (chol(d, P0, m->L0)) return -2;
     m->cstR = gauss_cst(dy, m->LR);
+    m->cstQ = gauss_cst(d, m->LQ);
+    m->cst0 = gauss_cst(d, m->L0);
     m->lq_diag = 1;
     for (int i = 0; i < d; ++i)
       for (int j = 0; j < i; ++j) if (m->LQ[i * d + j] != 0.0) m->lq_diag = 0;
@@ -452,6 +454,10 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     double var = p[4] * p[4];
     m->inv2v = 1.0 / (2.0 * var);
     m->cst = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * var);
+    m->inv2s = 1.0 / (2.0 * (p[1] * p[1]));
+    m->csts = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
+    m->inv2i = 1.0 / (2.0 * (p[3] * p[3]));
+    m->csti = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (p[3] * p[3]));
     for (int i = 0; i < dy; ++i) m->xs[i] = p[5 + i];
   } else {
     return -1;
@@ -724,6 +730,7 @@ struct orc_pf {
   double** hx;
   int32_t** hanc;
   int* hres;
+  obs_t* hobs;          /* every step's observation (trace scores) */
 };
 
 orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* params, int64_t np,
@@ -745,7 +752,7 @@ orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* par
 void orc_pf_destroy(orc_pf* pf) {
   if (!pf) return;
   for (int i = 0; i < pf->cap; ++i) { free(pf->hx[i]); free(pf->hanc[i]); }
-  free(pf->hx); free(pf->hanc); free(pf->hres);
+  free(pf->hx); free(pf->hanc); free(pf->hres); free(pf->hobs);
   free(pf->x); free(pf->xprev); free(pf->anc_state); free(pf->logw); free(pf->anc);
   model_free(&pf->m);
   free(pf);
@@ -760,12 +767,14 @@ static void record(orc_pf* pf) {
     pf->hx = realloc(pf->hx, sizeof(double*) * nc);
     pf->hanc = realloc(pf->hanc, sizeof(int32_t*) * nc);
     pf->hres = realloc(pf->hres, sizeof(int) * nc);
+    pf->hobs = realloc(pf->hobs, sizeof(obs_t) * nc);
     for (int i = pf->cap; i < nc; ++i) { pf->hx[i] = NULL; pf->hanc[i] = NULL; pf->hres[i] = 0; }
     pf->cap = nc;
   }
   size_t sz = (size_t)pf->m.d * pf->n;
   pf->hx[t - 1] = malloc(sizeof(double) * sz);
   memcpy(pf->hx[t - 1], pf->x, sizeof(double) * sz);
+  pf->hobs[t - 1] = pf->obs;
 }
 
 static double model_loglik(const model_t* m, const obs_t* o, const double* x);
@@ -1103,6 +1112,86 @@ void orc_pf_get_state(orc_pf* pf, double* out) {
 }
 void orc_pf_get_parents(orc_pf* pf, int64_t* out) { memcpy(out, pf->anc, sizeof(int64_t) * pf->n); }
 int orc_pf_num_steps(orc_pf* pf) { return pf->t; }
+
+/* The scores of one step's choices under the model (the per-choice score
+   fields of src/static_ir/trace.jl:91-129): the latent x_t | x_{t-1} (t = 1:
+   the initial distribution) and the observation y_t | x_t; the densities of
+   mvnormal.jl:12-16 (forward substitution with the Cholesky factor),
+   normal.jl:56-60, categorical.jl:10-12. */
+static void model_score(const model_t* m, const obs_t* o, int t, const double* xp, const double* x, double* lat,
+                        double* ob) {
+  if (m->family == ORC_LGSSM) {
+    int d = m->d;
+    const double* L = t == 1 ? m->L0 : m->LQ;
+    double u[64], quad = 0.0;
+    for (int i = 0; i < d; ++i) {
+      double mean;
+      if (t == 1) {
+        mean = m->mu0[i];
+      } else {
+        mean = m->b[i];
+        for (int k = 0; k < d; ++k) mean = fma(m->A[i * d + k], xp[k], mean);
+      }
+      double r = x[i] - mean;
+      if (t == 1 || !m->lq_diag)
+        for (int k = 0; k < i; ++k) r = fma(-L[i * d + k], u[k], r);
+      u[i] = r / L[i * d + i];
+      quad = fma(u[i], u[i], quad);
+    }
+    *lat = (t == 1 ? m->cst0 : m->cstQ) - 0.5 * quad;
+  } else if (m->family == ORC_KITAGAWA) {
+    double mean = m->mu1, inv2 = m->inv2v1, cst = m->cst1;
+    if (t > 1) {
+      double v = xp[0];
+      mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o->ct;
+      inv2 = m->inv2vx;
+      cst = m->cstx;
+    }
+    double dd = x[0] - mean;
+    *lat = -(dd * dd) * inv2 + cst;
+  } else if (m->family == ORC_HMM) {
+    int z = (int)x[0];
+    *lat = orc_log(t == 1 ? m->prior[z] : m->T[z * m->k + (int)xp[0]]);
+  } else {
+    double ds = x[0] - m->mu_s, di = x[1] - m->mu_i;
+    *lat = (-(ds * ds) * m->inv2s + m->csts) + (-(di * di) * m->inv2i + m->csti);
+  }
+  *ob = model_loglik(m, o, x);
+}
+
+/* get_score of every current particle's trace along its genealogy, with the
+   per-step latent / observation scores (per_step [t][2][n], nullable) */
+int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step) {
+  if (pf->t < 1 || (!pf->record_history && pf->t > 1) || pf->lo != 0 || pf->n != pf->n_global) return -1;
+  const int T = pf->t, D = pf->m.d;
+  const int64_t n = pf->n;
+  double* ps = per_step ? per_step : malloc(sizeof(double) * 2 * (size_t)T * (n ? n : 1));
+  for (int64_t j = 0; j < n; ++j) {
+    int64_t idx = pf->pending ? pf->anc[j] - pf->lo : j;
+    double x[64], xp[64];
+    const double* cur = pf->record_history ? pf->hx[T - 1] : pf->x;
+    for (int k = 0; k < D; ++k) x[k] = cur[(size_t)k * n + idx];
+    for (int s = T; s >= 1; --s) {
+      int64_t parent = idx;
+      if (s > 1) {
+        if (pf->hres[s - 1]) parent = pf->hanc[s - 1][idx];
+        for (int k = 0; k < D; ++k) xp[k] = pf->hx[s - 2][(size_t)k * n + parent];
+      }
+      const obs_t* o = pf->record_history ? &pf->hobs[s - 1] : &pf->obs;
+      double lat, ob;
+      model_score(&pf->m, o, s, xp, x, &lat, &ob);
+      ps[((size_t)(s - 1) * 2) * n + j] = lat;
+      ps[((size_t)(s - 1) * 2 + 1) * n + j] = ob;
+      for (int k = 0; k < D; ++k) x[k] = xp[k];
+      idx = parent;
+    }
+    double tot = 0.0;
+    for (int s = 1; s <= T; ++s) tot += ps[((size_t)(s - 1) * 2) * n + j] + ps[((size_t)(s - 1) * 2 + 1) * n + j];
+    total[j] = tot;
+  }
+  if (!per_step) free(ps);
+  return 0;
+}
 
 int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* resampled) {
   if (!pf->record_history || t < 1 || t > pf->t) return -1;

@@ -83,6 +83,9 @@ void orc_pf_get_state(orc_pf* pf, double* out);           /* [d][n_local] */
 void orc_pf_get_parents(orc_pf* pf, int64_t* out);        /* n_local, global ids */
 int orc_pf_num_steps(orc_pf* pf);
 int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* resampled);
+/* get_score of every current particle's trace (total [n]) and the per-step
+   latent / observation choice scores (per_step [t][2][n], nullable); one shard */
+int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step);
 
 /* distributed building blocks (sharded oracle, exercised with gloo) */
 void orc_pf_local_stats(orc_pf* pf, double out[3]);      /* (max, sum e, sum e^2) local */

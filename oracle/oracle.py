@@ -87,6 +87,7 @@ def _load(path):
             "orc_pf_get_parents": (None, [V, POINTER(c_int64)]),
             "orc_pf_num_steps": (I, [V]),
             "orc_pf_get_history": (I, [V, I, D, POINTER(c_int32), POINTER(c_int)]),
+            "orc_pf_get_scores": (I, [V, D, D]),
             "orc_pf_local_stats": (None, [V, D]),
             "orc_combine_stats": (I, [D, I, I64, c_double, D, D, D]),
             "orc_pf_local_qtotal": (U64, [V, c_double]),
@@ -248,6 +249,14 @@ class OraclePF:
         if rc:
             raise ValueError("no history")
         return x, (anc if res.value else None)
+
+    def scores(self, per_step=False):
+        """get_score of every particle's trace (and the [t, 2, n] choice scores)."""
+        tot = np.empty(self.n)
+        ps = np.empty((self.L.orc_pf_num_steps(self.h), 2, self.n)) if per_step else None
+        if self.L.orc_pf_get_scores(self.h, _d(tot), _d(ps)):
+            raise ValueError("oracle: scores need the history on one shard")
+        return (tot, ps) if per_step else tot
 
     def trajectory(self, t):
         """latent of step t along the genealogy of the current particles (single rank)."""
