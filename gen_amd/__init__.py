@@ -38,6 +38,7 @@ from .pf import (
     sample_unweighted_traces,
     set_default_context,
 )
+from .simulate import SimulatedTraces, simulate
 from ._lib import GenHipError
 
 __all__ = [
@@ -48,5 +49,5 @@ __all__ = [
     "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
     "conditional_particle_filter_step", "conditional_smc", "get_particle", "initialize_conditional_particle_filter",
     "particle_gibbs", "GenHipError", "ObservationBatch", "prepare_observations", "Selection", "select",
-    "metropolis_hastings", "mh",
+    "metropolis_hastings", "mh", "simulate", "SimulatedTraces",
 ]

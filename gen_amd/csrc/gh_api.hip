@@ -23,6 +23,7 @@
 #include "gh_pmmh.h"
 #include "gh_coal.h"
 #include "gh_scores.h"
+#include "gh_simulate.h"
 #include "gh_rejuv.h"
 #include "gh_csmc.h"
 
@@ -446,6 +447,10 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     h.insert(h.end(), LSig.begin(), LSig.end());
     h.insert(h.end(), WA.begin(), WA.end());
     h.insert(h.end(), LSig1.begin(), LSig1.end());
+    // simulate(): H | c | L_R
+    h.insert(h.end(), H, H + dy * d);
+    h.insert(h.end(), c, c + dy);
+    h.insert(h.end(), m->LR.begin(), m->LR.end());
   } else if (desc->family == GH_FAMILY_HMM) {
     const int K = desc->k, V = desc->v;
     if (K < 1 || K > 64 || V < 1) return fail(GH_E_INVAL, "HMM: need 1 <= k <= 64, v >= 1");
@@ -468,6 +473,7 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->kit.cstx = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * p[2]);
     m->kit.inv2v1 = 1.0 / (2.0 * (p[1] * p[1]));
     m->kit.cst1 = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
+    m->kit.sy = sqrt(p[3]);
     h.push_back(0.0);
   } else if (desc->family == GH_FAMILY_REGRESSION) {
     const int n = desc->dy;
@@ -487,6 +493,7 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->reg.csts = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
     m->reg.inv2i = 1.0 / (2.0 * (p[3] * p[3]));
     m->reg.csti = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (p[3] * p[3]));
+    m->reg.sigma = p[4];
     m->reg.n = n;
     for (int i = 0; i < n; ++i) m->reg.xs[i] = p[5 + i];
     h.push_back(0.0);
@@ -509,7 +516,10 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->lg.FA = q; q += d * d;
     m->lg.LSig = q; q += d * d;
     m->lg.WA = q; q += dy * d;
-    m->lg.LSig1 = q;
+    m->lg.LSig1 = q; q += d * d;
+    m->lg.H = q; q += dy * d;
+    m->lg.cv = q; q += dy;
+    m->lg.LR = q;
   } else if (m->family == GH_FAMILY_HMM) {
     const int K = m->k, V = m->v;
     m->hmm.base = m->dparams;
@@ -1837,6 +1847,66 @@ extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
       rc = set_err(GH_E_HIP, "gh_pf_get_scores: download");
   } while (0);
   cleanup();
+  return rc;
+}
+
+// simulate(model, (T,)) for n independent traces (gh_simulate.h).
+extern "C" int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double* xs, double* ys, double* per_step,
+                           double* total) {
+  if (!m) return set_err(GH_E_INVAL, "gh_simulate: null model");
+  if (T < 1) return set_err(GH_E_INVAL, "gh_simulate: T = %d (need >= 1)", T);
+  if (m->family == GH_FAMILY_REGRESSION && T != 1)
+    return set_err(GH_E_INVAL, "gh_simulate: the regression model has no time steps (T = 1)");
+  if (n < 0 || n > INT32_MAX) return set_err(GH_E_INVAL, "gh_simulate: n = %lld", (long long)n);
+  if (n == 0) return GH_OK;
+  HIP_TRY(hipSetDevice(m->ctx->device));
+  const int d = m->d;
+  const int dy = (m->family == GH_FAMILY_LGSSM || m->family == GH_FAMILY_REGRESSION) ? m->dy : 1;
+  std::vector<StepObs> hobs(T);
+  for (int t = 1; t <= T; ++t) CHECK(make_obs(m, t, nullptr, &hobs[t - 1]));
+  const size_t nx = (size_t)T * d * n, ny = (size_t)T * dy * n, ns = (size_t)T * 2 * n;
+  double* buf = nullptr;
+  StepObs* dobs = nullptr;
+  if (hipMalloc(&buf, sizeof(double) * (nx + ny + ns + n)) != hipSuccess ||
+      hipMalloc(&dobs, sizeof(StepObs) * T) != hipSuccess) {
+    hipFree(buf);
+    return set_err(GH_E_NOMEM, "gh_simulate: %d steps x %lld traces", T, (long long)n);
+  }
+  hipStream_t s = m->ctx->stream;
+  int rc = GH_OK;
+  do {
+    if (hipMemcpyAsync(dobs, hobs.data(), sizeof(StepObs) * T, hipMemcpyHostToDevice, s) != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_simulate: upload");
+      break;
+    }
+    SimArgs a{};
+    a.seed = seed;
+    a.n = n;
+    a.T = T;
+    a.dy = dy;
+    a.obs = dobs;
+    a.xs = buf;
+    a.ys = buf + nx;
+    a.per_step = buf + nx + ny;
+    a.total = buf + nx + ny + ns;
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    rc = with_model(m, [&](auto model, const auto& p) {
+      hipLaunchKernelGGL(k_simulate<decltype(model)>, grid, dim3(kBlock), 0, s, (const double*)m->dparams, p, a);
+    });
+    if (rc) break;
+    if (hipGetLastError() != hipSuccess) {
+      rc = set_err(GH_E_HIP, "gh_simulate: launch");
+      break;
+    }
+    if ((xs && hipMemcpyAsync(xs, a.xs, sizeof(double) * nx, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (ys && hipMemcpyAsync(ys, a.ys, sizeof(double) * ny, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (per_step && hipMemcpyAsync(per_step, a.per_step, sizeof(double) * ns, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        (total && hipMemcpyAsync(total, a.total, sizeof(double) * n, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+        hipStreamSynchronize(s) != hipSuccess)
+      rc = set_err(GH_E_HIP, "gh_simulate: download");
+  } while (0);
+  hipFree(buf);
+  hipFree(dobs);
   return rc;
 }
 

@@ -78,7 +78,9 @@ enum : uint32_t {
   STREAM_SAMPLE = 4,     // sample_unweighted_traces
   STREAM_IS = 5,         // importance sampling
   STREAM_MH = 6,         // MH proposals / accept tests
+  STREAM_SIM = 7,        // simulate(): latents from draw 0, observations from draw kSimObsDraw
 };
+constexpr uint32_t kSimObsDraw = 32;
 
 GH_HD u32x4 rng_block(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream,
                       uint32_t draw) {
@@ -443,6 +445,31 @@ __device__ __forceinline__ void normals_n(uint64_t seed, uint64_t id, uint32_t s
     box_muller(wd[3 * p], wd[3 * p + 1], wd[3 * p + 2], &a, &c, tab);
     z[2 * p] = a;
     if (2 * p + 1 < N) z[2 * p + 1] = c;
+  }
+}
+
+// normals_n with a run-time count (n <= 64): the same word layout, each block
+// generated when its first word is needed
+__device__ __forceinline__ void normals_rt(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream,
+                                           uint32_t draw0, int n, double* z, const double* tab = nullptr) {
+  u32x4 w{0, 0, 0, 0};
+  int cur = -1;
+  for (int p = 0; 2 * p < n; ++p) {
+    uint32_t wd[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int k = 3 * p + q;
+      if ((k >> 2) != cur) {
+        cur = k >> 2;
+        w = rng_block(seed, id, step, stream, draw0 + (uint32_t)cur);
+      }
+      const int e = k & 3;
+      wd[q] = e == 0 ? w.x : (e == 1 ? w.y : (e == 2 ? w.z : w.w));
+    }
+    double a, c;
+    box_muller(wd[0], wd[1], wd[2], &a, &c, tab);
+    z[2 * p] = a;
+    if (2 * p + 1 < n) z[2 * p + 1] = c;
   }
 }
 #endif

@@ -64,6 +64,9 @@ struct LGParams {
   const double* LSig; // d*d chol(Sigma), Sigma = F Q
   const double* WA;   // dy*d L_S^{-1} H A
   const double* LSig1;// d*d chol((I - K_1 H) P0), the t = 1 proposal
+  const double* H;    // dy*d  observation matrix  (simulate: y = H x + c + L_R z)
+  const double* cv;   // dy    observation offset c
+  const double* LR;   // dy*dy lower Cholesky factor of R
   int dy;
   double cstR;        // -0.5 (dy log 2pi + log det R)
   double cstS;        // -0.5 (dy log 2pi + log det S)
@@ -80,6 +83,9 @@ struct LGParams {
     q.LSig = rebased(*this, prm, LSig);
     q.WA = rebased(*this, prm, WA);
     q.LSig1 = rebased(*this, prm, LSig1);
+    q.H = rebased(*this, prm, H);
+    q.cv = rebased(*this, prm, cv);
+    q.LR = rebased(*this, prm, LR);
     return q;
   }
 };
@@ -153,6 +159,41 @@ struct LGModel {
     }
     *lat = (t == 1 ? p.cst0 : p.cstQ) - 0.5 * quad;
     *ob = obs(p, o, x);
+  }
+
+  // simulate()'s observation (static_ir/simulate.jl:23-34: value = random,
+  // score = logpdf of that value): y = H x + c + L_R z written with stride ys,
+  // scored as the filter scores a given y (make_obs: v = L_R^{-1}(y - c); obs())
+  __device__ static double sim_obs(const Params& p, uint64_t seed, uint64_t pid, uint32_t t, const double* x,
+                                   double* y, int64_t ys, const double* tab) {
+    double z[kMaxObs], v[kMaxObs];
+    normals_rt(seed, pid, t, STREAM_SIM, kSimObsDraw, p.dy, z, tab);
+    for (int r = 0; r < p.dy; ++r) {
+      double acc = p.cv[r];
+#pragma unroll
+      for (int j = 0; j < D; ++j) acc = fma(p.H[r * D + j], x[j], acc);
+      for (int k = 0; k <= r; ++k) acc = fma(p.LR[r * p.dy + k], z[k], acc);
+      y[r * ys] = acc;
+      double s = acc - p.cv[r];
+      for (int k = 0; k < r; ++k) s = fma(-p.LR[r * p.dy + k], v[k], s);
+      v[r] = s / p.LR[r * p.dy + r];
+    }
+    double quad = 0.0;
+    if (S & 2) {
+#pragma unroll
+      for (int r = 0; r < D; ++r) {
+        const double acc = fma(-p.M[r * D + r], x[r], v[r]);
+        quad = fma(acc, acc, quad);
+      }
+    } else {
+      for (int r = 0; r < p.dy; ++r) {
+        double acc = v[r];
+#pragma unroll
+        for (int j = 0; j < D; ++j) acc = fma(-p.M[r * D + j], x[j], acc);
+        quad = fma(acc, acc, quad);
+      }
+    }
+    return p.cstR - 0.5 * quad;
   }
 
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
@@ -325,6 +366,15 @@ struct HMMModel {
     *lat = gh_log(t == 1 ? p.prior[z] : p.T[z * p.k + (int)xp[0]]);
     *ob = loglik(p, o, x);
   }
+  // simulate(): the symbol ~ categorical(E[:, z]) and its log emission
+  __device__ static double sim_obs(const Params& p, uint64_t seed, uint64_t pid, uint32_t t, const double* x,
+                                   double* y, int64_t, const double*) {
+    const int z = (int)x[0];
+    const u32x4 w = rng_block(seed, pid, t, STREAM_SIM, kSimObsDraw);
+    const int sym = cat_sample(p.E + z, p.v, p.k, u53(w.x, w.y));
+    y[0] = (double)sym;
+    return p.logE[sym * p.k + z];
+  }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int proposal, double* x, Draw dr = {STREAM_INIT, 0}) {
     const u32x4 w = rng_block(seed, pid, 1, dr.stream, dr.base);
@@ -366,6 +416,7 @@ struct KitParams {
   double csty;      // -0.5 log(2 pi var_y)
   double inv2vx, cstx;  // the prior densities (Gaussian custom proposal's weight): 1/(2 var_x), -0.5 log(2 pi var_x)
   double inv2v1, cst1;  //   and at t = 1: 1/(2 s1^2), -0.5 log(2 pi s1^2)
+  double sy;            // sqrt(var_y) (simulate)
   __device__ KitParams rebase(const double* __restrict__) const { return *this; }
 };
 
@@ -393,6 +444,16 @@ struct KitModel {
     const double d = x[0] - mean;
     *lat = -(d * d) * inv2 + cst;
     *ob = obs(p, o, x[0]);
+  }
+  // simulate(): y ~ normal(x^2 / 20, sqrt(var_y)) (examples/pmmh/model.jl) and its logpdf
+  __device__ static double sim_obs(const Params& p, uint64_t seed, uint64_t pid, uint32_t t, const double* x,
+                                   double* y, int64_t, const double* tab) {
+    double z0, z1;
+    normal_pair(rng_block(seed, pid, t, STREAM_SIM, kSimObsDraw), &z0, &z1, tab);
+    const double m = x[0] * x[0] / 20.0;
+    y[0] = m + p.sy * z0;
+    const double diff = y[0] - m;
+    return -(diff * diff) * p.inv2vy + p.csty;
   }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
@@ -470,6 +531,7 @@ struct RegParams {
   double inv2v;  // 1 / (2 sigma^2)
   double cst;    // -0.5 log(2 pi sigma^2)
   double inv2s, csts, inv2i, csti;  // the same for the slope and intercept priors
+  double sigma;
   int n;
   double xs[kMaxObs];
   __device__ RegParams rebase(const double* __restrict__) const { return *this; }
@@ -503,6 +565,21 @@ struct RegModel {
     const double ds = x[0] - p.mu_s, di = x[1] - p.mu_i;
     *lat = (-(ds * ds) * p.inv2s + p.csts) + (-(di * di) * p.inv2i + p.csti);
     *ob = loglik(p, o, x);
+  }
+  // simulate(): y_i ~ normal(slope x_i + intercept, sigma) and their logpdfs in data order
+  __device__ static double sim_obs(const Params& p, uint64_t seed, uint64_t pid, uint32_t t, const double* x,
+                                   double* y, int64_t ys, const double* tab) {
+    double z[kMaxObs];
+    normals_rt(seed, pid, t, STREAM_SIM, kSimObsDraw, p.n, z, tab);
+    double s = 0.0;
+    for (int i = 0; i < p.n; ++i) {
+      const double m = x[0] * p.xs[i] + x[1];
+      const double yi = m + p.sigma * z[i];
+      y[i * ys] = yi;
+      const double diff = yi - m;
+      s += -(diff * diff) * p.inv2v + p.cst;
+    }
+    return s;
   }
   // regenerate the selected addresses from their prior (bit 0 :slope, bit 1
   // :intercept; the same draws as init), keep the others: the proposal of

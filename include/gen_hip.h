@@ -27,6 +27,8 @@
  *                           likelihood)                   examples/pmmh/pf.jl:14-73
  *   gh_coal_run             involutive (RJ) MH chains     examples/coal/coal.jl:126-336,
  *                                                         src/inference/mh.jl:85-98
+ *   gh_simulate             simulate(model, (T,)) for N  src/static_ir/simulate.jl:23-34,50-83,
+ *                           traces                       src/modeling_library/unfold/simulate.jl
  *   gh_model_create         a Static-DSL model + Unfold  src/static_ir/, src/modeling_library/unfold/
  *
  * Conventions
@@ -164,6 +166,18 @@ int gh_ctx_synchronize(gh_ctx* ctx);
 int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model** out);
 int gh_model_destroy(gh_model* m);
 int gh_model_state_dim(const gh_model* m, int* d);
+/* simulate(model, (T,)) n times (static_ir/simulate.jl:23-34: every choice
+   sampled from its distribution, score += logpdf of the sampled value; the
+   Unfold runs its kernel T times).  Trace i draws from (seed, i, t, simulate
+   stream), independent of n.  Outputs (host, each nullable, time-major):
+     xs[t-1][k][i]        latent component k of :chain => t => :x (regression: slope, intercept)
+     ys[t-1][r][i]        observation component r of :chain => t => :y (HMM: the symbol;
+                          regression: y-(r+1)); r < dy (1 for HMM and Kitagawa)
+     per_step[t-1][0|1][i] the latent's / the observation's score
+     total[i]             get_score(trace i), the scores summed in time order
+   The regression model takes T = 1. */
+int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double* xs, double* ys, double* per_step,
+                double* total);
 
 /* ---- particle filter -------------------------------------------------------- */
 void gh_pf_opts_default(gh_pf_opts* o);

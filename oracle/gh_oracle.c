@@ -50,7 +50,8 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
   out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-enum { S_INIT = 1, S_STEP = 2, S_RESAMPLE = 3, S_SAMPLE = 4, S_IS = 5, S_MH = 6 };
+enum { S_INIT = 1, S_STEP = 2, S_RESAMPLE = 3, S_SAMPLE = 4, S_IS = 5, S_MH = 6, S_SIM = 7 };
+enum { SIM_OBS_DRAW = 32 };
 
 static void rng(uint64_t seed, uint64_t id, uint32_t step, uint32_t stream, uint32_t draw,
                 uint32_t out[4]) {
@@ -328,10 +329,10 @@ typedef struct {
   /* Kitagawa; the prior densities for the Gaussian custom proposal's weight,
      and that proposal's arguments (alpha, beta, gamma, sigma_q) with
      1/(2 sigma_q^2), -0.5 log(2 pi sigma_q^2) */
-  double mu1, s1, sx, inv2vy, csty, inv2vx, cstx, inv2v1, cst1;
+  double mu1, s1, sx, sy, inv2vy, csty, inv2vx, cstx, inv2v1, cst1;
   double qa[6];
   /* regression (quickstart.jl:3-9): priors, 1/(2 sigma^2), -0.5 log(2 pi sigma^2), xs */
-  double mu_s, sd_s, mu_i, sd_i, inv2v, cst, inv2s, csts, inv2i, csti;
+  double mu_s, sd_s, mu_i, sd_i, sigma, inv2v, cst, inv2s, csts, inv2i, csti;
   double xs[32];
 } model_t;
 
@@ -441,6 +442,7 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->d = 1;
     m->mu1 = p[0]; m->s1 = p[1];
     m->sx = sqrt(p[2]);
+    m->sy = sqrt(p[3]);
     m->inv2vy = 1.0 / (2.0 * p[3]);
     m->csty = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * p[3]);
     m->inv2vx = 1.0 / (2.0 * p[2]);
@@ -451,6 +453,7 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     if (dy < 1 || dy > 32 || np < 5 + (int64_t)dy) return -1;
     m->d = 2;
     m->mu_s = p[0]; m->sd_s = p[1]; m->mu_i = p[2]; m->sd_i = p[3];
+    m->sigma = p[4];
     double var = p[4] * p[4];
     m->inv2v = 1.0 / (2.0 * var);
     m->cst = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * var);
@@ -1190,6 +1193,66 @@ int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step) {
     total[j] = tot;
   }
   if (!per_step) free(ps);
+  return 0;
+}
+
+/* simulate(model, (T,)) for n traces (static_ir/simulate.jl:23-34, 50-83;
+   unfold/simulate.jl): per step the latent is drawn as generate / update draw
+   it (particle_init / particle_step, stream S_SIM, no observation), then the
+   observation from draw SIM_OBS_DRAW on, scored as a given observation is
+   (obs_build + model_loglik); the latent's score is model_score's.  Outputs
+   time-major: xs[t][k][n], ys[t][r][n], per_step[t][2][n], total[n]. */
+int orc_simulate(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T, int64_t n,
+                 uint64_t seed, double* xs, double* ys, double* per_step, double* total) {
+  model_t m;
+  if (model_build(&m, family, d, dy, k, v, params, np) || T < 1 || (family == ORC_REGRESSION && T != 1)) {
+    model_free(&m);
+    return -1;
+  }
+  const int D = m.d, DY = (family == ORC_LGSSM || family == ORC_REGRESSION) ? m.dy : 1;
+#pragma omp parallel for schedule(static)
+  for (int64_t j = 0; j < n; ++j) {
+    double x[64], xp[64] = {0}, y[64], z[64];
+    double tot = 0.0;
+    for (int t = 1; t <= T; ++t) {
+      obs_t none, oy;
+      obs_build(&m, t, NULL, 0, &none);
+      if (t == 1) particle_init(&m, seed, (uint64_t)j, &none, 0, x, S_SIM, 0);
+      else particle_step(&m, seed, (uint64_t)j, (uint32_t)t, &none, 0, xp, x, S_SIM, 0);
+      if (family == ORC_LGSSM) {
+        normals_at(seed, (uint64_t)j, (uint32_t)t, S_SIM, SIM_OBS_DRAW, DY, z);
+        for (int r = 0; r < DY; ++r) {
+          double acc = m.c[r];
+          for (int q = 0; q < D; ++q) acc = fma(m.H[r * D + q], x[q], acc);
+          for (int q = 0; q <= r; ++q) acc = fma(m.LR[r * DY + q], z[q], acc);
+          y[r] = acc;
+        }
+      } else if (family == ORC_HMM) {
+        uint32_t w[4];
+        rng(seed, (uint64_t)j, (uint32_t)t, S_SIM, SIM_OBS_DRAW, w);
+        y[0] = (double)cat_sample(m.E + (int)x[0], m.v, m.k, unif53(w[0], w[1]));
+      } else if (family == ORC_KITAGAWA) {
+        normals_at(seed, (uint64_t)j, (uint32_t)t, S_SIM, SIM_OBS_DRAW, 1, z);
+        y[0] = x[0] * x[0] / 20.0 + m.sy * z[0];
+      } else {
+        normals_at(seed, (uint64_t)j, (uint32_t)t, S_SIM, SIM_OBS_DRAW, DY, z);
+        for (int i = 0; i < DY; ++i) y[i] = (x[0] * m.xs[i] + x[1]) + m.sigma * z[i];
+      }
+      obs_build(&m, t, y, 1, &oy);
+      double lat, ob;
+      model_score(&m, &oy, t, xp, x, &lat, &ob);
+      if (xs) for (int q = 0; q < D; ++q) xs[((size_t)(t - 1) * D + q) * n + j] = x[q];
+      if (ys) for (int r = 0; r < DY; ++r) ys[((size_t)(t - 1) * DY + r) * n + j] = y[r];
+      if (per_step) {
+        per_step[((size_t)(t - 1) * 2) * n + j] = lat;
+        per_step[((size_t)(t - 1) * 2 + 1) * n + j] = ob;
+      }
+      tot += lat + ob;
+      for (int q = 0; q < D; ++q) xp[q] = x[q];
+    }
+    if (total) total[j] = tot;
+  }
+  model_free(&m);
   return 0;
 }
 

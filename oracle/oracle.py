@@ -88,6 +88,7 @@ def _load(path):
             "orc_pf_num_steps": (I, [V]),
             "orc_pf_get_history": (I, [V, I, D, POINTER(c_int32), POINTER(c_int)]),
             "orc_pf_get_scores": (I, [V, D, D]),
+            "orc_simulate": (I, [I, I, I, I, I, D, I64, I, I64, U64, D, D, D, D]),
             "orc_pf_local_stats": (None, [V, D]),
             "orc_combine_stats": (I, [D, I, I64, c_double, D, D, D]),
             "orc_pf_local_qtotal": (U64, [V, c_double]),
@@ -317,6 +318,18 @@ def importance_sampling(model, y, n, seed, proposal=DEFAULT):
     if rc:
         raise ValueError("oracle IS failed")
     return st, lnw, lml.value
+
+
+def simulate(model, T, n, seed):
+    """simulate(model, (T,)) n times: (xs [T, d, n], ys [T, dy, n], per_step [T, 2, n], total [n])."""
+    fam, d, dy, k, v, p = model_args(model)
+    dd = d if fam in (LGSSM, REGRESSION) else 1
+    ddy = dy if fam in (LGSSM, REGRESSION) else 1
+    xs, ys = np.empty((T, dd, n)), np.empty((T, ddy, n))
+    ps, tot = np.empty((T, 2, n)), np.empty(n)
+    if lib().orc_simulate(fam, d, dy, k, v, _d(p), p.size, T, n, seed, _d(xs), _d(ys), _d(ps), _d(tot)):
+        raise ValueError("oracle simulate failed")
+    return xs, ys, ps, tot
 
 
 def run_pf(model, ys, n, seed, thr=None, resampler=SYSTEMATIC, proposal=DEFAULT, record_history=True):
