@@ -39,6 +39,7 @@ from .pf import (
     set_default_context,
 )
 from .simulate import SimulatedTraces, simulate
+from . import dists
 from ._lib import GenHipError
 
 __all__ = [
@@ -49,5 +50,5 @@ __all__ = [
     "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
     "conditional_particle_filter_step", "conditional_smc", "get_particle", "initialize_conditional_particle_filter",
     "particle_gibbs", "GenHipError", "ObservationBatch", "prepare_observations", "Selection", "select",
-    "metropolis_hastings", "mh", "simulate", "SimulatedTraces",
+    "metropolis_hastings", "mh", "simulate", "SimulatedTraces", "dists",
 ]

@@ -96,6 +96,10 @@ SIGNATURES = {
     "gh_pf_rejuvenate": (c_int, [c_void_p, c_int, POINTER(c_int64)]),
     "gh_pf_mh_select": (c_int, [c_void_p, ctypes.c_uint32, c_int, POINTER(c_int64)]),
     "gh_pf_get_scores": (c_int, [c_void_p, POINTER(c_double), POINTER(c_double)]),
+    "gh_dist_logpdf": (c_int, [c_void_p, c_void_p, c_int64, POINTER(c_double), POINTER(c_double)]),
+    "gh_dist_random": (c_int, [c_void_p, c_void_p, c_int64, c_uint64, POINTER(c_double)]),
+    "gh_dist_logpdf_dev": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "gh_dist_random_dev": (c_int, [c_void_p, c_void_p, c_int64, c_uint64, c_void_p]),
     "gh_simulate": (c_int, [c_void_p, c_int, c_int64, c_uint64, POINTER(c_double), POINTER(c_double),
                             POINTER(c_double), POINTER(c_double)]),
     "gh_pf_init_conditional": (c_int, [c_void_p, POINTER(Obs), c_int64, c_uint64, POINTER(PFOpts), POINTER(c_double),

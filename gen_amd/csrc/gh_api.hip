@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/gen_hip.h"
@@ -24,6 +25,7 @@
 #include "gh_coal.h"
 #include "gh_scores.h"
 #include "gh_simulate.h"
+#include "gh_dists.h"
 #include "gh_rejuv.h"
 #include "gh_csmc.h"
 
@@ -1908,6 +1910,175 @@ extern "C" int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double*
   hipFree(buf);
   hipFree(dobs);
   return rc;
+}
+
+// ------------------------------------------------------------ distributions
+// Batched logpdf / random of Gen's distribution library (gh_dists.h).
+struct DistShape {
+  int dim = 1, K = 0, prow = 0;  // value components, bins, doubles per device parameter row
+};
+
+static int dist_shape(const gh_dist_desc* d, DistShape* s) {
+  const int np = d->n_params, dim = d->dim < 1 ? 1 : d->dim;
+  auto need = [&](int k) { return np == k ? GH_OK : set_err(GH_E_INVAL, "distribution %d takes %d parameters, got %d", d->dist, k, np); };
+  s->dim = 1;
+  s->K = 0;
+  s->prow = np;
+  switch (d->dist) {
+    case DIST_NORMAL: case DIST_UNIFORM_CONTINUOUS: case DIST_UNIFORM_DISCRETE: case DIST_GAMMA: case DIST_INV_GAMMA:
+    case DIST_BETA: case DIST_BINOMIAL: case DIST_NEG_BINOMIAL: case DIST_LAPLACE: case DIST_CAUCHY:
+      return need(2);
+    case DIST_BERNOULLI: case DIST_EXPONENTIAL: case DIST_POISSON: case DIST_GEOMETRIC:
+      return need(1);
+    case DIST_BETA_UNIFORM:
+      return need(3);
+    case DIST_BROADCASTED_NORMAL:
+      if (dim > 32) return set_err(GH_E_INVAL, "broadcasted_normal: dim <= 32");
+      s->dim = dim;
+      return need(2 * dim);
+    case DIST_MVNORMAL:
+      if (dim > 32) return set_err(GH_E_INVAL, "mvnormal: dim <= 32");
+      if (d->param_stride != 0) return set_err(GH_E_INVAL, "mvnormal: one shared (mu, cov) row");
+      s->dim = dim;
+      s->prow = dim + dim * dim + 1;
+      return need(dim + dim * dim);
+    case DIST_CATEGORICAL:
+      if (np < 1) return set_err(GH_E_INVAL, "categorical: at least one probability");
+      s->K = np;
+      return GH_OK;
+    case DIST_PIECEWISE_UNIFORM:
+      if (np < 3 || np % 2 == 0) return set_err(GH_E_INVAL, "piecewise_uniform: bounds[K+1] then probs[K]");
+      s->K = (np - 1) / 2;
+      return GH_OK;
+    default:
+      return set_err(GH_E_INVAL, "unknown distribution %d", d->dist);
+  }
+}
+
+template <class F>
+static void with_dist(int dist, F&& f) {
+  switch (dist) {
+#define GH_DIST_CASE(D) case D: f(std::integral_constant<int, D>{}); break;
+    GH_DIST_CASE(DIST_NORMAL) GH_DIST_CASE(DIST_BROADCASTED_NORMAL) GH_DIST_CASE(DIST_MVNORMAL)
+    GH_DIST_CASE(DIST_UNIFORM_CONTINUOUS) GH_DIST_CASE(DIST_UNIFORM_DISCRETE) GH_DIST_CASE(DIST_BERNOULLI)
+    GH_DIST_CASE(DIST_CATEGORICAL) GH_DIST_CASE(DIST_GAMMA) GH_DIST_CASE(DIST_INV_GAMMA) GH_DIST_CASE(DIST_BETA)
+    GH_DIST_CASE(DIST_EXPONENTIAL) GH_DIST_CASE(DIST_POISSON) GH_DIST_CASE(DIST_BINOMIAL)
+    GH_DIST_CASE(DIST_NEG_BINOMIAL) GH_DIST_CASE(DIST_GEOMETRIC) GH_DIST_CASE(DIST_LAPLACE) GH_DIST_CASE(DIST_CAUCHY)
+    GH_DIST_CASE(DIST_PIECEWISE_UNIFORM) GH_DIST_CASE(DIST_BETA_UNIFORM)
+#undef GH_DIST_CASE
+    default: break;
+  }
+}
+
+// the device parameter rows: mvnormal's derived row, else the caller's rows
+static int dist_params(gh_ctx* ctx, const gh_dist_desc* d, const DistShape& sh, int64_t n, double** dparams,
+                       bool* owned) {
+  *owned = false;
+  if (!d->params) return set_err(GH_E_INVAL, "distribution parameters are NULL");
+  if (d->param_stride != 0 && d->param_stride != d->n_params)
+    return set_err(GH_E_INVAL, "param_stride must be 0 (shared row) or n_params (a row per value)");
+  if (d->params_on_device) {
+    if (d->dist == DIST_MVNORMAL) return set_err(GH_E_INVAL, "mvnormal parameters are host memory (Cholesky on the host)");
+    *dparams = const_cast<double*>(d->params);
+    return GH_OK;
+  }
+  std::vector<double> row;
+  const double* src = d->params;
+  size_t count = d->param_stride ? (size_t)n * d->n_params : (size_t)d->n_params;
+  if (d->dist == DIST_MVNORMAL) {
+    const int D = sh.dim;
+    row.assign(sh.prow, 0.0);
+    std::copy(src, src + D, row.begin());
+    if (chol(D, src + D, row.data() + D)) return set_err(GH_E_INVAL, "mvnormal: covariance not positive definite");
+    row[D + D * D] = gauss_cst(D, row.data() + D);
+    src = row.data();
+    count = row.size();
+  }
+  if (hipMalloc(dparams, sizeof(double) * (count ? count : 1)) != hipSuccess) return set_err(GH_E_NOMEM, "distribution parameters");
+  *owned = true;
+  if (hipMemcpyAsync(*dparams, src, sizeof(double) * count, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return set_err(GH_E_HIP, "distribution parameters: upload");
+  return GH_OK;
+}
+
+static int dist_launch(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t seed, const double* x, double* out,
+                       bool random) {
+  if (!ctx || !d) return set_err(GH_E_INVAL, "null argument");
+  if (n < 0 || n > ((int64_t)1 << 40)) return set_err(GH_E_INVAL, "batch size %lld", (long long)n);
+  DistShape sh;
+  CHECK(dist_shape(d, &sh));
+  if (n == 0) return GH_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  double* dp = nullptr;
+  bool owned = false;
+  int rc = dist_params(ctx, d, sh, n, &dp, &owned);
+  if (rc == GH_OK) {
+    DistArgs a{};
+    a.n = n;
+    a.dim = sh.dim;
+    a.K = sh.K;
+    a.prow = sh.prow;
+    a.pstride = d->param_stride ? sh.prow : 0;
+    a.params = dp;
+    a.x = x;
+    a.out = out;
+    a.seed = seed;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    with_dist(d->dist, [&](auto id) {
+      constexpr int D = decltype(id)::value;
+      if (random)
+        hipLaunchKernelGGL(k_dist_random<D>, grid, dim3(256), 0, ctx->stream, a);
+      else
+        hipLaunchKernelGGL(k_dist_logpdf<D>, grid, dim3(256), 0, ctx->stream, a);
+    });
+    if (hipGetLastError() != hipSuccess) rc = set_err(GH_E_HIP, "distribution kernel launch");
+  }
+  if (owned) {
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == GH_OK) rc = set_err(GH_E_HIP, "distribution kernel");
+    hipFree(dp);
+  }
+  return rc;
+}
+
+extern "C" int gh_dist_logpdf_dev(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, const double* x, double* out) {
+  return dist_launch(ctx, d, n, 0, x, out, false);
+}
+extern "C" int gh_dist_random_dev(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t seed, double* out) {
+  return dist_launch(ctx, d, n, seed, nullptr, out, true);
+}
+
+// host-buffer forms: stage through device memory and synchronise
+static int dist_host(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t seed, const double* x, double* out,
+                     bool random) {
+  if (!ctx || !d || !out || (!random && !x)) return set_err(GH_E_INVAL, "null argument");
+  DistShape sh;
+  CHECK(dist_shape(d, &sh));
+  if (n <= 0) return n == 0 ? GH_OK : set_err(GH_E_INVAL, "batch size %lld", (long long)n);
+  HIP_TRY(hipSetDevice(ctx->device));
+  const size_t nx = (size_t)sh.dim * n, nout = random ? nx : (size_t)n;
+  double *dx = nullptr, *dout = nullptr;
+  if ((!random && hipMalloc(&dx, sizeof(double) * nx) != hipSuccess) || hipMalloc(&dout, sizeof(double) * nout) != hipSuccess) {
+    hipFree(dx);
+    return set_err(GH_E_NOMEM, "distribution batch of %lld", (long long)n);
+  }
+  int rc = GH_OK;
+  if (!random && hipMemcpyAsync(dx, x, sizeof(double) * nx, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    rc = set_err(GH_E_HIP, "distribution values: upload");
+  if (rc == GH_OK) rc = dist_launch(ctx, d, n, seed, dx, dout, random);
+  if (rc == GH_OK && (hipMemcpyAsync(out, dout, sizeof(double) * nout, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                      hipStreamSynchronize(ctx->stream) != hipSuccess))
+    rc = set_err(GH_E_HIP, "distribution results: download");
+  hipFree(dx);
+  hipFree(dout);
+  return rc;
+}
+
+extern "C" int gh_dist_logpdf(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, const double* x, double* out) {
+  return dist_host(ctx, d, n, 0, x, out, false);
+}
+extern "C" int gh_dist_random(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t seed, double* out) {
+  return dist_host(ctx, d, n, seed, nullptr, out, true);
 }
 
 extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {

@@ -29,6 +29,8 @@
  *                                                         src/inference/mh.jl:85-98
  *   gh_simulate             simulate(model, (T,)) for N  src/static_ir/simulate.jl:23-34,50-83,
  *                           traces                       src/modeling_library/unfold/simulate.jl
+ *   gh_dist_logpdf /        logpdf / random of the       src/modeling_library/modeling_library.jl:15-41,
+ *   gh_dist_random          distribution library         src/modeling_library/distributions/ (all files)
  *   gh_model_create         a Static-DSL model + Unfold  src/static_ir/, src/modeling_library/unfold/
  *
  * Conventions
@@ -178,6 +180,46 @@ int gh_model_state_dim(const gh_model* m, int* d);
    The regression model takes T = 1. */
 int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double* xs, double* ys, double* per_step,
                 double* total);
+
+/* ---- distributions ----------------------------------------------------------- */
+/* Gen's distribution library (src/modeling_library/distributions/), batched:
+   n values, one parameter row shared by all (param_stride 0) or one row per
+   value (param_stride = n_params).  Parameter rows, in Gen's argument order:
+     NORMAL mu std | BROADCASTED_NORMAL mu[dim] std[dim] | MVNORMAL mu[dim] cov[dim*dim]
+     UNIFORM_CONTINUOUS low high | UNIFORM_DISCRETE low high | BERNOULLI prob
+     CATEGORICAL probs[K] (K = n_params) | GAMMA shape scale | INV_GAMMA shape scale
+     BETA alpha beta | EXPONENTIAL rate | POISSON lambda | BINOMIAL n p
+     NEG_BINOMIAL r p | GEOMETRIC p | LAPLACE loc scale | CAUCHY x0 gamma
+     PIECEWISE_UNIFORM bounds[K+1] probs[K] | BETA_UNIFORM theta alpha beta
+   Values are doubles, component-major [dim][n] for the vector distributions;
+   integer values are stored exactly, bernoulli is 0/1, categorical is 1-based
+   (as Gen's).  random(): value i draws from the Philox stream keyed
+   (seed, i), independent of n.  The *_dev forms take device x / out and
+   enqueue on the context's stream (params_on_device: params is a device
+   pointer; not for MVNORMAL, whose Cholesky factor is taken on the host). */
+typedef enum {
+  GH_DIST_NORMAL = 1, GH_DIST_BROADCASTED_NORMAL = 2, GH_DIST_MVNORMAL = 3, GH_DIST_UNIFORM_CONTINUOUS = 4,
+  GH_DIST_UNIFORM_DISCRETE = 5, GH_DIST_BERNOULLI = 6, GH_DIST_CATEGORICAL = 7, GH_DIST_GAMMA = 8,
+  GH_DIST_INV_GAMMA = 9, GH_DIST_BETA = 10, GH_DIST_EXPONENTIAL = 11, GH_DIST_POISSON = 12, GH_DIST_BINOMIAL = 13,
+  GH_DIST_NEG_BINOMIAL = 14, GH_DIST_GEOMETRIC = 15, GH_DIST_LAPLACE = 16, GH_DIST_CAUCHY = 17,
+  GH_DIST_PIECEWISE_UNIFORM = 18, GH_DIST_BETA_UNIFORM = 19
+} gh_dist;
+
+typedef struct {
+  int32_t dist;             /* gh_dist */
+  int32_t dim;              /* value components (BROADCASTED_NORMAL, MVNORMAL); else 1 */
+  int32_t n_params;         /* doubles per parameter row */
+  int32_t param_stride;     /* 0: one shared row; n_params: row i for value i */
+  int32_t params_on_device; /* *_dev forms: params is a device pointer */
+  int32_t reserved;
+  const double* params;
+} gh_dist_desc;
+
+int gh_dist_logpdf(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, const double* x /* [dim][n] */,
+                   double* out /* [n] */);
+int gh_dist_random(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t seed, double* out /* [dim][n] */);
+int gh_dist_logpdf_dev(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, const double* x, double* out);
+int gh_dist_random_dev(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t seed, double* out);
 
 /* ---- particle filter -------------------------------------------------------- */
 void gh_pf_opts_default(gh_pf_opts* o);

@@ -1736,3 +1736,332 @@ int orc_coal_run(int64_t chain0, int64_t n_chains, const double* ev, int E, int 
   }
   return 0;
 }
+
+/* ------------------------------------------------------ distribution library
+   Gen's distributions (src/modeling_library/distributions/) for the batched
+   gh_dist_logpdf / gh_dist_random: the logpdf formulas of the reference files
+   (file:line at each case) and exact samplers on the Philox stream S_DIST
+   keyed (seed, value index, 0, S_DIST | draw) — the specification the engine's
+   gen_amd/csrc/gh_dists.h follows operation by operation:
+     Box–Muller normals; inversion for the uniforms, bernoulli, categorical,
+     exponential, geometric, laplace, cauchy; Marsaglia–Tsang (2000) for gamma
+     (boost U^(1/a) below shape 1), inv_gamma = s / G, beta = G1 / (G1 + G2);
+     chop-down inversion from the mode for poisson and binomial;
+     neg_binomial = poisson(gamma(r, (1-p)/p)) (Distributions.jl's sampler).
+   log Gamma is Stirling's series after the recurrence to x >= 8. */
+enum { S_DIST = 8 };
+enum {
+  OD_NORMAL = 1, OD_BNORMAL, OD_MVNORMAL, OD_UNIF, OD_UDISC, OD_BERN, OD_CAT, OD_GAMMA, OD_INVGAMMA, OD_BETA,
+  OD_EXP, OD_POIS, OD_BINOM, OD_NEGBINOM, OD_GEOM, OD_LAPLACE, OD_CAUCHY, OD_PWUNIF, OD_BETAUNIF
+};
+#define OD_PI 0x1.921fb54442d18p+1
+#define OD_GAMMA_ITERS 60
+#define OD_GAMMA_BOOST 120u
+#define OD_SECOND 128u
+#define OD_CHOP_MAX (1 << 24)
+
+double orc_log1p(double y) {
+  double u = 1.0 + y;
+  if (u == 1.0) return y;
+  if (u == 0.0) return -INFINITY;
+  return orc_log(u) - ((u - 1.0) - y) / u;
+}
+
+/* log Gamma(x) = Stirling (x - 1/2) log x - x + log sqrt(2 pi) + sum B_2k / (2k (2k-1) x^(2k-1)) */
+double orc_lgamma(double x) {
+  if (x != x) return x;
+  if (x <= 0.0) return x == 0.0 ? INFINITY : NAN;
+  if (x == INFINITY) return x;
+  double prod = 1.0;
+  while (x < 8.0) { prod *= x; x += 1.0; }
+  double r = 1.0 / x, r2 = r * r;
+  static const double B[7] = {1.0 / 12.0, -1.0 / 360.0, 1.0 / 1260.0, -1.0 / 1680.0, 1.0 / 1188.0,
+                              -691.0 / 360360.0, 1.0 / 156.0};
+  double s = B[6];
+  for (int k = 5; k >= 0; --k) s = fma(s, r2, B[k]);
+  double st = ((x - 0.5) * orc_log(x) - x) + (0x1.d67f1c864beb5p-1 + s * r);
+  return prod == 1.0 ? st : st - orc_log(prod);
+}
+
+static double od_xlogy(double x, double y) { return x == 0.0 ? 0.0 : x * orc_log(y); }
+static double od_xlog1py(double x, double y) { return x == 0.0 ? 0.0 : x * orc_log1p(y); }
+
+static double od_u(uint64_t seed, uint64_t id, uint32_t draw) {
+  uint32_t w[4];
+  rng(seed, id, 0, S_DIST, draw, w);
+  return unif53(w[0], w[1]);
+}
+static double od_one_minus_u(uint32_t a, uint32_t b) {
+  uint32_t hi = a >> 11, lo = ((a << 21) & 0xFC000000u) | (b >> 6);
+  return fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0));
+}
+static double od_upos(uint64_t seed, uint64_t id, uint32_t draw) {
+  uint32_t w[4];
+  rng(seed, id, 0, S_DIST, draw, w);
+  return od_one_minus_u(w[0], w[1]);
+}
+static double od_normal(uint64_t seed, uint64_t id, uint32_t draw) {
+  uint32_t w[4];
+  rng(seed, id, 0, S_DIST, draw, w);
+  double z0, z1;
+  box_muller(w[0], w[1], w[2], &z0, &z1);
+  return z0;
+}
+static int od_cat(const double* p, int K, double u) {
+  double total = 0.0;
+  for (int k = 0; k < K; ++k) total += p[k];
+  double target = u * total, cum = 0.0;
+  int last = -1;
+  for (int k = 0; k < K; ++k) {
+    cum += p[k];
+    if (p[k] > 0.0) last = k;
+    if (cum > target && p[k] > 0.0) return k;
+  }
+  return last;
+}
+
+/* Gamma(a, 1): Marsaglia & Tsang, "A simple method for generating gamma
+   variables" (2000); round i: normal from draw d0 + 2i, uniform from d0 + 2i + 1 */
+static double od_gamma(uint64_t seed, uint64_t id, double a, uint32_t d0) {
+  if (!(a > 0.0)) return NAN;
+  double boost = 1.0;
+  if (a < 1.0) {
+    boost = orc_exp(orc_log(od_upos(seed, id, d0 + OD_GAMMA_BOOST)) / a);
+    a = a + 1.0;
+  }
+  double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
+  for (int i = 0; i < OD_GAMMA_ITERS; ++i) {
+    double x = od_normal(seed, id, d0 + 2u * (uint32_t)i);
+    double v = 1.0 + c * x;
+    if (v <= 0.0) continue;
+    v = v * v * v;
+    double u = od_upos(seed, id, d0 + 2u * (uint32_t)i + 1u);
+    double x2 = x * x;
+    if (u < 1.0 - 0.0331 * (x2 * x2)) return (d * v) * boost;
+    if (orc_log(u) < 0.5 * x2 + d * ((1.0 - v) + orc_log(v))) return (d * v) * boost;
+  }
+  return NAN;
+}
+
+/* chop-down inversion from the mode: U - pmf(m) - pmf(m+1) - pmf(m-1) - ... */
+static double od_poisson(uint64_t seed, uint64_t id, double lam, uint32_t draw) {
+  if (lam == 0.0) return 0.0;
+  if (!(lam > 0.0) || lam == INFINITY) return NAN;
+  double m = floor(lam), u = od_u(seed, id, draw);
+  double pm = orc_exp(od_xlogy(m, lam) - lam - orc_lgamma(m + 1.0));
+  u -= pm;
+  if (u <= 0.0) return m;
+  double lo = m, hi = m, pl = pm, ph = pm;
+  for (int it = 0; it < OD_CHOP_MAX; ++it) {
+    hi += 1.0; ph = ph * lam / hi; u -= ph;
+    if (u <= 0.0) return hi;
+    if (lo > 0.0) { pl = pl * lo / lam; lo -= 1.0; u -= pl; if (u <= 0.0) return lo; }
+    if (ph == 0.0 && (lo <= 0.0 || pl == 0.0)) break;
+  }
+  return m;
+}
+
+static double od_binomial(uint64_t seed, uint64_t id, double n, double p, uint32_t draw) {
+  if (!(p >= 0.0 && p <= 1.0) || !(n >= 0.0)) return NAN;
+  if (p == 0.0 || n == 0.0) return 0.0;
+  if (p == 1.0) return n;
+  double q = 1.0 - p, m = floor((n + 1.0) * p);
+  if (m > n) m = n;
+  double u = od_u(seed, id, draw);
+  double pm = orc_exp(((orc_lgamma(n + 1.0) - orc_lgamma(m + 1.0)) - orc_lgamma(n - m + 1.0)) + od_xlogy(m, p) +
+                      od_xlog1py(n - m, -p));
+  u -= pm;
+  if (u <= 0.0) return m;
+  double pq = p / q, qp = q / p, lo = m, hi = m, pl = pm, ph = pm;
+  for (int it = 0; it < OD_CHOP_MAX; ++it) {
+    if (hi < n) { ph = ph * ((n - hi) / (hi + 1.0)) * pq; hi += 1.0; u -= ph; if (u <= 0.0) return hi; }
+    if (lo > 0.0) { pl = pl * (lo / (n - lo + 1.0)) * qp; lo -= 1.0; u -= pl; if (u <= 0.0) return lo; }
+    if ((hi >= n || ph == 0.0) && (lo <= 0.0 || pl == 0.0)) break;
+  }
+  return m;
+}
+
+static double od_beta_lp(double v, double a, double b) { /* beta.jl:13-16 */
+  if (v < 0.0 || v > 1.0) return -INFINITY;
+  double lb = (orc_lgamma(a) + orc_lgamma(b)) - orc_lgamma(a + b);
+  return ((a - 1.0) * orc_log(v) + (b - 1.0) * orc_log1p(-v)) - lb;
+}
+
+/* row P of one value; x[k * xs] its components; mvnormal's row is derived: mu | L | cst */
+static double od_logpdf(int dist, const double* x, int64_t xs, const double* P, int D, int K) {
+  double v = x[0];
+  switch (dist) {
+    case OD_NORMAL: { /* normal.jl:56-60 */
+      double var = P[1] * P[1], diff = v - P[0];
+      return -(diff * diff) / (2.0 * var) - 0.5 * orc_log(2.0 * OD_PI * var);
+    }
+    case OD_BNORMAL: { /* normal.jl:62-71: sum of the elementwise logpdfs */
+      double s = 0.0;
+      for (int k = 0; k < D; ++k) {
+        double var = P[D + k] * P[D + k], diff = x[k * xs] - P[k];
+        s += -(diff * diff) / (2.0 * var) - 0.5 * orc_log(2.0 * OD_PI * var);
+      }
+      return s;
+    }
+    case OD_MVNORMAL: { /* mvnormal.jl:12-16 */
+      const double* L = P + D;
+      double u[32], quad = 0.0;
+      for (int i = 0; i < D; ++i) {
+        double r = x[i * xs] - P[i];
+        for (int k = 0; k < i; ++k) r = fma(-L[i * D + k], u[k], r);
+        u[i] = r / L[i * D + i];
+        quad = fma(u[i], u[i], quad);
+      }
+      return P[D + D * D] - 0.5 * quad;
+    }
+    case OD_UNIF: return (v >= P[0] && v <= P[1]) ? -orc_log(P[1] - P[0]) : -INFINITY; /* uniform_continuous.jl:12-14 */
+    case OD_UDISC: return (v >= P[0] && v <= P[1] && v == floor(v)) ? -orc_log((P[1] - P[0]) + 1.0) : -INFINITY;
+    case OD_BERN: return v != 0.0 ? orc_log(P[0]) : orc_log(1.0 - P[0]); /* bernoulli.jl:10-12 */
+    case OD_CAT: return (v > 0.0 && v <= (double)K && v == floor(v)) ? orc_log(P[(int)v - 1]) : -INFINITY;
+    case OD_GAMMA: /* gamma.jl:10-16 */
+      return v > 0.0 ? (((P[0] - 1.0) * orc_log(v) - (v / P[1])) - P[0] * orc_log(P[1])) - orc_lgamma(P[0]) : -INFINITY;
+    case OD_INVGAMMA: /* inv_gamma.jl:12-18 */
+      return v > 0.0 ? ((P[0] * orc_log(P[1]) - (P[0] + 1.0) * orc_log(v)) - orc_lgamma(P[0])) - (P[1] / v) : -INFINITY;
+    case OD_BETA: return od_beta_lp(v, P[0], P[1]);
+    case OD_EXP: { double sc = 1.0 / P[0]; return v < 0.0 ? -INFINITY : -orc_log(sc) - v / sc; } /* exponential.jl:10-13 */
+    case OD_POIS: return v < 0.0 ? -INFINITY : (v * orc_log(P[0]) - P[0]) - orc_lgamma(v + 1.0); /* poisson.jl:10-12 */
+    case OD_BINOM:
+      if (v < 0.0 || v > P[0] || v != floor(v)) return -INFINITY;
+      return (((orc_lgamma(P[0] + 1.0) - orc_lgamma(v + 1.0)) - orc_lgamma(P[0] - v + 1.0)) + od_xlogy(v, P[1])) +
+             od_xlog1py(P[0] - v, -P[1]);
+    case OD_NEGBINOM:
+      if (v < 0.0 || v != floor(v)) return -INFINITY;
+      return (((orc_lgamma(v + P[0]) - orc_lgamma(P[0])) - orc_lgamma(v + 1.0)) + od_xlogy(P[0], P[1])) +
+             od_xlog1py(v, -P[1]);
+    case OD_GEOM:
+      if (v < 0.0 || v != floor(v)) return -INFINITY;
+      return orc_log(P[0]) + od_xlog1py(v, -P[0]);
+    case OD_LAPLACE: return -fabs(v - P[0]) / P[1] - orc_log(2.0 * P[1]); /* laplace.jl:10-13 */
+    case OD_CAUCHY: { double z = (v - P[0]) / P[1]; return -(orc_log(OD_PI * P[1]) + orc_log1p(z * z)); }
+    case OD_PWUNIF: { /* piecewise_uniform.jl:30-43 */
+      if (v <= P[0] || v >= P[K]) return -INFINITY;
+      int bin = 0;
+      while (v > P[bin + 1]) ++bin;
+      return orc_log(P[K + 1 + bin]) - orc_log(P[bin + 1] - P[bin]);
+    }
+    default: { /* beta_uniform.jl:12-20 */
+      if (v < 0.0 || v > 1.0) return -INFINITY;
+      double lbeta = orc_log(P[0]) + od_beta_lp(v, P[1], P[2]), lunif = orc_log(1.0 - P[0]);
+      double m = lbeta > lunif ? lbeta : lunif;
+      if (m == -INFINITY) return m;
+      return m + orc_log(orc_exp(lbeta - m) + orc_exp(lunif - m));
+    }
+  }
+}
+
+static void od_random(int dist, uint64_t seed, uint64_t id, double* x, int64_t xs, const double* P, int D, int K) {
+  switch (dist) {
+    case OD_NORMAL: x[0] = P[0] + P[1] * od_normal(seed, id, 0); return; /* normal.jl:96 */
+    case OD_BNORMAL:
+    case OD_MVNORMAL: {
+      double z[32];
+      normals_at(seed, id, 0, S_DIST, 0, D, z);
+      if (dist == OD_BNORMAL) {
+        for (int k = 0; k < D; ++k) x[k * xs] = P[k] + P[D + k] * z[k];
+      } else {
+        const double* L = P + D;
+        for (int i = 0; i < D; ++i) {
+          double acc = P[i];
+          for (int k = 0; k <= i; ++k) acc = fma(L[i * D + k], z[k], acc);
+          x[i * xs] = acc;
+        }
+      }
+      return;
+    }
+    case OD_UNIF: x[0] = od_u(seed, id, 0) * (P[1] - P[0]) + P[0]; return; /* uniform_continuous.jl:21-23 */
+    case OD_UDISC: x[0] = P[0] + floor(od_u(seed, id, 0) * ((P[1] - P[0]) + 1.0)); return;
+    case OD_BERN: x[0] = od_u(seed, id, 0) < P[0] ? 1.0 : 0.0; return; /* bernoulli.jl:19 */
+    case OD_CAT: x[0] = (double)(od_cat(P, K, od_u(seed, id, 0)) + 1); return;
+    case OD_GAMMA: x[0] = P[1] * od_gamma(seed, id, P[0], 0); return;
+    case OD_INVGAMMA: x[0] = P[1] / od_gamma(seed, id, P[0], 0); return;
+    case OD_BETA: {
+      double g1 = od_gamma(seed, id, P[0], 0), g2 = od_gamma(seed, id, P[1], OD_SECOND);
+      x[0] = g1 / (g1 + g2);
+      return;
+    }
+    case OD_EXP: x[0] = (1.0 / P[0]) * -orc_log(od_upos(seed, id, 0)); return;
+    case OD_POIS: x[0] = od_poisson(seed, id, P[0], 0); return;
+    case OD_BINOM: x[0] = od_binomial(seed, id, P[0], P[1], 0); return;
+    case OD_NEGBINOM: {
+      double lam = ((1.0 - P[1]) / P[1]) * od_gamma(seed, id, P[0], 0);
+      x[0] = od_poisson(seed, id, lam, OD_SECOND);
+      return;
+    }
+    case OD_GEOM: x[0] = floor(orc_log(od_upos(seed, id, 0)) / orc_log1p(-P[0])) + 0.0; return;
+    case OD_LAPLACE: {
+      uint32_t w[4];
+      rng(seed, id, 0, S_DIST, 0, w);
+      double e = -orc_log(od_one_minus_u(w[0], w[1]));
+      x[0] = P[0] + P[1] * ((w[2] & 1u) ? -e : e);
+      return;
+    }
+    case OD_CAUCHY: {
+      uint32_t w[4];
+      rng(seed, id, 0, S_DIST, 0, w);
+      double u = ((double)bits53(w[0], w[1]) + 0.5) * 0x1p-53, s, c;
+      orc_sincos_2pi(u * 0.5, &s, &c);
+      x[0] = P[0] - P[1] * (c / s);
+      return;
+    }
+    case OD_PWUNIF: {
+      int bin = od_cat(P + K + 1, K, od_u(seed, id, 0));
+      x[0] = od_u(seed, id, 1) * (P[bin + 1] - P[bin]) + P[bin];
+      return;
+    }
+    default: /* beta_uniform.jl:36-42 */
+      if (od_u(seed, id, 255) < P[0]) {
+        double g1 = od_gamma(seed, id, P[1], 0), g2 = od_gamma(seed, id, P[2], OD_SECOND);
+        x[0] = g1 / (g1 + g2);
+      } else {
+        x[0] = od_u(seed, id, 254);
+      }
+  }
+}
+
+/* the parameter row layout of gh_dist_desc; returns the derived row length or -1 */
+static int od_row(int dist, int dim, int np, const double* params, double* row, int* D, int* K) {
+  *D = 1; *K = 0;
+  if (dist == OD_BNORMAL) { *D = dim; }
+  if (dist == OD_CAT) *K = np;
+  if (dist == OD_PWUNIF) *K = (np - 1) / 2;
+  if (dist == OD_MVNORMAL) {
+    int d = dim;
+    *D = d;
+    memset(row, 0, sizeof(double) * (d + d * d + 1));
+    memcpy(row, params, sizeof(double) * d);
+    if (chol(d, params + d, row + d)) return -1;
+    row[d + d * d] = gauss_cst(d, row + d);
+    return d + d * d + 1;
+  }
+  memcpy(row, params, sizeof(double) * np);
+  return np;
+}
+
+int orc_dist_logpdf(int dist, int dim, int np, int stride, const double* params, int64_t n, const double* x,
+                    double* out) {
+  double row[32 + 32 * 32 + 1];
+  int D, K;
+  if (np > 1024 + 33) return -1;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i == 0 || stride) if (od_row(dist, dim, np, params + i * stride, row, &D, &K) < 0) return -1;
+    out[i] = od_logpdf(dist, x + i, n, row, D, K);
+  }
+  return 0;
+}
+
+int orc_dist_random(int dist, int dim, int np, int stride, const double* params, int64_t n, uint64_t seed,
+                    double* out) {
+  double row[32 + 32 * 32 + 1];
+  int D, K;
+  if (np > 1024 + 33) return -1;
+  for (int64_t i = 0; i < n; ++i) {
+    if (i == 0 || stride) if (od_row(dist, dim, np, params + i * stride, row, &D, &K) < 0) return -1;
+    od_random(dist, seed, (uint64_t)i, out + i, n, row, D, K);
+  }
+  return 0;
+}

@@ -86,6 +86,12 @@ int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* 
 /* get_score of every current particle's trace (total [n]) and the per-step
    latent / observation choice scores (per_step [t][2][n], nullable); one shard */
 int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step);
+double orc_log1p(double y);
+double orc_lgamma(double x);
+int orc_dist_logpdf(int dist, int dim, int np, int stride, const double* params, int64_t n, const double* x,
+                    double* out);
+int orc_dist_random(int dist, int dim, int np, int stride, const double* params, int64_t n, uint64_t seed,
+                    double* out);
 int orc_simulate(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T, int64_t n,
                  uint64_t seed, double* xs, double* ys, double* per_step, double* total);
 

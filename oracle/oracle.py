@@ -88,6 +88,10 @@ def _load(path):
             "orc_pf_num_steps": (I, [V]),
             "orc_pf_get_history": (I, [V, I, D, POINTER(c_int32), POINTER(c_int)]),
             "orc_pf_get_scores": (I, [V, D, D]),
+            "orc_lgamma": (c_double, [c_double]),
+            "orc_log1p": (c_double, [c_double]),
+            "orc_dist_logpdf": (I, [I, I, I, I, D, I64, D, D]),
+            "orc_dist_random": (I, [I, I, I, I, D, I64, U64, D]),
             "orc_simulate": (I, [I, I, I, I, I, D, I64, I, I64, U64, D, D, D, D]),
             "orc_pf_local_stats": (None, [V, D]),
             "orc_combine_stats": (I, [D, I, I64, c_double, D, D, D]),
@@ -330,6 +334,34 @@ def simulate(model, T, n, seed):
     if lib().orc_simulate(fam, d, dy, k, v, _d(p), p.size, T, n, seed, _d(xs), _d(ys), _d(ps), _d(tot)):
         raise ValueError("oracle simulate failed")
     return xs, ys, ps, tot
+
+
+DISTS = {"normal": 1, "broadcasted_normal": 2, "mvnormal": 3, "uniform_continuous": 4, "uniform_discrete": 5,
+         "bernoulli": 6, "categorical": 7, "gamma": 8, "inv_gamma": 9, "beta": 10, "exponential": 11, "poisson": 12,
+         "binomial": 13, "neg_binomial": 14, "geometric": 15, "laplace": 16, "cauchy": 17, "piecewise_uniform": 18,
+         "beta_uniform": 19}
+
+
+def dist_logpdf(name, params, x, dim=1, per_value=False):
+    """logpdf of n values x ([dim, n] or [n]) under one shared parameter row
+    (or, per_value, rows params[n, n_params])."""
+    p = np.ascontiguousarray(params, dtype=np.float64)
+    xv = np.ascontiguousarray(x, dtype=np.float64)
+    n = xv.shape[-1]
+    np_ = p.shape[-1] if per_value else p.size
+    out = np.empty(n)
+    if lib().orc_dist_logpdf(DISTS[name], dim, np_, np_ if per_value else 0, _d(p), n, _d(xv), _d(out)):
+        raise ValueError("oracle dist_logpdf failed")
+    return out
+
+
+def dist_random(name, params, n, seed, dim=1, per_value=False):
+    p = np.ascontiguousarray(params, dtype=np.float64)
+    np_ = p.shape[-1] if per_value else p.size
+    out = np.empty((dim, n)) if dim > 1 else np.empty(n)
+    if lib().orc_dist_random(DISTS[name], dim, np_, np_ if per_value else 0, _d(p), n, seed, _d(out)):
+        raise ValueError("oracle dist_random failed")
+    return out
 
 
 def run_pf(model, ys, n, seed, thr=None, resampler=SYSTEMATIC, proposal=DEFAULT, record_history=True):
