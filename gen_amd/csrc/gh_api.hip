@@ -663,6 +663,7 @@ struct gh_pf {
   uint64_t* bsum = nullptr;
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
+  int64_t nb_part = 0;             // block partials the last step kernel wrote (pair kernels: n / 512)
   double *pm = nullptr, *ps = nullptr, *ps2 = nullptr;
   DevScalars* dev = nullptr;
   double* stats_all = nullptr;    // [3*world]
@@ -675,6 +676,7 @@ struct gh_pf {
   double* rows_send = nullptr;    // [send_cap][D+1] rows this rank sends
   int32_t* xanc = nullptr;        // [send_cap] local ancestors of the sent rows
   int64_t send_cap = 0;
+  int send_grows = 0;              // resamples whose rows overflowed the bounded send buffer
   int64_t* gparent = nullptr;     // [n] global parent ids of the last exchange
   hipStream_t aux = nullptr;      // multi-rank: side stream (the plan's D2H read, the row exchange)
   hipEvent_t ev_tot = nullptr;    // multi-rank: totals all-gathered
@@ -735,7 +737,7 @@ static void pick_resample_tiles(gh_pf* pf, int64_t n) {
   pf->rs_it = 0;
   // k_resample1's wave 0 polls every tile total: at most 64 * kRsPoll tiles
   const int64_t gmax = 64 * kRsPoll;
-  if (pf->nb_step <= kRsPart * kRsBlock && grid4 <= std::min<int64_t>(gmax, resample_cap<4>(cus))) {
+  if (pf->nb_part <= kRsPart * kRsBlock && grid4 <= std::min<int64_t>(gmax, resample_cap<4>(cus))) {
     pf->rs_it = 4;
     pf->rs_grid = (int)grid4;
   } else if (grid8 <= std::min<int64_t>(gmax, resample_cap<8>(cus))) {
@@ -846,11 +848,39 @@ extern "C" int gh_pf_destroy(gh_pf* pf) {
 // synchronisation, which acquires anyway.
 constexpr unsigned kTimingEventFlags = hipEventDisableSystemFence;
 
+template <class M, class = void>
+struct has_pairs : std::false_type {};
+template <class M>
+struct has_pairs<M, std::void_t<decltype(M::kPairs)>> : std::bool_constant<M::kPairs> {};
+
+// the pair kernel steps the single-rank filters of paired models (pair mates
+// in one lane needs a particle offset that is a multiple of 128)
+template <class Model>
+static bool use_pairs(const gh_pf* pf) {
+  // (conditional filters re-fold block 0 as 256 particles: k_pin_post)
+  if constexpr (has_pairs<Model>::value) return pf->ctx->world == 1 && (pf->lo & 127) == 0 && !pf->cond;
+  return false;
+}
+
 template <class Model>
 static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const StepObs& o,
                           const StepArgs& a0, bool init, hipEvent_t e0, hipEvent_t e1) {
   StepArgs a = a0;
   a.nvb = (a.n + kBlock - 1) / kBlock;
+  if constexpr (has_pairs<Model>::value) {
+    if (use_pairs<Model>(pf) && a.part == 0) {
+      const dim3 grid((unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock))), block(kBlock);
+      pf->nb_part = grid.x;
+      if (init)
+        hipExtLaunchKernelGGL((k_step_pairs<Model, true>), grid, block, 0, pf->s, e0, e1, 0,
+                              (const double*)pf->m->dparams, p, o, a);
+      else
+        hipExtLaunchKernelGGL((k_step_pairs<Model, false>), grid, block, 0, pf->s, e0, e1, 0,
+                              (const double*)pf->m->dparams, p, o, a);
+      return;
+    }
+  }
+  pf->nb_part = pf->nb_step;
   const dim3 grid((unsigned)(a.part == 2 ? a.nvb : pf->nb_step)), block(kBlock);
   // the timed launch records its events at the kernel's own start and end
   if (init)
@@ -872,7 +902,7 @@ static int ensure_stats(gh_pf* pf) {
   if (pf->ctx->world > 1 || pf->stats_valid) return GH_OK;
   if (pf->max_only)  // cannot happen: a max-only step is always followed by the fused resample
     return set_err(GH_E_STATE, "internal: step partials hold block maxima only");
-  hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_step,
+  hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_part,
                      pf->stats_all, pf->dev, 0, 0.0, pf->n_global);
   HIP_TRY(hipGetLastError());
   pf->stats_valid = true;
@@ -1116,6 +1146,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->ctx = ctx;
   pf->s = ctx->stream;
   pf->D = m->d;
+  pf->cond = pin_ref != nullptr;  // before the first step kernel (use_pairs)
   for (int i = 0; i < 4; ++i) pf->qargs[i] = q0[i];
   pf->has_q = has_q;
   if (opts) pf->opts = *opts;
@@ -1130,6 +1161,12 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->seed = seed;
   const int64_t n = pf->n > 0 ? pf->n : 1;
   pf->nb_step = (n + kBlock - 1) / kBlock;
+  pf->nb_part = pf->nb_step;
+  {  // the partial count of the family's step kernel (resample tile choice)
+    bool pairs = false;
+    with_model(m, [&](auto model, const auto&) { pairs = use_pairs<decltype(model)>(pf); });
+    if (pairs) pf->nb_part = (n + 2 * kBlock - 1) / (2 * kBlock);
+  }
   pf->nb_scan = (n + kScanTile - 1) / kScanTile;
   auto fail = [&](int rc) { pf_free(pf); return rc; };
 #define ALLOC(ptr, bytes) \
@@ -1343,6 +1380,23 @@ static void launch_rank_b(gh_pf* pf, const RankBArgs& rb) {
   }
 }
 
+// The grouped exchange of one multi-rank resample: to / from each other rank r
+// the rows of its slot block, packed by rank (sends at their k_rank_b offsets)
+static void exchange_lists(int R, int q, int D, const int64_t* slo, const int64_t* shi, const int64_t* rlo,
+                           const int64_t* rhi, double* rows_send, double* rows_recv, std::vector<CommMsg>* sends,
+                           std::vector<CommMsg>* recvs) {
+  const size_t row_bytes = sizeof(double) * (D + 1);
+  int64_t soff = 0, roff = 0;
+  for (int r = 0; r < R; ++r) {
+    if (r == q) continue;
+    const int64_t ls = shi[r] - slo[r], lr = rhi[r] - rlo[r];
+    if (ls > 0) sends->push_back({r, rows_send + soff * (D + 1), (size_t)ls * row_bytes});
+    if (lr > 0) recvs->push_back({r, rows_recv + roff * (D + 1), (size_t)lr * row_bytes});
+    soff += ls > 0 ? ls : 0;
+    roff += lr > 0 ? lr : 0;
+  }
+}
+
 // Multi-rank systematic resample: decision + quantise + rank
 // total (k_rank_a), all-gather of the totals, marks + outgoing rows
 // (k_rank_b).  Nothing here waits for the device: the fire flag and the
@@ -1355,10 +1409,10 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   const int R = c->world, q = c->rank;
   const int D = pf->D;
   if (pf->send_cap < 1) {
-    // every row this rank could send: its particles may cover every other
-    // rank's slots (all the weight on this rank), so the worst case is sized
-    // once and the packing never has to be redone
-    const int64_t cap = std::max<int64_t>(pf->n_global - pf->n, 1);
+    // bounded: up to twice this rank's own particles (the worst case, every
+    // other rank's slots, grows with the world size); a resample that needs
+    // more keeps its CDF and finish_plan regrows the buffer (k_rows_fill)
+    const int64_t cap = std::max<int64_t>(std::min<int64_t>(pf->n_global - pf->n, 2 * pf->n), 1);
     if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess)
       return set_err(GH_E_NOMEM, "send rows (%lld)", (long long)cap);
     pf->send_cap = cap;
@@ -1400,6 +1454,7 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.D = D;
   rb.rows = pf->rows_send;
   rb.rows_cap = pf->send_cap;
+  rb.C = pf->C;
   launch_rank_b(pf, rb);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
@@ -1448,18 +1503,43 @@ static int finish_plan(gh_pf* pf) {
   pf->rem_rb = clamp_own(sys_count_host(base + tot[q], N, S, o)) - own_lo;
   std::vector<int64_t> slo(R), shi(R), rlo(R), rhi(R);
   sys_plan(pf->n_global, R, q, tot, o, slo.data(), shi.data(), rlo.data(), rhi.data());
-  std::vector<CommMsg> sends, recvs;
-  const size_t row_bytes = sizeof(double) * (D + 1);
-  int64_t soff = 0, roff = 0;
-  for (int r = 0; r < R; ++r) {
-    if (r == q) continue;
-    const int64_t ls = shi[r] - slo[r], lr = rhi[r] - rlo[r];
-    if (ls > 0) sends.push_back({r, pf->rows_send + soff * (D + 1), (size_t)ls * row_bytes});
-    if (lr > 0) recvs.push_back({r, pf->rows_recv + roff * (D + 1), (size_t)lr * row_bytes});
-    soff += ls > 0 ? ls : 0;
-    roff += lr > 0 ? lr : 0;
+  int64_t n_send = 0;
+  for (int r = 0; r < R; ++r)
+    if (r != q && shi[r] > slo[r]) n_send += shi[r] - slo[r];
+  if (n_send > pf->send_cap) {
+    // k_rank_b kept the CDF instead of the rows: regrow (synchronously: this
+    // rank holds most of the weight, a rare step) and write every row from it
+    HIP_TRY(hipStreamSynchronize(pf->s));
+    hipFree(pf->rows_send);
+    pf->rows_send = nullptr;
+    pf->send_cap = 0;
+    const int64_t cap = n_send + n_send / 4 + 64;
+    if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess)
+      return set_err(GH_E_NOMEM, "send rows (%lld)", (long long)cap);
+    pf->send_cap = cap;
+    RowsFillArgs fa{};
+    fa.C = pf->C;
+    fa.n = pf->n;
+    fa.R = R;
+    fa.rank = q;
+    fa.lo = pf->lo;
+    fa.dev = pf->dev;
+    fa.totals = pf->totals_all;
+    fa.n_global = pf->n_global;
+    fa.xprev = slot_x(pf, t);
+    fa.D = D;
+    fa.rows = pf->rows_send;
+    fa.rows_cap = pf->send_cap;
+    hipLaunchKernelGGL(k_rows_fill, dim3((unsigned)((pf->n + 255) / 256)), dim3(256), 0, pf->s, fa);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
+    pf->send_grows++;
   }
-  if (soff > pf->send_cap) return set_err(GH_E_STATE, "internal: %lld send rows > capacity", (long long)soff);
+  // the same message lists serve both transports (RCCL grouped send/recv,
+  // or the host-staged sendrecv): exchange_lists, also exported for tests
+  std::vector<CommMsg> sends, recvs;
+  exchange_lists(R, q, D, slo.data(), shi.data(), rlo.data(), rhi.data(), pf->rows_send, pf->rows_recv, &sends,
+                 &recvs);
   if (sends.empty() && recvs.empty()) return GH_OK;
   HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_rb, 0));
   CHECK(comm_exchange(c, sends, recvs, pf->aux));
@@ -1498,7 +1578,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     ra.pm = pf->pm;
     ra.ps = pf->ps;
     ra.ps2 = pf->ps2;
-    ra.nb_part = (int)pf->nb_step;
+    ra.nb_part = (int)pf->nb_part;
     ra.logw = pf->logw;
     ra.n = n;
     ra.shift = g.shift;
@@ -1642,6 +1722,8 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
   // other value is the threshold itself: ess < 0 never holds, so a threshold
   // <= 0 turns resampling off exactly as in maybe_resample! (:194)
   if (thr != thr) thr = (double)pf->n_global / 2.0;
+  if (thr < 0.0)
+    return set_err(GH_E_INVAL, "ess_threshold %g < 0: pass NaN for the default N/2, 0 to never resample", thr);
   CHECK(resample_enqueue(pf, thr));
   // conditional SMC: the distinguished particle's parent is itself (smc.jl:139);
   // the ancestor array is only read if the resample fired
@@ -2333,6 +2415,29 @@ extern "C" int gh_sys_plan(int64_t n_global, int world, int rank, const uint64_t
   for (int r = 0; r < world; ++r) S += totals[r];
   if (S == 0 || offset >= S) return set_err(GH_E_INVAL, "gh_sys_plan: offset must be < sum(totals) > 0");
   sys_plan(n_global, world, rank, totals, offset, send_lo, send_hi, recv_lo, recv_hi);
+  return GH_OK;
+}
+
+// The message lists one rank posts for a resample with these totals (host
+// arithmetic only; tests): peers and byte counts, sends then receives.
+extern "C" int gh_debug_exchange_lists(int64_t n_global, int world, int rank, const uint64_t* totals, uint64_t offset,
+                                       int D, int* n_send, int* send_peer, uint64_t* send_bytes, int* n_recv,
+                                       int* recv_peer, uint64_t* recv_bytes) {
+  if (world < 1 || world > kMaxRanks || D < 1 || !n_send || !n_recv) return set_err(GH_E_INVAL, "bad argument");
+  std::vector<int64_t> slo(world), shi(world), rlo(world), rhi(world);
+  CHECK(gh_sys_plan(n_global, world, rank, totals, offset, slo.data(), shi.data(), rlo.data(), rhi.data()));
+  std::vector<CommMsg> sends, recvs;
+  exchange_lists(world, rank, D, slo.data(), shi.data(), rlo.data(), rhi.data(), nullptr, nullptr, &sends, &recvs);
+  *n_send = (int)sends.size();
+  *n_recv = (int)recvs.size();
+  for (size_t k = 0; k < sends.size(); ++k) {
+    send_peer[k] = sends[k].peer;
+    send_bytes[k] = sends[k].bytes;
+  }
+  for (size_t k = 0; k < recvs.size(); ++k) {
+    recv_peer[k] = recvs[k].peer;
+    recv_bytes[k] = recvs[k].bytes;
+  }
   return GH_OK;
 }
 

@@ -351,7 +351,9 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
       }
       if (j < a.n) a.anc[j] = (int32_t)src;  // genealogy record
     }
-    if (j < a.n) {
+    // part 1 of a split multi-rank step: slots that take a received row are
+    // stepped by part 2 once the rows have landed (no read of rows_recv here)
+    if (j < a.n && !(a.part == 1 && src < 0)) {
       double x[D];
       if (INIT) {
         lw = Model::init(p, o, a.seed, (uint64_t)(a.lo + j), a.proposal, x, dr_init);
@@ -394,6 +396,110 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
 #endif
   if (a.max_only) block_max_partial(lw, sm, a.pm + vb);
   else block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
+}
+
+// k_step for one-dimensional models whose particles p, p + 64 share their
+// draws (Model::kPairs, KitModel): each lane steps the particle of its lane in
+// two consecutive 64-particle tiles, so one counter block and one Box–Muller
+// evaluation serve both; a 256-thread block covers 512 particles and writes
+// one partial.  Single rank, particle offset lo a multiple of 128 (the pair
+// mates are then in the same lane); values identical to k_step's.
+__device__ __forceinline__ void block_partial2(double lw0, double lw1, double (*sm)[4], double* pm, double* ps,
+                                               double* ps2) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double mw = wave_max(fmax(lw0, lw1));
+  if (lane == 0) sm[0][w] = mw;
+  lds_barrier();
+  const double mb = fmax(fmax(sm[0][0], sm[0][1]), fmax(sm[0][2], sm[0][3]));
+  double e0 = 0.0, e1 = 0.0;
+  if (lw0 > -INFINITY) e0 = gh_exp_nonpos(lw0 - mb);
+  if (lw1 > -INFINITY) e1 = gh_exp_nonpos(lw1 - mb);
+  if (lw0 != lw0) e0 = lw0;  // NaN poisons the statistics
+  if (lw1 != lw1) e1 = lw1;
+  const double sw = wave_sum(e0 + e1), s2w = wave_sum(e0 * e0 + e1 * e1);
+  if (lane == 0) {
+    sm[1][w] = sw;
+    sm[2][w] = s2w;
+  }
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    *pm = mb;
+    *ps = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
+    *ps2 = (sm[2][0] + sm[2][1]) + (sm[2][2] + sm[2][3]);
+  }
+}
+
+template <class Model, bool INIT>
+__global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const double* __restrict__ prm,
+                                                                          typename Model::Params p0, StepObs o,
+                                                                          StepArgs a) {
+  static_assert(Model::kD == 1 && Model::kPairs, "pair stepping: one-dimensional paired models");
+  const typename Model::Params p = p0.rebase(prm);
+  __shared__ double sm[3][4];
+  __shared__ double logtab[kMathTabDoubles];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t vb = blockIdx.x;
+  const int64_t tile0 = (vb * (kBlock / 64) + w) * 2;
+  const int64_t j0 = tile0 * 64 + lane, j1 = j0 + 64;
+  uint64_t mv0 = 0, mv1 = 0, cv0 = 0, cv1 = 0;
+  int pending = 0, fire = 0;
+  if (!INIT && a.resampled) {
+    pending = a.dev->pending;
+    fire = a.dev->fire;
+    if (a.mark_mode) {
+      const int64_t last = a.n > 0 ? a.n - 1 : 0, lt = last >> 6;
+      mv0 = a.mark[j0 < last ? j0 : last];
+      mv1 = a.mark[j1 < last ? j1 : last];
+      cv0 = a.carry[tile0 < lt ? tile0 : lt];
+      cv1 = a.carry[tile0 + 1 < lt ? tile0 + 1 : lt];
+    }
+  }
+  load_math_tab256(logtab);
+  lds_barrier();
+  asm volatile("" : "+v"(mv0), "+v"(cv0), "+v"(mv1), "+v"(cv1));
+  const int pend = pending | fire;
+  const int use_marks = a.mark_mode && fire && !pending;
+  const Draw dr_init{STREAM_INIT, 0, logtab}, dr_step{STREAM_STEP, 0, logtab};
+  double lw0 = -INFINITY, lw1 = -INFINITY;
+  if (tile0 * 64 < a.n) {  // wave-uniform
+    const bool has1 = j1 < a.n;
+    int64_t s0 = j0, s1 = j1;
+    if (use_marks) {  // both tiles: prefix max seeded with the tile's carry
+      uint64_t v0 = j0 < a.n ? mv0 : 0, v1 = has1 ? mv1 : 0;
+      v0 = wave_incl_max_u64(v0 > cv0 ? v0 : cv0);
+      v1 = wave_incl_max_u64(v1 > cv1 ? v1 : cv1);
+      s0 = (int64_t)(uint32_t)v0;
+      s1 = (int64_t)(uint32_t)v1;
+      if (j0 < a.n) a.anc[j0] = (int32_t)s0;
+      if (has1) a.anc[j1] = (int32_t)s1;
+    }
+    if (j0 < a.n) {
+      const uint64_t g0 = (uint64_t)(a.lo + j0);
+      double x0, x1, w0, w1;
+      if (INIT) {
+        Model::init2(p, o, a.seed, g0, &x0, &x1, &w0, &w1, dr_init);
+      } else {
+        if (pend && !use_marks) {
+          s0 = a.anc[j0];
+          s1 = has1 ? a.anc[j1] : s0;
+        }
+        if (!has1) s1 = s0;
+        Model::step2(p, o, a.seed, g0, a.t, a.xprev[s0], a.xprev[s1], &x0, &x1, &w0, &w1, dr_step);
+        w0 = (pend ? 0.0 : a.logw[j0]) + w0;
+        if (has1) w1 = (pend ? 0.0 : a.logw[j1]) + w1;
+      }
+      a.xout[j0] = x0;
+      a.logw[j0] = w0;
+      lw0 = w0;
+      if (has1) {
+        a.xout[j1] = x1;
+        a.logw[j1] = w1;
+        lw1 = w1;
+      }
+    }
+  }
+  if (a.max_only) block_max_partial(fmax(lw0, lw1), sm, a.pm + vb);
+  else block_partial2(lw0, lw1, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
 }
 
 // --------------------------------------------------------------- decision
@@ -1493,7 +1599,52 @@ struct RankBArgs {
   int D;
   double* rows;           // send rows [(D+1)] per slot
   int64_t rows_cap;
+  uint64_t* C;            // more rows than rows_cap: the inclusive CDF, for k_rows_fill
 };
+
+// The send layout of one rank's resample (as gh_sys_plan): destination rank k
+// owns global slots [dlo_k, dhi_k); this rank's particles cover [cov_lo,
+// cov_hi); the rows for rank k != rank start at soff_k, in slot order.
+__device__ __forceinline__ int64_t send_tables(const DevScalars* sd, uint64_t N, int R, int q, uint64_t local,
+                                               int64_t* dst_lo, int64_t* seg_lo, int64_t* soffs, int64_t* cov_lo_out,
+                                               int64_t* cov_hi_out) {
+  const int64_t cov_lo = sys_count_exact(sd, N, sd->base);
+  const int64_t cov_hi = sys_count_exact(sd, N, sd->base + local);
+  int64_t soff = 0;
+  for (int k = 0; k < R; ++k) {
+    const int64_t dlo = (int64_t)(((__int128)N * k) / R), dhi = (int64_t)(((__int128)N * (k + 1)) / R);
+    const int64_t a = cov_lo > dlo ? cov_lo : dlo, b = cov_hi < dhi ? cov_hi : dhi;
+    dst_lo[k] = dlo;
+    seg_lo[k] = a;
+    soffs[k] = soff;
+    if (k != q && b > a) soff += b - a;
+  }
+  *cov_lo_out = cov_lo;
+  *cov_hi_out = cov_hi;
+  return soff;
+}
+
+// the state rows of particle i's slots [s0, s1) that other ranks own
+__device__ __forceinline__ void send_rows(int64_t s0, int64_t s1, int64_t i, int64_t own_lo, int64_t own_hi, int R,
+                                          uint64_t N, const int64_t* dst_lo, const int64_t* seg_lo,
+                                          const int64_t* soffs, int64_t rows_cap, double* rows, const double* xprev,
+                                          int D, int64_t lo) {
+  for (int64_t sl = s0; sl < s1; ++sl) {
+    if (sl >= own_lo && sl < own_hi) {
+      sl = own_hi - 1;  // skip the own block
+      continue;
+    }
+    int dst = (int)(((__int128)sl * R) / (int64_t)N);  // owner of global slot sl
+    while (dst + 1 < R && dst_lo[dst + 1] <= sl) ++dst;
+    while (dst > 0 && dst_lo[dst] > sl) --dst;
+    const int64_t row = soffs[dst] + (sl - seg_lo[dst]);
+    if (row < rows_cap) {
+      double* rw = rows + row * (D + 1);
+      for (int c = 0; c < D; ++c) rw[c] = xprev[xidx(i, c, D)];
+      rw[D] = __longlong_as_double(lo + i);
+    }
+  }
+}
 
 template <int IT>
 __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
@@ -1501,7 +1652,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ uint64_t smu[16];
   __shared__ DevScalars sd;
   __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
-  __shared__ int64_t sown_lo, sown_hi, sra, srb;
+  __shared__ int64_t sown_lo, sown_hi, sra, srb, ssend;
   __shared__ uint64_t sbase;
   __shared__ int32_t se[(kRsBlock * IT)];
   __shared__ int64_t sfirst;
@@ -1526,20 +1677,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     sd.Qs = udiv_n(S, N, sd.invN);
     sd.Rs = S - sd.Qs * N;
     sd.invS = 1.0 / (double)S;
-    const int64_t cov_lo = sys_count_exact(&sd, N, base);
-    const int64_t cov_hi = sys_count_exact(&sd, N, base + sd.local);
     const int64_t own_lo = r.lo, own_hi = r.lo + r.n;
     // rows this rank sends: destination blocks in rank order (lower ranks,
     // then higher ranks), each the part of [cov_lo, cov_hi) it owns
-    int64_t soff = 0;
-    for (int k = 0; k < R; ++k) {
-      const int64_t dlo = (int64_t)(((__int128)N * k) / R), dhi = (int64_t)(((__int128)N * (k + 1)) / R);
-      const int64_t a = cov_lo > dlo ? cov_lo : dlo, b = cov_hi < dhi ? cov_hi : dhi;
-      sdst_lo[k] = dlo;
-      sseg_lo[k] = a;
-      ssoff[k] = soff;
-      if (k != q && b > a) soff += b - a;
-    }
+    int64_t cov_lo, cov_hi;
+    ssend = send_tables(&sd, N, R, q, sd.local, sdst_lo, sseg_lo, ssoff, &cov_lo, &cov_hi);
     sown_lo = own_lo;
     sown_hi = own_hi;
     const int64_t ca = cov_lo < own_lo ? own_lo : (cov_lo > own_hi ? own_hi : cov_lo);
@@ -1575,6 +1717,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   auto clamp_own = [&](int64_t s) { return s < own_lo ? own_lo : (s > own_hi ? own_hi : s); };
   int64_t s0 = sys_count(&sd, N, run);
   if (threadIdx.x == 0) sfirst = clamp_own(s0) - own_lo;
+  // more rows than the bounded send buffer holds (this rank carries most of
+  // the weight): keep the CDF, the host regrows the buffer and k_rows_fill
+  // writes every row from it (rare; the hot path only tests the flag)
+  const bool spill = ssend > r.rows_cap;
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     run += qv[k];
@@ -1583,22 +1729,10 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     const int64_t l0 = clamp_own(s0), l1 = clamp_own(s1);
     se[threadIdx.x * IT + k] = (int32_t)(l1 - own_lo);
     if (l1 > l0) r.mk.mark[l0 - own_lo] = (r.mk.epoch << 32) | (uint64_t)i;
+    if (spill && i < r.n) r.C[i] = run;
     // slots of other ranks: state rows, by destination then slot
-    for (int64_t sl = s0; sl < s1; ++sl) {
-      if (sl >= own_lo && sl < own_hi) {
-        sl = own_hi - 1;  // skip the own block
-        continue;
-      }
-      int dst = (int)(((__int128)sl * R) / (int64_t)N);  // owner of global slot sl
-      while (dst + 1 < R && sdst_lo[dst + 1] <= sl) ++dst;
-      while (dst > 0 && sdst_lo[dst] > sl) --dst;
-      const int64_t row = ssoff[dst] + (sl - sseg_lo[dst]);
-      if (row < r.rows_cap) {
-        double* rw = r.rows + row * (r.D + 1);
-        for (int c = 0; c < r.D; ++c) rw[c] = r.xprev[xidx(i, c, r.D)];
-        rw[r.D] = __longlong_as_double(r.lo + i);
-      }
-    }
+    if (!spill)
+      send_rows(s0, s1, i, own_lo, own_hi, R, N, sdst_lo, sseg_lo, ssoff, r.rows_cap, r.rows, r.xprev, r.D, r.lo);
     s0 = s1;
   }
   __syncthreads();
@@ -1616,6 +1750,40 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     }
     r.mk.cmark[g] = (r.mk.epoch << 32) | (uint64_t)(pbase + lo);
   }
+}
+
+// The send rows of a resample whose rows overflowed the bounded buffer, from
+// the CDF k_rank_b kept (one thread per particle; the plan's scalars from dev)
+struct RowsFillArgs {
+  const uint64_t* C;
+  int64_t n;
+  int R, rank;
+  int64_t lo;
+  const DevScalars* dev;
+  const uint64_t* totals;
+  int64_t n_global;
+  const double* xprev;
+  int D;
+  double* rows;
+  int64_t rows_cap;
+};
+
+__global__ __launch_bounds__(256) void k_rows_fill(RowsFillArgs r) {
+  __shared__ DevScalars sd;
+  __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
+  const uint64_t N = (uint64_t)r.n_global;
+  if (threadIdx.x == 0) {
+    sd = *r.dev;
+    int64_t a, b;
+    send_tables(&sd, N, r.R, r.rank, r.totals[r.rank], sdst_lo, sseg_lo, ssoff, &a, &b);
+  }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= r.n) return;
+  const uint64_t prev = i == 0 ? sd.base : r.C[i - 1], cur = r.C[i];
+  const int64_t s0 = sys_count(&sd, N, prev);
+  const int64_t s1 = cur > prev ? sys_count(&sd, N, cur) : s0;
+  send_rows(s0, s1, i, r.lo, r.lo + r.n, r.R, N, sdst_lo, sseg_lo, ssoff, r.rows_cap, r.rows, r.xprev, r.D, r.lo);
 }
 
 enum SearchMode { SEARCH_SYSTEMATIC = 0, SEARCH_MULTINOMIAL = 1, SEARCH_SAMPLE = 2 };

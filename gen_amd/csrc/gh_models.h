@@ -420,9 +420,17 @@ struct KitParams {
   __device__ KitParams rebase(const double* __restrict__) const { return *this; }
 };
 
+// The Kitagawa latent draws come in pairs: particles p and p + 64 of every
+// 128-particle group (the two 64-particle tiles a pair-stepping lane owns)
+// share one Philox block and its Box–Muller pair — z0 for p, z1 for p + 64 —
+// so k_step_pairs spends one counter block and one log / sqrt / sincos per two
+// particles.  The draw of a particle is a function of its global id alone.
+__device__ __forceinline__ uint64_t kit_pair_id(uint64_t pid) { return ((pid >> 7) << 6) | (pid & 63); }
+
 struct KitModel {
   static constexpr int kD = 1;
   static constexpr int kMinWaves = 8;
+  static constexpr bool kPairs = true;  // k_step_pairs: two particles per lane
   using Params = KitParams;
 
   __device__ static double obs(const Params& p, const StepObs& o, double x) {
@@ -455,26 +463,49 @@ struct KitModel {
     const double diff = y[0] - m;
     return -(diff * diff) * p.inv2vy + p.csty;
   }
+  __device__ static double mean(const StepObs& o, double v) { return ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct; }
+  // the particle's standard normal of step t (its half of the shared pair)
+  __device__ static double znorm(uint64_t seed, uint64_t pid, uint32_t t, const Draw& dr) {
+    double z0, z1;
+    normal_pair(rng_block(seed, kit_pair_id(pid), t, dr.stream, dr.base), &z0, &z1, dr.tab);
+    return ((pid >> 6) & 1) ? z1 : z0;
+  }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
-    double z0, z1;
-    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1, dr.tab);
-    x[0] = p.mu1 + p.s1 * z0;
+    x[0] = p.mu1 + p.s1 * znorm(seed, pid, 1, dr);
     return obs(p, o, x[0]);
   }
   __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 uint32_t t, int /*proposal*/, const double* xp, double* x,
                                 Draw dr = {STREAM_STEP, 0}) {
-    double z0, z1;
-    normal_pair(rng_block(seed, pid, t, dr.stream, dr.base), &z0, &z1, dr.tab);
-    const double v = xp[0];
-    const double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
-    x[0] = mean + p.sx * z0;
+    x[0] = mean(o, xp[0]) + p.sx * znorm(seed, pid, t, dr);
     return obs(p, o, x[0]);
+  }
+  // both particles of a pair (pid0 with bit 6 clear, pid0 + 64) from one block:
+  // the same values as init / step of each
+  __device__ static void init2(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid0, double* x0,
+                               double* x1, double* w0, double* w1, const Draw& dr) {
+    double z0, z1;
+    normal_pair(rng_block(seed, kit_pair_id(pid0), 1, dr.stream, dr.base), &z0, &z1, dr.tab);
+    *x0 = p.mu1 + p.s1 * z0;
+    *x1 = p.mu1 + p.s1 * z1;
+    *w0 = obs(p, o, *x0);
+    *w1 = obs(p, o, *x1);
+  }
+  __device__ static void step2(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid0, uint32_t t,
+                               double xp0, double xp1, double* x0, double* x1, double* w0, double* w1,
+                               const Draw& dr) {
+    double z0, z1;
+    normal_pair(rng_block(seed, kit_pair_id(pid0), t, dr.stream, dr.base), &z0, &z1, dr.tab);
+    *x0 = mean(o, xp0) + p.sx * z0;
+    *x1 = mean(o, xp1) + p.sx * z1;
+    *w0 = obs(p, o, *x0);
+    *w1 = obs(p, o, *x1);
   }
 };
 
 // ------------------------------------- nonlinear SSM, Gaussian custom proposal
+// (draws: the nonlinear SSM's paired normals, KitModel::znorm)
 // A user-parameterised custom proposal in Gen's sense (particle_filter.jl:
 // 79-91,139-154 via the SimpleExtendingTraceTranslator, trace_translators.jl:
 // 775-802): x_t ~ q = normal(mu_q, sigma_q), mu_q = alpha m + beta y_t + gamma
@@ -505,18 +536,12 @@ struct KitGaussModel {
   __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return KitModel::obs(p, o, x[0]); }
   __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 int /*proposal*/, double* x, Draw dr = {STREAM_INIT, 0}) {
-    double z0, z1;
-    normal_pair(rng_block(seed, pid, 1, dr.stream, dr.base), &z0, &z1, dr.tab);
-    return propose(p, o, p.mu1, p.inv2v1, p.cst1, z0, x);
+    return propose(p, o, p.mu1, p.inv2v1, p.cst1, KitModel::znorm(seed, pid, 1, dr), x);
   }
   __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid,
                                 uint32_t t, int /*proposal*/, const double* xp, double* x,
                                 Draw dr = {STREAM_STEP, 0}) {
-    double z0, z1;
-    normal_pair(rng_block(seed, pid, t, dr.stream, dr.base), &z0, &z1, dr.tab);
-    const double v = xp[0];
-    const double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o.ct;
-    return propose(p, o, mean, p.inv2vx, p.cstx, z0, x);
+    return propose(p, o, KitModel::mean(o, xp[0]), p.inv2vx, p.cstx, KitModel::znorm(seed, pid, t, dr), x);
   }
 };
 

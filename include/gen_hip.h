@@ -235,8 +235,10 @@ int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal);
 int gh_pf_init_q(gh_model* m, const gh_obs* obs, int proposal, const double* proposal_args, int n_proposal_args,
                  int64_t n_particles, uint64_t seed, const gh_pf_opts* opts, gh_pf** out);
 int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const double* proposal_args, int n_proposal_args);
-/* ess_threshold NaN means the reference's default N/2; any other value is the
-   threshold as given (resample iff ESS < ess_threshold, so <= 0 never resamples).  If did_resample/ess are non-NULL the
+/* ess_threshold NaN means the reference's default N/2; any other value >= 0 is
+   the threshold as given (resample iff ESS < ess_threshold, so 0 never
+   resamples, as in Gen); a negative threshold is GH_E_INVAL (before round 3,
+   values <= 0 selected N/2).  If did_resample/ess are non-NULL the
    call synchronises and reports them; otherwise the decision stays on the
    device and the call is asynchronous. */
 int gh_pf_maybe_resample(gh_pf* pf, double ess_threshold, int* did_resample, double* ess);
@@ -299,6 +301,13 @@ int gh_pf_kernel_time(gh_pf* pf, double* avg_ms, int64_t* n_launches, int reset)
    the plan gh_pf_maybe_resample follows; exposed for tests and integrators. */
 int gh_sys_plan(int64_t n_global, int world, int rank, const uint64_t* totals, uint64_t offset,
                 int64_t* send_lo, int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi);
+/* the grouped messages that plan becomes (host only): peers and byte counts of
+   the sends and receives, rows of d + 1 doubles, in the order both transports
+   post them (RCCL ncclSend/ncclRecv in one group, or gh_host_comm.sendrecv).
+   Arrays hold up to world - 1 entries. */
+int gh_debug_exchange_lists(int64_t n_global, int world, int rank, const uint64_t* totals, uint64_t offset, int d,
+                            int* n_send, int* send_peer, uint64_t* send_bytes, int* n_recv, int* recv_peer,
+                            uint64_t* recv_bytes);
 
 /* ---- importance sampling ---------------------------------------------------- */
 int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t seed,

@@ -592,6 +592,17 @@ static double kit_gauss(const model_t* m, const obs_t* o, double mean, double in
   return w - kit_lpn(x[0], mq, m->qa[4], m->qa[5]);
 }
 
+/* The nonlinear SSM's latent draw: particles p and p + 64 of every 128-particle
+   group share one counter block (id ((p >> 7) << 6) | (p & 63)) and its
+   Box–Muller pair, z0 for p and z1 for p + 64. */
+static double kit_z(uint64_t seed, uint64_t pid, uint32_t t, uint32_t stream, uint32_t base) {
+  uint32_t w[4];
+  rng(seed, ((pid >> 7) << 6) | (pid & 63), t, stream, base, w);
+  double z0, z1;
+  box_muller(w[0], w[1], w[2], &z0, &z1);
+  return ((pid >> 6) & 1) ? z1 : z0;
+}
+
 static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
                             int proposal, double* x, uint32_t stream, uint32_t base) {
   if (m->family == ORC_REGRESSION) {
@@ -620,10 +631,8 @@ static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const
     }
     return lgssm_obs(m, x, o);
   } else if (m->family == ORC_KITAGAWA) {
-    double z[2];
-    normals_at(seed, pid, 1, stream, base, 1, z);
-    if (proposal == ORC_PROPOSAL_GAUSSIAN) return kit_gauss(m, o, m->mu1, m->inv2v1, m->cst1, z[0], x);
-    x[0] = m->mu1 + m->s1 * z[0];
+    if (proposal == ORC_PROPOSAL_GAUSSIAN) return kit_gauss(m, o, m->mu1, m->inv2v1, m->cst1, kit_z(seed, pid, 1, stream, base), x);
+    x[0] = m->mu1 + m->s1 * kit_z(seed, pid, 1, stream, base);
     if (!o->present) return 0.0;
     double diff = o->bt[0] - x[0] * x[0] / 20.0;
     return -(diff * diff) * m->inv2vy + m->csty;
@@ -682,12 +691,10 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
     }
     return lgssm_obs(m, x, o);
   } else if (m->family == ORC_KITAGAWA) {
-    double z[2];
-    normals_at(seed, pid, t, stream, base, 1, z);
     double v = xp[0];
     double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o->ct;
-    if (proposal == ORC_PROPOSAL_GAUSSIAN) return kit_gauss(m, o, mean, m->inv2vx, m->cstx, z[0], x);
-    x[0] = mean + m->sx * z[0];
+    if (proposal == ORC_PROPOSAL_GAUSSIAN) return kit_gauss(m, o, mean, m->inv2vx, m->cstx, kit_z(seed, pid, t, stream, base), x);
+    x[0] = mean + m->sx * kit_z(seed, pid, t, stream, base);
     if (!o->present) return 0.0;
     double diff = o->bt[0] - x[0] * x[0] / 20.0;
     return -(diff * diff) * m->inv2vy + m->csty;

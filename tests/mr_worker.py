@@ -24,6 +24,8 @@ def build_model(name):
         return gen.LinearGaussianSSM.benchmark(10)
     if name == "kit":
         return gen.KitagawaSSM(10.0, 1.0)
+    if name == "kit_sharp":  # peaked weights: one particle (one rank) holds nearly all of them
+        return gen.KitagawaSSM(10.0, 0.01)
     raise ValueError(name)
 
 

@@ -81,6 +81,53 @@ def test_sys_plan_matches_bruteforce(R):
                 assert (slo[r], shi[r]) == (plans[r][2][q], plans[r][3][q])
 
 
+def exchange_lists(n, R, q, totals, o, d):
+    lib = _lib.load()
+    tot = np.ascontiguousarray(totals, dtype=np.uint64)
+    ns, nr = ctypes.c_int(), ctypes.c_int()
+    sp, rp = np.zeros(R, dtype=np.int32), np.zeros(R, dtype=np.int32)
+    sb, rb = np.zeros(R, dtype=np.uint64), np.zeros(R, dtype=np.uint64)
+    i32 = POINTER(ctypes.c_int)
+    _lib.check(lib.gh_debug_exchange_lists(
+        ctypes.c_int64(n), R, q, tot.ctypes.data_as(POINTER(c_uint64)), ctypes.c_uint64(int(o)), d, ctypes.byref(ns),
+        sp.ctypes.data_as(i32), sb.ctypes.data_as(POINTER(c_uint64)), ctypes.byref(nr), rp.ctypes.data_as(i32),
+        rb.ctypes.data_as(POINTER(c_uint64))))
+    return sp[: ns.value], sb[: ns.value], rp[: nr.value], rb[: nr.value]
+
+
+@pytest.mark.parametrize("R", [2, 3, 5, 8])
+def test_exchange_lists_pair_up(R):
+    """The grouped messages both transports post (finish_plan's lists): every
+    send of q to r is the receive of r from q with the same byte count, the
+    rows are gh_sys_plan's slot ranges, no rank messages itself, and peers are
+    in rank order on both sides (RCCL's grouped send/recv and the host
+    transport's sendrecv take the lists as they are)."""
+    rng = np.random.default_rng(100 + R)
+    d = 4
+    for trial in range(20):
+        n = int(rng.integers(R, 5000))
+        totals = rng.integers(0, 1 << 40, size=R).astype(np.uint64)
+        if trial % 4 == 0:  # one rank holds (nearly) all the weight: it sends to everyone
+            totals[:] = 0
+            totals[rng.integers(0, R)] = 1 << 41
+        if totals.sum() == 0:
+            totals[0] = 7
+        o = int(rng.integers(0, int(sum(int(t) for t in totals))))
+        lists = [exchange_lists(n, R, q, totals, o, d) for q in range(R)]
+        for q in range(R):
+            sp, sb, rp, rb = lists[q]
+            slo, shi, rlo, rhi = plan(n, R, q, totals, o)
+            assert q not in sp and q not in rp
+            assert list(sp) == sorted(sp) and list(rp) == sorted(rp)
+            for peer, b in zip(sp, sb):
+                assert b == (shi[peer] - slo[peer]) * (d + 1) * 8
+                osp, osb, orp, orb = lists[peer]
+                assert b == orb[list(orp).index(q)]
+            for peer, b in zip(rp, rb):
+                assert b == (rhi[peer] - rlo[peer]) * (d + 1) * 8
+            assert len(rp) == sum(1 for r in range(R) if r != q and rhi[r] > rlo[r])
+
+
 def test_sys_plan_rejects_bad_arguments():
     lib = _lib.load()
     tot = np.array([0, 0], dtype=np.uint64)
@@ -231,12 +278,15 @@ def test_gloo_sharded_oracle_with_product_plan(tmp_path, R):
 # reference's default N/2 (the worker passes no --thr)
 @pytest.mark.parametrize("model,R,thr,n", [("lg4", 2, 3001.0, 3001), ("lg4", 3, None, 3001), ("kit", 2, None, 3001),
                                             ("kit", 2, 0.0, 3001), ("lg10", 2, 3001.0, 3001),
-                                            ("lg4", 2, 1e9, 20011), ("kit", 4, 1e9, 4003)])
+                                            ("lg4", 2, 1e9, 20011), ("kit", 4, 1e9, 4003),
+                                            ("kit_sharp", 4, None, 4003)])
 def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr, n):
     """R ranks share GPU 0 through the gloo host transport; the gathered shards
     equal the single-rank oracle bit for bit (log-ML within 1e-9).  n = 20011
     spans several 4096-particle tiles per rank; R = 4 with the peaked
-    Kitagawa weights moves rows across several ranks."""
+    Kitagawa weights moves rows across several ranks; kit_sharp (var_y = 0.01)
+    puts nearly all the weight on one rank, whose rows overflow the bounded send
+    buffer (2 n rows) and are written by the regrow path (k_rows_fill)."""
     from oracle import oracle as O
     from tests.mr_worker import build_model
 
