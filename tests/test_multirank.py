@@ -89,7 +89,7 @@ def exchange_lists(n, R, q, totals, o, d):
     sb, rb = np.zeros(R, dtype=np.uint64), np.zeros(R, dtype=np.uint64)
     i32 = POINTER(ctypes.c_int)
     _lib.check(lib.gh_debug_exchange_lists(
-        ctypes.c_int64(n), R, q, tot.ctypes.data_as(POINTER(c_uint64)), ctypes.c_uint64(int(o)), d, ctypes.byref(ns),
+        n, R, q, tot.ctypes.data_as(POINTER(c_uint64)), int(o), d, ctypes.byref(ns),
         sp.ctypes.data_as(i32), sb.ctypes.data_as(POINTER(c_uint64)), ctypes.byref(nr), rp.ctypes.data_as(i32),
         rb.ctypes.data_as(POINTER(c_uint64))))
     return sp[: ns.value], sb[: ns.value], rp[: nr.value], rb[: nr.value]
