@@ -995,7 +995,7 @@ constexpr int kRsBlock = 1024;
 constexpr int kRsItems = 4;
 constexpr int kRsTile = kRsBlock * kRsItems;  // particles per block
 constexpr int kRsPart = 4;                    // step partials per thread (nb_part <= 4096)
-constexpr int kRsPoll = 8;                    // tile totals polled per lane of wave 0 (grid <= 512)
+constexpr int kRsPoll = 8;                    // polling waves x 64 tiles: grid <= 512
 
 struct Resample1Args {
   const double* pm;        // step-kernel block partials
@@ -1194,7 +1194,7 @@ __device__ uint64_t g_rs_stamps[1024 * 8];
 #define GH_RS_STAMP(k)
 #endif
 
-template <bool MARKS, int IT>
+template <bool MARKS, int IT, bool SUMS>
 __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   __shared__ double smd[32];
   __shared__ uint64_t smu[32];
@@ -1220,7 +1220,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
 #pragma unroll
   for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
   double M, s1 = 0.0, s2 = 0.0;
-  const bool sums = r.sums_in_pass != 0;  // uniform
+  constexpr bool sums = SUMS;  // the step wrote block maxima only: the sums come from this pass
   // KP partials per thread stay in registers (one round trip for the maxima;
   // the sums of small tiles ride along, larger tiles load them once M is known)
   constexpr int KP = IT > kRsPart ? IT : kRsPart;
@@ -1354,89 +1354,91 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     st_sc1(&r.ts1[blockIdx.x], (as_u64(s1) & ~kTag) | par);
     st_sc1(&r.ts2[blockIdx.x], (as_u64(s2) & ~kTag) | par);
   }
-  if (threadIdx.x < 64) {  // wave 0 reads every tile total (DPP sums, no block reduction)
-    const u32x4 wr = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);  // independent of the totals
-    // the grid is at most kRsPoll * 64 blocks (host-checked): each lane polls
-    // its kRsPoll tiles together (one round trip per sweep, not per tile)
-    // one sweep polls the tile totals and, with sums_in_pass, the tile sums
-    uint64_t v[kRsPoll], v1[kRsPoll], v2[kRsPoll];
-    bool ok[kRsPoll];
-#pragma unroll
-    for (int k = 0; k < kRsPoll; ++k) {
-      ok[k] = threadIdx.x + 64 * k >= gridDim.x;
-      v[k] = v1[k] = v2[k] = par;
-    }
-    for (unsigned spins = 0;; ++spins) {  // bounded (~0.5 s): a grid that is not co-resident errors out
-#pragma unroll
-      for (int k = 0; k < kRsPoll; ++k)
-        if (!ok[k]) {
-          const unsigned b = threadIdx.x + 64 * k;
-          v[k] = ld_sc1(&r.tsum[b]);
+  // waves 0..7 read the tile words, 64 tiles each (grid <= 512, host-checked):
+  // one poll in flight per lane, so the kernel's register budget stays at two
+  // resident 1024-thread blocks per CU; the wave sums (integer totals in any
+  // order, the weight sums by the DPP tree) are combined by thread 0 in wave
+  // order — the same arithmetic in every block
+  __shared__ uint64_t spa[8], spb[8];
+  __shared__ double spg[2][8];
+  {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (w < 8) {
+      const unsigned b = (unsigned)(w * 64 + lane);
+      const bool mine = b < gridDim.x;
+      uint64_t v = par, v1 = par, v2 = par;
+      bool ok = !mine;
+      for (unsigned spins = 0;; ++spins) {  // bounded (~0.5 s): a grid that is not co-resident errors out
+        if (!ok) {
+          v = ld_sc1(&r.tsum[b]);
           if (sums) {
-            v1[k] = ld_sc1(&r.ts1[b]);
-            v2[k] = ld_sc1(&r.ts2[b]);
+            v1 = ld_sc1(&r.ts1[b]);
+            v2 = ld_sc1(&r.ts2[b]);
           }
         }
-      bool all_ok = true;
-#pragma unroll
-      for (int k = 0; k < kRsPoll; ++k) {
-        ok[k] = ok[k] || ((v[k] & kTag) == par && (v1[k] & kTag) == par && (v2[k] & kTag) == par);
-        all_ok = all_ok && ok[k];
+        ok = ok || ((v & kTag) == par && (v1 & kTag) == par && (v2 & kTag) == par);
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spins == (1u << 22)) {
+          r.dev->error = 7;  // GH_E_STATE
+          sfail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      if (__builtin_amdgcn_ballot_w64(!all_ok) == 0) break;
-      if (spins == (1u << 22)) {
-        r.dev->error = 7;  // GH_E_STATE
-        if (threadIdx.x == 0) sfail = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    GH_RS_STAMP(3);
-    uint64_t before = 0, all = 0;
-    double g1 = 0.0, g2 = 0.0;  // tile order within each lane, then the DPP tree: the same in every block
-#pragma unroll
-    for (int k = 0; k < kRsPoll; ++k) {
-      const unsigned b = threadIdx.x + 64 * k;
-      if (b >= gridDim.x) continue;
-      const uint64_t x = v[k] & ~kTag;
-      all += x;
-      if (b < blockIdx.x) before += x;
-      g1 += as_f64(v1[k] & ~kTag);
-      g2 += as_f64(v2[k] & ~kTag);
-    }
-    all = wave_sum_u64(all);
-    before = wave_sum_u64(before);
-    if (sums) {
-      g1 = wave_sum(g1);
-      g2 = wave_sum(g2);
-    }
-    if (threadIdx.x == 0) {
+      const uint64_t x = mine ? (v & ~kTag) : 0ull;
+      const uint64_t all = wave_sum_u64(x);
+      const uint64_t before = wave_sum_u64(b < blockIdx.x ? x : 0ull);
+      double g1 = 0.0, g2 = 0.0;
       if (sums) {
-        sS[0] = g1;
-        sS[1] = g2;
-        sfire = (g1 * g1) / g2 < r.d.thr;
+        g1 = wave_sum(mine ? as_f64(v1 & ~kTag) : 0.0);
+        g2 = wave_sum(mine ? as_f64(v2 & ~kTag) : 0.0);
       }
-      const uint64_t N = (uint64_t)r.d.n_global;
-      sd.S = all;
-      sd.base = 0;
-      sd.local = all;
-      sd.o = scale_u53(u53_bits(wr.x, wr.y), all);
-      sd.invN = r.d.inv_n;
-      sd.Qs = udiv_n(all, N, sd.invN);
-      sd.Rs = all - sd.Qs * N;
-      sd.invS = recip_est((double)all);
-      sbase = before;
-      if (blockIdx.x == 0) {
-        r.dev->bar_gen = sgen;  // every block has published, so has read the old value
-        r.dev->S = sd.S;
-        r.dev->base = 0;
-        r.dev->local = sd.local;
-        r.dev->o = sd.o;
-        r.dev->Qs = sd.Qs;
-        r.dev->Rs = sd.Rs;
-        r.dev->invN = sd.invN;
-        r.dev->invS = sd.invS;
+      if (lane == 0) {
+        spa[w] = all;
+        spb[w] = before;
+        spg[0][w] = g1;
+        spg[1][w] = g2;
       }
+    }
+  }
+  lds_barrier();
+  GH_RS_STAMP(3);
+  if (threadIdx.x == 0) {
+    const u32x4 wr = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);  // independent of the totals
+    uint64_t all = 0, before = 0;
+    double g1 = 0.0, g2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      all += spa[k];
+      before += spb[k];
+      g1 += spg[0][k];
+      g2 += spg[1][k];
+    }
+    if (sums) {
+      sS[0] = g1;
+      sS[1] = g2;
+      sfire = (g1 * g1) / g2 < r.d.thr;
+    }
+    const uint64_t N = (uint64_t)r.d.n_global;
+    sd.S = all;
+    sd.base = 0;
+    sd.local = all;
+    sd.o = scale_u53(u53_bits(wr.x, wr.y), all);
+    sd.invN = r.d.inv_n;
+    sd.Qs = udiv_n(all, N, sd.invN);
+    sd.Rs = all - sd.Qs * N;
+    sd.invS = recip_est((double)all);
+    sbase = before;
+    if (blockIdx.x == 0) {
+      r.dev->bar_gen = sgen;  // every block has published, so has read the old value
+      r.dev->S = sd.S;
+      r.dev->base = 0;
+      r.dev->local = sd.local;
+      r.dev->o = sd.o;
+      r.dev->Qs = sd.Qs;
+      r.dev->Rs = sd.Rs;
+      r.dev->invN = sd.invN;
+      r.dev->invS = sd.invS;
     }
   }
   lds_barrier();
