@@ -29,6 +29,8 @@ from .pf import (
     maybe_resample,
     maybe_resample_async,
     metropolis_hastings,
+    gaussian_drift,
+    GaussianDriftProposal,
     mh,
     particle_filter_step,
     rejuvenate,
@@ -50,5 +52,5 @@ __all__ = [
     "particle_filter_step", "rejuvenate", "run_particle_filter", "sample_unweighted_traces", "set_default_context",
     "conditional_particle_filter_step", "conditional_smc", "get_particle", "initialize_conditional_particle_filter",
     "particle_gibbs", "GenHipError", "ObservationBatch", "prepare_observations", "Selection", "select",
-    "metropolis_hastings", "mh", "simulate", "SimulatedTraces", "dists",
+    "metropolis_hastings", "mh", "simulate", "SimulatedTraces", "dists", "gaussian_drift", "GaussianDriftProposal",
 ]

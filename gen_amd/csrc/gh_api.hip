@@ -2296,6 +2296,75 @@ extern "C" int gh_pf_mh_select(gh_pf* pf, uint32_t selection, int n_moves, int64
   return GH_OK;
 }
 
+// mh(trace, drift, (sd,)) on every particle (gh_rejuv.h k_mh_drift)
+extern "C" int gh_pf_mh_drift(gh_pf* pf, uint32_t selection, const double* sd, int n_moves, int64_t* accepted) {
+  if (!pf || !sd) return set_err(GH_E_INVAL, "gh_pf_mh_drift: null argument");
+  if (n_moves < 0) return set_err(GH_E_INVAL, "gh_pf_mh_drift: n_moves < 0");
+  if (pf->m->family == GH_FAMILY_HMM)
+    return set_err(GH_E_INVAL, "gh_pf_mh_drift: a Gaussian drift needs a continuous latent (not the HMM)");
+  if (selection == 0 || (selection & ~latent_addresses(pf->m)) != 0)
+    return set_err(GH_E_INVAL, "gh_pf_mh_drift: selection 0x%x names no latent address of this step (valid: 0x%x)",
+                   selection, latent_addresses(pf->m));
+  if (pf->m->family == GH_FAMILY_REGRESSION && pf->t != 1)
+    return set_err(GH_E_STATE, "gh_pf_mh_drift: the regression is a static model (t = 1)");
+  if (pf->resample_calls > 0) return set_err(GH_E_STATE, "gh_pf_mh_drift: call after a step and before maybe_resample");
+  if (pf->cond) return set_err(GH_E_STATE, "gh_pf_mh_drift: the distinguished particle of a conditional filter is fixed");
+  if ((uint64_t)pf->rejuv_moves + (uint64_t)n_moves > kRejuvMaxMoves)
+    return set_err(GH_E_INVAL, "gh_pf_mh_drift: more than %u moves at one step", kRejuvMaxMoves);
+  const int D = pf->D;
+  DriftSd dsd{};
+  for (int k = 0; k < D; ++k) {
+    // the regression's components are its addresses; an Unfold latent drifts as a whole
+    const bool sel = pf->m->family == GH_FAMILY_REGRESSION ? ((selection >> k) & 1u) != 0 : true;
+    if (sel && !(sd[k] > 0.0 && sd[k] < INFINITY))
+      return set_err(GH_E_INVAL, "gh_pf_mh_drift: sd[%d] = %g must be finite and > 0", k, sd[k]);
+    dsd.v[k] = sel ? sd[k] : 0.0;
+  }
+  HIP_TRY(hipSetDevice(pf->ctx->device));
+  if (!pf->acc_count) HIP_TRY(hipMalloc(&pf->acc_count, sizeof(unsigned long long)));
+  HIP_TRY(hipMemsetAsync(pf->acc_count, 0, sizeof(unsigned long long), pf->s));
+  const int t = pf->t;
+  if (n_moves > 0 && pf->n > 0) {
+    RejuvArgs a{};
+    if (t >= 2) {
+      a.xprev = slot_x(pf, t - 1);
+      a.anc = anc_for_step(pf, t);
+      a.res = pf->res_hist + t;
+      a.remote = pf->rows_recv;
+      a.ld_remote = pf->D + 1;
+    }
+    a.x = slot_x(pf, t);
+    a.n = pf->n;
+    a.lo = pf->lo;
+    a.seed = pf->seed;
+    a.t = (uint32_t)t;
+    a.move0 = pf->rejuv_moves;
+    a.select = selection;
+    a.n_moves = n_moves;
+    a.accepted = pf->acc_count;
+    const dim3 grid((unsigned)pf->nb_step), block(kBlock);
+    CHECK(with_model(pf->m, [&](auto model, const auto& p) {
+      using M = decltype(model);
+      if constexpr (!std::is_same<M, HMMModel>::value) {
+        if (t == 1)
+          hipLaunchKernelGGL((k_mh_drift<M, true>), grid, block, 0, pf->s, (const double*)pf->m->dparams, p,
+                             pf->last_obs, a, dsd);
+        else
+          hipLaunchKernelGGL((k_mh_drift<M, false>), grid, block, 0, pf->s, (const double*)pf->m->dparams, p,
+                             pf->last_obs, a, dsd);
+      }
+    }));
+    HIP_TRY(hipGetLastError());
+  }
+  pf->rejuv_moves += (uint32_t)n_moves;
+  if (accepted) {
+    unsigned long long h = 0;
+    CHECK(d2h(pf, &h, pf->acc_count, sizeof h));
+    *accepted = (int64_t)h;
+  }
+  return GH_OK;
+}
+
 extern "C" int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int32_t* did) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
   const int T = pf->t < max_steps ? pf->t : max_steps;

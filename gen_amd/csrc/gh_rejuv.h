@@ -51,6 +51,11 @@ struct RejuvArgs {
   unsigned long long* accepted;  // accepted moves (summed over particles)
 };
 
+// the drift's standard deviation per state component (0: not selected)
+struct DriftSd {
+  double v[16];
+};
+
 template <class Model, bool INIT>
 __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm, typename Model::Params p0,
                                                   StepObs o, RejuvArgs a) {
@@ -92,6 +97,74 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
 #pragma unroll
         for (int k = 0; k < D; ++k) x[k] = y[k];
         ll = ll2;
+        ++acc;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) a.x[xidx(j, k, D)] = x[k];
+  }
+  const uint64_t tot = wave_sum_u64((uint64_t)acc);
+  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(a.accepted, (unsigned long long)tot);
+}
+
+}  // namespace gh
+
+namespace gh {
+
+// mh(trace, drift, (sd,)) on every particle (src/inference/mh.jl:41-62, the
+// proposal form): a Gaussian drift proposal — `@trace(normal(trace[a], sd), a)`
+// for each selected latent address a of the current step (the LG-SSM's :x
+// drifts componentwise by the sd vector, a diagonal mvnormal) — then
+// update and accept iff log(rand()) < weight - fwd score + bwd score.  The
+// drift is symmetric, its forward and backward scores are the same number
+// ((x' - x)^2 = (x - x')^2 in floating point), so the acceptance ratio is the
+// update weight: the step's latent and observation scores (Model::score, the
+// trace's score columns) at x' minus those at x — the current step's latent
+// has no children yet.  Draws: move w's window as k_rejuv (normals from its
+// first blocks, the uniform from its last).
+template <class Model, bool INIT>
+__global__ __launch_bounds__(kBlock) void k_mh_drift(const double* __restrict__ prm, typename Model::Params p0,
+                                                     StepObs o, RejuvArgs a, DriftSd sd) {
+  constexpr int D = Model::kD;
+  const typename Model::Params p = p0.rebase(prm);
+  __shared__ double tab[kMathTabDoubles];
+  load_math_tab(tab);
+  lds_barrier();
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  unsigned acc = 0;
+  if (j < a.n) {
+    const uint64_t pid = (uint64_t)(a.lo + j);
+    double x[D], xp[D], y[D], z[D + 1];
+#pragma unroll
+    for (int k = 0; k < D; ++k) x[k] = a.x[xidx(j, k, D)];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xp[k] = 0.0;
+    if (!INIT) {
+      const int64_t src = *a.res ? (int64_t)a.anc[j] : j;
+      if (src >= 0) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) xp[k] = a.xprev[xidx(src, k, D)];
+      } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
+      }
+    }
+    double lat, ob;
+    Model::score(p, o, a.t, xp, x, &lat, &ob);
+    double s = lat + ob;
+    for (int m = 0; m < a.n_moves; ++m) {
+      const Draw dr = rejuv_draw(a.move0 + (uint32_t)m);
+      normals_n<D>(a.seed, pid, a.t, dr.stream, dr.base, z, tab);
+#pragma unroll
+      for (int k = 0; k < D; ++k) y[k] = sd.v[k] > 0.0 ? x[k] + sd.v[k] * z[k] : x[k];
+      Model::score(p, o, a.t, xp, y, &lat, &ob);
+      const double s2 = lat + ob;
+      const u32x4 w = rng_block(a.seed, pid, a.t, dr.stream, dr.base + kRejuvDraws - 1);
+      const double logu = gh_log(u53(w.x, w.y));
+      if (logu < s2 - s) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) x[k] = y[k];
+        s = s2;
         ++acc;
       }
     }

@@ -551,14 +551,24 @@ def rejuvenate(state: ParticleFilterState, n_moves: int = 1) -> int:
     return int(acc.value)
 
 
-def metropolis_hastings(state: ParticleFilterState, selection, n_moves: int = 1) -> int:
-    """``metropolis_hastings(trace, selection)`` (src/inference/mh.jl:14-28; alias
-    ``mh``) applied to every particle's trace: regenerate the selected choices
-    from their prior and accept with log(rand()) < the regenerate weight.  The
-    selection names latent addresses of the current step — the regression's
-    "slope" / "intercept" (examples/regression/quickstart.jl:17-22), or the
-    Unfold models' latent of the last step — and the particles' log weights
-    are unchanged.  Returns the accepted moves over this rank's particles."""
+class GaussianDriftProposal:
+    """The Gaussian drift proposal generative function, the proposal form of
+    ``metropolis_hastings(trace, proposal, proposal_args)`` (src/inference/mh.jl:41-62):
+
+        @gen function gaussian_drift(trace, selection, sd)
+            for a in selection: @trace(normal(trace[a], sd), a)   # mvnormal(x, diag(sd^2)) for a vector latent
+
+    ``proposal_args = (selection, sd)``, sd a scalar or one value per state
+    component."""
+
+    def __repr__(self):
+        return "gaussian_drift"
+
+
+gaussian_drift = GaussianDriftProposal()
+
+
+def _latent_mask(state: ParticleFilterState, selection) -> int:
     from .choicemap import Selection, select as _select
 
     sel = selection if isinstance(selection, Selection) else _select(*selection)
@@ -573,8 +583,38 @@ def metropolis_hastings(state: ParticleFilterState, selection, n_moves: int = 1)
             raise _lib.GenHipError(1, f"selection names {a}: only {sorted(names)} (the current step's latent "
                                       "addresses) are lowered")
         mask |= names[a]
+    return mask
+
+
+def metropolis_hastings(state: ParticleFilterState, selection, *args, n_moves: int | None = None) -> int:
+    """``metropolis_hastings`` (alias ``mh``) applied to every particle's trace;
+    the particles' log weights are unchanged.  Returns the accepted moves over
+    this rank's particles.
+
+    * ``mh(state, selection[, n_moves])`` — the selection form (mh.jl:14-28):
+      regenerate the selected choices from their prior, accept with
+      log(rand()) < the regenerate weight.  The selection names latent
+      addresses of the current step: the regression's "slope" / "intercept"
+      (examples/regression/quickstart.jl:17-22), or the Unfold models' latent
+      of the last step.
+    * ``mh(state, gaussian_drift, (selection, sd)[, n_moves])`` — the proposal
+      form (mh.jl:41-62) with the Gaussian drift proposal: accept with
+      log(rand()) < update weight - forward score + backward score."""
+    if selection is gaussian_drift or isinstance(selection, GaussianDriftProposal):
+        pargs = tuple(args[0]) if args else ()
+        n = n_moves if n_moves is not None else (int(args[1]) if len(args) > 1 else 1)
+        if len(pargs) != 2:
+            raise _lib.GenHipError(1, "gaussian_drift takes proposal_args = (selection, sd)")
+        mask = _latent_mask(state, pargs[0])
+        d = state.model.d
+        sd = np.ascontiguousarray(np.broadcast_to(np.asarray(pargs[1], dtype=np.float64), (d,)))
+        acc = c_int64()
+        _lib.check(_lib.load().gh_pf_mh_drift(state.h, mask, _lib.dptr(sd), int(n), byref(acc)))
+        return int(acc.value)
+    n = n_moves if n_moves is not None else (int(args[0]) if args else 1)
+    mask = _latent_mask(state, selection)
     acc = c_int64()
-    _lib.check(_lib.load().gh_pf_mh_select(state.h, mask, int(n_moves), byref(acc)))
+    _lib.check(_lib.load().gh_pf_mh_select(state.h, mask, int(n), byref(acc)))
     return int(acc.value)
 
 

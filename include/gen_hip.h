@@ -20,6 +20,8 @@
  *                           every particle               particle, as callers of the PF do)
  *   gh_pf_mh_select         mh(trace, selection) on      src/inference/mh.jl:14-28,
  *                           every particle               examples/regression/quickstart.jl:17-22
+ *   gh_pf_mh_drift          mh(trace, drift, (sd,)) on   src/inference/mh.jl:41-62 (proposal form)
+ *                           every particle
  *   gh_pf_init_conditional /
  *   gh_pf_step_conditional  conditional_smc              examples/pmmh/smc.jl:100-151
  *   gh_is_run               importance_sampling          src/inference/importance.jl:20-52
@@ -280,6 +282,15 @@ int gh_pf_rejuvenate(gh_pf* pf, int n_moves, int64_t* accepted);
    mh(trace, select(:slope)) / mh(trace, select(:intercept))).  The moves share
    gh_pf_rejuvenate's draw windows and per-step move counter. */
 int gh_pf_mh_select(gh_pf* pf, uint32_t selection, int n_moves, int64_t* accepted);
+/* mh(trace, drift, (sd,)) on every particle (src/inference/mh.jl:41-62, a
+   proposal generative function): the Gaussian drift proposal
+   `@trace(normal(trace[a], sd), a)` on the selected latent addresses of the
+   current step (bit layout as gh_pf_mh_select; the LG-SSM's vector :x drifts
+   componentwise with sd[0..d), a diagonal mvnormal), accept iff log(rand()) <
+   update weight - fwd score + bwd score (the symmetric drift's two scores
+   cancel exactly).  sd[d]: > 0 for the selected components.  Not for the
+   HMM (a discrete latent).  Same calling rules and draws as gh_pf_rejuvenate. */
+int gh_pf_mh_drift(gh_pf* pf, uint32_t selection, const double* sd /* [d] */, int n_moves, int64_t* accepted);
 /* Conditional SMC (examples/pmmh/smc.jl:100-151, the particle-Gibbs sweep):
    particle 0 is the distinguished particle, pinned to ref_x1 at init and to
    ref_xt at each step, its parent always itself, its weight the observation

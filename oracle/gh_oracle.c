@@ -952,6 +952,61 @@ int orc_pf_mh_select(orc_pf* pf, uint32_t mask, int n_moves, int64_t* accepted) 
   return 0;
 }
 
+static void model_score(const model_t* m, const obs_t* o, int t, const double* xp, const double* x, double* lat,
+                        double* ob);
+
+/* mh(trace, drift, (sd,)) on every particle (src/inference/mh.jl:41-62): the
+   Gaussian drift proposal on the selected latent addresses (the Unfold
+   families' x_t as a whole, the regression's :slope / :intercept by bit), the
+   update weight as the acceptance ratio (the symmetric drift's forward and
+   backward scores are equal); the trace scores of model_score. */
+int orc_pf_mh_drift(orc_pf* pf, uint32_t mask, const double* sd_in, int n_moves, int64_t* accepted) {
+  const uint32_t all = pf->m.family == ORC_REGRESSION ? 3u : 1u;
+  if (pf->m.family == ORC_HMM || mask == 0 || (mask & ~all)) return -1;
+  if (pf->m.family == ORC_REGRESSION && pf->t != 1) return -1;
+  if (pf->cond || pf->pending || pf->t < 1 || n_moves < 0 || (uint64_t)pf->moves + (uint64_t)n_moves > (1u << 24)) return -1;
+  const int D = pf->m.d;
+  double sd[64];
+  for (int k = 0; k < D; ++k) {
+    int sel = pf->m.family == ORC_REGRESSION ? (int)((mask >> k) & 1u) : 1;
+    if (sel && !(sd_in[k] > 0.0 && sd_in[k] < INFINITY)) return -1;
+    sd[k] = sel ? sd_in[k] : 0.0;
+  }
+  const int64_t n = pf->n;
+  const uint32_t t = (uint32_t)pf->t;
+  int64_t acc = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t pid = (uint64_t)(pf->lo + i);
+    double x[64], xp[64] = {0}, y[64], z[64], lat, ob;
+    for (int k = 0; k < D; ++k) x[k] = pf->x[(size_t)k * n + i];
+    if (t >= 2)
+      for (int k = 0; k < D; ++k) xp[k] = pf->xprev[(size_t)k * n + i];
+    model_score(&pf->m, &pf->obs, (int)t, xp, x, &lat, &ob);
+    double s = lat + ob;
+    for (int m = 0; m < n_moves; ++m) {
+      const uint32_t mv = pf->moves + (uint32_t)m;
+      const uint32_t stream = (uint32_t)S_MH + ((mv >> 12) << 4), base = (mv & 4095u) * 16u;
+      normals_at(pf->seed, pid, t, stream, base, D, z);
+      for (int k = 0; k < D; ++k) y[k] = sd[k] > 0.0 ? x[k] + sd[k] * z[k] : x[k];
+      model_score(&pf->m, &pf->obs, (int)t, xp, y, &lat, &ob);
+      const double s2 = lat + ob;
+      uint32_t w[4];
+      rng(pf->seed, pid, t, stream, base + 15u, w);
+      if (orc_log(unif53(w[0], w[1])) < s2 - s) {
+        for (int k = 0; k < D; ++k) x[k] = y[k];
+        s = s2;
+        ++acc;
+      }
+    }
+    for (int k = 0; k < D; ++k) pf->x[(size_t)k * n + i] = x[k];
+  }
+  pf->moves += (uint32_t)n_moves;
+  if (pf->record_history && pf->hx && pf->hx[t - 1])
+    memcpy(pf->hx[t - 1], pf->x, sizeof(double) * (size_t)D * n);
+  if (accepted) *accepted = acc;
+  return 0;
+}
+
 void orc_pf_local_stats(orc_pf* pf, double out[3]) {
   double M = -INFINITY;
   for (int64_t i = 0; i < pf->n; ++i) {

@@ -85,6 +85,7 @@ int orc_pf_num_steps(orc_pf* pf);
 int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* resampled);
 /* get_score of every current particle's trace (total [n]) and the per-step
    latent / observation choice scores (per_step [t][2][n], nullable); one shard */
+int orc_pf_mh_drift(orc_pf* pf, uint32_t mask, const double* sd, int n_moves, int64_t* accepted);
 int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step);
 double orc_log1p(double y);
 double orc_lgamma(double x);

@@ -79,6 +79,7 @@ def _load(path):
             "orc_pf_maybe_resample": (I, [V, c_double, D]),
             "orc_pf_rejuvenate": (I, [V, I, POINTER(c_int64)]),
             "orc_pf_mh_select": (I, [V, U32, I, POINTER(c_int64)]),
+            "orc_pf_mh_drift": (I, [V, U32, D, I, POINTER(c_int64)]),
             "orc_pf_init_conditional": (I, [V, D, I, D]),
             "orc_pf_step_conditional": (I, [V, D, I, D]),
             "orc_pf_log_ml_estimate": (c_double, [V]),
@@ -226,6 +227,14 @@ class OraclePF:
         acc = c_int64()
         if self.L.orc_pf_mh_select(self.h, int(mask), n_moves, ctypes.byref(acc)):
             raise RuntimeError("oracle: bad selection / mh after a resample")
+        return acc.value
+
+    def mh_drift(self, mask, sd, n_moves=1):
+        """mh(trace, drift, (sd,)) on every particle: Gaussian drift of the selected latent addresses."""
+        acc = c_int64()
+        sdv = np.ascontiguousarray(np.atleast_1d(sd), dtype=np.float64)
+        if self.L.orc_pf_mh_drift(self.h, int(mask), _d(sdv), n_moves, ctypes.byref(acc)):
+            raise RuntimeError("oracle: bad drift arguments / mh after a resample")
         return acc.value
 
     def log_ml_estimate(self):
