@@ -250,7 +250,7 @@ def secondary_c4(gen, ctx, a):
     the 16M-particle 8-GPU configuration (BASELINE.json configs[3])."""
     model = gen.KitagawaSSM(10.0, 1.0)  # examples/pmmh/run.jl:69 (var_x = 10, var_y = 1)
     n = 1 << 21
-    r = pf_run(gen, ctx, None, 1, a, model, n, "k_step<KitModel,false>",
+    r = pf_run(gen, ctx, None, 1, a, model, n, "k_step_pairs<KitModel,false>",
                lambda n_res: 16 * 1 + 16 + 4.0 * n_res / max(1, a.steps))
     pmc = pmc_profile("pmc_k_step_kitagawa.json")
     r["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
@@ -297,11 +297,13 @@ def secondary_c3(gen, ctx, a):
                    "chains": chains, "steps": steps},
         "kernel_ms": kms,
         "k_posterior": [round(float(x), 4) for x in ks],
-        "roofline": {"bound": "valu", "kernel": "k_coal",
+        "roofline": {"bound": "latency", "kernel": "k_coal",
                      "hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch") if pmc else None,
                      "valu_frac": pmc.get("valu_frac") if pmc else None,
                      "source": pmc.get("source") if pmc else None,
-                     "note": "state in LDS for the launch: HBM = one read + one write of the 544-byte rows"},
+                     "note": ("state in LDS for the launch: HBM = one read + one write of the 544-byte rows; "
+                              "VALU busy ~30 %: the chains wait on dependent LDS reads (event-count scans, "
+                              "per-move segment lookups), neither HBM nor VALU saturates")},
     }
     if not a.no_cpu_baseline:
         def make(threads):
@@ -393,7 +395,7 @@ def main(argv=None):
     else:
         model = gen.KitagawaSSM(10.0, 1.0)  # examples/pmmh/run.jl:69 (var_x = 10, var_y = 1)
         d = 1
-        kname = "k_step<KitModel,false>"
+        kname = "k_step_pairs<KitModel,false>" if world == 1 else "k_step<KitModel,false>"
     r = pf_run(gen, ctx, dist, world, a, model, a.particles, kname,
                lambda n_res: 16 * d + 16 + 4.0 * n_res / max(1, a.steps))
     # PMC HBM bytes per step-kernel launch of the profiled configs (tools/pmc_json.py)
