@@ -240,7 +240,9 @@ def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn):
             "bytes_per_particle_step": bytes_pp,
             # the whole step (every kernel and gap) against the same bytes
             "step_frac": bytes_pp * particles / (dt / a.steps) / 1e9 / HBM_PEAK_GBS,
-        },
+        } | ({"kernel_time_note": ("multi-rank: a resample step's kernel is split; the timed launch is part 1 "
+                                   "over every tile (slots taking received rows skipped), the part-2 re-runs "
+                                   "of those tiles are not in kernel_avg_ms")} if world > 1 else {}),
     }
 
 
