@@ -5,7 +5,9 @@ change points, min_uniform_continuous positions (:18-33), gamma(1, 1/200)
 rates and a piecewise Poisson process over the event times
 (poisson_process.jl:9-67); `mcmc_step` (:329-336) applies rate_move,
 position_move (when k > 0) and birth_death_move, each an involutive MH step
-(src/inference/mh.jl:85-98).  One device thread per chain.
+(src/inference/mh.jl:85-98); `simple_mcmc_step` (:338-345) replaces the
+birth/death move by mh(trace, select(:k)), the Dynamic DSL regenerate of k.
+One device thread per chain.
 """
 from __future__ import annotations
 
@@ -25,7 +27,9 @@ class CoalChains:
     run() continues them without moving their state over PCIe; `state` is
     read back on demand."""
 
-    def __init__(self, events, n_chains: int, seed: int = 0, chain0: int = 0, ctx: Context | None = None):
+    def __init__(self, events, n_chains: int, seed: int = 0, chain0: int = 0, ctx: Context | None = None,
+                 kernel: str = "mcmc_step"):
+        """kernel: "mcmc_step" (coal.jl:329-336) or "simple_mcmc_step" (:338-345)."""
         self.ctx = ctx or default_context()
         self.events = np.ascontiguousarray(np.sort(np.asarray(events, dtype=np.float64)))
         self.n_chains, self.seed, self.chain0 = int(n_chains), int(seed), int(chain0)
@@ -36,6 +40,9 @@ class CoalChains:
         self.h = c_void_p()
         _lib.check(_lib.load().gh_coal_create(self.ctx.h, self.chain0, self.n_chains, _lib.dptr(self.events),
                                               self.events.size, self.seed, byref(self.h)))
+        if kernel not in ("mcmc_step", "simple_mcmc_step"):
+            raise _lib.GenHipError(1, f"unknown coal kernel {kernel!r}")
+        _lib.check(_lib.load().gh_coal_set_kernel(self.h, 1 if kernel == "simple_mcmc_step" else 0))
 
     def run(self, n_iters: int, k_history: bool = False, accepts: bool = True):
         """n_iters mcmc_steps (the first call draws the start from the prior

@@ -344,7 +344,7 @@ struct gh_model {
   RegParams reg{};
 };
 
-static bool lg_supported(int d) { return (d >= 1 && d <= 8) || d == 10 || d == 12 || d == 16; }
+static bool lg_supported(int d) { return d >= 1 && d <= 16; }
 
 extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model** out) {
   if (!ctx || !desc || !out) return set_err(GH_E_INVAL, "gh_model_create: null argument");
@@ -365,7 +365,7 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
   if (!p) return fail(GH_E_INVAL, "params is NULL");
   if (desc->family == GH_FAMILY_LGSSM) {
     const int d = desc->d, dy = desc->dy;
-    if (!lg_supported(d)) return fail(GH_E_INVAL, "LGSSM: unsupported d (1..8, 10, 12, 16)");
+    if (!lg_supported(d)) return fail(GH_E_INVAL, "LGSSM: unsupported d (1..16)");
     if (dy < 1 || dy > kMaxObs) return fail(GH_E_INVAL, "LGSSM: dy must be in 1..32");
     const int64_t need = (int64_t)d * d + d + (int64_t)d * d + (int64_t)dy * d + dy +
                          (int64_t)dy * dy + d + (int64_t)d * d;
@@ -942,7 +942,8 @@ static int with_model(const gh_model* m, F&& f) {
     }                                                    \
     break;
         GH_LG_CASE(1) GH_LG_CASE(2) GH_LG_CASE(3) GH_LG_CASE(4) GH_LG_CASE(5) GH_LG_CASE(6)
-        GH_LG_CASE(7) GH_LG_CASE(8) GH_LG_CASE(10) GH_LG_CASE(12) GH_LG_CASE(16)
+        GH_LG_CASE(7) GH_LG_CASE(8) GH_LG_CASE(9) GH_LG_CASE(10) GH_LG_CASE(11) GH_LG_CASE(12)
+        GH_LG_CASE(13) GH_LG_CASE(14) GH_LG_CASE(15) GH_LG_CASE(16)
 #undef GH_LG_CASE
         default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", m->d);
       }
@@ -971,7 +972,8 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
 #define GH_LGO_CASE(DD) \
   case DD: launch_step_t<LGOptModel<DD>>(pf, pf->m->lg, o, a, init, e0, e1); break;
       GH_LGO_CASE(1) GH_LGO_CASE(2) GH_LGO_CASE(3) GH_LGO_CASE(4) GH_LGO_CASE(5) GH_LGO_CASE(6)
-      GH_LGO_CASE(7) GH_LGO_CASE(8) GH_LGO_CASE(10) GH_LGO_CASE(12) GH_LGO_CASE(16)
+      GH_LGO_CASE(7) GH_LGO_CASE(8) GH_LGO_CASE(9) GH_LGO_CASE(10) GH_LGO_CASE(11) GH_LGO_CASE(12)
+      GH_LGO_CASE(13) GH_LGO_CASE(14) GH_LGO_CASE(15) GH_LGO_CASE(16)
 #undef GH_LGO_CASE
       default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", pf->m->d);
     }
@@ -2853,6 +2855,7 @@ struct gh_coal {
   int64_t chain0 = 0, n = 0;
   uint64_t seed = 0;
   int iters = 0;
+  int simple = 0;           // 1: simple_mcmc_step (regenerate k as the third move)
   bool started = false;
   hipEvent_t e0 = nullptr, e1 = nullptr;
 };
@@ -2908,6 +2911,15 @@ extern "C" int gh_coal_create(gh_ctx* ctx, int64_t chain0, int64_t n_chains, con
   return GH_OK;
 }
 
+// which MCMC kernel gh_coal_step applies: 0 = mcmc_step (rate, position,
+// birth/death; coal.jl:329-336), 1 = simple_mcmc_step (rate, position,
+// mh(trace, select(K)); coal.jl:338-345)
+extern "C" int gh_coal_set_kernel(gh_coal* h, int kernel) {
+  if (!h || kernel < 0 || kernel > 1) return set_err(GH_E_INVAL, "gh_coal_set_kernel: kernel 0 (mcmc_step) or 1 (simple_mcmc_step)");
+  h->simple = kernel;
+  return GH_OK;
+}
+
 extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* khist, double* kernel_ms) {
   if (!h || n_iters < 0) return set_err(GH_E_INVAL, "gh_coal_step: bad argument");
   HIP_TRY(hipSetDevice(h->ctx->device));
@@ -2929,6 +2941,7 @@ extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* 
   a.ld = h->n;
   a.accepts = h->acc;
   a.khist = d_kh;
+  a.simple = h->simple;
   hipExtLaunchKernelGGL(k_coal, dim3((unsigned)((nc + kCoalBlock - 1) / kCoalBlock)), dim3(kCoalBlock),
                         coal_lds_bytes(h->E), s, h->e0, h->e1, 0, a);
   int rc = GH_OK;

@@ -58,8 +58,9 @@ struct CoalArgs {
   int init;              // 1: draw the start from the prior (generate)
   double* state;         // SoA [kCoalW][ld] rows (k, score, cp[32], h[33], pad); unused fields 0
   int64_t ld;            // chains per field column (>= n_chains)
-  int32_t* accepts;      // [n_chains][3] rate, position, birth/death
+  int32_t* accepts;      // [n_chains][3] rate, position, birth/death (simple: regenerate k)
   int32_t* khist;        // optional [n_chains][n_iters] k after each iteration
+  int simple;            // 1: simple_mcmc_step (coal.jl:338-345), mh(trace, select(K)) as the third move
 };
 
 // the two uniforms of Philox block b of an iteration: u53(x, y), u53(z, w);
@@ -94,6 +95,41 @@ struct CoalLds {
 __device__ __forceinline__ double coal_u(uint64_t seed, uint64_t c, uint32_t step, uint32_t d) {
   const u32x4 w = rng_block(seed, c, step, STREAM_MH, d);
   return u53(w.x, w.y);
+}
+
+// the piecewise Poisson process's logpdf (poisson_process.jl:32-51) in the
+// segment form sum_i [c_i log h_i - len_i h_i], segments in order
+__device__ __forceinline__ double coal_events_lp(const CoalArgs& a, int k, const CoalLds& s, const double* ev,
+                                                 const int32_t* bk, const double* tab) {
+  double lp = 0.0, b_lo = 0.0;
+  int n_lo = 0;
+  for (int i = 1; i <= k + 1; ++i) {
+    const double b_hi = i <= k ? s.cp(i) : a.T;
+    const int n_hi = i <= k ? coal_count(ev, bk, a.E, a.bscale, b_hi) : a.E;
+    const double h = s.h(i);
+    lp += (double)(n_hi - n_lo) * gh_log_unit(h, tab) - (b_hi - b_lo) * h;
+    n_lo = n_hi;
+    b_lo = b_hi;
+  }
+  return lp;
+}
+
+// the score from scratch (the decomposition of the header), segment by segment
+__device__ __forceinline__ double coal_full_score(const CoalArgs& a, int k, const CoalLds& s, const double* ev,
+                                                  const int32_t* bk, const double* tab) {
+  double sc = (double)k * a.kb - 3.0;
+  int n_lo = 0;
+  double b_lo = 0.0;
+  for (int i = 1; i <= k + 1; ++i) {
+    const double b_hi = i <= k ? s.cp(i) : a.T;
+    const int n_hi = i <= k ? coal_count(ev, bk, a.E, a.bscale, b_hi) : a.E;
+    const double h = s.h(i);
+    sc += a.ktheta - h * kCoalRate;
+    sc += (double)(n_hi - n_lo) * gh_log_unit(h, tab) - (b_hi - b_lo) * h;
+    n_lo = n_hi;
+    b_lo = b_hi;
+  }
+  return sc;
 }
 
 // generate(model, (T,), observations): k, change points and rates from the
@@ -141,21 +177,71 @@ __device__ int coal_init(const CoalArgs& a, uint64_t c, const CoalLds& s, const 
   }
   for (int i = k + 1; i <= kCoalKMax; ++i) s.cp(i) = 0.0;
   for (int i = k + 2; i <= kCoalKMax + 1; ++i) s.h(i) = 0.0;
-  // the score (the decomposition of the header), segment by segment
-  double sc = (double)k * a.kb - 3.0;
-  int n_lo = 0;
-  double b_lo = 0.0;
-  for (int i = 1; i <= k + 1; ++i) {
-    const double b_hi = i <= k ? s.cp(i) : a.T;
-    const int n_hi = i <= k ? coal_count(ev, bk, a.E, a.bscale, b_hi) : a.E;
-    const double h = s.h(i);
-    sc += a.ktheta - h * kCoalRate;
-    sc += (double)(n_hi - n_lo) * gh_log_unit(h, tab) - (b_hi - b_lo) * h;
-    n_lo = n_hi;
-    b_lo = b_hi;
-  }
-  *score = sc;
+  *score = coal_full_score(a, k, s, ev, bk, tab);
   return k;
+}
+
+// mh(trace, select(K)) (coal.jl:338-345 simple_mcmc_step; the Dynamic DSL's
+// regenerate, src/dynamic/regenerate.jl): k' ~ poisson(3); change points
+// 1..min(k, k') and rates 1..min(k, k')+1 keep their values, the others are
+// drawn from their distributions under the new k' (min_uniform_continuous,
+// gamma) or discarded; the weight is, over the kept unselected choices, new
+// score - old score (change point i: its min_uniform_continuous(cp_{i-1}, T,
+// k - i + 1) density under k' and under k; the rates' gamma arguments do not
+// change) plus the events' new logpdf - old.  Draws of iteration `step`:
+// block 6 (k', acceptance), 8 + i (new change point i), 48 + i (new rate i).
+// Returns whether the move was accepted (the LDS row and k, score updated).
+__device__ bool coal_regen_k(const CoalArgs& a, uint64_t c, uint32_t step, const CoalLds& s, const double* ev,
+                             const int32_t* bk, const double* tab, int* k_io, double* score_io) {
+  const int k = *k_io;
+  const CoalU B6 = coal_block(a.seed, c, step, 6);
+  const double u = u53(B6.x, B6.y);
+  double p = gh_exp(-3.0), cum = p;
+  int kk = 0;
+  while (u >= cum && kk < 200) {
+    ++kk;
+    p = p * (3.0 / (double)kk);
+    cum += p;
+  }
+  if (kk > kCoalKMax) return false;  // beyond the engine's capacity: refused (P < 1e-21)
+  const double T = a.T;
+  const int m = k < kk ? k : kk;
+  const double dk = (double)(kk - k);
+  double w = 0.0, lower = 0.0;
+  for (int i = 1; i <= m; ++i) {  // kept change points, re-scored under k'
+    const double x = s.cp(i);
+    w += dk * (gh_log_unit(T - x, tab) - gh_log_unit(T - lower, tab)) +
+         (gh_log_unit((double)(kk - i + 1), tab) - gh_log_unit((double)(k - i + 1), tab));
+    lower = x;
+  }
+  const double old_ev = coal_events_lp(a, k, s, ev, bk, tab);
+  // the new choices, written into the free LDS fields (zeroed again on rejection)
+  bool ok = true;
+  for (int i = k + 1; i <= kk; ++i) {
+    const double q = coal_u(a.seed, c, step, 8u + (uint32_t)i);
+    const double mm = (double)(kk - i + 1);
+    const double x = T - (T - lower) * gh_exp(gh_log(1.0 - q) / mm);
+    if (!(x > lower && x < T)) ok = false;
+    s.cp(i) = x;
+    lower = x;
+  }
+  for (int i = k + 2; i <= kk + 1; ++i) {
+    const double q = coal_u(a.seed, c, step, 48u + (uint32_t)i);
+    const double x = -gh_log(1.0 - q) / kCoalRate;
+    if (!(x > 0.0)) ok = false;
+    s.h(i) = x;
+  }
+  double alpha = -INFINITY;
+  if (ok) alpha = w + (coal_events_lp(a, kk, s, ev, bk, tab) - old_ev);
+  const bool acc = gh_log_unit(one_minus_u53(B6.z, B6.w), tab) < alpha;
+  const int keep = acc ? kk : k;
+  for (int i = keep + 1; i <= kCoalKMax; ++i) s.cp(i) = 0.0;
+  for (int i = keep + 2; i <= kCoalKMax + 1; ++i) s.h(i) = 0.0;
+  if (acc) {
+    *k_io = kk;
+    *score_io = coal_full_score(a, kk, s, ev, bk, tab);
+  }
+  return acc;
 }
 
 __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
@@ -232,8 +318,10 @@ __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
         acc[1] += 1;
       }
     }
-    // ---- birth / death move (coal.jl:173-318)
-    {
+    // ---- simple_mcmc_step: regenerate k (coal.jl:338-345)
+    if (a.simple) {
+      if (coal_regen_k(a, c, step, s, ev, bk, tab, &k, &score)) acc[2] += 1;
+    } else {  // ---- birth / death move (coal.jl:173-318)
       const CoalU B3 = coal_block(a.seed, c, step, 3);
       const CoalU B4 = coal_block(a.seed, c, step, 4);
       const bool birth = k == 0 || u53(B3.x, B3.y) < 0.5;

@@ -103,7 +103,7 @@ struct LGModel {
   static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 10 ? (S == 3 ? GH_LG10_WAVES : 5) : 4);
 #else
   static constexpr int kMinWaves =
-      (D <= 3) ? 8 : (D <= 5 ? 7 : (D < 10 ? (S == 3 && D != 7 ? 6 : 5) : (D == 10 ? (S == 3 ? 7 : 5) : 4)));
+      (D <= 3) ? 8 : (D <= 5 ? 7 : (D < 10 ? (S == 3 && D != 7 && D != 9 ? 6 : 5) : (D == 10 ? (S == 3 ? 7 : 5) : 4)));
 #endif
   using Params = LGParams;
 
@@ -252,7 +252,7 @@ struct LGModel {
 template <int D>
 struct LGOptModel {
   static constexpr int kD = D;
-  static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 8 ? 5 : 4);
+  static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 8 ? 5 : (D <= 14 ? 4 : 3));
   using Params = LGParams;
   using Prior = LGModel<D, 0>;
 

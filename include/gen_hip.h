@@ -75,7 +75,7 @@ typedef enum {
 typedef enum {
   /* x_1 ~ mvnormal(mu0, P0); x_t ~ mvnormal(A x_{t-1} + b, Q); y_t ~ mvnormal(H x_t + c, R)
      params (row-major doubles): A[d*d] b[d] Q[d*d] H[dy*d] c[dy] R[dy*dy] mu0[d] P0[d*d]
-     supported d: 1..8, 10, 12, 16; dy <= 32.  Multi-rank filters use systematic resampling. */
+     supported d: 1..16; dy <= 32.  Multi-rank filters use systematic resampling. */
   GH_FAMILY_LGSSM = 1,
   /* categorical HMM (test/inference/particle_filter.jl:50-78):
      z_1 ~ categorical(prior); z_t ~ categorical(T[:, z_{t-1}]); x_t ~ categorical(E[:, z_t])
@@ -360,6 +360,12 @@ typedef struct gh_coal gh_coal;
 int gh_coal_create(gh_ctx* ctx, int64_t chain0, int64_t n_chains, const double* events, int E, uint64_t seed,
                    gh_coal** out);
 int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* khist, double* kernel_ms);
+/* the MCMC kernel of the following gh_coal_step calls: 0 = mcmc_step (rate,
+   position, birth/death; coal.jl:329-336, the default), 1 = simple_mcmc_step
+   (rate, position, then mh(trace, select(:k)) — the Dynamic DSL regenerate of
+   k with the change points and rates it adds or drops; coal.jl:338-345);
+   accepts[2] counts the third move's acceptances either way */
+int gh_coal_set_kernel(gh_coal* h, int kernel);
 int gh_coal_read_state(gh_coal* h, double* state);
 int gh_coal_destroy(gh_coal* h);
 

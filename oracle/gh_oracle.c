@@ -1743,6 +1743,78 @@ static double coal_propose(const coal_m* M, const double* s, int move, const dou
   return ((delta + bwd) - fwd) + logj;
 }
 
+/* sum_i [c_i log h_i - len_i h_i]: the piecewise Poisson process of the row */
+static double coal_events_lp(const coal_m* M, const double* row) {
+  int k = (int)row[0];
+  const double* cp = row + 2;
+  const double* h = row + 2 + COAL_KMAX;
+  double lp = 0.0, b_lo = 0.0;
+  int n_lo = 0;
+  for (int i = 1; i <= k + 1; ++i) {
+    double b_hi = i <= k ? cp[i - 1] : M->T;
+    int n_hi = i <= k ? coal_count(M->ev, M->E, b_hi) : M->E;
+    lp += (double)(n_hi - n_lo) * orc_log_unit(h[i - 1]) - (b_hi - b_lo) * h[i - 1];
+    n_lo = n_hi;
+    b_lo = b_hi;
+  }
+  return lp;
+}
+
+/* mh(trace, select(K)) (coal.jl:338-345; src/dynamic/regenerate.jl): k' by
+   inverse CDF from u[0]; the kept change points 1..min(k, k') and rates keep
+   their values, change point i > k is drawn by min_uniform_continuous's
+   inverse CDF from u[i] (i = 1..32), rate i > k + 1 as gamma(1, 1/200) from
+   u[32 + i] (i = 1..33); weight = sum over the kept change points of their
+   density under k' minus under k, plus the events' new minus old logpdf.
+   Writes the proposed row (score from scratch) and returns the weight
+   (-inf: refused or invalid). */
+static double coal_regen_k(const coal_m* M, const double* s, const double* u, double* out) {
+  const double T = M->T;
+  int k = (int)s[0];
+  memcpy(out, s, sizeof(double) * COAL_W);
+  double p = orc_exp(-3.0), cum = p;
+  int kk = 0;
+  while (u[0] >= cum && kk < 200) { ++kk; p = p * (3.0 / (double)kk); cum += p; }
+  if (kk > COAL_KMAX) return -INFINITY;
+  const double* cp = s + 2;
+  double* ocp = out + 2;
+  double* oh = out + 2 + COAL_KMAX;
+  int m = k < kk ? k : kk;
+  double dk = (double)(kk - k), w = 0.0, lower = 0.0;
+  for (int i = 1; i <= m; ++i) {
+    double x = cp[i - 1];
+    w += dk * (orc_log_unit(T - x) - orc_log_unit(T - lower)) +
+         (orc_log_unit((double)(kk - i + 1)) - orc_log_unit((double)(k - i + 1)));
+    lower = x;
+  }
+  double old_ev = coal_events_lp(M, s);
+  int ok = 1;
+  for (int i = k + 1; i <= kk; ++i) {
+    double mm = (double)(kk - i + 1);
+    double x = T - (T - lower) * orc_exp(orc_log(1.0 - u[i]) / mm);
+    if (!(x > lower && x < T)) ok = 0;
+    ocp[i - 1] = x;
+    lower = x;
+  }
+  for (int i = k + 2; i <= kk + 1; ++i) {
+    double x = -orc_log(1.0 - u[32 + i]) / COAL_RATE;
+    if (!(x > 0.0)) ok = 0;
+    oh[i - 1] = x;
+  }
+  for (int i = kk + 1; i <= COAL_KMAX; ++i) ocp[i - 1] = 0.0;
+  for (int i = kk + 2; i <= COAL_KMAX + 1; ++i) oh[i - 1] = 0.0;
+  out[0] = (double)kk;
+  if (!ok) return -INFINITY;
+  double alpha = w + (coal_events_lp(M, out) - old_ev);
+  out[1] = coal_score(M, out);
+  return alpha;
+}
+
+double orc_coal_regen_k(const double* row, const double* ev, int E, const double* u, double* out) {
+  coal_m M = coal_model(ev, E);
+  return coal_regen_k(&M, row, u, out);
+}
+
 double orc_coal_score(const double* row, const double* ev, int E) {
   coal_m M = coal_model(ev, E);
   return coal_score(&M, row);
@@ -1754,7 +1826,7 @@ double orc_coal_propose(const double* row, const double* ev, int E, int move, co
 }
 
 int orc_coal_run(int64_t chain0, int64_t n_chains, const double* ev, int E, int n_iters, int iter0,
-                 uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist) {
+                 uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist, int simple) {
   if (E < 1) return 1;
   coal_m M = coal_model(ev, E);
 #pragma omp parallel for schedule(dynamic, 4)
@@ -1783,6 +1855,19 @@ int orc_coal_run(int64_t chain0, int64_t n_chains, const double* ev, int E, int 
         u[1] = unif53(B[2][0], B[2][1]);
         alpha = coal_propose(&M, cur, COAL_POSITION, u, 0.0, prop);
         if (orc_log_unit(one_minus53(B[2][2], B[2][3])) < alpha) { memcpy(cur, prop, sizeof prop); acc[1]++; }
+      }
+      if (simple) { /* regenerate k (simple_mcmc_step) */
+        double ur[66];
+        uint32_t w6[4];
+        rng(seed, c, step, S_MH, 6u, w6);
+        ur[0] = unif53(w6[0], w6[1]);
+        int k0 = (int)cur[0];
+        for (int i = 1; i <= 32; ++i) ur[i] = i > k0 ? coal_u(seed, c, step, 8u + (uint32_t)i) : 0.0;
+        for (int i = 1; i <= 33; ++i) ur[32 + i] = i > k0 + 1 ? coal_u(seed, c, step, 48u + (uint32_t)i) : 0.0;
+        alpha = coal_regen_k(&M, cur, ur, prop);
+        if (orc_log_unit(one_minus53(w6[2], w6[3])) < alpha) { memcpy(cur, prop, sizeof prop); acc[2]++; }
+        if (khist) khist[cl * n_iters + it] = (int32_t)cur[0];
+        continue;
       }
       /* birth / death move */
       int k = (int)cur[0];

@@ -126,7 +126,8 @@ int orc_pmmh_run(int64_t chain0, int64_t n_chains, int n_inner, const double* ys
    examples/coal/coal.jl:47-62, :103-336): chains [chain0, chain0 + n_chains);
    state rows of 68 doubles (k, score, cp[32], h[33], pad; unused fields 0) */
 int orc_coal_run(int64_t chain0, int64_t n_chains, const double* events, int E, int n_iters, int iter0,
-                 uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist);
+                 uint64_t seed, int init, double* state, int32_t* accepts, int32_t* khist, int simple);
+double orc_coal_regen_k(const double* row, const double* ev, int E, const double* u, double* out);
 /* the score of a row from scratch, and one move's proposal (move 0 rate, 1
    position, 2 birth, 3 death) from explicit uniforms u[3]: returns the MH
    log acceptance ratio, writes the proposed row (tests/test_coal_pins.py) */

@@ -102,7 +102,8 @@ def _load(path):
             "orc_importance_sampling": (I, [I, I, I, I, I, D, I64, D, I, I, I64, U64, D, D, D]),
             "orc_normal_logpdf": (c_double, [c_double, c_double, c_double]),
             "orc_pmmh_run": (I, [I64, I64, I, D, I, I, I, U64, I, D, D, D, POINTER(ctypes.c_int32), D]),
-            "orc_coal_run": (I, [I64, I64, D, I, I, I, U64, I, D, POINTER(ctypes.c_int32), POINTER(ctypes.c_int32)]),
+            "orc_coal_run": (I, [I64, I64, D, I, I, I, U64, I, D, POINTER(ctypes.c_int32), POINTER(ctypes.c_int32), I]),
+            "orc_coal_regen_k": (c_double, [D, D, I, D, D]),
             "orc_coal_score": (c_double, [D, D, I]),
             "orc_coal_propose": (c_double, [D, D, I, I, D, D]),
             "orc_pmmh_loglik": (c_double, [U64, U64, U32, c_double, c_double, I, D, I]),
@@ -415,18 +416,30 @@ def pmmh_run(ys, n_chains, n_inner, n_iters, seed, chain0=0, iter0=0, state=None
 COAL_W = 68
 
 
-def coal_run(events, n_chains, n_iters, seed, chain0=0, iter0=0, state=None, khist=False):
-    """CPU RJMCMC on the coal model (orc_coal_run): (state[n,68], accepts[n,3], khist)."""
+def coal_run(events, n_chains, n_iters, seed, chain0=0, iter0=0, state=None, khist=False, simple=False):
+    """CPU RJMCMC on the coal model (orc_coal_run): (state[n,68], accepts[n,3], khist).
+    simple: simple_mcmc_step (regenerate k as the third move)."""
     ev = np.ascontiguousarray(np.asarray(events, dtype=np.float64))
     st = np.zeros((n_chains, COAL_W)) if state is None else np.array(state, dtype=np.float64)
     acc = np.zeros((n_chains, 3), dtype=np.int32)
     kh = np.zeros((n_chains, max(n_iters, 1)), dtype=np.int32) if khist else None
     rc = lib().orc_coal_run(chain0, n_chains, _d(ev), ev.size, n_iters, iter0, seed, 1 if state is None else 0,
                             _d(st), acc.ctypes.data_as(POINTER(ctypes.c_int32)),
-                            None if kh is None else kh.ctypes.data_as(POINTER(ctypes.c_int32)))
+                            None if kh is None else kh.ctypes.data_as(POINTER(ctypes.c_int32)), int(simple))
     if rc:
         raise ValueError("oracle coal failed")
     return st, acc, kh
+
+
+def coal_regen_k(row, events, u):
+    """mh(trace, select(:k)) on one row with explicit uniforms u[66] (u[0]: k',
+    u[i]: change point i, u[32 + i]: rate i): (weight, proposed row)."""
+    ev = np.ascontiguousarray(np.asarray(events, dtype=np.float64))
+    r = np.ascontiguousarray(row, dtype=np.float64)
+    uu = np.ascontiguousarray(u, dtype=np.float64)
+    out = np.zeros(COAL_W)
+    a = lib().orc_coal_regen_k(_d(r), _d(ev), ev.size, _d(uu), _d(out))
+    return a, out
 
 
 def coal_score(row, events):

@@ -58,6 +58,35 @@ def test_oracle_coal_posterior_over_k():
     assert np.all((rates > 0.05) & (rates < 0.8)), rates
 
 
+def test_oracle_simple_mcmc_posterior_over_k():
+    """simple_mcmc_step (rate, position, mh(trace, select(:k))) targets the same
+    posterior as mcmc_step: the regenerate of k leaves it invariant."""
+    st, acc, kh = O.coal_run(EVENTS, 32, 4000, seed=2, khist=True, simple=True)
+    _valid(st)
+    post = np.bincount(kh[:, 1500:].ravel(), minlength=33) / kh[:, 1500:].size
+    assert post[0] < 0.01
+    assert post[1:8].sum() > 0.97
+    assert 2 <= int(np.argmax(post)) <= 3
+    st2, _, kh2 = O.coal_run(EVENTS, 32, 4000, seed=2, khist=True)
+    post2 = np.bincount(kh2[:, 1500:].ravel(), minlength=33) / kh2[:, 1500:].size
+    assert np.abs(post[:8] - post2[:8]).max() < 0.08, (post[:8], post2[:8])
+    assert 0.001 < acc[:, 2].sum() / (32 * 4000) < 0.5
+    for row in st:  # the cached scores are the scores of the states
+        assert row[1] == pytest.approx(O.coal_score(row, EVENTS), rel=1e-11, abs=1e-8)
+
+
+@pytest.mark.gpu
+def test_gpu_coal_simple_matches_oracle(gh_ctx):
+    from gen_amd.coal import CoalChains
+
+    ref = O.coal_run(EVENTS, 300, 40, seed=5, chain0=3, khist=True, simple=True)
+    ch = CoalChains(EVENTS, 300, seed=5, chain0=3, ctx=gh_ctx, kernel="simple_mcmc_step")
+    kh = ch.run(40, k_history=True)
+    assert np.array_equal(ch.state, ref[0])
+    assert np.array_equal(ch.accepts, ref[1])
+    assert np.array_equal(kh, ref[2])
+
+
 @pytest.mark.gpu
 def test_gpu_coal_matches_oracle(gh_ctx):
     from gen_amd.coal import CoalChains

@@ -216,6 +216,51 @@ def test_move_alpha_equals_involutive_mh_weight(move):
     assert n >= 60
 
 
+def ref_regen_k(k, cp, h, u):
+    """regenerate(trace, select(:k)) of the Dynamic DSL (src/dynamic/regenerate.jl:
+    kept unselected choices add new score - old score; new choices are drawn
+    from their distributions; discarded choices drop out) on the coal model,
+    with k' from poisson(3)'s inverse CDF."""
+    kk, cum = 0, stats.poisson.pmf(0, 3.0)
+    while u[0] >= cum:
+        kk += 1
+        cum += stats.poisson.pmf(kk, 3.0)
+    w, lower = 0.0, 0.0
+    for i in range(1, min(k, kk) + 1):  # kept change points: min_uniform(lower, T, k - i + 1) -> (.., kk - i + 1)
+        w += min_uniform_logpdf(cp[i - 1], lower, T, kk - i + 1) - min_uniform_logpdf(cp[i - 1], lower, T, k - i + 1)
+        lower = cp[i - 1]
+    cp2, h2 = list(cp[: min(k, kk)]), list(h[: min(k, kk) + 1])
+    for i in range(k + 1, kk + 1):  # new change points by min_uniform's inverse CDF (coal.jl:28-32)
+        x = T - (T - lower) * (1.0 - u[i]) ** (1.0 / (kk - i + 1))
+        cp2.append(x)
+        lower = x
+    for i in range(k + 2, kk + 2):  # new rates: gamma(1, 1/200) by inversion
+        h2.append(-math.log(1.0 - u[32 + i]) / 200.0)
+    w += piecewise_poisson_logpdf(EV, [0.0] + cp2 + [T], h2) - piecewise_poisson_logpdf(EV, [0.0] + list(cp[:k]) + [T],
+                                                                                        list(h[: k + 1]))
+    return w, kk, cp2, h2
+
+
+def test_regen_k_weight_equals_dynamic_regenerate():
+    rng = np.random.default_rng(7)
+    n = 0
+    for r in STATES:
+        k = int(r[0])
+        for _ in range(3):
+            u = rng.uniform(0.001, 0.999, 66)
+            u[0] = rng.uniform(0.0, 0.97)  # k' <= 7 mostly, all sizes over the loop
+            a, out = O.coal_regen_k(r, EV, u)
+            want, kk, cp2, h2 = ref_regen_k(k, list(r[2 : 2 + k]), list(r[34 : 34 + k + 1]), u)
+            assert int(out[0]) == kk
+            np.testing.assert_allclose(out[2 : 2 + kk], cp2, rtol=1e-13)
+            np.testing.assert_allclose(out[34 : 34 + kk + 1], h2, rtol=1e-13)
+            assert not out[2 + kk : 34].any() and not out[34 + kk + 1 : 67].any()
+            assert a == pytest.approx(want, rel=1e-10, abs=1e-8), (k, kk)
+            assert out[1] == pytest.approx(ref_score(kk, cp2, h2), rel=1e-11, abs=1e-8)
+            n += 1
+    assert n >= 200
+
+
 def test_birth_is_refused_at_capacity_and_outside_support():
     full = row(KMAX, np.sort(np.random.default_rng(5).uniform(0, T, KMAX)), np.full(KMAX + 1, 0.002))
     a, _ = O.coal_propose(full, EV, "birth", [0.5, 0.5, 0.5])

@@ -117,7 +117,7 @@ def assert_lml_close(st, orc, rel=1e-9):
 
 
 # ------------------------------------------------------------------ LGSSM
-@pytest.mark.parametrize("d", [1, 2, 4, 10])
+@pytest.mark.parametrize("d", [1, 2, 4, 9, 10, 13, 16])
 @pytest.mark.parametrize("thr", [None, "always"])
 def test_lgssm_parity(gh_ctx, d, thr):
     m = gen.LinearGaussianSSM.benchmark(d)

@@ -28,7 +28,7 @@ lib = _lib.load()
 buf = (ctypes.c_uint64 * (1024 * 8))()
 lib.gh_debug_rs_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 _lib.check(lib.gh_debug_rs_stamps(buf, 1024 * 8))
-grid = -(-n // (1024 * (4 if n <= 1 << 20 else 8)))
+grid = -(-n // (1024 * 4))  # IT = 4 (two blocks per CU at 2^21)
 print(f"{name} n={n} grid={grid}")
 a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[:grid, :8].astype(np.int64)
 t0 = a[:, 0].min()
