@@ -21,7 +21,6 @@
 
 #include "../../include/gen_hip.h"
 #include "gh_kernels.h"
-#include "gh_fused.h"
 #include "gh_pmmh.h"
 #include "gh_coal.h"
 #include "gh_scores.h"
@@ -661,8 +660,6 @@ struct gh_pf {
   bool step_max_only = false;     // gh_pf_run: the next step may write block maxima only
   int rs_grid = 0;                // k_resample1 / k_rank_* tiles (blocks); 0: not usable
   int rs_it = 0;                  // particles per thread of those kernels (4, 8 or 16)
-  unsigned* fz_cnt = nullptr;     // gh_fused.h: done-counter shards, then the decision word
-  unsigned fz_gen = 0;            // fused launches so far (the counters reach fz_gen * tiles)
   uint64_t* bsum = nullptr;
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
@@ -835,7 +832,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->tsum); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
-  hipFree(pf->acc_count); hipFree(pf->pin); hipFree(pf->fz_cnt);
+  hipFree(pf->acc_count); hipFree(pf->pin);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
   if (pf->ev_plan) hipEventDestroy(pf->ev_plan);
@@ -1188,10 +1185,8 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   auto fail = [&](int rc) { pf_free(pf); return rc; };
 #define ALLOC(ptr, bytes) \
   if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return fail(set_err(GH_E_NOMEM, "hipMalloc %s", #ptr));
-  // padded to whole 4096-particle tiles: the fused resample loads its tile
-  // with 16-byte loads and masks the slots past n
-  ALLOC(pf->logw, sizeof(double) * (((n + kRsTile - 1) / kRsTile) * kRsTile));
-  ALLOC(pf->C, sizeof(uint64_t) * (((n + kRsTile - 1) / kRsTile) * kRsTile));  // also the fused resample's scratch
+  ALLOC(pf->logw, sizeof(double) * n);
+  ALLOC(pf->C, sizeof(uint64_t) * n);
   ALLOC(pf->mark, sizeof(uint64_t) * n);
   ALLOC(pf->cmark, sizeof(uint64_t) * ((n + 63) / 64));
   ALLOC(pf->bsum, sizeof(uint64_t) * pf->nb_scan);
@@ -1206,7 +1201,6 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->n_tiles = (n + kRsTile - 1) / kRsTile;
   ALLOC(pf->tsum, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles));
   pick_resample_tiles(pf, n);
-  if (ctx->world == 1) ALLOC(pf->fz_cnt, sizeof(unsigned) * (kFzShards * kFzShardStride + 32));
   if (ctx->world > 1) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
@@ -1239,9 +1233,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
       return fail(set_err(GH_E_HIP, "init scalars"));
     if (hipMemsetAsync(pf->mark, 0, sizeof(uint64_t) * n, pf->s) != hipSuccess ||
         hipMemsetAsync(pf->tsum, 0, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles), pf->s) != hipSuccess ||
-        hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * ((n + 63) / 64), pf->s) != hipSuccess ||
-        (pf->fz_cnt &&
-         hipMemsetAsync(pf->fz_cnt, 0, sizeof(unsigned) * (kFzShards * kFzShardStride + 32), pf->s) != hipSuccess))
+        hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * ((n + 63) / 64), pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init marks"));
     if (hipStreamSynchronize(pf->s) != hipSuccess) return fail(set_err(GH_E_HIP, "sync"));
   }
@@ -1765,137 +1757,6 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
   return GH_OK;
 }
 
-// ---- gh_pf_run's one-launch maybe_resample! + particle_filter_step!
-// (gh_fused.h): one rank, systematic, default proposal, the tile geometry of
-// k_resample1<., 4, .>, and a family with a fused kernel.
-template <class Model>
-struct has_fused : std::false_type {};
-template <int D>
-struct has_fused<LGModel<D, 3>> : std::true_type {};
-template <>
-struct has_fused<KitModel> : std::true_type {};
-
-static bool fused_ok(const gh_pf* pf, int proposal) {
-  if (pf->opts.two_launch || pf->ctx->world != 1 || pf->cond || pf->n <= 0 || !pf->fz_cnt) return false;
-  if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC || proposal != GH_PROPOSAL_DEFAULT) return false;
-  if (pf->rs_grid <= 0 || pf->rs_it != 4 || pf->rs_grid != pf->n_tiles || pf->n_tiles > kFzMaxTiles) return false;
-  if (pf->resample_calls != 0 || pf->t < 1 || pf->marks_pending) return false;
-  if (slot_doubles(pf->n, pf->D) * 8 >= (1LL << 32)) return false;  // buffer-descriptor addressing
-  if (pf->m->family == GH_FAMILY_KITAGAWA) return use_pairs<KitModel>(pf);
-  return pf->m->family == GH_FAMILY_LGSSM && pf->m->lg_struct == 3;
-}
-
-static int fused_step(gh_pf* pf, const gh_obs* obs, int proposal, double thr, bool max_only) {
-  if (thr != thr) thr = (double)pf->n_global / 2.0;  // as gh_pf_maybe_resample
-  if (thr < 0.0)
-    return set_err(GH_E_INVAL, "ess_threshold %g < 0: pass NaN for the default N/2, 0 to never resample", thr);
-  const int t0 = pf->t, t = t0 + 1;
-  CHECK(grow_for_step(pf, t));
-  StepObs o;
-  CHECK(make_obs(pf->m, t, obs, &o));
-  const int64_t n = pf->n;
-  // the resample role: k_resample1's arguments (resample_enqueue)
-  FusedArgs f{};
-  Resample1Args& ra = f.r;
-  ra.d.stats_all = pf->stats_all;
-  ra.d.R = 1;
-  ra.d.n_global = pf->n_global;
-  ra.d.log_n = gh_log((double)pf->n_global);
-  ra.d.inv_n = 1.0 / (double)pf->n_global;
-  ra.d.thr = thr;
-  ra.d.ess_hist = pf->ess_hist;
-  ra.d.res_hist = pf->res_hist;
-  ra.d.t = t0;
-  ra.pm = pf->pm;
-  ra.ps = pf->ps;
-  ra.ps2 = pf->ps2;
-  ra.nb_part = (int)pf->nb_part;  // the previous step's partials
-  ra.logw = pf->logw;
-  ra.n = n;
-  ra.shift = quant_shift((uint64_t)pf->n_global);
-  ra.stats_out = pf->stats_all;
-  ra.dev = pf->dev;
-  ra.tsum = pf->tsum;
-  ra.ts1 = pf->tsum + pf->n_tiles;
-  ra.ts2 = pf->tsum + 2 * pf->n_tiles;
-  ra.sums_in_pass = pf->max_only ? 1 : 0;
-  ra.mk.mark = pf->mark;
-  ra.mk.cmark = pf->cmark;
-  ra.mk.epoch = ++pf->epoch;
-  ra.mk.n_global = pf->n_global;
-  ra.mk.n_groups = (n + 63) / 64;
-  ra.mk.enabled = 1;
-  ra.C = pf->C;
-  ra.seed = pf->seed;
-  ra.t = (uint32_t)t0;
-  f.cnt = pf->fz_cnt;
-  f.fire = pf->fz_cnt + kFzShards * kFzShardStride;
-  f.gen = ++pf->fz_gen;
-  f.G = (int)pf->n_tiles;
-  // the step role: pf_step_impl's arguments after a systematic resample
-  StepArgs a{};
-  a.xprev = slot_x(pf, t - 1);
-  a.anc = anc_for_step(pf, t);
-  a.mark = pf->mark;
-  a.carry = pf->cmark;
-  a.mark_mode = 1;
-  a.resampled = 1;
-  a.xout = slot_x(pf, t);
-  a.logw = pf->logw;
-  a.n = n;
-  a.nvb = (n + kBlock - 1) / kBlock;
-  a.lo = pf->lo;
-  a.seed = pf->seed;
-  a.t = (uint32_t)t;
-  a.proposal = proposal;
-  a.dev = pf->dev;
-  a.pm = pf->pm;
-  a.ps = pf->ps;
-  a.ps2 = pf->ps2;
-  a.stats_out = pf->stats_all;
-  a.buf = 1;
-  a.max_only = max_only ? 1 : 0;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  const int every = pf->opts.time_kernels;
-  if (every > 0 && (a.t - 1) % (uint32_t)every == 0) {
-    if (pf->ev_used + 2 > pf->ev.size()) {
-      for (int i = 0; i < 64; ++i) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, kTimingEventFlags));
-        pf->ev.push_back(e);
-      }
-    }
-    e0 = pf->ev[pf->ev_used];
-    e1 = pf->ev[pf->ev_used + 1];
-    pf->ev_used += 2;
-  }
-  bool launched = false;
-  CHECK(with_model(pf->m, [&](auto model, const auto& p) {
-    using Model = decltype(model);
-    if constexpr (has_fused<Model>::value) {
-      constexpr bool kPairs = has_pairs<Model>::value;
-      const int64_t nb = kPairs ? (n + 2 * kBlock - 1) / (2 * kBlock) : pf->nb_step;
-      pf->nb_part = nb;
-      const dim3 grid((unsigned)(f.G + nb)), block(kBlock);
-      hipExtLaunchKernelGGL((k_fused<Model, kPairs>), grid, block, 0, pf->s, e0, e1, 0,
-                            (const double*)pf->m->dparams, p, o, a, f);
-      launched = true;
-    }
-  }));
-  if (!launched) return set_err(GH_E_STATE, "internal: no fused kernel for this model");
-  HIP_TRY(hipGetLastError());
-  pf->stats_valid = false;
-  pf->marks_pending = false;
-  pf->resample_calls = 0;
-  pf->t = t;
-  pf->max_only = max_only;
-  pf->last_obs = o;
-  if ((int)pf->obs_hist.size() < t) pf->obs_hist.resize(t);
-  pf->obs_hist[t - 1] = o;
-  pf->rejuv_moves = 0;
-  return GH_OK;
-}
-
 extern "C" int gh_pf_run(gh_pf* pf, int n_steps, const gh_obs* obs, int proposal, double thr) {
   if (!pf || n_steps < 0) return set_err(GH_E_INVAL, "gh_pf_run: bad argument");
   // A step followed by this loop's own maybe_resample! leaves the weight sums
@@ -1903,10 +1764,6 @@ extern "C" int gh_pf_run(gh_pf* pf, int n_steps, const gh_obs* obs, int proposal
   // fused path only); the last step writes full partials for other readers.
   const bool fused = pf->ctx->world == 1 && pf->rs_grid > 0 && !pf->cond && pf->n > 0;
   for (int i = 0; i < n_steps; ++i) {
-    if (fused_ok(pf, proposal)) {  // resample + step in one launch (gh_fused.h)
-      CHECK(fused_step(pf, obs ? &obs[i] : nullptr, proposal, thr, fused && i + 1 < n_steps));
-      continue;
-    }
     CHECK(gh_pf_maybe_resample(pf, thr, nullptr, nullptr));
     pf->step_max_only = fused && i + 1 < n_steps;
     const int rc = gh_pf_step(pf, obs ? &obs[i] : nullptr, proposal);

@@ -397,22 +397,20 @@ def _normal_lp(x, mu, sd) -> float:
 
 
 # --------------------------------------------------------------- the API
-def _opts(resampler: str, record_history: bool, history_capacity: int, time_kernels: int,
-          two_launch: bool = False) -> _lib.PFOpts:
+def _opts(resampler: str, record_history: bool, history_capacity: int, time_kernels: int) -> _lib.PFOpts:
     o = _lib.PFOpts()
     _lib.load().gh_pf_opts_default(byref(o))
     o.resampler = {"systematic": _lib.RESAMPLE_SYSTEMATIC, "multinomial": _lib.RESAMPLE_MULTINOMIAL}[resampler]
     o.record_history = int(record_history)
     o.history_capacity = int(history_capacity)
     o.time_kernels = int(time_kernels)
-    o.two_launch = int(two_launch)
     return o
 
 
 def initialize_particle_filter(model: Model, model_args: tuple, observations, *args, seed: int = 0,
                                resampler: str = "systematic", record_history: bool = True,
                                history_capacity: int = 0, time_kernels: int = 0,
-                               two_launch: bool = False, ctx: Context | None = None) -> ParticleFilterState:
+                               ctx: Context | None = None) -> ParticleFilterState:
     """initialize_particle_filter(model, model_args, observations, num_particles)
     initialize_particle_filter(model, model_args, observations, proposal, proposal_args, num_particles)
 
@@ -435,7 +433,7 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
     mh = ctx.model_handle(model)
     obs, keep = _step_obs(model, 1, observations)
     h = c_void_p()
-    opts = _opts(resampler, record_history, history_capacity, time_kernels, two_launch)
+    opts = _opts(resampler, record_history, history_capacity, time_kernels)
     qa, nq = _qargs(proposal, proposal_args)
     _lib.check(_lib.load().gh_pf_init_q(mh, byref(obs), _proposal_code(proposal),
                                         _lib.dptr(qa) if qa is not None else None, nq, int(num_particles),

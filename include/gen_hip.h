@@ -138,9 +138,7 @@ typedef struct {
   int32_t history_capacity; /* steps to preallocate when record_history (0 = grow) */
   int32_t block_size;     /* 0 = default (256) */
   int32_t time_kernels;   /* k > 0: time every k-th step kernel with hipEvents (gh_pf_kernel_time) */
-  int32_t two_launch;     /* gh_pf_run: 1 = resample and step as two launches; 0 (default) = one fused
-                             launch where available (one rank, systematic, default proposal); same results */
-  int32_t reserved[2];
+  int32_t reserved[3];
 } gh_pf_opts;
 
 /* ---- context ------------------------------------------------------------ */

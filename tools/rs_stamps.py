@@ -21,8 +21,7 @@ name = sys.argv[1] if len(sys.argv) > 1 else "lg10"
 n = 1 << (int(sys.argv[2]) if len(sys.argv) > 2 else 20)
 m = gen.LinearGaussianSSM.benchmark(10) if name == "lg10" else gen.KitagawaSSM(10.0, 1.0)
 _, ys = m.simulate(12, np.random.default_rng(2))
-st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=42, record_history=False,
-                                    two_launch=True)
+st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=42, record_history=False)
 gen.run_particle_filter(st, list(ys[1:10]))
 ctx.synchronize()
 lib = _lib.load()
