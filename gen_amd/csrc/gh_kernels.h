@@ -125,6 +125,11 @@ template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ double dpp_f64(double v, double old) {
   return as_f64(dpp_u64<CTRL, ROW_MASK>(as_u64(v), as_u64(old)));
 }
+__device__ __forceinline__ uint64_t readfirstlane_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint64_t readlane63_u64(uint64_t v) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);

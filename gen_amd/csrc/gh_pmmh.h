@@ -19,7 +19,10 @@
 // Randomness: move counter u = 0 for the initial generate,
 // u = 1 + 4k + m for move m of (global) iteration k; particle p of chain c uses id
 // (u << 32) | (c << 10) | p; the chain's own draws (prior / proposal,
-// acceptance, resampling offsets) use id (u << 32) | (c << 10).
+// acceptance, resampling offsets) use id (u << 32) | (c << 10).  The state
+// noise of steps t and t + 1 (t even) is the pair (z0, z1) of ONE Box–Muller
+// evaluation of the block at step t: half the Philox and Box–Muller work of a
+// filter (the kernel is VALU-bound), still a function of (seed, id, t) alone.
 #pragma once
 #include "gh_kernels.h"
 
@@ -118,6 +121,7 @@ __device__ double pmmh_filter(const PmmhArgs& a, PmmhShared& sh, uint64_t c, uin
   const uint64_t cid = ((uint64_t)u << 32) | (c << 10);
   const uint64_t pid = cid | (uint64_t)j;
   const double logN = gh_log((double)N);
+  const double invN = 1.0 / (double)N;
   const int shift = quant_shift((uint64_t)N);
   auto obs = [&](double y, double x) {
     const double diff = y - x * x / 20.0;
@@ -129,6 +133,7 @@ __device__ double pmmh_filter(const PmmhArgs& a, PmmhShared& sh, uint64_t c, uin
   double x = 0.0 + 5.0 * z0;
   double lw = obs(a.ys[0], x);
   double log_ml = 0.0;
+  double zk = 0.0;  // the second normal of the last even step's pair
   for (int t = 2; t <= a.T; ++t) {
     // maybe_resample! (particle_filter.jl:189-213), threshold N/2
     const double M = blkn_max(lw, sh.smd, nw);
@@ -145,11 +150,20 @@ __device__ double pmmh_filter(const PmmhArgs& a, PmmhShared& sh, uint64_t c, uin
       sh.C[j] = incl;
       sh.x[j] = x;
       lds_barrier();
-      const uint64_t Stot = sh.C[N - 1];
+      // the block constants on the scalar unit; per lane, floor((j Rs + o) / N)
+      // = o / N + floor((j Rs + o % N) / N) with j Rs + o % N < 2^21: a
+      // double estimate and one correction (the same integers as the
+      // reference division)
+      const uint64_t Stot = readfirstlane_u64(sh.C[N - 1]);
       const u32x4 w = rng_block(a.seed, cid, (uint32_t)(t - 1), STREAM_RESAMPLE, 0);
-      const uint64_t o = scale_u53(u53_bits(w.x, w.y), Stot);
-      const uint64_t Qs = Stot / (uint64_t)N, Rs = Stot % (uint64_t)N;
-      const uint64_t target = (uint64_t)j * Qs + ((uint64_t)j * Rs + o) / (uint64_t)N;
+      const uint64_t o = readfirstlane_u64(scale_u53(u53_bits(w.x, w.y), Stot));
+      const uint64_t Qs = Stot / (uint64_t)N, Rs = Stot - Qs * (uint64_t)N;
+      const uint64_t oq = o / (uint64_t)N, orr = o - oq * (uint64_t)N;
+      const uint32_t num = (uint32_t)((uint64_t)j * Rs + orr);
+      uint32_t qq = (uint32_t)((double)num * invN);
+      qq += (qq + 1u) * (uint32_t)N <= num ? 1u : 0u;
+      qq -= qq * (uint32_t)N > num ? 1u : 0u;
+      const uint64_t target = (uint64_t)j * Qs + oq + qq;
       int lo = 0, hi = N - 1;  // first i with C[i] > target
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -161,9 +175,14 @@ __device__ double pmmh_filter(const PmmhArgs& a, PmmhShared& sh, uint64_t c, uin
       lds_barrier();
     }
     // particle_filter_step!: x_t ~ normal(x_mean(x_{t-1}, t), sqrt(var_x))
-    normal_pair(rng_block(a.seed, pid, (uint32_t)t, STREAM_STEP, 0), &z0, &z1, sh.tab);
+    double z = zk;
+    if ((t & 1) == 0) {  // uniform: a new pair every second step
+      normal_pair(rng_block(a.seed, pid, (uint32_t)t, STREAM_STEP, 0), &z0, &z1, sh.tab);
+      z = z0;
+      zk = z1;
+    }
     const double mean = ((xp / 2.0) + 25.0 * (xp / (1.0 + xp * xp))) + a.ct[t - 1];
-    x = mean + sx * z0;
+    x = mean + sx * z;
     lw = base + obs(a.ys[t - 1], x);
   }
   // log_ml_estimate (particle_filter.jl:52-55)

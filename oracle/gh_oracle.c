@@ -1367,7 +1367,8 @@ int orc_importance_sampling(int family, int d, int dy, int k, int v, const doubl
    mh(tr, var_x_proposal) / var_y_proposal, normal(cur, sqrt(0.5)), weight =
    prior ratio + log-ML ratio, alpha = weight - fwd + bwd (mh.jl:41-62).
    Randomness: move counter u (0 = generate, 1 + 4 iter + m), particle id
-   (u << 32) | (chain << 10) | p.  tests/test_pmmh.py checks
+   (u << 32) | (chain << 10) | p; the state noise of steps t
+   and t + 1 (t even) is one Box-Muller pair drawn at step t.  tests/test_pmmh.py checks
    the inner estimate against the PF oracle (run_pf) on the same model. */
 static double pmmh_filter(uint64_t seed, uint64_t c, uint32_t u, double lvx, double lvy, int N,
                           const double* ys, const double* ct, int T, double* x, double* lw, double* xp,
@@ -1413,10 +1414,12 @@ static double pmmh_filter(uint64_t seed, uint64_t c, uint32_t u, double lvx, dou
       for (int p = 0; p < N; ++p) xp[p] = x[p];
     }
     for (int p = 0; p < N; ++p) {
-      orc_normals(seed, cid | (uint64_t)p, (uint32_t)t, S_STEP, 1, z);
+      /* steps t and t + 1 (t even) take z0 and z1 of one Box-Muller pair, the
+         block of step t (gh_pmmh.h) */
+      orc_normals(seed, cid | (uint64_t)p, (uint32_t)(t & ~1), S_STEP, 2, z);
       double v = xp[p];
       double mean = ((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + ct[t - 1];
-      x[p] = mean + sx * z[0];
+      x[p] = mean + sx * z[t & 1];
       double diff = ys[t - 1] - x[p] * x[p] / 20.0;
       lw[p] = (fire ? 0.0 : lw[p]) + (-(diff * diff) * inv2vy + csty);
     }
