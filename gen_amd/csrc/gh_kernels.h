@@ -1371,20 +1371,33 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     if (w < 8) {
       const unsigned b = (unsigned)(w * 64 + lane);
       const bool mine = b < gridDim.x;
+      // the totals alone while the grid publishes, then the tile sums
+      // (published with them) until their tags match too: a third of the
+      // polling traffic while lagging blocks still load their tiles (C4, 512
+      // tiles: barrier 2.2 us sooner, 39.7 -> 37.8 us per step; C2 -0.9 us)
       uint64_t v = par, v1 = par, v2 = par;
       bool ok = !mine;
       for (unsigned spins = 0;; ++spins) {  // bounded (~0.5 s): a grid that is not co-resident errors out
-        if (!ok) {
-          v = ld_sc1(&r.tsum[b]);
-          if (sums) {
-            v1 = ld_sc1(&r.ts1[b]);
-            v2 = ld_sc1(&r.ts2[b]);
-          }
-        }
-        ok = ok || ((v & kTag) == par && (v1 & kTag) == par && (v2 & kTag) == par);
+        if (!ok) v = ld_sc1(&r.tsum[b]);
+        ok = ok || (v & kTag) == par;
         if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
         if (spins == (1u << 22)) {
           r.dev->error = 7;  // GH_E_STATE
+          sfail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      ok = !mine || !sums;
+      for (unsigned spins = 0;; ++spins) {
+        if (!ok) {
+          v1 = ld_sc1(&r.ts1[b]);
+          v2 = ld_sc1(&r.ts2[b]);
+        }
+        ok = ok || ((v1 & kTag) == par && (v2 & kTag) == par);
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spins == (1u << 22)) {
+          r.dev->error = 7;
           sfail = 1;
           break;
         }
