@@ -660,6 +660,9 @@ struct gh_pf {
   bool step_max_only = false;     // gh_pf_run: the next step may write block maxima only
   int rs_grid = 0;                // k_resample1 / k_rank_* tiles (blocks); 0: not usable
   int rs_it = 0;                  // particles per thread of those kernels (4, 8 or 16)
+  uint64_t* amax = nullptr;       // [2][kAmaxShards * kAmaxStride] a max_only step's atomic-max shards (by t & 1)
+  bool amax_armed = false;        // k_resample1 emptied the shards of the next step
+  bool amax_valid = false;        // the last step wrote its shards
   uint64_t* bsum = nullptr;
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
@@ -832,7 +835,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->tsum); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
-  hipFree(pf->acc_count); hipFree(pf->pin);
+  hipFree(pf->acc_count); hipFree(pf->pin); hipFree(pf->amax);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
   if (pf->ev_plan) hipEventDestroy(pf->ev_plan);
@@ -1201,6 +1204,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->n_tiles = (n + kRsTile - 1) / kRsTile;
   ALLOC(pf->tsum, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles));
   pick_resample_tiles(pf, n);
+  if (ctx->world == 1) ALLOC(pf->amax, sizeof(uint64_t) * 2 * kAmaxShards * kAmaxStride);
   if (ctx->world > 1) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
@@ -1235,6 +1239,11 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
         hipMemsetAsync(pf->tsum, 0, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles), pf->s) != hipSuccess ||
         hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * ((n + 63) / 64), pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init marks"));
+    if (pf->amax) {
+      std::vector<uint64_t> e(2 * kAmaxShards * kAmaxStride, kAmaxEmpty);
+      if (hipMemcpyAsync(pf->amax, e.data(), sizeof(uint64_t) * e.size(), hipMemcpyHostToDevice, pf->s) != hipSuccess)
+        return fail(set_err(GH_E_HIP, "init shards"));
+    }
     if (hipStreamSynchronize(pf->s) != hipSuccess) return fail(set_err(GH_E_HIP, "sync"));
   }
   const int cap0 = pf->opts.history_capacity > 0 ? pf->opts.history_capacity : 16;
@@ -1343,6 +1352,11 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   a.max_only = pf->step_max_only && !pin_ref ? 1 : 0;
+  // (not for the pair-stepped kernel: its 4096 atomics cost C4's short step
+  // more than the fold they save, measured)
+  a.amax = a.max_only && pf->amax_armed && pf->nb_part == pf->nb_step
+               ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride
+               : nullptr;
   // multi-rank after a resample: the local half now, the rest once the rows arrive
   a.part = pf->plan_pending && a.mark_mode == 2 ? 1 : 0;
   if (pin_ref) {
@@ -1354,6 +1368,8 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   CHECK(share_stats(pf));
   pf->t = t;
   pf->max_only = a.max_only != 0;
+  pf->amax_valid = a.amax != nullptr;
+  pf->amax_armed = false;
   pf->resample_calls = 0;
   pf->marks_pending = false;
   pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
@@ -1612,6 +1628,11 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     ra.C = pf->C;
     ra.seed = pf->seed;
     ra.t = (uint32_t)t;
+    if (pf->amax) {  // the step's own max fold (when it wrote one); the next step's shards emptied
+      ra.amax_in = pf->max_only && pf->amax_valid ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride : nullptr;
+      ra.amax_reset = pf->amax + ((t + 1) & 1) * kAmaxShards * kAmaxStride;
+      pf->amax_armed = true;
+    }
     // grid <= co-resident capacity of an idle device (rs_cap), so every block
     // is eventually resident; the barrier wait is bounded as a backstop
     const dim3 grid((unsigned)pf->rs_grid), blk(kRsBlock);

@@ -96,6 +96,9 @@ struct StepArgs {
   double* ps;            //                 sum e
   double* ps2;           //                 sum e^2
   double* stats_out;     // where the rank's (M, S, S2) goes
+  uint64_t* amax;        // max_only steps of gh_pf_run: the block maximum also goes into
+                         // kAmaxShards order-keyed atomic-max words (k_resample1 folds
+                         // those instead of every block maximum); nullptr: not written
   // multi-rank split of a step after a resample: part 1 runs
   // every tile before the received rows exist (its results for slots [0, ra)
   // and [rb, n) are discarded), part 2 runs again the tiles holding such
@@ -284,14 +287,38 @@ __device__ __forceinline__ void block_partial(double lw, double (*sm)[4], double
   }
 }
 
+// The rank maximum of a max_only step, folded by the step kernel itself:
+// every block adds its maximum to one of kAmaxShards words (128 B apart) by an
+// agent-scope atomic max on an order-preserving key, so the resample reads 32
+// words instead of every block's maximum (MI355X_MICROARCH.md: one address
+// takes ~11-13 ns per atomic; 4096 blocks over 32 shards and a ~36 us launch
+// is far below that).  NaN maxima are keyed as -inf, as fmax ignores them.
+constexpr int kAmaxShards = 32;
+constexpr int kAmaxStride = 16;  // u64 words between shards
+constexpr uint64_t kAmaxEmpty = 0x000fffffffffffffull;  // the key of -inf
+__host__ __device__ __forceinline__ uint64_t amax_key(double x) {
+  const uint64_t b = x == x ? as_u64(x) : as_u64(-INFINITY);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__host__ __device__ __forceinline__ double amax_value(uint64_t k) {
+  return as_f64((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k);
+}
+
 // Block maximum only (the fused resample computes the weight sums in its own
 // pass over the log-weights, where it evaluates exp(w - M) anyway).
-__device__ __forceinline__ void block_max_partial(double lw, double (*sm)[4], double* pm) {
+__device__ __forceinline__ void block_max_partial(double lw, double (*sm)[4], double* pm, uint64_t* amax,
+                                                  int64_t vb) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const double mw = wave_max(lw);
   if (lane == 0) sm[0][w] = mw;
   lds_barrier();
-  if (threadIdx.x == 0) *pm = fmax(fmax(sm[0][0], sm[0][1]), fmax(sm[0][2], sm[0][3]));
+  if (threadIdx.x == 0) {
+    const double mb = fmax(fmax(sm[0][0], sm[0][1]), fmax(sm[0][2], sm[0][3]));
+    *pm = mb;
+    if (amax)
+      __hip_atomic_fetch_max(&amax[(vb & (kAmaxShards - 1)) * kAmaxStride], amax_key(mb), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // One particle per lane, 64-particle tiles per wave, 4 waves per block, one
@@ -399,7 +426,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   asm volatile("" ::"v"(lw));
   return;
 #endif
-  if (a.max_only) block_max_partial(lw, sm, a.pm + vb);
+  if (a.max_only) block_max_partial(lw, sm, a.pm + vb, a.amax, vb);
   else block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
 }
 
@@ -503,7 +530,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
       }
     }
   }
-  if (a.max_only) block_max_partial(fmax(lw0, lw1), sm, a.pm + vb);
+  if (a.max_only) block_max_partial(fmax(lw0, lw1), sm, a.pm + vb, a.amax, vb);
   else block_partial2(lw0, lw1, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
 }
 
@@ -1019,6 +1046,8 @@ struct Resample1Args {
   int sums_in_pass;        // the step wrote block maxima only: S, S2 from this pass
   MarkArgs mk;             // enabled: systematic marks; else write C
   uint64_t* C;
+  const uint64_t* amax_in; // the step's atomic-max shards (sums-in-pass only; nullptr: fold pm)
+  uint64_t* amax_reset;    // the other parity's shards, emptied for the next step
   uint64_t seed;
   uint32_t t;
 };
@@ -1230,7 +1259,15 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   // the sums of small tiles ride along, larger tiles load them once M is known)
   constexpr int KP = IT > kRsPart ? IT : kRsPart;
   constexpr bool kSumsEarly = IT <= kRsPart;
-  if (IT <= 8 && r.nb_part <= KP * kRsBlock) {  // uniform; always true at IT <= kRsPart (host-checked)
+  if (threadIdx.x < kAmaxShards && blockIdx.x == 0 && r.amax_reset)
+    r.amax_reset[threadIdx.x * kAmaxStride] = kAmaxEmpty;  // the next step's shards (read by nobody here)
+  if (sums && r.amax_in) {  // uniform: the step folded its maxima itself; every wave reads the shards
+    const int lane = threadIdx.x & 63;
+    uint64_t key = lane < kAmaxShards ? r.amax_in[lane * kAmaxStride] : 0ull;
+    key = wave_incl_max_u64(key);
+    M = amax_value(readlane63_u64(key));
+    GH_RS_STAMP(7);
+  } else if (IT <= 8 && r.nb_part <= KP * kRsBlock) {  // uniform; always true at IT <= kRsPart (host-checked)
     double pmv[KP], psv[kSumsEarly ? KP : 1], ps2v[kSumsEarly ? KP : 1];
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
