@@ -872,6 +872,25 @@ __device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, 
   return sys_count_exact(dev, N, X);
 }
 
+// sys_count for whole waves: the estimate and its clamps as selects, and the
+// exact count (probability ~2^-15 per call) behind a wave-uniform branch, so
+// the marks loops run straight-line code instead of nested divergent branches
+// (k_resample1's marks phase: 2.7 us of the C2 resample).  Same results.
+__device__ __forceinline__ int64_t sys_count_w(const DevScalars* dev, uint64_t N, uint64_t X) {
+  const double v = fma((double)X, (double)N, -(double)dev->o) * dev->invS;
+  const double fl = floor(v);
+  const double fr = v - fl;
+  const double jd = fmin(fmax(fl + 1.0, 0.0), (double)N);
+  int64_t j = N < (1ull << 31) ? (int64_t)(int32_t)jd : (int64_t)jd;
+  const bool edge = X == 0 || X >= dev->S;
+  j = X == 0 ? 0 : (X >= dev->S ? (int64_t)N : j);
+  const bool near = !edge && !(fr > 0x1p-16 && fr < 1.0 - 0x1p-16);
+  if (__builtin_amdgcn_ballot_w64(near) != 0) {
+    if (near) j = sys_count_exact(dev, N, X);
+  }
+  return j;
+}
+
 struct MarkArgs {
   uint64_t* mark;     // [n slots] tagged (epoch << 32 | ancestor) at each range start
   uint64_t* cmark;    // [64-slot groups] tagged ancestor of the group's first slot
@@ -1229,23 +1248,19 @@ __device__ uint64_t g_rs_stamps[1024 * 8];
 #endif
 
 template <bool MARKS, int IT, bool SUMS>
-__global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
+__global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resample1Args r) {
   __shared__ double smd[32];
   __shared__ uint64_t smu[32];
   __shared__ DevScalars sd;
   __shared__ uint64_t sbase;
-  __shared__ int32_t se[(kRsBlock * IT)];
-  __shared__ int64_t sfirst;
   __shared__ unsigned sgen;
   __shared__ int sfail;  // the barrier wait timed out: write nothing
-  __shared__ int smany;  // a particle of the tile covers more than two 64-slot group starts
   GH_RS_STAMP(0);
   GH_RS_EXIT_AT(0);
   // barrier generation of this launch: read before this block publishes
   if (threadIdx.x == 0) {
     sgen = r.dev->bar_gen + 1;
     sfail = 0;
-    smany = 0;
   }
   // ---- fold the step partials (same order in every block: same result)
   // this tile's log-weights are loaded up front, beside the partials
@@ -1403,8 +1418,13 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   // order — the same arithmetic in every block
   __shared__ uint64_t spa[8], spb[8];
   __shared__ double spg[2][8];
+  __shared__ uint64_t su53;
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 8 * 64) {  // a non-polling wave draws the systematic offset's uniform meanwhile
+      const u32x4 wr = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);  // independent of the totals
+      su53 = u53_bits(wr.x, wr.y);
+    }
     if (w < 8) {
       const unsigned b = (unsigned)(w * 64 + lane);
       const bool mine = b < gridDim.x;
@@ -1459,7 +1479,6 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   lds_barrier();
   GH_RS_STAMP(3);
   if (threadIdx.x == 0) {
-    const u32x4 wr = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);  // independent of the totals
     uint64_t all = 0, before = 0;
     double g1 = 0.0, g2 = 0.0;
 #pragma unroll
@@ -1478,7 +1497,7 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
     sd.S = all;
     sd.base = 0;
     sd.local = all;
-    sd.o = scale_u53(u53_bits(wr.x, wr.y), all);
+    sd.o = scale_u53(su53, all);
     sd.invN = r.d.inv_n;
     sd.Qs = udiv_n(all, N, sd.invN);
     sd.Rs = all - sd.Qs * N;
@@ -1523,46 +1542,35 @@ __global__ __launch_bounds__(kRsBlock) void k_resample1(Resample1Args r) {
   }
   const uint64_t N = (uint64_t)r.mk.n_global;
   int64_t s_i = sys_count(&sd, N, run);
-  if (threadIdx.x == 0) sfirst = s_i;
   // particle i owns the slots [s_i, e_i): a tagged mark at s_i, and the carry
   // of every 64-slot group that starts inside the range; a lane writes up to
-  // two carries itself, a longer range (a particle with > 64 offspring) makes
-  // the block write its whole span's carries by the search below
-  bool many = false;
+  // two carries itself, a longer range (a particle with > 64 offspring) gets
+  // its carries from the whole wave (one wave-wide store loop per such
+  // particle, no block barrier)
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     run += q[k];
-    const int64_t e_i = (i0 + k < r.n && q[k]) ? sys_count(&sd, N, run) : s_i;
-    se[threadIdx.x * IT + k] = (int32_t)e_i;
+    // (a particle past n or of zero weight leaves run, hence the count, unchanged)
+    const int64_t e_i = sys_count_w(&sd, N, run);
     const uint64_t tagged = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
     if (e_i > s_i) r.mk.mark[s_i] = tagged;
     const int64_t g0 = (s_i + 63) >> 6, g1 = (e_i + 63) >> 6;  // groups g with 64 g in [s_i, e_i)
-    if (g1 - g0 <= 2) {
+    const bool many = g1 - g0 > 2;
+    if (!many) {
       if (g1 > g0) r.mk.cmark[g0] = tagged;
       if (g1 > g0 + 1) r.mk.cmark[g0 + 1] = tagged;
-    } else {
-      many = true;
+    }
+    uint64_t bm = __builtin_amdgcn_ballot_w64(many);
+    while (bm) {
+      const int L = __builtin_ctzll(bm);
+      bm &= bm - 1;
+      const int32_t a0 = __builtin_amdgcn_readlane((int32_t)g0, L), a1 = __builtin_amdgcn_readlane((int32_t)g1, L);
+      const uint64_t tg = (r.mk.epoch << 32) | (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(i0 + k), L);
+      for (int32_t g = a0 + (threadIdx.x & 63); g < a1; g += 64) r.mk.cmark[g] = tg;
     }
     s_i = e_i;
   }
-  if (many) smany = 1;
-  lds_barrier();  // se[] and smany; the mark and carry stores need not have landed
   GH_RS_STAMP(5);
-  if (smany) {
-    // 64-slot groups starting inside this tile's slot span get their carry
-    const int64_t s_lo = sfirst, s_hi = se[(kRsBlock * IT) - 1];
-    const int64_t pbase = (int64_t)blockIdx.x * (kRsBlock * IT);
-    for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
-      const int32_t slot = (int32_t)(g * 64);
-      int lo = 0, hi = (kRsBlock * IT) - 1;  // first particle p with se[p] > slot
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (se[mid] > slot) hi = mid;
-        else lo = mid + 1;
-      }
-      r.mk.cmark[g] = (r.mk.epoch << 32) | (uint64_t)(pbase + lo);
-    }
-  }
   commit();
   GH_RS_STAMP(6);
 }
