@@ -16,39 +16,68 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgen_hip.so")
-SOURCES = [os.path.join(CSRC, "gh_api.hip")]
+SOURCES = [os.path.join(CSRC, "gh_api.hip")] + sorted(glob.glob(os.path.join(CSRC, "gh_inst_lg*.hip")))
 HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "gen_hip.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GH_OFFLOAD_ARCH", "gfx950")
+JOBS = int(os.environ.get("GH_BUILD_JOBS", str(min(16, os.cpu_count() or 4))))
+
+FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-ffp-contract=off",
+    "-fno-fast-math",
+    # keep constant materialisation next to its uses inside the persistent
+    # loops (hoisted fp64 polynomial constants otherwise spill)
+    "-mllvm",
+    "-disable-machine-licm",
+    "-fPIC",
+    "-Wall",
+    "-Wno-unused-function",
+    "-Wno-unused-value",
+    "-I" + os.path.join(ROOT, "include"),
+]
+
+
+def compile_cmd(src: str, obj: str, extra: list[str] | None = None) -> list[str]:
+    return [HIPCC, *FLAGS, *(extra or []), "-c", src, "-o", obj]
+
+
+def link_cmd(objs: list[str], out: str) -> list[str]:
+    return [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-o", out, "-L/opt/rocm/lib", "-lrccl",
+            "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def hipcc_cmd(out: str = LIB, extra: list[str] | None = None) -> list[str]:
-    return [
-        HIPCC,
-        f"--offload-arch={ARCH}",
-        "-O3",
-        "-std=c++17",
-        "-ffp-contract=off",
-        "-fno-fast-math",
-        # keep constant materialisation next to its uses inside the persistent
-        # loops (hoisted fp64 polynomial constants otherwise spill)
-        "-mllvm",
-        "-disable-machine-licm",
-        "-fPIC",
-        "-shared",
-        "-Wall",
-        "-Wno-unused-function",
-        "-Wno-unused-value",
-        "-I" + os.path.join(ROOT, "include"),
-        *(extra or []),
-        *SOURCES,
-        "-o",
-        out,
-        "-L/opt/rocm/lib",
-        "-lrccl",
-        "-Wl,-rpath,/opt/rocm/lib",
-    ]
+    """One-shot command (all sources in one hipcc call); kept for tools that
+    print or reuse the flags."""
+    return [HIPCC, *FLAGS, "-shared", *(extra or []), *SOURCES, "-o", out, "-L/opt/rocm/lib", "-lrccl",
+            "-Wl,-rpath,/opt/rocm/lib"]
+
+
+def _compile_all(out: str, obj_dir: str, extra: list[str] | None, verbose: bool) -> None:
+    """Every translation unit to an object in parallel, then one link."""
+    os.makedirs(obj_dir, exist_ok=True)
+    objs = [os.path.join(obj_dir, os.path.basename(s).replace(".hip", ".o")) for s in SOURCES]
+    cmds = [compile_cmd(s, o, extra) for s, o in zip(SOURCES, objs)]
+    if verbose:
+        print(" ".join(cmds[0]), f"(+{len(cmds) - 1} units, {JOBS} jobs)", flush=True)
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run(cmd):
+        return subprocess.run(cmd, capture_output=True, text=True)
+
+    # the biggest unit (gh_api.hip) first
+    with ThreadPoolExecutor(max_workers=JOBS) as ex:
+        results = list(ex.map(run, cmds))
+    failed = [(c, r) for c, r in zip(cmds, results) if r.returncode != 0]
+    for c, r in failed:
+        sys.stderr.write(r.stdout + r.stderr)
+    if failed:
+        raise subprocess.CalledProcessError(failed[0][1].returncode, failed[0][0])
+    subprocess.run(link_cmd(objs, out), check=True)
 
 
 def up_to_date() -> bool:
@@ -64,10 +93,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not shutil.which(HIPCC) and not os.path.exists(HIPCC):
         raise RuntimeError(f"hipcc not found at {HIPCC}")
     tmp = LIB + ".tmp"
-    cmd = hipcc_cmd(out=tmp)
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    _compile_all(tmp, os.path.join(HERE, "build_obj"), None, verbose)
     os.replace(tmp, LIB)
     return LIB
 
@@ -78,7 +104,7 @@ def build_variant(name: str, defines: list[str]) -> str:
     out_dir = os.path.join(HERE, "variants")
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, f"{name}.so")
-    subprocess.run(hipcc_cmd(out=out, extra=[f"-D{d}" for d in defines]), check=True)
+    _compile_all(out, os.path.join(out_dir, f"obj_{name}"), [f"-D{d}" for d in defines], True)
     return out
 
 

@@ -28,8 +28,18 @@
 #include "gh_dists.h"
 #include "gh_rejuv.h"
 #include "gh_csmc.h"
+#include "gh_inst.h"
 
 using namespace gh;
+
+// LG-SSM kernels come from gh_inst_lg*.hip (parallel build units)
+GH_LG_UNIT0(GH_EXTERN_TEMPLATE)
+GH_LG_UNIT1(GH_EXTERN_TEMPLATE)
+GH_LG_UNIT2(GH_EXTERN_TEMPLATE)
+GH_LG_UNIT3(GH_EXTERN_TEMPLATE)
+GH_LG_UNIT4(GH_EXTERN_TEMPLATE)
+GH_LG_UNIT5(GH_EXTERN_TEMPLATE)
+GH_LG_UNIT6(GH_EXTERN_TEMPLATE)
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_err;
@@ -1653,9 +1663,6 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     pf->stats_valid = true;
     if (sys) {
       pf->marks_pending = true;
-#if defined(GH_ABLATE_MARKS)  // timing-only variant: expand the marks in their own launch
-      CHECK(materialize_marks(pf));
-#endif
     } else {
       SearchArgs sa{};
       sa.C = pf->C;
@@ -1725,9 +1732,6 @@ static int resample_enqueue(gh_pf* pf, double thr) {
                          pf->anc_scratch, anc_target, n);
     } else {
       pf->marks_pending = true;
-#if defined(GH_ABLATE_MARKS)  // timing-only variant: expand the marks in their own launch
-      CHECK(materialize_marks(pf));
-#endif
     }
   } else if (R == 1) {
     SearchArgs sa{};

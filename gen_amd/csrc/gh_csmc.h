@@ -49,7 +49,7 @@ __global__ void k_pin_pre(const double* __restrict__ prm, typename Model::Params
   *a.w0 = base + Model::loglik(p, o, x);
 }
 
-__global__ __launch_bounds__(kBlock) void k_pin_post(PinArgs a, int D) {
+static __global__ __launch_bounds__(kBlock) void k_pin_post(PinArgs a, int D) {
   __shared__ double sm[3][4];
   const int64_t j = threadIdx.x;
   double lw = j < a.n ? a.logw[j] : -INFINITY;

@@ -253,11 +253,7 @@ __device__ __forceinline__ void buf_st_f64x2(const double* in, __amdgpu_buffer_r
 // accesses (lgkmcnt) but not for its global stores, so the states a wave has
 // just written drain while it computes the next tile.  (__syncthreads()'s
 // release fence would emit vmcnt(0) and expose every store's latency.)
-#if defined(GH_STEP_SYNCBAR)  // timing-only variant: the fenced barrier
-__device__ __forceinline__ void lds_barrier() { __syncthreads(); }
-#else
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-#endif
 
 // Block partial of the step kernel: the block max first (wave DPP max, then
 // the 4 waves through LDS), then every lane's e = exp(lw - max) and the wave
@@ -422,10 +418,6 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
       a.logw[j] = lw;
     }
   }
-#if defined(GH_ABLATE_REDUCE)  // timing-only variant: no statistics at all
-  asm volatile("" ::"v"(lw));
-  return;
-#endif
   if (a.max_only) block_max_partial(lw, sm, a.pm + vb, a.amax, vb);
   else block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
 }
@@ -601,7 +593,7 @@ __device__ __forceinline__ void commit_decision(const DecideArgs& d, const Decis
 
 // Stand-alone decision: used for a second maybe_resample without a step in
 // between (commits the first one; weights are then all 0).
-__global__ void k_decide(DecideArgs d, DevScalars* dev) {
+static __global__ void k_decide(DecideArgs d, DevScalars* dev) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   if (dev->fire) {
     dev->pending = 1;
@@ -615,7 +607,7 @@ __global__ void k_decide(DecideArgs d, DevScalars* dev) {
 // the resample flags the step consumed (one 1024-thread block, partial loads
 // issued eight at a time).  On a single rank it also pre-evaluates the next
 // maybe_resample! decision for `thr_hint` (> 0), so k_qsum's blocks need not.
-__global__ __launch_bounds__(1024) void k_fold(const double* pm, const double* ps, const double* ps2, int nb,
+static __global__ __launch_bounds__(1024) void k_fold(const double* pm, const double* ps, const double* ps2, int nb,
                                                double* stats_out, DevScalars* dev, int clear_flags,
                                                double thr_hint, int64_t n_global) {
   __shared__ double sm[16];
@@ -760,7 +752,7 @@ __device__ __forceinline__ void st_sc1(T* p, T v) {
 // Integer block sums of the quantised weights.  With `fused` the launch also
 // takes the maybe_resample! decision: every block evaluates it from the same
 // inputs (identical result), block 0 commits it, blocks exit unless it fires.
-__global__ __launch_bounds__(kBlock) void k_qsum(const double* logw, int64_t n, GateArgs g,
+static __global__ __launch_bounds__(kBlock) void k_qsum(const double* logw, int64_t n, GateArgs g,
                                                  uint64_t* bsum, int fused, DecideArgs d,
                                                  DevScalars* dev) {
   __shared__ uint64_t sm[4];
@@ -803,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void k_qsum(const double* logw, int64_t n, 
 }
 
 // multi-rank: this rank's integer total (input of the all-gather)
-__global__ __launch_bounds__(kBlock) void k_rank_total(const int* gate, const uint64_t* bsum, int64_t nb,
+static __global__ __launch_bounds__(kBlock) void k_rank_total(const int* gate, const uint64_t* bsum, int64_t nb,
                                                        DevScalars* dev) {
   if (!*gate) return;
   __shared__ uint64_t sm[4];
@@ -918,7 +910,7 @@ struct CdfArgs {
 // systematic resampling on one rank, the range marks: particle i owns slots
 // [count(C_{i-1}), count(C_i)); its range start gets a tagged mark, and every
 // step-block start slot the block's particles cover gets its ancestor in cmark.
-__global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, GateArgs g, CdfArgs ca,
+static __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, GateArgs g, CdfArgs ca,
                                                 DevScalars* dev, uint64_t* C, MarkArgs mk) {
   if (!*g.gate) return;
   __shared__ uint64_t sm4[4];
@@ -1013,7 +1005,7 @@ __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64_t n, G
 
 // systematic ancestors (materialised outside a step): wave-level prefix max
 // of the slot marks seeded with the carry of the 64-slot group
-__global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const int* zero_w,
+static __global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const int* zero_w,
                                                           const uint64_t* mark, const uint64_t* carry,
                                                           int64_t n, const int32_t* anc_old,
                                                           int32_t* anc_out, const DevScalars* dev, int mode) {
@@ -1240,7 +1232,7 @@ __device__ __forceinline__ uint64_t f64_to_u52(double x) {
 #endif
 
 #if defined(GH_RS_STAMPS)  // timing-only variant: per-block phase clocks
-__device__ uint64_t g_rs_stamps[1024 * 8];
+static __device__ uint64_t g_rs_stamps[1024 * 8];
 #define GH_RS_STAMP(k) \
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_rs_stamps[blockIdx.x * 8 + (k)] = wall_clock64();
 #else
@@ -1833,7 +1825,7 @@ struct RowsFillArgs {
   int64_t rows_cap;
 };
 
-__global__ __launch_bounds__(256) void k_rows_fill(RowsFillArgs r) {
+static __global__ __launch_bounds__(256) void k_rows_fill(RowsFillArgs r) {
   __shared__ DevScalars sd;
   __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
   const uint64_t N = (uint64_t)r.n_global;
@@ -1896,7 +1888,7 @@ constexpr int kSearchWin = 256;  // CDF entries a wave stages in LDS
 // and each lane finishes with an 8-step LDS search.  Wider windows (many
 // zero-offspring particles between the wave's ancestors) and random targets
 // (multinomial, sampling) use a per-lane binary search over the global CDF.
-__global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs g, const DevScalars* dev) {
+static __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs g, const DevScalars* dev) {
   if (!*g.gate) return;
   __shared__ uint64_t win[kBlock / 64][kSearchWin];
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1939,7 +1931,7 @@ __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs g, con
 
 // ------------------------------------------------- multi-rank exchange
 // Rows sent to other ranks: row j = (x[:, anc[j]], global id of anc[j]).
-__global__ __launch_bounds__(kBlock) void k_pack_rows(const int32_t* anc, int64_t rows, const double* x,
+static __global__ __launch_bounds__(kBlock) void k_pack_rows(const int32_t* anc, int64_t rows, const double* x,
                                                       int D, int64_t lo, double* out) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= rows) return;
@@ -1950,13 +1942,13 @@ __global__ __launch_bounds__(kBlock) void k_pack_rows(const int32_t* anc, int64_
 }
 
 // slots fed by received rows: ancestor = -1 - (row index in the receive buffer)
-__global__ void k_assign_remote(int32_t* anc, int64_t len, int64_t row0) {
+static __global__ void k_assign_remote(int32_t* anc, int64_t len, int64_t row0) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j < len) anc[j] = (int32_t)(-1 - (row0 + j));
 }
 
 // global parent ids of this rank's slots after an exchange
-__global__ void k_global_parents(const int32_t* anc, int64_t n, int64_t lo, const double* rows, int D,
+static __global__ void k_global_parents(const int32_t* anc, int64_t n, int64_t lo, const double* rows, int D,
                                  int64_t* gparent) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
@@ -1964,7 +1956,7 @@ __global__ void k_global_parents(const int32_t* anc, int64_t n, int64_t lo, cons
   gparent[j] = a >= 0 ? lo + a : __double_as_longlong(rows[(int64_t)(-1 - a) * (D + 1) + D]);
 }
 
-__global__ void k_copy_anc(const int* gate, const int32_t* src, int32_t* dst, int64_t n) {
+static __global__ void k_copy_anc(const int* gate, const int32_t* src, int32_t* dst, int64_t n) {
   if (!*gate) return;
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j < n) dst[j] = src[j];
@@ -1982,7 +1974,7 @@ struct TrajArgs {
   double* out;                // [D][n]
 };
 
-__global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevScalars* dev) {
+static __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevScalars* dev) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= a.n) return;
   int64_t idx = j;
@@ -1994,7 +1986,7 @@ __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevScalars* d
 }
 
 // sample_unweighted: prepare max / equal-weight flag from the current stats
-__global__ void k_prep_sample(DevScalars* dev, const double* stats_all, int R, int live) {
+static __global__ void k_prep_sample(DevScalars* dev, const double* stats_all, int R, int live) {
   if (threadIdx.x != 0) return;
   double M = -INFINITY;
   for (int r = 0; r < R; ++r) M = fmax(M, stats_all[3 * r]);
@@ -2004,7 +1996,7 @@ __global__ void k_prep_sample(DevScalars* dev, const double* stats_all, int R, i
 }
 
 // ------------------------------------------------------------ self tests
-__global__ void k_selftest_math(int64_t n, const double* in, double* oe, double* ol, double* os,
+static __global__ void k_selftest_math(int64_t n, const double* in, double* oe, double* ol, double* os,
                                 double* od) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
@@ -2016,7 +2008,7 @@ __global__ void k_selftest_math(int64_t n, const double* in, double* oe, double*
 }
 
 // Box–Muller stages for given words: u1, r, z0, z1 per triple
-__global__ void k_selftest_boxmuller(int64_t n, const uint32_t* w, double* out) {
+static __global__ void k_selftest_boxmuller(int64_t n, const uint32_t* w, double* out) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const uint32_t a = w[3 * i], b = w[3 * i + 1], c = w[3 * i + 2];
@@ -2029,7 +2021,7 @@ __global__ void k_selftest_boxmuller(int64_t n, const uint32_t* w, double* out) 
   out[4 * i + 3] = z1;
 }
 
-__global__ void k_selftest_normals(uint64_t seed, int64_t n, uint32_t step, uint32_t stream,
+static __global__ void k_selftest_normals(uint64_t seed, int64_t n, uint32_t step, uint32_t stream,
                                    int dim, double* out) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;

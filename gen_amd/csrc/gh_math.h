@@ -260,23 +260,17 @@ constexpr int kMathTabDoubles = 768;
 constexpr int kTrigOff = 256;
 static const double gh_math_tab_host[kMathTabDoubles] = {GH_LOG_TABLE_DATA, GH_TRIG_TABLE_DATA};
 #if defined(__HIPCC__)
-__constant__ double gh_math_tab_dev[kMathTabDoubles] = {GH_LOG_TABLE_DATA, GH_TRIG_TABLE_DATA};
+static __constant__ double gh_math_tab_dev[kMathTabDoubles] = {GH_LOG_TABLE_DATA, GH_TRIG_TABLE_DATA};
 // Copy the tables into a block's LDS (kMathTabDoubles doubles); callers
 // barrier before the first read.  Per-lane table reads then are ds_read_b128
 // instead of vector-memory loads.
 __device__ __forceinline__ void load_math_tab(double* lds) {
-#if defined(GH_ABLATE_TABLE)  // timing-only variant (with GH_ABLATE_BOXMULLER): no table copy
-  return;
-#endif
   for (int i = threadIdx.x; i < kMathTabDoubles / 2; i += blockDim.x)
     reinterpret_cast<double2*>(lds)[i] = reinterpret_cast<const double2*>(gh_math_tab_dev)[i];
 }
 // The same for a block of exactly 256 threads: both loads of a thread are
 // issued before its first LDS write (one memory round trip, no loop).
 __device__ __forceinline__ void load_math_tab256(double* lds) {
-#if defined(GH_ABLATE_TABLE)
-  return;
-#endif
   static_assert(kMathTabDoubles / 2 > 256 && kMathTabDoubles / 2 <= 512, "two double2 per thread");
   const double2* src = reinterpret_cast<const double2*>(gh_math_tab_dev);
   double2* dst = reinterpret_cast<double2*>(lds);
@@ -405,11 +399,6 @@ GH_HD double sqrt_radius(double x) {
 // angle from the 32-bit word c.  Four Philox words per block
 // serve 4/3 pairs, so d normals take ceil(3 ceil(d/2) / 4) blocks.
 GH_HD void box_muller(uint32_t a, uint32_t b, uint32_t c, double* z0, double* z1, const double* tab = nullptr) {
-#if defined(GH_ABLATE_BOXMULLER)  // timing-only variant: uniforms instead of normals
-  *z0 = u53(a, b) - 0.5;
-  *z1 = (double)c * 0x1p-32 - 0.5;
-  return;
-#endif
   const double u1 = one_minus_u53(a, b);  // (0, 1]
   const double r = sqrt_radius(-2.0 * gh_log_unit(u1, tab));
   double s, co;

@@ -218,12 +218,8 @@ struct LGModel {
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       double acc = p.b[i];
-#if defined(GH_ABLATE_MATVEC)  // timing-only variant: no transition matrix product
-      acc += xp[i];
-#else
 #pragma unroll
       for (int k = 0; k < D; ++k) acc = fma(p.A[i * D + k], xp[k], acc);
-#endif
       if (S & 1) {
         acc = fma(p.LQ[i * D + i], z[i], acc);
       } else {

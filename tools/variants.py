@@ -12,20 +12,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "base": [],
-    "no_bm_philox1": ["GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
-    "no_reduce": ["GH_ABLATE_REDUCE"],
-    "no_reduce_no_rng": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1"],
     "occ8": ["GH_LG10_WAVES=8"],
     "occ6": ["GH_LG10_WAVES=6"],
     "philox1": ["GH_PHILOX_ROUNDS=1"],
-    "no_bm": ["GH_ABLATE_BOXMULLER"],
     "philox7": ["GH_PHILOX_ROUNDS=7"],
-    "syncbar": ["GH_STEP_SYNCBAR"],
-    "skel_nomv": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_ABLATE_MATVEC"],
-    "skel_occ8": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_LG10_WAVES=8"],
-    "skel_notab": ["GH_ABLATE_REDUCE", "GH_ABLATE_BOXMULLER", "GH_PHILOX_ROUNDS=1", "GH_ABLATE_TABLE"],
-    "early": ["GH_EARLY_PHILOX"],
-    "early_occ6": ["GH_EARLY_PHILOX", "GH_LG10_WAVES=6"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
