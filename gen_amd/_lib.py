@@ -70,6 +70,7 @@ SIGNATURES = {
     "gh_ctx_create_dist": (c_int, [c_int, c_int, c_int, POINTER(c_uint8), c_void_p, POINTER(c_void_p)]),
     "gh_ctx_create_hostcomm": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, POINTER(c_void_p)]),
     "gh_ctx_destroy": (c_int, [c_void_p]),
+    "gh_ctx_force_multirank": (c_int, [c_void_p]),
     "gh_ctx_rank": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
     "gh_ctx_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
     "gh_ctx_synchronize": (c_int, [c_void_p]),

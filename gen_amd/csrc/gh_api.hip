@@ -99,7 +99,13 @@ struct gh_ctx {
   gh_host_comm hc{};
   char* stage = nullptr;  // pinned staging buffer
   size_t stage_bytes = 0;
+  // gh_ctx_force_multirank: filters take the multi-rank path even at world 1
+  // (a one-rank RCCL communicator; tests and timing on a one-GPU box)
+  bool force_multi = false;
 };
+
+// the filter's multi-rank path (collectives, split steps) is in use
+static bool mr(const gh_ctx* c) { return c->world > 1 || c->force_multi; }
 
 static int ctx_setup(int device, void* stream, gh_ctx* c) {
   c->device = device;
@@ -165,6 +171,19 @@ extern "C" int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_
   c->host_comm = true;
   c->hc = *comm;
   *out = c;
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_force_multirank(gh_ctx* c) {
+  if (!c) return set_err(GH_E_INVAL, "null ctx");
+  if (c->force_multi) return GH_OK;
+  if (c->world == 1 && !c->host_comm && !c->comm) {  // a one-rank RCCL communicator
+    ncclUniqueId u;
+    NCCL_TRY(ncclGetUniqueId(&u));
+    HIP_TRY(hipSetDevice(c->device));
+    NCCL_TRY(ncclCommInitRank(&c->comm, 1, u, 0));
+  }
+  c->force_multi = true;
   return GH_OK;
 }
 
@@ -240,10 +259,18 @@ static int comm_exchange(gh_ctx* c, const std::vector<CommMsg>& sends, const std
                          hipStream_t s) {
   if (sends.empty() && recvs.empty()) return GH_OK;
   if (!c->host_comm) {
+    // an error inside the group still closes it (an open group leaves the
+    // communicator unusable); the first error is reported
     NCCL_TRY(ncclGroupStart());
-    for (const auto& m : sends) NCCL_TRY(ncclSend(m.dptr, m.bytes, ncclUint8, m.peer, c->comm, s));
-    for (const auto& m : recvs) NCCL_TRY(ncclRecv(m.dptr, m.bytes, ncclUint8, m.peer, c->comm, s));
-    NCCL_TRY(ncclGroupEnd());
+    ncclResult_t r = ncclSuccess;
+    const char* what = "";
+    for (const auto& m : sends)
+      if (r == ncclSuccess && (r = ncclSend(m.dptr, m.bytes, ncclUint8, m.peer, c->comm, s)) != ncclSuccess) what = "ncclSend";
+    for (const auto& m : recvs)
+      if (r == ncclSuccess && (r = ncclRecv(m.dptr, m.bytes, ncclUint8, m.peer, c->comm, s)) != ncclSuccess) what = "ncclRecv";
+    const ncclResult_t re = ncclGroupEnd();
+    if (r != ncclSuccess) return set_err(GH_E_RCCL, "%s: %s", what, ncclGetErrorString(r));
+    if (re != ncclSuccess) return set_err(GH_E_RCCL, "ncclGroupEnd: %s", ncclGetErrorString(re));
     return GH_OK;
   }
   size_t total = 0;
@@ -677,6 +704,8 @@ struct gh_pf {
   int64_t nb_scan = 0;
   int64_t nb_step = 0;
   int64_t nb_part = 0;             // block partials the last step kernel wrote (pair kernels: n / 512)
+  bool pairs = false;             // the default step runs the pair kernel (512 particles per block)
+  bool last_pairs = false;        // the last step kernel was the pair kernel
   double *pm = nullptr, *ps = nullptr, *ps2 = nullptr;
   DevScalars* dev = nullptr;
   double* stats_all = nullptr;    // [3*world]
@@ -696,7 +725,12 @@ struct gh_pf {
   hipEvent_t ev_plan = nullptr;   //   fire flag + totals landed in h_plan
   hipEvent_t ev_rb = nullptr;     //   k_rank_b packed the rows
   hipEvent_t ev_x = nullptr;      //   rows exchanged
-  uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]]
+  uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]] (k_rank_a) or the R rank records (k_rank_a2)
+  bool plan_recs = false;         // the pending plan is k_rank_a2's records (the host takes the decision)
+  double plan_thr = 0.0;          //   at this threshold
+  uint64_t* amax_all = nullptr;   // multi-rank: [R][kAmaxShards * kAmaxStride] all-gathered shard words
+  uint64_t* rec = nullptr;        // multi-rank: [kRecWords] this rank's record (k_rank_a2)
+  uint64_t* recs_all = nullptr;   //   [R][kRecWords] all-gathered
   bool plan_pending = false;      // k_rank_b enqueued; the host has not read the totals yet
   bool rem_fire = false;          // the resample fired (read by finish_plan)
   int64_t rem_ra = 0, rem_rb = 0; // local slots [0, ra) and [rb, n) take received rows
@@ -757,7 +791,7 @@ static void pick_resample_tiles(gh_pf* pf, int64_t n) {
     int cap;
   };
   std::vector<Cand> cands;
-  if (pf->ctx->world == 1) {
+  if (!mr(pf->ctx)) {
     // (IT = 2, two 1024-thread blocks per CU, measured slower: 59.4 vs 54.7 us per C2 step)
     cands = {{4, resample_cap<4>(cus)}, {8, resample_cap<8>(cus)}, {16, resample_cap<16>(cus)}};
   } else {
@@ -846,6 +880,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
   hipFree(pf->acc_count); hipFree(pf->pin); hipFree(pf->amax);
+  hipFree(pf->amax_all); hipFree(pf->rec); hipFree(pf->recs_all);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
   if (pf->ev_plan) hipEventDestroy(pf->ev_plan);
@@ -878,12 +913,13 @@ struct has_pairs : std::false_type {};
 template <class M>
 struct has_pairs<M, std::void_t<decltype(M::kPairs)>> : std::bool_constant<M::kPairs> {};
 
-// the pair kernel steps the single-rank filters of paired models (pair mates
-// in one lane needs a particle offset that is a multiple of 128)
+// the pair kernel steps the filters of paired models (pair mates in one lane
+// needs a particle offset that is a multiple of 128; every rank decides for
+// itself — the values are the same either way)
 template <class Model>
 static bool use_pairs(const gh_pf* pf) {
   // (conditional filters re-fold block 0 as 256 particles: k_pin_post)
-  if constexpr (has_pairs<Model>::value) return pf->ctx->world == 1 && (pf->lo & 127) == 0 && !pf->cond;
+  if constexpr (has_pairs<Model>::value) return (pf->lo & 127) == 0 && !pf->cond;
   return false;
 }
 
@@ -893,9 +929,12 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
   StepArgs a = a0;
   a.nvb = (a.n + kBlock - 1) / kBlock;
   if constexpr (has_pairs<Model>::value) {
-    if (use_pairs<Model>(pf) && a.part == 0) {
+    if (use_pairs<Model>(pf)) {
       const dim3 grid((unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock))), block(kBlock);
-      pf->nb_part = grid.x;
+      if (a.part != 2) {
+        pf->nb_part = grid.x;
+        pf->last_pairs = true;
+      }
       if (init)
         hipExtLaunchKernelGGL((k_step_pairs<Model, true>), grid, block, 0, pf->s, e0, e1, 0,
                               (const double*)pf->m->dparams, p, o, a);
@@ -905,7 +944,10 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
       return;
     }
   }
-  pf->nb_part = pf->nb_step;
+  if (a.part != 2) {
+    pf->nb_part = pf->nb_step;
+    pf->last_pairs = false;
+  }
   const dim3 grid((unsigned)(a.part == 2 ? a.nvb : pf->nb_step)), block(kBlock);
   // the timed launch records its events at the kernel's own start and end
   if (init)
@@ -924,7 +966,7 @@ static void launch_fold(gh_pf* pf, const StepArgs& a, bool init, int64_t nb) {
 
 // one rank: make stats_all current (the fold is otherwise done by k_resample1)
 static int ensure_stats(gh_pf* pf) {
-  if (pf->ctx->world > 1 || pf->stats_valid) return GH_OK;
+  if (mr(pf->ctx) || pf->stats_valid) return GH_OK;
   if (pf->max_only)  // cannot happen: a max-only step is always followed by the fused resample
     return set_err(GH_E_STATE, "internal: step partials hold block maxima only");
   hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_part,
@@ -1010,10 +1052,12 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
   if (a.part == 1) {
     CHECK(finish_plan(pf));
     if (pf->rem_fire) {
-      // tiles [0, tA) and [tB, nb) hold the slots [0, ra) and [rb, n)
-      const int64_t n = pf->n, nb = pf->nb_step, ra = pf->rem_ra, rb = pf->rem_rb;
-      int64_t tA = (ra + kBlock - 1) / kBlock;
-      int64_t tB = rb < n ? rb / kBlock : nb;
+      // tiles [0, tA) and [tB, nb) hold the slots [0, ra) and [rb, n) (tiles
+      // of the step kernel's blocks: 512 slots for the pair kernel)
+      const int64_t kb = pf->last_pairs ? 2 * kBlock : kBlock;
+      const int64_t n = pf->n, nb = (n + kb - 1) / kb, ra = pf->rem_ra, rb = pf->rem_rb;
+      int64_t tA = (ra + kb - 1) / kb;
+      int64_t tB = rb < n ? rb / kb : nb;
       if (tB <= tA) {  // the ranges meet: one launch over every tile
         tA = nb;
         tB = nb;
@@ -1021,11 +1065,11 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
       if (tA > 0) {
         StepArgs b = a;
         b.part = 2;
-        b.n = std::min<int64_t>(n, tA * kBlock);
+        b.n = std::min<int64_t>(n, tA * kb);
         CHECK(launch_step(pf, o, b, init));
       }
       if (tB < nb) {  // every per-slot pointer advanced to tile tB
-        const int64_t off = tB * kBlock;
+        const int64_t off = tB * kb;
         StepArgs b = a;
         b.part = 2;
         b.j0 = off;
@@ -1043,7 +1087,7 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
       }
     }
   }
-  launch_fold(pf, a, init, pf->nb_step);
+  if (!a.max_only) launch_fold(pf, a, init, pf->nb_part);
   return GH_OK;
 }
 
@@ -1056,7 +1100,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   const int every = pf->opts.time_kernels;
   if (every <= 0 || (a.t - 1) % (uint32_t)every != 0) {
     CHECK(launch_step(pf, o, a, init));
-    if (pf->ctx->world > 1) CHECK(finish_split(pf, o, a, init));
+    if (mr(pf->ctx)) CHECK(finish_split(pf, o, a, init));
     HIP_TRY(hipGetLastError());
     return GH_OK;
   }
@@ -1070,14 +1114,14 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
   hipEvent_t e0 = pf->ev[pf->ev_used], e1 = pf->ev[pf->ev_used + 1];
   pf->ev_used += 2;
   CHECK(launch_step(pf, o, a, init, e0, e1));
-  if (pf->ctx->world > 1) CHECK(finish_split(pf, o, a, init));
+  if (mr(pf->ctx)) CHECK(finish_split(pf, o, a, init));
   HIP_TRY(hipGetLastError());
   return GH_OK;
 }
 
 // after the step kernel: share the rank's (M, S, S2) with every rank
 static int share_stats(gh_pf* pf) {
-  if (pf->ctx->world == 1) return GH_OK;
+  if (!mr(pf->ctx)) return GH_OK;
   return comm_allgather(pf->ctx, pf->dev->stats, pf->stats_all, 3 * sizeof(double), pf->s);
 }
 
@@ -1149,7 +1193,7 @@ extern "C" int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_
   if (!m || !ref_x1 || !out) return set_err(GH_E_INVAL, "gh_pf_init_conditional: null argument");
   if (!opts || opts->resampler != GH_RESAMPLE_MULTINOMIAL)
     return set_err(GH_E_INVAL, "conditional SMC uses multinomial resampling (examples/pmmh/smc.jl:132)");
-  if (m->ctx->world != 1) return set_err(GH_E_INVAL, "conditional SMC runs on one rank");
+  if (mr(m->ctx)) return set_err(GH_E_INVAL, "conditional SMC runs on one rank");
   if (m->family == GH_FAMILY_REGRESSION) return set_err(GH_E_INVAL, "conditional SMC needs a state-space model");
   return pf_init_impl(m, obs, GH_PROPOSAL_DEFAULT, n_particles, seed, opts, ref_x1, out);
 }
@@ -1192,6 +1236,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   {  // the partial count of the family's step kernel (resample tile choice)
     bool pairs = false;
     with_model(m, [&](auto model, const auto&) { pairs = use_pairs<decltype(model)>(pf); });
+    pf->pairs = pairs;
     if (pairs) pf->nb_part = (n + 2 * kBlock - 1) / (2 * kBlock);
   }
   pf->nb_scan = (n + kScanTile - 1) / kScanTile;
@@ -1214,18 +1259,24 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->n_tiles = (n + kRsTile - 1) / kRsTile;
   ALLOC(pf->tsum, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles));
   pick_resample_tiles(pf, n);
-  if (ctx->world == 1) ALLOC(pf->amax, sizeof(uint64_t) * 2 * kAmaxShards * kAmaxStride);
-  if (ctx->world > 1) {
+  ALLOC(pf->amax, sizeof(uint64_t) * 2 * kAmaxShards * kAmaxStride);
+  if (mr(ctx)) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
     ALLOC(pf->rows_recv, sizeof(double) * (pf->D + 1) * n);
     ALLOC(pf->gparent, sizeof(int64_t) * n);
+    ALLOC(pf->amax_all, sizeof(uint64_t) * kAmaxShards * kAmaxStride * ctx->world);
+    ALLOC(pf->rec, sizeof(uint64_t) * kRecWords);
+    ALLOC(pf->recs_all, sizeof(uint64_t) * kRecWords * ctx->world);
+    // the shards are empty between uses: k_rank_a2 empties what it consumed
+    pf->amax_armed = true;
     if (hipStreamCreateWithFlags(&pf->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&pf->ev_tot, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&pf->ev_plan, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&pf->ev_rb, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&pf->ev_x, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void**)&pf->h_plan, sizeof(uint64_t) * (ctx->world + 1), hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc((void**)&pf->h_plan, sizeof(uint64_t) * std::max(ctx->world + 1, kRecWords * ctx->world),
+                      hipHostMallocDefault) != hipSuccess)
       return fail(set_err(GH_E_NOMEM, "multi-rank plan buffers"));
   }
   if (!pf->opts.record_history) {
@@ -1281,7 +1332,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   a.pm = pf->pm;
   a.ps = pf->ps;
   a.ps2 = pf->ps2;
-  a.stats_out = ctx->world == 1 ? pf->stats_all : pf->dev->stats;
+  a.stats_out = !mr(ctx) ? pf->stats_all : pf->dev->stats;
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   rc = timed_step(pf, o, a, true);
   if (rc) return fail(rc);
@@ -1359,12 +1410,14 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.pm = pf->pm;
   a.ps = pf->ps;
   a.ps2 = pf->ps2;
-  a.stats_out = pf->ctx->world == 1 ? pf->stats_all : pf->dev->stats;
+  a.stats_out = !mr(pf->ctx) ? pf->stats_all : pf->dev->stats;
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
-  a.max_only = pf->step_max_only && !pin_ref ? 1 : 0;
-  // (not for the pair-stepped kernel: its 4096 atomics cost C4's short step
-  // more than the fold they save, measured)
-  a.amax = a.max_only && pf->amax_armed && pf->nb_part == pf->nb_step
+  const bool multi = mr(pf->ctx);
+  // multi-rank: a max-only step needs the shards (the rank maximum has no other fold)
+  a.max_only = pf->step_max_only && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
+  // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
+  // short step more than the fold they save, measured)
+  a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
                ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride
                : nullptr;
   // multi-rank after a resample: the local half now, the rest once the rows arrive
@@ -1375,11 +1428,11 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   }
   CHECK(timed_step(pf, o, a, false));
   if (pin_ref) CHECK(pin_launch(pf, o, false, false));
-  CHECK(share_stats(pf));
+  if (!a.max_only) CHECK(share_stats(pf));  // (max-only: the resample's own all-gathers)
   pf->t = t;
   pf->max_only = a.max_only != 0;
   pf->amax_valid = a.amax != nullptr;
-  pf->amax_armed = false;
+  if (!multi) pf->amax_armed = false;
   pf->resample_calls = 0;
   pf->marks_pending = false;
   pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
@@ -1457,20 +1510,48 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
       return set_err(GH_E_NOMEM, "send rows (%lld)", (long long)cap);
     pf->send_cap = cap;
   }
-  RankAArgs ra{};
-  ra.logw = pf->logw;
-  ra.n = pf->n;
-  ra.shift = shift;
-  ra.dev = pf->dev;
-  ra.d = d;
-  ra.tsum = pf->tsum;
-  switch (pf->rs_it) {
-    case 4: hipLaunchKernelGGL(k_rank_a<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
-    case 8: hipLaunchKernelGGL(k_rank_a<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
-    default: hipLaunchKernelGGL(k_rank_a<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
+  // after a max-only step (gh_pf_run): the shards' all-gather, k_rank_a2
+  // (global max, quantisation + sums, rank record), the records' all-gather;
+  // otherwise k_rank_a on the all-gathered triples and the totals' all-gather
+  const bool sums = pf->max_only && pf->amax_valid;
+  if (sums) {
+    uint64_t* shards = pf->amax + (t & 1) * kAmaxShards * kAmaxStride;
+    CHECK(comm_allgather(c, shards, pf->amax_all, sizeof(uint64_t) * kAmaxShards * kAmaxStride, pf->s));
+    RankA2Args a2{};
+    a2.logw = pf->logw;
+    a2.n = pf->n;
+    a2.shift = shift;
+    a2.dev = pf->dev;
+    a2.amax_all = pf->amax_all;
+    a2.R = R;
+    a2.amax_reset = shards;
+    a2.tsum = pf->tsum;
+    a2.ts1 = pf->tsum + pf->n_tiles;
+    a2.ts2 = pf->tsum + 2 * pf->n_tiles;
+    a2.rec = pf->rec;
+    switch (pf->rs_it) {
+      case 4: hipLaunchKernelGGL(k_rank_a2<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
+      case 8: hipLaunchKernelGGL(k_rank_a2<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
+      default: hipLaunchKernelGGL(k_rank_a2<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
+    }
+    HIP_TRY(hipGetLastError());
+    CHECK(comm_allgather(c, pf->rec, pf->recs_all, sizeof(uint64_t) * kRecWords, pf->s));
+  } else {
+    RankAArgs ra{};
+    ra.logw = pf->logw;
+    ra.n = pf->n;
+    ra.shift = shift;
+    ra.dev = pf->dev;
+    ra.d = d;
+    ra.tsum = pf->tsum;
+    switch (pf->rs_it) {
+      case 4: hipLaunchKernelGGL(k_rank_a<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
+      case 8: hipLaunchKernelGGL(k_rank_a<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
+      default: hipLaunchKernelGGL(k_rank_a<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
+    }
+    HIP_TRY(hipGetLastError());
+    CHECK(comm_allgather(c, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
   }
-  HIP_TRY(hipGetLastError());
-  CHECK(comm_allgather(c, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
   HIP_TRY(hipEventRecord(pf->ev_tot, pf->s));
   RankBArgs rb{};
   rb.logw = pf->logw;
@@ -1478,7 +1559,10 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.shift = shift;
   rb.dev = pf->dev;
   rb.tsum = pf->tsum;
-  rb.totals = pf->totals_all;
+  rb.totals = sums ? pf->recs_all : pf->totals_all;
+  rb.tot_stride = sums ? kRecWords : 1;
+  rb.recs = sums ? pf->recs_all : nullptr;
+  rb.d = d;
   rb.R = R;
   rb.rank = q;
   rb.lo = pf->lo;
@@ -1500,9 +1584,16 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
   // the decision and the totals, read on the side stream while k_rank_b runs
   HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_tot, 0));
-  HIP_TRY(hipMemcpyAsync(pf->h_plan, &pf->dev->fire, sizeof(int), hipMemcpyDeviceToHost, pf->aux));
-  HIP_TRY(hipMemcpyAsync(pf->h_plan + 1, pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->aux));
+  if (sums) {  // the host takes the decision from the records itself (decide_records)
+    HIP_TRY(hipMemcpyAsync(pf->h_plan, pf->recs_all, sizeof(uint64_t) * kRecWords * R, hipMemcpyDeviceToHost,
+                           pf->aux));
+  } else {
+    HIP_TRY(hipMemcpyAsync(pf->h_plan, &pf->dev->fire, sizeof(int), hipMemcpyDeviceToHost, pf->aux));
+    HIP_TRY(hipMemcpyAsync(pf->h_plan + 1, pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->aux));
+  }
   HIP_TRY(hipEventRecord(pf->ev_plan, pf->aux));
+  pf->plan_recs = sums;
+  pf->plan_thr = d.thr;
   pf->mark_mode = 2;
   pf->marks_pending = true;  // harmless when it did not fire: k_step gates on the device flag
   pf->plan_pending = true;
@@ -1523,9 +1614,16 @@ static int finish_plan(gh_pf* pf) {
   const int t = pf->t;
   HIP_TRY(hipEventSynchronize(pf->ev_plan));
   int fire = 0;
-  memcpy(&fire, pf->h_plan, sizeof(int));
+  std::vector<uint64_t> totv(R);
+  if (pf->plan_recs) {  // k_rank_b takes the same decision from the same records
+    fire = decide_records(pf->h_plan, R, pf->plan_thr).fire;
+    for (int r = 0; r < R; ++r) totv[r] = pf->h_plan[kRecWords * r];
+  } else {
+    memcpy(&fire, pf->h_plan, sizeof(int));
+    for (int r = 0; r < R; ++r) totv[r] = pf->h_plan[1 + r];
+  }
   if (!fire) return GH_OK;
-  const uint64_t* tot = pf->h_plan + 1;
+  const uint64_t* tot = totv.data();
   uint64_t S = 0, base = 0;
   for (int r = 0; r < R; ++r) {
     if (r < q) base += tot[r];
@@ -1564,7 +1662,8 @@ static int finish_plan(gh_pf* pf) {
     fa.rank = q;
     fa.lo = pf->lo;
     fa.dev = pf->dev;
-    fa.totals = pf->totals_all;
+    fa.totals = pf->plan_recs ? pf->recs_all : pf->totals_all;
+    fa.tot_stride = pf->plan_recs ? kRecWords : 1;
     fa.n_global = pf->n_global;
     fa.xprev = slot_x(pf, t);
     fa.D = D;
@@ -1592,6 +1691,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   const int t = pf->t;
   CHECK(grow_for_step(pf, t + 1));
   const int R = pf->ctx->world;
+  const bool multi = mr(pf->ctx);
   const int64_t n = pf->n;
   const bool second = pf->resample_calls > 0;
   DecideArgs d{};
@@ -1612,7 +1712,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   // The common case fuses the decision into the first resample kernel; a
   // second call without a step (or an empty shard) decides in its own launch.
   const bool sys = pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
-  if (R == 1 && !second && n > 0 && pf->rs_grid > 0) {
+  if (!multi && !second && n > 0 && pf->rs_grid > 0) {
     // one launch: fold + decision + quantise + one grid barrier + marks / CDF
     Resample1Args ra{};
     ra.pm = pf->pm;
@@ -1681,7 +1781,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     pf->resample_calls++;
     return GH_OK;
   }
-  if (R > 1 && R <= kMaxRanks && !second && n > 0 && sys && pf->rs_grid > 0) {
+  if (multi && R <= kMaxRanks && !second && n > 0 && sys && pf->rs_grid > 0) {
     CHECK(rank_resample(pf, d, g.shift, t));
     pf->resample_calls++;
     return GH_OK;
@@ -1694,13 +1794,13 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   if (n > 0)
     hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum,
                        fmode, d, pf->dev);
-  if (R > 1) {
+  if (multi) {
     hipLaunchKernelGGL(k_rank_total, dim3(1), dim3(kBlock), 0, pf->s, g.gate, pf->bsum, n > 0 ? pf->nb_scan : 0,
                        pf->dev);
     CHECK(comm_allgather(pf->ctx, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
   }
   int32_t* anc_target = anc_for_step(pf, t + 1);
-  const bool sys1 = R == 1 && pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
+  const bool sys1 = !multi && pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
   MarkArgs mk{};
   mk.mark = pf->mark;
   mk.cmark = pf->cmark;
@@ -1711,7 +1811,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   CdfArgs ca{};
   ca.bsum = pf->bsum;
   ca.nb = pf->nb_scan;
-  ca.totals = R > 1 ? pf->totals_all : nullptr;
+  ca.totals = multi ? pf->totals_all : nullptr;
   ca.R = R;
   ca.rank = pf->ctx->rank;
   ca.n_global = pf->n_global;
@@ -1733,7 +1833,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     } else {
       pf->marks_pending = true;
     }
-  } else if (R == 1) {
+  } else if (!multi) {
     SearchArgs sa{};
     sa.C = pf->C;
     sa.n_cdf = n;
@@ -1787,7 +1887,11 @@ extern "C" int gh_pf_run(gh_pf* pf, int n_steps, const gh_obs* obs, int proposal
   // A step followed by this loop's own maybe_resample! leaves the weight sums
   // to the fused resample kernel (k_step writes block maxima only; one rank,
   // fused path only); the last step writes full partials for other readers.
-  const bool fused = pf->ctx->world == 1 && pf->rs_grid > 0 && !pf->cond && pf->n > 0;
+  // Multi-rank (systematic): the maxima go to the step's atomic-max shards and
+  // the sums into k_rank_a2's pass (no fold launch, no all-gather of triples).
+  const bool multi = mr(pf->ctx);
+  const bool fused = pf->rs_grid > 0 && !pf->cond && pf->n > 0 &&
+                     (!multi || (pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC && pf->ctx->world <= kMaxRanks));
   for (int i = 0; i < n_steps; ++i) {
     CHECK(gh_pf_maybe_resample(pf, thr, nullptr, nullptr));
     pf->step_max_only = fused && i + 1 < n_steps;
@@ -1866,7 +1970,7 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   if (t < 1 || t > pf->t) return set_err(GH_E_INVAL, "step %d outside 1..%d", t, pf->t);
   if (!pf->opts.record_history && t != pf->t)
     return set_err(GH_E_STATE, "record_history is off: only the current step is kept");
-  if (pf->ctx->world > 1 && t != pf->t)
+  if (mr(pf->ctx) && t != pf->t)
     return set_err(GH_E_STATE, "multi-rank: trajectories before the current step are not materialised");
   const int64_t n = pf->n;
   if (n == 0) return GH_OK;
@@ -1889,7 +1993,7 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   ta.xs = dxs;
   ta.ancs = dancs;
   ta.res_before = pf->res_hist;
-  ta.anc_pending = (pf->ctx->world == 1 && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
+  ta.anc_pending = (!mr(pf->ctx) && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
   ta.live = flags_live(pf);
   ta.n = n;
   ta.t_target = t;
@@ -1914,7 +2018,7 @@ extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
   const int T = pf->t;
   if (T < 1) return set_err(GH_E_STATE, "gh_pf_get_scores before init");
   if (!pf->opts.record_history && T > 1) return set_err(GH_E_STATE, "gh_pf_get_scores needs record_history");
-  if (pf->ctx->world > 1 && T > 1)
+  if (mr(pf->ctx) && T > 1)
     return set_err(GH_E_STATE, "multi-rank: the genealogy before the current step is not materialised");
   if ((int)pf->obs_hist.size() < T) return set_err(GH_E_STATE, "internal: observation history");
   const int64_t n = pf->n;
@@ -1949,7 +2053,7 @@ extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
     sa.xs = dxs;
     sa.ancs = dancs;
     sa.res_before = pf->res_hist;
-    sa.anc_pending = (pf->ctx->world == 1 && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
+    sa.anc_pending = (!mr(pf->ctx) && pf->cap >= T + 1) ? anc_for_step(pf, T + 1) : nullptr;
     sa.live = flags_live(pf);
     sa.obs = dobs;
     sa.n = n;
@@ -2134,6 +2238,7 @@ static int dist_launch(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t s
   DistShape sh;
   CHECK(dist_shape(d, &sh));
   if (n == 0) return GH_OK;
+  if (!out || (!random && !x)) return set_err(GH_E_INVAL, "null %s buffer", out ? "x" : "out");
   HIP_TRY(hipSetDevice(ctx->device));
   double* dp = nullptr;
   bool owned = false;
@@ -2208,7 +2313,7 @@ extern "C" int gh_dist_random(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uin
 
 extern "C" int gh_pf_get_states(gh_pf* pf, double* out) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
-  if (pf->ctx->world > 1) {
+  if (mr(pf->ctx)) {
     DevScalars h;
     CHECK(read_scalars(pf, &h, nullptr));
     if (flags_live(pf) && (h.pending | h.fire))
@@ -2231,7 +2336,7 @@ extern "C" int gh_pf_get_parents(gh_pf* pf, int64_t* out) {
     for (int64_t i = 0; i < pf->n; ++i) out[i] = pf->lo + i;
     return GH_OK;
   }
-  if (pf->ctx->world > 1) {
+  if (mr(pf->ctx)) {
     // the most recent resample (before step s_last): local ancestors plus the
     // global ids carried by the received rows
     hipLaunchKernelGGL(k_global_parents, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s,
@@ -2409,7 +2514,7 @@ extern "C" int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int3
 
 extern "C" int gh_pf_sample_unweighted(gh_pf* pf, int64_t ns, uint64_t seed, int64_t* idx) {
   if (!pf || !idx || ns < 0) return set_err(GH_E_INVAL, "bad argument");
-  if (pf->ctx->world > 1) return set_err(GH_E_STATE, "sample_unweighted: single rank only");
+  if (mr(pf->ctx)) return set_err(GH_E_STATE, "sample_unweighted: single rank only");
   if (ns == 0) return GH_OK;
   const int64_t n = pf->n;
   CHECK(ensure_stats(pf));

@@ -426,8 +426,10 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
 // draws (Model::kPairs, KitModel): each lane steps the particle of its lane in
 // two consecutive 64-particle tiles, so one counter block and one Box–Muller
 // evaluation serve both; a 256-thread block covers 512 particles and writes
-// one partial.  Single rank, particle offset lo a multiple of 128 (the pair
-// mates are then in the same lane); values identical to k_step's.
+// one partial.  Particle offset lo a multiple of 128 (the pair mates are then
+// in the same lane); values identical to k_step's.  Multi-rank (mark_mode 2,
+// received rows, split steps) as k_step; a part-2 launch starts at a multiple
+// of 512 slots.
 __device__ __forceinline__ void block_partial2(double lw0, double lw1, double (*sm)[4], double* pm, double* ps,
                                                double* ps2) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -494,12 +496,23 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
       v1 = wave_incl_max_u64(v1 > cv1 ? v1 : cv1);
       s0 = (int64_t)(uint32_t)v0;
       s1 = (int64_t)(uint32_t)v1;
+      if (a.mark_mode == 2) {  // multi-rank: slots outside [ra, rb) take the received rows in slot order
+        const int64_t ra = a.dev->ra, rb = a.dev->rb, js0 = a.j0 + j0, js1 = a.j0 + j1;
+        if (js0 < ra) s0 = -1 - js0;
+        else if (js0 >= rb) s0 = -1 - (ra + (js0 - rb));
+        if (js1 < ra) s1 = -1 - js1;
+        else if (js1 >= rb) s1 = -1 - (ra + (js1 - rb));
+      }
       if (j0 < a.n) a.anc[j0] = (int32_t)s0;
       if (has1) a.anc[j1] = (int32_t)s1;
     }
     if (j0 < a.n) {
       const uint64_t g0 = (uint64_t)(a.lo + j0);
       double x0, x1, w0, w1;
+      // part 1 of a split multi-rank step: a slot that takes a received row is
+      // computed from a stand-in and not stored (part 2 steps it once the rows
+      // have landed; the pair's draws do not depend on the parent)
+      bool skip0 = false, skip1 = false;
       if (INIT) {
         Model::init2(p, o, a.seed, g0, &x0, &x1, &w0, &w1, dr_init);
       } else {
@@ -508,14 +521,26 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
           s1 = has1 ? a.anc[j1] : s0;
         }
         if (!has1) s1 = s0;
-        Model::step2(p, o, a.seed, g0, a.t, a.xprev[s0], a.xprev[s1], &x0, &x1, &w0, &w1, dr_step);
+        double xp0, xp1;
+        if (a.remote) {  // uniform (multi-rank): a negative ancestor is row -1 - s of the receive buffer
+          skip0 = a.part == 1 && s0 < 0;
+          skip1 = a.part == 1 && s1 < 0;
+          xp0 = s0 >= 0 ? a.xprev[s0] : (skip0 ? 0.0 : a.remote[(-1 - s0) * a.ld_remote]);
+          xp1 = s1 >= 0 ? a.xprev[s1] : (skip1 ? 0.0 : a.remote[(-1 - s1) * a.ld_remote]);
+        } else {
+          xp0 = a.xprev[s0];
+          xp1 = a.xprev[s1];
+        }
+        Model::step2(p, o, a.seed, g0, a.t, xp0, xp1, &x0, &x1, &w0, &w1, dr_step);
         w0 = (pend ? 0.0 : a.logw[j0]) + w0;
         if (has1) w1 = (pend ? 0.0 : a.logw[j1]) + w1;
       }
-      a.xout[j0] = x0;
-      a.logw[j0] = w0;
-      lw0 = w0;
-      if (has1) {
+      if (!skip0) {
+        a.xout[j0] = x0;
+        a.logw[j0] = w0;
+        lw0 = w0;
+      }
+      if (has1 && !skip1) {
         a.xout[j1] = x1;
         a.logw[j1] = w1;
         lw1 = w1;
@@ -1425,7 +1450,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       // polling traffic while lagging blocks still load their tiles (C4, 512
       // tiles: barrier 2.2 us sooner, 39.7 -> 37.8 us per step; C2 -0.9 us)
       uint64_t v = par, v1 = par, v2 = par;
-      bool ok = !mine;
+      bool ok = !mine, timed_out = false;  // (wave-uniform)
       for (unsigned spins = 0;; ++spins) {  // bounded (~0.5 s): a grid that is not co-resident errors out
         if (!ok) v = ld_sc1(&r.tsum[b]);
         ok = ok || (v & kTag) == par;
@@ -1433,11 +1458,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
         if (spins == (1u << 22)) {
           r.dev->error = 7;  // GH_E_STATE
           sfail = 1;
+          timed_out = true;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      ok = !mine || !sums;
+      ok = !mine || !sums || timed_out;  // (a timed-out wave does not wait a second time)
       for (unsigned spins = 0;; ++spins) {
         if (!ok) {
           v1 = ld_sc1(&r.ts1[b]);
@@ -1632,6 +1658,166 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
   }
 }
 
+// Multi-rank resample of the batched loop (gh_pf_run), phase A
+// with the weight sums in the quantisation pass: the step kernels wrote their
+// block maxima into kAmaxShards order-keyed atomic-max words per rank (no fold
+// launch), all-gathered.  Every block folds the R x kAmaxShards keys into the
+// global max M, quantises its tile against M, sums e = exp(w - M) and e^2 from
+// the same exps and publishes the tile total and sums (tagged, as
+// k_resample1).  Only block 0 needs the rank's totals: it alone polls the tile
+// words and writes the rank record (integer total, S_r, S2_r, M) that the
+// second all-gather carries; the other blocks leave after publishing.  The
+// decision is taken from the R records by k_rank_b (and by the host, the same
+// arithmetic, for the split of the next step).
+constexpr int kRecWords = 4;  // rank record: integer total, S_r, S2_r (f64 bits), M (f64 bits)
+struct RankA2Args {
+  const double* logw;
+  int64_t n;
+  int shift;
+  DevScalars* dev;
+  const uint64_t* amax_all;  // [R][kAmaxShards * kAmaxStride] all-gathered shard words
+  int R;
+  uint64_t* amax_reset;      // this rank's shards just consumed (read from the gathered copy): emptied
+  uint64_t* tsum;            // [grid] tile totals (bit 63: generation parity)
+  uint64_t* ts1;             // [grid] tile sums of e, e^2 (tagged bits)
+  uint64_t* ts2;
+  uint64_t* rec;             // [kRecWords] this rank's record (input of the second all-gather)
+};
+
+template <int IT>
+__global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_a2(RankA2Args r) {
+  __shared__ double smd[32];
+  __shared__ uint64_t smu[32];
+  __shared__ unsigned sgen;
+  __shared__ int sfail;
+  __shared__ uint64_t spa[8];
+  __shared__ double spg[2][8];
+  if (threadIdx.x == 0) {
+    sgen = r.dev->bar_gen + 1;
+    sfail = 0;
+  }
+  const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
+  double lw[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
+  // the global max from every rank's shards (the same keys, the same M in every block)
+  uint64_t key = kAmaxEmpty;
+  for (int idx = threadIdx.x; idx < r.R * kAmaxShards; idx += kRsBlock) {
+    const uint64_t v = r.amax_all[(idx / kAmaxShards) * (kAmaxShards * kAmaxStride) + (idx % kAmaxShards) * kAmaxStride];
+    key = v > key ? v : key;
+  }
+  const double M = blk16_max1(amax_value(key), smd);
+  if (blockIdx.x == 0 && threadIdx.x < kAmaxShards) r.amax_reset[threadIdx.x * kAmaxStride] = kAmaxEmpty;
+  const bool m_ok = M > -INFINITY && M != INFINITY && M == M;
+  if (!m_ok) {  // uniform over every rank's grid: no tile publishes; the decision raises GH_E_NUMERIC
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      r.rec[0] = 0;
+      r.rec[1] = 0;
+      r.rec[2] = 0;
+      r.rec[3] = as_u64(M);
+      r.dev->local = 0;
+    }
+    return;
+  }
+  const double qscale = as_f64((uint64_t)(r.shift + 1023) << 52);
+  uint64_t tsum = 0;
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const bool in = i0 + k < r.n;
+    const double e = in ? gh_exp_nonpos(lw[k] - M) : 0.0;
+    tsum += e == e ? f64_to_u52(e * qscale) : 0;  // = quantize_weight (k_rank_b re-quantises the same)
+    const double ee = lw[k] != lw[k] ? lw[k] : e;  // NaN poisons the statistics
+    s1 += ee;
+    s2 += ee * ee;
+  }
+  const uint64_t incl = blk16_scan<true>(tsum, &s1, &s2, smu, smd);
+  const uint64_t kTag = 1ull << 63;
+  const uint64_t par = (sgen & 1u) ? kTag : 0ull;
+  if (threadIdx.x == kRsBlock - 1) st_sc1(&r.tsum[blockIdx.x], incl | par);
+  if (threadIdx.x == 0) {
+    st_sc1(&r.ts1[blockIdx.x], (as_u64(s1) & ~kTag) | par);
+    st_sc1(&r.ts2[blockIdx.x], (as_u64(s2) & ~kTag) | par);
+  }
+  if (blockIdx.x != 0) return;
+  // block 0: the rank totals (waves 0..7 poll 64 tiles each, as k_resample1)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w < 8) {
+    const unsigned b = (unsigned)(w * 64 + lane);
+    const bool mine = b < gridDim.x;
+    uint64_t v = par, v1 = par, v2 = par;
+    bool ok = !mine, fail = false;
+    for (unsigned spins = 0;; ++spins) {  // bounded (~0.5 s): a grid that is not co-resident errors out
+      if (!ok) {
+        v = ld_sc1(&r.tsum[b]);
+        v1 = ld_sc1(&r.ts1[b]);
+        v2 = ld_sc1(&r.ts2[b]);
+      }
+      ok = ok || ((v & kTag) == par && (v1 & kTag) == par && (v2 & kTag) == par);
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+      if (spins == (1u << 22)) {
+        fail = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const uint64_t all = wave_sum_u64(mine ? (v & ~kTag) : 0ull);
+    const double g1 = wave_sum(mine ? as_f64(v1 & ~kTag) : 0.0);
+    const double g2 = wave_sum(mine ? as_f64(v2 & ~kTag) : 0.0);
+    if (lane == 0) {
+      spa[w] = all;
+      spg[0][w] = g1;
+      spg[1][w] = g2;
+      if (fail) sfail = 1;
+    }
+  }
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    uint64_t all = 0;
+    double g1 = 0.0, g2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      all += spa[k];
+      g1 += spg[0][k];
+      g2 += spg[1][k];
+    }
+    if (sfail) {
+      r.dev->error = 7;  // GH_E_STATE: partial totals
+      g1 = NAN;
+    }
+    r.rec[0] = all;
+    r.rec[1] = as_u64(g1);
+    r.rec[2] = as_u64(g2);
+    r.rec[3] = as_u64(M);
+    r.dev->local = all;
+    r.dev->bar_gen = sgen;  // every block has published, so has read the old value
+  }
+}
+
+// The decision of a multi-rank resample from the R rank records (rank order):
+// the sums share the global max, so S = sum S_r, S2 = sum S2_r; host and
+// device evaluate the same arithmetic (finish_plan needs the fire flag before
+// the device has taken it).
+GH_HD Decision decide_records(const uint64_t* recs, int R, double thr) {
+  Decision d{};
+  const double M = as_f64(recs[3]);
+  double S = 0.0, S2 = 0.0;
+  for (int q = 0; q < R; ++q) {
+    S += as_f64(recs[kRecWords * q + 1]);
+    S2 += as_f64(recs[kRecWords * q + 2]);
+  }
+  d.M = M;
+  if (!(M > -INFINITY) || M == INFINITY || M != M) {
+    d.err = 3;  // GH_E_NUMERIC
+    d.ess = NAN;
+    return d;
+  }
+  d.L = M + gh_log(S);
+  d.ess = (S * S) / S2;
+  d.fire = d.ess < thr;
+  return d;
+}
+
 // Phase B (after the all-gather): every block derives the global systematic
 // constants and the slot coverage of every rank from the totals (the same
 // integers on every rank), re-quantises its tile, and for each particle's
@@ -1646,7 +1832,10 @@ struct RankBArgs {
   int shift;
   DevScalars* dev;
   const uint64_t* tsum;   // tile totals of phase A (tagged)
-  const uint64_t* totals; // [R] all-gathered rank totals
+  const uint64_t* totals; // all-gathered rank totals, rank k's at totals[k * tot_stride]
+  int tot_stride;         // 1: k_rank_a's totals; kRecWords: k_rank_a2's records
+  const uint64_t* recs;   // k_rank_a2's records: this launch takes (and block 0 commits) the decision
+  DecideArgs d;           //   (with recs) the decision's threshold and histories
   int R, rank;
   int64_t lo;             // global id of this rank's first particle
   uint64_t seed;
@@ -1705,7 +1894,24 @@ __device__ __forceinline__ void send_rows(int64_t s0, int64_t s1, int64_t i, int
 
 template <int IT>
 __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
-  if (!r.dev->fire) return;
+  __shared__ int sfire;
+  __shared__ double sMq;
+  if (threadIdx.x == 0) {
+    if (r.recs) {  // the decision from the R rank records (every block the same)
+      const Decision dec = decide_records(r.recs, r.R, r.d.thr);
+      sfire = dec.fire;
+      sMq = dec.M;
+      if (blockIdx.x == 0) {
+        r.dev->pending = 0;
+        commit_decision(r.d, dec, r.dev, 0);
+      }
+    } else {  // k_rank_a decided
+      sfire = r.dev->fire;
+      sMq = r.dev->M;
+    }
+  }
+  __syncthreads();
+  if (!sfire) return;
   __shared__ uint64_t smu[16];
   __shared__ DevScalars sd;
   __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
@@ -1722,12 +1928,12 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   if (threadIdx.x == 0) {
     uint64_t S = 0, base = 0;
     for (int k = 0; k < R; ++k) {
-      if (k < q) base += r.totals[k];
-      S += r.totals[k];
+      if (k < q) base += r.totals[k * r.tot_stride];
+      S += r.totals[k * r.tot_stride];
     }
     sd.S = S;
     sd.base = base;
-    sd.local = r.totals[q];
+    sd.local = r.totals[q * r.tot_stride];
     const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
     sd.o = scale_u53(u53_bits(w.x, w.y), S);
     sd.invN = 1.0 / (double)N;
@@ -1759,7 +1965,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     }
   }
   __syncthreads();
-  const double M = r.dev->M;
+  const double M = sMq;
   const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
   uint64_t qv[IT];
   uint64_t tsum = 0;
@@ -1817,7 +2023,8 @@ struct RowsFillArgs {
   int R, rank;
   int64_t lo;
   const DevScalars* dev;
-  const uint64_t* totals;
+  const uint64_t* totals;  // rank k's total at totals[k * tot_stride] (as RankBArgs)
+  int tot_stride;
   int64_t n_global;
   const double* xprev;
   int D;
@@ -1832,7 +2039,7 @@ static __global__ __launch_bounds__(256) void k_rows_fill(RowsFillArgs r) {
   if (threadIdx.x == 0) {
     sd = *r.dev;
     int64_t a, b;
-    send_tables(&sd, N, r.R, r.rank, r.totals[r.rank], sdst_lo, sseg_lo, ssoff, &a, &b);
+    send_tables(&sd, N, r.R, r.rank, r.totals[r.rank * r.tot_stride], sdst_lo, sseg_lo, ssoff, &a, &b);
   }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;

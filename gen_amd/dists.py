@@ -92,11 +92,17 @@ class Distribution:
         _lib.check(_lib.load().gh_dist_logpdf(ctx.h, byref(d), n, _lib.dptr(xv), _lib.dptr(out)))
         return float(out[0]) if scalar else out
 
-    def random(self, *args, n: int | None = None, seed: int = 0, ctx=None):
-        """n draws (one draw, as a scalar / vector, when n is None)."""
+    def random(self, *args, n: int | None = None, seed: int | None = None, ctx=None):
+        """n draws (one draw, as a scalar / vector, when n is None).  Without a
+        seed every call draws fresh randomness, as Gen's random(dist, args...)
+        does from Julia's global RNG (the seeds come from a host generator,
+        reseedable with gen_amd.dists.seed); an explicit seed gives a
+        reproducible batch: draw i is a function of (seed, i) alone."""
         from .pf import default_context
 
         ctx = ctx or default_context()
+        if seed is None:
+            seed = _fresh_seed()
         nn = 1 if n is None else int(n)
         rows, np_, per_value, dim = self._rows(args, nn)
         out = np.empty((dim, nn)) if dim > 1 else np.empty(nn)
@@ -106,8 +112,22 @@ class Distribution:
             return out[:, 0].copy() if dim > 1 else float(out[0])
         return out
 
-    def __call__(self, *args, seed: int = 0):
+    def __call__(self, *args, seed: int | None = None):
         return self.random(*args, seed=seed)
+
+
+_seed_rng = np.random.default_rng()
+
+
+def seed(s: int | None) -> None:
+    """Reseed the host generator behind unseeded draws (Random.seed! for
+    random(dist, args...) calls without a seed); None: fresh OS entropy."""
+    global _seed_rng
+    _seed_rng = np.random.default_rng(s)
+
+
+def _fresh_seed() -> int:
+    return int(_seed_rng.integers(0, 1 << 63))
 
 
 def _vdim(args):
@@ -145,6 +165,6 @@ def logpdf(dist: Distribution, x, *args, ctx=None):
     return dist.logpdf(x, *args, ctx=ctx)
 
 
-def random(dist: Distribution, *args, n: int | None = None, seed: int = 0, ctx=None):
+def random(dist: Distribution, *args, n: int | None = None, seed: int | None = None, ctx=None):
     """Gen.random(dist, args...)"""
     return dist.random(*args, n=n, seed=seed, ctx=ctx)

@@ -68,10 +68,13 @@ class Context:
     """One GPU (and, for multi-GPU, one rank of an RCCL communicator)."""
 
     def __init__(self, device: int | None = None, rank: int = 0, world: int = 1, unique_id: bytes | None = None,
-                 transport=None):
+                 transport=None, force_multirank: bool = False):
         """`unique_id`: RCCL communicator id (Context.unique_id() on rank 0,
         broadcast to the others).  `transport`: a host-staged transport
-        (gen_amd.transport.GlooTransport) used instead of RCCL."""
+        (gen_amd.transport.GlooTransport) used instead of RCCL.
+        `force_multirank`: filters take the multi-rank path even at world 1
+        (a one-rank RCCL communicator; gh_ctx_force_multirank, for tests and
+        timing on one GPU)."""
         lib = _lib.load()
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
@@ -91,6 +94,8 @@ class Context:
         self.h = h
         self.rank, self.world = rank, world
         self._models = {}
+        if force_multirank:
+            _lib.check(lib.gh_ctx_force_multirank(h))
 
     @staticmethod
     def unique_id() -> bytes:
@@ -182,6 +187,7 @@ class ParticleFilterState:
     def __init__(self, ctx: Context, model: Model, handle, num_particles: int):
         self.ctx, self.model, self.h = ctx, model, handle
         self.num_particles = num_particles
+        self.moves = 0  # MH moves applied (trace views drop their cached columns when it changes)
         ng, nl, lo = c_int64(), c_int64(), c_int64()
         _lib.check(_lib.load().gh_pf_num_particles(handle, byref(ng), byref(nl), byref(lo)))
         self.n_local, self.first = nl.value, lo.value
@@ -252,6 +258,13 @@ class ParticleTraces:
     def __init__(self, state: ParticleFilterState):
         self.state = state
         self._cache = {}
+        self._moves = state.moves
+
+    def _fresh(self):
+        # an MH move rewrote the current step's latents in place: cached columns are stale
+        if self._moves != self.state.moves:
+            self._cache.clear()
+            self._moves = self.state.moves
 
     def __len__(self):
         return self.state.n_local
@@ -274,6 +287,7 @@ class ParticleTraces:
         t, kind = self._step_of(tuple(addr))
         if kind == "obs":
             raise KeyError(f"{addr} is an observation; it is constrained to the same value in every trace")
+        self._fresh()
         if t not in self._cache:
             self._cache[t] = self.state.states(t)
         col = self._cache[t]
@@ -284,6 +298,7 @@ class ParticleTraces:
 
     def step_states(self, t: int) -> np.ndarray:
         """[n_local, d] latents of step t along every particle's genealogy (cached)."""
+        self._fresh()
         if t not in self._cache:
             self._cache[t] = self.state.states(t)
         return self._cache[t]
@@ -294,6 +309,7 @@ class ParticleTraces:
         per_step the [t, 2, n_local] scores of each step's latent and
         observation choices."""
         key = "_scores_ps" if per_step else "_scores"
+        self._fresh()
         if key not in self._cache:
             st = self.state
             tot = np.empty(st.n_local)
@@ -498,6 +514,10 @@ def run_particle_filter(state: ParticleFilterState, observations_per_step, ess_t
     proposal_args, or the last ones given."""
     model = state.model
     if isinstance(observations_per_step, ObservationBatch):
+        if proposal_args is not None:
+            raise ValueError("run_particle_filter: proposal_args with a prepared ObservationBatch; pass the "
+                             "observations as a list (its first step takes the arguments) or set them with a "
+                             "particle_filter_step first")
         batch = observations_per_step
     else:
         if proposal_args is not None and len(observations_per_step) > 0:
@@ -548,6 +568,7 @@ def rejuvenate(state: ParticleFilterState, n_moves: int = 1) -> int:
     summed over this rank's particles."""
     acc = c_int64()
     _lib.check(_lib.load().gh_pf_rejuvenate(state.h, int(n_moves), byref(acc)))
+    state.moves += 1
     return int(acc.value)
 
 
@@ -610,11 +631,13 @@ def metropolis_hastings(state: ParticleFilterState, selection, *args, n_moves: i
         sd = np.ascontiguousarray(np.broadcast_to(np.asarray(pargs[1], dtype=np.float64), (d,)))
         acc = c_int64()
         _lib.check(_lib.load().gh_pf_mh_drift(state.h, mask, _lib.dptr(sd), int(n), byref(acc)))
+        state.moves += 1
         return int(acc.value)
     n = n_moves if n_moves is not None else (int(args[0]) if args else 1)
     mask = _latent_mask(state, selection)
     acc = c_int64()
     _lib.check(_lib.load().gh_pf_mh_select(state.h, mask, int(n), byref(acc)))
+    state.moves += 1
     return int(acc.value)
 
 

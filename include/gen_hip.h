@@ -162,6 +162,12 @@ typedef struct {
 int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_host_comm* comm, void* hip_stream,
                            gh_ctx** out);
 int gh_ctx_destroy(gh_ctx* ctx);
+/* Debug / timing: filters created on this context afterwards take the
+   multi-rank code path (collectives, split step after a resample, k_rank_a/b)
+   even at world 1 — over a one-rank RCCL communicator for a gh_ctx_create /
+   gh_ctx_create_dist context, over the user's functions for a host-comm one.
+   Results are the same filter's (bit-exact against the one-rank path). */
+int gh_ctx_force_multirank(gh_ctx* ctx);
 int gh_ctx_rank(const gh_ctx* ctx, int* rank, int* world);
 int gh_ctx_stream(const gh_ctx* ctx, void** hip_stream);
 int gh_ctx_synchronize(gh_ctx* ctx);

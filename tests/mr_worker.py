@@ -36,7 +36,10 @@ def main():
     p.add_argument("--T", type=int, default=8)
     p.add_argument("--thr", type=float, default=None, help="ESS threshold (default: N/2)")
     p.add_argument("--seed", type=int, default=9)
-    p.add_argument("--transport", default="gloo")
+    p.add_argument("--transport", default="gloo", help="gloo (host-staged), rccl, or rccl1: one rank forced onto "
+                   "the multi-rank path over a one-rank RCCL communicator (gh_ctx_force_multirank)")
+    p.add_argument("--batched", action="store_true", help="steps 2..T through run_particle_filter (gh_pf_run: "
+                   "max-only steps, the resample's sums in k_rank_a2)")
     p.add_argument("--rejuv", type=int, default=0, help="rejuvenation moves after init and every step")
     p.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK)")
     p.add_argument("--out", required=True)
@@ -52,6 +55,9 @@ def main():
     if a.transport == "gloo":
         tr = GlooTransport()
         ctx = gen.Context(device=0, transport=tr)
+    elif a.transport == "rccl1":
+        assert world == 1
+        ctx = gen.Context(device=a.device or 0, force_multirank=True)
     else:
         uid = [gen.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -65,7 +71,9 @@ def main():
     if a.rejuv:
         gen.rejuvenate(st, a.rejuv)
     did = []
-    for t in range(2, a.T + 1):
+    if a.batched:
+        gen.run_particle_filter(st, list(ys[1 : a.T]), a.thr)
+    for t in range(2, a.T + 1) if not a.batched else ():
         did.append(gen.maybe_resample(st, a.thr))
         gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})
         if a.rejuv:

@@ -139,6 +139,9 @@ def test_gpu_drift_ssm_bitexact(gh_ctx, name):
     n, seed = 4099, 13
     st, pf = _filters(m, ys, n, seed, 4)
     sd = 0.3 if name == "lg4" else 1.0
+    tr = gen.get_traces(st)
+    before = tr.step_states(4).copy()
+    score_before = tr.scores().copy()
     acc = gen.mh(st, gen.gaussian_drift, (gen.select(m.latent_address(4)), sd), n_moves=5)
     acc2 = gen.mh(st, gen.select(m.latent_address(4)), 2)  # then selection moves: fresh draw windows
     oacc = pf.mh_drift(1, np.full(m.d if name == "lg4" else 1, sd), 5)
@@ -147,6 +150,10 @@ def test_gpu_drift_ssm_bitexact(gh_ctx, name):
     assert np.array_equal(st.states().T.view(np.uint64), pf.state().view(np.uint64))
     # the moved particles keep their weights
     assert np.array_equal(gen.get_log_weights(st).view(np.uint64), pf.log_weights().view(np.uint64))
+    # a traces view taken before the moves reads the moved latents and scores
+    assert np.array_equal(tr.step_states(4).T.view(np.uint64), pf.state().view(np.uint64))
+    assert not np.array_equal(tr.step_states(4), before)
+    assert not np.array_equal(tr.scores(), score_before)
 
 
 @pytest.mark.gpu

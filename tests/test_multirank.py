@@ -305,3 +305,56 @@ def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr
     lml = float(parts[0]["lml"])
     assert all(float(p["lml"]) == lml for p in parts)
     assert abs(lml - ref.log_ml_estimate()) <= 1e-9 * abs(ref.log_ml_estimate())
+
+
+def _check_against_oracle(out, model, R, n, T, seed, thr):
+    from oracle import oracle as O
+    from tests.mr_worker import build_model
+
+    m = build_model(model)
+    _, ys = m.simulate(T, np.random.default_rng(5))
+    ref = O.run_pf(m, ys, n, seed, thr=thr)
+    parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
+    states = np.concatenate([p["states"] for p in parts], axis=0)  # [n, d]
+    assert np.array_equal(states.T, ref.state())
+    assert np.array_equal(np.concatenate([p["logw"] for p in parts]), ref.log_weights())
+    assert np.array_equal(np.concatenate([p["parents"] for p in parts]), ref.parents())
+    lml = float(parts[0]["lml"])
+    assert all(float(p["lml"]) == lml for p in parts)
+    assert abs(lml - ref.log_ml_estimate()) <= 1e-9 * abs(ref.log_ml_estimate())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,R,thr,n", [("lg4", 2, None, 3001), ("lg4", 3, 1e9, 20011), ("kit", 2, None, 4096),
+                                            ("kit", 4, 1e9, 8192), ("kit_sharp", 4, None, 4003),
+                                            ("lg10", 2, 3001.0, 3001)])
+def test_gpu_multirank_batched_host_transport(tmp_path, model, R, thr, n):
+    """The batched loop on R ranks (gh_pf_run: max-only steps whose maxima go to
+    the atomic-max shards, the shards' all-gather, k_rank_a2's quantisation +
+    sums, the records' all-gather, k_rank_b's decision; the Kitagawa ranks
+    whose first particle is a multiple of 128 step with the pair kernel, split
+    around the row exchange) equals the single-rank oracle bit for bit."""
+    out = str(tmp_path / "b")
+    T, seed = 8, 9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--batched", "--out", out], R,
+                 timeout=400)
+    _check_against_oracle(out, model, R, n, T, seed, thr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,thr,n,batched", [("lg4", None, 20011, False), ("lg4", None, 20011, True),
+                                                  ("lg10", 1e9, 9000, True), ("kit", None, 8192, True),
+                                                  ("kit", 1e9, 8192, False), ("kit_sharp", None, 4003, True)])
+def test_gpu_multirank_path_over_rccl_one_rank(tmp_path, model, thr, n, batched):
+    """gh_ctx_force_multirank: one rank on the multi-rank code path over a
+    one-rank RCCL communicator (ncclAllGather of the triples / shards / records,
+    k_rank_a or k_rank_a2, k_rank_b, the split step) equals the single-rank
+    oracle bit for bit.  (A one-rank exchange sends no rows: the grouped
+    send/recv is exercised by the 2..4-rank host-transport tests.)"""
+    out = str(tmp_path / "r")
+    T, seed = 8, 9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--transport", "rccl1",
+                  "--device", "0", *(["--batched"] if batched else []), "--out", out], 1, timeout=300)
+    _check_against_oracle(out, model, 1, n, T, seed, thr)
