@@ -20,13 +20,15 @@ Also reported:
                traffic = PMC HBM bytes per launch from profiles/ when present;
                step_frac = the same bytes per whole step / ms_per_step / peak.
   cpu_baseline the CPU oracle (C restatement of Gen's PF) on a bounded sample
-               of the same workload, timed on this host on every core
-               (OpenMP build) with the one-core figure beside it (median of
-               5 repetitions each, CPU model and thread count stated); its
-               "parity" entry runs the GPU filter and the oracle on the same
-               observations, seed and 2^16 particles and reports the log-ML
-               relative difference (north star: <= 1e-6) and whether the final
-               ancestors agree bit for bit.
+               of the same workload, timed on this host with the OpenMP build
+               on the CPU share the GPU box gives this job (OMP_NUM_THREADS;
+               the host's CPU count, affinity and cgroup quota are recorded
+               beside it) and on one core (median of 5 repetitions each); its
+               "parity" entry runs the GPU filter and the oracle on the
+               headline configuration itself — the same observations (every
+               step of the run), seed and 2^20 particles — and reports the
+               log-ML relative difference (north star: <= 1e-6) and whether
+               the final states and ancestors agree bit for bit.
   secondary    (one GPU, rank 0) the other GPU configurations of BASELINE.json
                measured in the same run, each with its own CPU baseline:
                C4 the nonlinear SSM at 2^21 particles per GPU (the 8-GPU
@@ -88,7 +90,14 @@ def host_info():
     except OSError:
         pass
     aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff}
+    quota = None
+    try:  # cgroup v2 CPU bandwidth: "max 100000" or "<quota> <period>"
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
 
 
 def median_rate(fn, reps=5):
@@ -101,8 +110,9 @@ def median_rate(fn, reps=5):
 
 
 def cpu_pair(make_sample, unit, sample_desc, reps=5):
-    """The oracle on every host core (OpenMP build) and on one core, median of
-    `reps` repetitions each: the all-cores value is the reported baseline."""
+    """The oracle on the job's CPU share (OpenMP build, omp_get_max_threads()
+    threads) and on one core, median of `reps` repetitions each: the OpenMP
+    value is the reported baseline, `cores` the threads it used."""
     from oracle import oracle as O
 
     out = {}
@@ -112,16 +122,23 @@ def cpu_pair(make_sample, unit, sample_desc, reps=5):
         med, rates = median_rate(make_sample(threads), reps)
         out[omp] = {"value": med, "cores": threads, "repetitions": [round(r, 1) for r in rates]}
     O.set_openmp(False)
+    host = host_info()
+    cores = out[True]["cores"]
+    why = None
+    if cores != host["affinity_cpus"]:
+        why = (f"{cores} threads = OMP_NUM_THREADS={host['OMP_NUM_THREADS']} set by the GPU box: this job's CPU "
+               f"share of a host whose {host['affinity_cpus']} CPUs serve every GPU of the machine")
     return {
         "value": out[True]["value"],
         "unit": unit,
-        "cores": out[True]["cores"],
+        "cores": cores,
+        "cores_note": why,
         "kind": "port",
         "sample": sample_desc + " (oracle/gh_oracle.c, the C restatement of Gen's algorithm — not Gen.jl: no "
-                                "Julia on the box; OpenMP build, median of 5)",
+                                f"Julia on the box; OpenMP build on {cores} threads, median of 5)",
         "single_core": {"value": out[False]["value"], "cores": 1, "repetitions": out[False]["repetitions"]},
         "repetitions": out[True]["repetitions"],
-        "host": host_info(),
+        "host": host,
     }
 
 
@@ -151,10 +168,11 @@ def pf_cpu_baseline(model, ys, budget_s):
 
 
 def cpu_parity(model, ys, n, resampler, proposal):
-    """The GPU filter and the CPU restatement of Gen's filter (oracle/) on the
-    same workload, seed and N = n over every observation of the run: their
-    log-ML estimates (the north star's "within 1e-6 relative on fixed RNG
-    seeds") and whether the final ancestors agree bit for bit."""
+    """The GPU filter and the CPU restatement of Gen's filter (oracle/, the
+    OpenMP build: identical results on any thread count) on the same
+    workload, seed and N = n over every observation of the run: their log-ML
+    estimates (the north star's "within 1e-6 relative on fixed RNG seeds")
+    and whether the final states and ancestors agree bit for bit."""
     import gen_amd as gen
     from oracle import oracle as O
 
@@ -164,12 +182,19 @@ def cpu_parity(model, ys, n, resampler, proposal):
     gen.run_particle_filter(st, list(ys[1:]), None, proposal=prop)
     gpu = gen.log_ml_estimate(st)
     gpu_parents = st.parents
+    gpu_states = st.states()
     st.close()
+    O.set_openmp(True)
+    t0 = time.perf_counter()
     orc = O.run_pf(model, ys, n, 42, resampler=O.SYSTEMATIC if resampler == "systematic" else O.MULTINOMIAL,
                    proposal=O.OPTIMAL if prop is not None else O.DEFAULT, record_history=False)
+    cpu_s = time.perf_counter() - t0
+    O.set_openmp(False)
     cpu = orc.log_ml_estimate()
     return {"particles": n, "steps": len(ys), "seed": 42, "log_ml_gpu": gpu, "log_ml_cpu": cpu,
-            "rel": abs(gpu - cpu) / abs(cpu), "parents_bitexact": bool((gpu_parents == orc.parents()).all())}
+            "rel": abs(gpu - cpu) / abs(cpu), "parents_bitexact": bool((gpu_parents == orc.parents()).all()),
+            "states_bitexact": bool(np.array_equal(gpu_states.T.view(np.uint64), orc.state().view(np.uint64))),
+            "cpu_seconds": round(cpu_s, 2)}
 
 
 def pmc_profile(name):
@@ -269,6 +294,29 @@ def secondary_c4(gen, ctx, a):
     }
     if not a.no_cpu_baseline:
         out["cpu_baseline"] = pf_cpu_baseline(model, r["ys"], a.cpu_seconds)
+    return out
+
+
+def secondary_multirank_path(gen, a, c2_ms, c4_ms):
+    """The multi-rank code path timed on this one GPU (gh_ctx_force_multirank:
+    a one-rank RCCL communicator): per step the shards' and the records'
+    ncclAllGather, k_rank_a2, k_rank_b and the split step, against the one-rank
+    path's ms_per_step measured above (DESIGN.md §7 projects the 8-GPU step
+    from the difference)."""
+    ctx = gen.Context(device=0, force_multirank=True)
+    out = {}
+    try:
+        for name, model, n, d, base in (("C2", gen.LinearGaussianSSM.benchmark(a.d), a.particles, a.d, c2_ms),
+                                        ("C4", gen.KitagawaSSM(10.0, 1.0), 1 << 21, 1, c4_ms)):
+            r = pf_run(gen, ctx, None, 1, a, model, n, "", lambda n_res, d=d: 16 * d + 16)
+            ms = r["dt"] * 1e3 / a.steps
+            out[name] = {"ms_per_step": ms, "one_rank_ms_per_step": base,
+                         "extra_us_per_step": None if base is None else round((ms - base) * 1e3, 2),
+                         "resample_steps_timed": r["n_res"], "log_ml": r["lml"]}
+    finally:
+        ctx.close()
+    out["note"] = ("world = 1 on the multi-rank path over RCCL: the collectives are one-rank copies and no rows "
+                   "move, so the extra time is the path's launches, host plan and all-gather kernels, not xGMI")
     return out
 
 
@@ -397,7 +445,8 @@ def main(argv=None):
     else:
         model = gen.KitagawaSSM(10.0, 1.0)  # examples/pmmh/run.jl:69 (var_x = 10, var_y = 1)
         d = 1
-        kname = "k_step_pairs<KitModel,false>" if world == 1 else "k_step<KitModel,false>"
+        # (the pair kernel on every rank whose first particle is a multiple of 128)
+        kname = "k_step_pairs<KitModel,false>" if a.particles % 128 == 0 else "k_step<KitModel,false>"
     r = pf_run(gen, ctx, dist, world, a, model, a.particles, kname,
                lambda n_res: 16 * d + 16 + 4.0 * n_res / max(1, a.steps))
     # PMC HBM bytes per step-kernel launch of the profiled configs (tools/pmc_json.py)
@@ -449,14 +498,18 @@ def main(argv=None):
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = pf_cpu_baseline(model, ys, a.cpu_seconds)
-        # same seed, same observations, N = 2^16: GPU vs the CPU restatement
-        par = cpu_parity(model, ys, 1 << 16, a.resampler, a.proposal)
+        # the headline configuration itself (N = the bench's particles, every
+        # step of the run, same seed and observations): GPU vs the CPU restatement
+        par = cpu_parity(model, ys, a.particles, a.resampler, a.proposal)
         out["cpu_baseline"]["parity"] = par
         if out["log_ml_error"] is not None:
             out["log_ml_error"]["vs_cpu_reference_same_seed"] = {"particles": par["particles"], "rel": par["rel"]}
     if rank == 0 and world == 1 and not a.no_secondary and a.model == "lgssm":
-        out["secondary"] = {"C4": secondary_c4(gen, ctx, a), "C3": secondary_c3(gen, ctx, a),
-                            "C5": secondary_c5(gen, ctx, a)}
+        c4 = secondary_c4(gen, ctx, a)
+        out["secondary"] = {"C4": c4, "C3": secondary_c3(gen, ctx, a), "C5": secondary_c5(gen, ctx, a)}
+        if a.proposal == "default" and a.transport == "rccl":
+            out["secondary"]["multirank_path"] = secondary_multirank_path(gen, a, out["ms_per_step"],
+                                                                          c4["ms_per_step"])
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

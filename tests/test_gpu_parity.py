@@ -333,6 +333,34 @@ def test_lgssm_full_size_first_steps_bitexact(gh_ctx):
     assert_lml_close(st, orc)
 
 
+def test_headline_config_every_step_bitexact(gh_ctx):
+    """The headline configuration itself (BASELINE.json configs[1], the bench's
+    C2 workload): d = 10, 2^20 particles, systematic resampling at ESS < N/2,
+    26 steps of the batched loop as bench.py drives it (max-only steps, the
+    fused resample) from the bench's own observations (numpy seed 2) and
+    seed 42.  Final states, log-weights and parents bit-exact against the CPU
+    restatement (its OpenMP build: the same bits on any thread count), log-ML
+    within 1e-9 (the north star asks 1e-6).  Reference loop:
+    src/inference/particle_filter.jl:162-213."""
+    m = gen.LinearGaussianSSM.benchmark(10)
+    n, T = 1 << 20, 27
+    _, ys = m.simulate(T, np.random.default_rng(2))
+    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=42, history_capacity=T + 2)
+    gen.run_particle_filter(st, list(ys[1:]))
+    O.set_openmp(True)
+    try:
+        orc = O.run_pf(m, ys, n, 42, record_history=False)
+    finally:
+        O.set_openmp(False)
+    ess, did = st.ess_history()
+    assert did.sum() >= 5  # resampling fires on many of the steps
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.parents, orc.parents())
+    assert_lml_close(st, orc)
+    st.close()
+
+
 @pytest.mark.parametrize("n", [1_500_007, 4_200_001])
 def test_kitagawa_large_tiles_bitexact(gh_ctx, n):
     """Past 2^20 particles the one-launch resample kernel takes 8 / 16
