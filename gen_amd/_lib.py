@@ -122,6 +122,7 @@ SIGNATURES = {
     "gh_coal_set_kernel": (c_int, [c_void_p, c_int]),
     "gh_coal_step": (c_int, [c_void_p, c_int, POINTER(c_int32), POINTER(c_int32), POINTER(c_double)]),
     "gh_coal_read_state": (c_int, [c_void_p, POINTER(c_double)]),
+    "gh_coal_write_state": (c_int, [c_void_p, POINTER(c_double), c_int]),
     "gh_coal_destroy": (c_int, [c_void_p]),
     "gh_is_run": (c_int, [c_void_p, POINTER(Obs), c_int, c_int64, c_uint64, POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
     "gh_last_error": (c_char_p, []),

@@ -68,6 +68,14 @@ class CoalChains:
             self._state = st
         return self._state
 
+    def load_state(self, state, iterations: int = 0):
+        """Resume from [n_chains][68] rows (gh_coal_write_state); the next run
+        continues at iteration `iterations` + 1."""
+        st = np.ascontiguousarray(np.asarray(state, dtype=np.float64).reshape(self.n_chains, STATE_W))
+        _lib.check(_lib.load().gh_coal_write_state(self.h, _lib.dptr(st), int(iterations)))
+        self.iterations = int(iterations)
+        self._state = None
+
     def close(self):
         if self.h:
             _lib.load().gh_coal_destroy(self.h)

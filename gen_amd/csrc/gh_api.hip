@@ -3094,6 +3094,41 @@ extern "C" int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* 
   return rc;
 }
 
+// resume the chains from given rows (a checkpoint, or states the prior rarely
+// visits): the next gh_coal_step continues at iteration iter0 + 1
+extern "C" int gh_coal_write_state(gh_coal* h, const double* state, int iter0) {
+  if (!h || !state || iter0 < 0) return set_err(GH_E_INVAL, "gh_coal_write_state: bad argument");
+  const size_t nc = (size_t)h->n;
+  for (size_t c = 0; c < nc; ++c) {  // rows must keep the layout k_coal relies on
+    const double* r = state + c * kCoalW;
+    const double kd = r[0];
+    if (!(kd >= 0.0 && kd <= (double)kCoalKMax) || kd != (double)(int)kd)
+      return set_err(GH_E_INVAL, "gh_coal_write_state: chain %zu has k = %g (0..%d)", c, kd, kCoalKMax);
+    const int k = (int)kd;
+    for (int i = k; i < kCoalKMax; ++i)
+      if (r[2 + i] != 0.0) return set_err(GH_E_INVAL, "gh_coal_write_state: chain %zu: change point %d past k is not 0", c, i + 1);
+    for (int i = k + 1; i <= kCoalKMax; ++i)
+      if (r[2 + kCoalKMax + i] != 0.0) return set_err(GH_E_INVAL, "gh_coal_write_state: chain %zu: rate %d past k+1 is not 0", c, i + 1);
+  }
+  HIP_TRY(hipSetDevice(h->ctx->device));
+  double* rows = nullptr;
+  if (hipMalloc(&rows, sizeof(double) * kCoalW * nc) != hipSuccess)
+    return set_err(GH_E_NOMEM, "gh_coal_write_state: row buffer");
+  int rc = GH_OK;
+  if (hipMemcpyAsync(rows, state, sizeof(double) * kCoalW * nc, hipMemcpyHostToDevice, h->ctx->stream) != hipSuccess)
+    rc = set_err(GH_E_HIP, "gh_coal_write_state: upload");
+  if (!rc)
+    hipLaunchKernelGGL(k_coal_rows, dim3((unsigned)((nc * kCoalW + 255) / 256)), dim3(256), 0, h->ctx->stream, h->st,
+                       h->n, rows, h->n, 1);
+  if (!rc && hipStreamSynchronize(h->ctx->stream) != hipSuccess) rc = set_err(GH_E_HIP, "gh_coal_write_state: sync");
+  hipFree(rows);
+  if (!rc) {
+    h->iters = iter0;
+    h->started = true;
+  }
+  return rc;
+}
+
 extern "C" int gh_coal_read_state(gh_coal* h, double* state) {
   if (!h || !state) return set_err(GH_E_INVAL, "gh_coal_read_state: null argument");
   HIP_TRY(hipSetDevice(h->ctx->device));

@@ -24,10 +24,15 @@
 // segment i, a position move segments i and i+1, a birth / death the segment
 // split or merged — no copy of the state, no full re-score.
 //
-// One thread per chain; a chain's change points and rates live in LDS for the
-// whole launch ([field][lane] per wave: conflict-free for any per-lane
-// index), k and the score in registers; HBM is read once and written once per
-// launch.  Event counts come from the sorted event times in LDS through a
+// One thread per chain; a window of a chain's change points and rates (cp
+// 1..kCoalWin, h 1..kCoalWin+1) lives in LDS for the whole launch
+// ([field][lane] per wave: conflict-free for any per-lane index), k and the
+// score in registers; the fields past the window (a chain with more than
+// kCoalWin change points: the posterior puts < 0.1 % of its mass there) are
+// read and written in place in the chain's HBM row.  The window keeps a
+// chain's LDS at 31 fields instead of 65, so twice the waves fit a CU (the
+// kernel waits on dependent LDS reads; more resident waves hide them).  HBM:
+// the window read once and written once per launch.  Event counts come from the sorted event times in LDS through a
 // bucket table (start index) and a short scan.  The oracle
 // (oracle/gh_oracle.c, orc_coal_run) restates the same arithmetic.
 #pragma once
@@ -39,7 +44,12 @@ constexpr int kCoalKMax = 32;
 constexpr int kCoalW = 2 + kCoalKMax + (kCoalKMax + 1) + 1;  // 68: k, score, cp[32], h[33], pad
 constexpr int kCoalF = kCoalKMax + (kCoalKMax + 1);          // 65 LDS fields per chain: cp[32], h[33]
 constexpr int kCoalMaxEvents = 4096;
-constexpr int kCoalBlock = 128;                              // two waves: 2 blocks (66.5 KB state each) per CU
+#ifndef GH_COAL_WIN
+#define GH_COAL_WIN 15
+#endif
+constexpr int kCoalWin = GH_COAL_WIN;                        // change points in LDS (rates: kCoalWin + 1)
+constexpr int kCoalLF = 2 * kCoalWin + 1;                    // LDS fields per chain
+constexpr int kCoalBlock = 128;                              // two waves: 4 blocks (31.8 KB window each + tables) per CU
 constexpr int kCoalBuckets = 256;                            // event-count start table
 constexpr double kCoalRate = 200.0;                          // gamma(1, 1/200) rate prior: 1 / theta (coal.jl:56-58)
 
@@ -85,11 +95,39 @@ __device__ __forceinline__ int coal_count(const double* ev, const int32_t* bk, i
   return j;
 }
 
-// one chain's LDS fields: cp[i - 1] at f(i - 1), h[i - 1] at f(kCoalKMax + i - 1)
+// one chain's fields: cp[i] (i = 1..k) and h[i] (i = 1..k+1) in the LDS window
+// (cp at f = i - 1, h at f = kCoalWin + i - 1), past it in the chain's HBM row
+// (field 2 + i - 1, resp. 2 + kCoalKMax + i - 1, of the SoA rows)
 struct CoalLds {
   double* p;  // wave base + lane
-  __device__ __forceinline__ double& cp(int i) const { return p[(i - 1) * 64]; }              // i = 1..k
-  __device__ __forceinline__ double& h(int i) const { return p[(kCoalKMax + i - 1) * 64]; }  // i = 1..k+1
+  double* g;  // the chain's HBM row: field f at g[f * ld]
+  int64_t ld;
+  __device__ __forceinline__ double cp(int i) const {
+    return i <= kCoalWin ? p[(i - 1) * 64] : g[(2 + i - 1) * ld];
+  }
+  __device__ __forceinline__ double h(int i) const {
+    return i <= kCoalWin + 1 ? p[(kCoalWin + i - 1) * 64] : g[(2 + kCoalKMax + i - 1) * ld];
+  }
+  __device__ __forceinline__ void set_cp(int i, double v) const {
+    if (i <= kCoalWin) p[(i - 1) * 64] = v;
+    else g[(2 + i - 1) * ld] = v;
+  }
+  __device__ __forceinline__ void set_h(int i, double v) const {
+    if (i <= kCoalWin + 1) p[(kCoalWin + i - 1) * 64] = v;
+    else g[(2 + kCoalKMax + i - 1) * ld] = v;
+  }
+  // zero cp(i), h(i + 1) for i = k + 1 .. kCoalKMax: the whole window, past it
+  // only up to khi (the largest k this row held: beyond that the row is 0)
+  __device__ __forceinline__ void clear_above(int k, int khi) const {
+    for (int i = k + 1; i <= kCoalKMax; ++i) {
+      if (i > kCoalWin && i > khi) break;
+      set_cp(i, 0.0);
+    }
+    for (int i = k + 2; i <= kCoalKMax + 1; ++i) {
+      if (i > kCoalWin + 1 && i > khi + 1) break;
+      set_h(i, 0.0);
+    }
+  }
 };
 
 __device__ __forceinline__ double coal_u(uint64_t seed, uint64_t c, uint32_t step, uint32_t d) {
@@ -136,7 +174,7 @@ __device__ __forceinline__ double coal_full_score(const CoalArgs& a, int k, cons
 // prior (attempt a uses draws 100 a + ...; a degenerate draw retries), then
 // the score from scratch.  Returns k.
 __device__ int coal_init(const CoalArgs& a, uint64_t c, const CoalLds& s, const double* ev, const int32_t* bk,
-                         const double* tab, double* score) {
+                         const double* tab, double* score, int* khi) {
   int k = 0;
   bool done = false;
   for (int att = 0; att < 64 && !done; ++att) {
@@ -151,6 +189,7 @@ __device__ int coal_init(const CoalArgs& a, uint64_t c, const CoalLds& s, const 
       cum += p;
     }
     if (k > kCoalKMax) continue;
+    *khi = k > *khi ? k : *khi;  // (a retried attempt may leave fields up to here)
     bool ok = true;
     double lower = 0.0;
     for (int i = 1; i <= k; ++i) {
@@ -159,7 +198,7 @@ __device__ int coal_init(const CoalArgs& a, uint64_t c, const CoalLds& s, const 
       const double m = (double)(k - i + 1);
       const double x = a.T - (a.T - lower) * gh_exp(gh_log(1.0 - q) / m);
       if (!(x > lower && x < a.T)) ok = false;
-      s.cp(i) = x;
+      s.set_cp(i, x);
       lower = x;
     }
     for (int i = 1; i <= k + 1; ++i) {
@@ -167,16 +206,15 @@ __device__ int coal_init(const CoalArgs& a, uint64_t c, const CoalLds& s, const 
       const double q = coal_u(a.seed, c, 0, d0 + 40u + (uint32_t)i);
       const double x = -gh_log(1.0 - q) / kCoalRate;
       if (!(x > 0.0)) ok = false;
-      s.h(i) = x;
+      s.set_h(i, x);
     }
     done = ok;
   }
   if (!done) {  // unreachable in practice: k = 0 with the mean rate
     k = 0;
-    s.h(1) = (double)a.E / a.T;
+    s.set_h(1, (double)a.E / a.T);
   }
-  for (int i = k + 1; i <= kCoalKMax; ++i) s.cp(i) = 0.0;
-  for (int i = k + 2; i <= kCoalKMax + 1; ++i) s.h(i) = 0.0;
+  s.clear_above(k, *khi);
   *score = coal_full_score(a, k, s, ev, bk, tab);
   return k;
 }
@@ -192,7 +230,7 @@ __device__ int coal_init(const CoalArgs& a, uint64_t c, const CoalLds& s, const 
 // block 6 (k', acceptance), 8 + i (new change point i), 48 + i (new rate i).
 // Returns whether the move was accepted (the LDS row and k, score updated).
 __device__ bool coal_regen_k(const CoalArgs& a, uint64_t c, uint32_t step, const CoalLds& s, const double* ev,
-                             const int32_t* bk, const double* tab, int* k_io, double* score_io) {
+                             const int32_t* bk, const double* tab, int* k_io, double* score_io, int* khi) {
   const int k = *k_io;
   const CoalU B6 = coal_block(a.seed, c, step, 6);
   const double u = u53(B6.x, B6.y);
@@ -204,6 +242,7 @@ __device__ bool coal_regen_k(const CoalArgs& a, uint64_t c, uint32_t step, const
     cum += p;
   }
   if (kk > kCoalKMax) return false;  // beyond the engine's capacity: refused (P < 1e-21)
+  *khi = kk > *khi ? kk : *khi;
   const double T = a.T;
   const int m = k < kk ? k : kk;
   const double dk = (double)(kk - k);
@@ -222,21 +261,20 @@ __device__ bool coal_regen_k(const CoalArgs& a, uint64_t c, uint32_t step, const
     const double mm = (double)(kk - i + 1);
     const double x = T - (T - lower) * gh_exp(gh_log(1.0 - q) / mm);
     if (!(x > lower && x < T)) ok = false;
-    s.cp(i) = x;
+    s.set_cp(i, x);
     lower = x;
   }
   for (int i = k + 2; i <= kk + 1; ++i) {
     const double q = coal_u(a.seed, c, step, 48u + (uint32_t)i);
     const double x = -gh_log(1.0 - q) / kCoalRate;
     if (!(x > 0.0)) ok = false;
-    s.h(i) = x;
+    s.set_h(i, x);
   }
   double alpha = -INFINITY;
   if (ok) alpha = w + (coal_events_lp(a, kk, s, ev, bk, tab) - old_ev);
   const bool acc = gh_log_unit(one_minus_u53(B6.z, B6.w), tab) < alpha;
   const int keep = acc ? kk : k;
-  for (int i = keep + 1; i <= kCoalKMax; ++i) s.cp(i) = 0.0;
-  for (int i = keep + 2; i <= kCoalKMax + 1; ++i) s.h(i) = 0.0;
+  s.clear_above(keep, *khi);
   if (acc) {
     *k_io = kk;
     *score_io = coal_full_score(a, kk, s, ev, bk, tab);
@@ -245,7 +283,7 @@ __device__ bool coal_regen_k(const CoalArgs& a, uint64_t c, uint32_t step, const
 }
 
 __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
-  __shared__ double st[kCoalBlock / 64][kCoalF * 64];  // per wave: [field][lane]
+  __shared__ double st[kCoalBlock / 64][kCoalLF * 64];  // per wave: [field][lane]
   __shared__ double tab[kMathTabDoubles / 3];          // the log bins (gh_log_unit)
   extern __shared__ double dyn[];                      // E event times, then the bucket table
   double* ev = dyn;
@@ -257,19 +295,23 @@ __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
   const int64_t cl = (int64_t)blockIdx.x * kCoalBlock + threadIdx.x;
   if (cl >= a.n_chains) return;  // no block barrier below
   const int lane = threadIdx.x & 63;
-  const CoalLds s{&st[threadIdx.x >> 6][lane]};
+  double* g = a.state + cl;  // field f at g[f * ld]
+  const CoalLds s{&st[threadIdx.x >> 6][lane], g, a.ld};
   const uint64_t c = (uint64_t)(a.chain0 + cl);
   const double T = a.T;
-  const double* g = a.state + cl;  // field f at g[f * ld]
-  int k;
+  int k, khi = 0;  // khi: the largest k the row has held (its fields past khi are 0)
   double score;
   if (a.init) {
-    k = coal_init(a, c, s, ev, bk, tab, &score);
+    k = coal_init(a, c, s, ev, bk, tab, &score, &khi);
   } else {
     k = (int)g[0];
+    khi = k;
     score = g[a.ld];
-#pragma unroll 5
-    for (int f = 0; f < kCoalF; ++f) s.p[f * 64] = g[(2 + f) * a.ld];
+    // the window: cp 1..kCoalWin (row fields 0..), h 1..kCoalWin+1 (row fields kCoalKMax..)
+#pragma unroll
+    for (int f = 0; f < kCoalWin; ++f) s.p[f * 64] = g[(2 + f) * a.ld];
+#pragma unroll
+    for (int f = 0; f <= kCoalWin; ++f) s.p[(kCoalWin + f) * 64] = g[(2 + kCoalKMax + f) * a.ld];
   }
   int acc[3] = {0, 0, 0};
   for (int it = 0; it < a.n_iters; ++it) {
@@ -279,7 +321,7 @@ __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
     // ---- rate move (coal.jl:103-134): segment i's rate h -> nh ~ U(h/2, 2h)
     {
       const int i = (int)(u53(B0.x, B0.y) * (double)(k + 1)) + 1;  // uniform_discrete(1, k+1)
-      const double h = s.h(i);
+      const double h = s.h(i);  // (a read past the window goes to HBM)
       const double lo = h * 0.5, hi = h * 2.0;
       const double nh = lo + (hi - lo) * u53(B0.z, B0.w);
       const double b_lo = i == 1 ? 0.0 : s.cp(i - 1);
@@ -292,7 +334,7 @@ __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
       // fwd - bwd: the uniform_discrete terms cancel; the new_rate densities
       const double alpha = delta + (gh_log_unit(hi - lo, tab) - gh_log_unit(nh * 2.0 - nh * 0.5, tab));
       if (gh_log_unit(one_minus_u53(B1.x, B1.y), tab) < alpha) {
-        s.h(i) = nh;
+        s.set_h(i, nh);
         score += delta;
         acc[0] += 1;
       }
@@ -313,14 +355,14 @@ __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
         alpha = delta;  // the neighbours bound both proposals: fwd == bwd
       }
       if (gh_log_unit(one_minus_u53(B2.z, B2.w), tab) < alpha) {
-        s.cp(i) = nx;
+        s.set_cp(i, nx);
         score += delta;
         acc[1] += 1;
       }
     }
     // ---- simple_mcmc_step: regenerate k (coal.jl:338-345)
     if (a.simple) {
-      if (coal_regen_k(a, c, step, s, ev, bk, tab, &k, &score)) acc[2] += 1;
+      if (coal_regen_k(a, c, step, s, ev, bk, tab, &k, &score, &khi)) acc[2] += 1;
     } else {  // ---- birth / death move (coal.jl:173-318)
       const CoalU B3 = coal_block(a.seed, c, step, 3);
       const CoalU B4 = coal_block(a.seed, c, step, 4);
@@ -386,18 +428,19 @@ __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
       const CoalU B5 = coal_block(a.seed, c, step, 5);
       if (gh_log_unit(one_minus_u53(B5.x, B5.y), tab) < alpha) {
         if (birth) {  // birth(k, i) (coal.jl:260-283): insert cp at i, rates (hp, hn) at (i, i+1)
-          for (int j = k; j >= i; --j) s.cp(j + 1) = s.cp(j);
-          s.cp(i) = x;
-          for (int j = k + 1; j >= i + 1; --j) s.h(j + 1) = s.h(j);
-          s.h(i) = hp;
-          s.h(i + 1) = hn;
+          for (int j = k; j >= i; --j) s.set_cp(j + 1, s.cp(j));
+          s.set_cp(i, x);
+          for (int j = k + 1; j >= i + 1; --j) s.set_h(j + 1, s.h(j));
+          s.set_h(i, hp);
+          s.set_h(i + 1, hn);
           k += 1;
+          khi = k > khi ? k : khi;
         } else {  // death(k, i) (coal.jl:285-305): remove cp i, rate h at i
-          for (int j = i; j <= k - 1; ++j) s.cp(j) = s.cp(j + 1);
-          s.cp(k) = 0.0;
-          s.h(i) = h;
-          for (int j = i + 1; j <= k; ++j) s.h(j) = s.h(j + 1);
-          s.h(k + 1) = 0.0;
+          for (int j = i; j <= k - 1; ++j) s.set_cp(j, s.cp(j + 1));
+          s.set_cp(k, 0.0);
+          s.set_h(i, h);
+          for (int j = i + 1; j <= k; ++j) s.set_h(j, s.h(j + 1));
+          s.set_h(k + 1, 0.0);
           k -= 1;
         }
         score += delta;
@@ -406,12 +449,13 @@ __global__ __launch_bounds__(kCoalBlock) void k_coal(CoalArgs a) {
     }
     if (a.khist) a.khist[cl * a.n_iters + it] = (int32_t)k;
   }
-  double* gw = a.state + cl;
-  gw[0] = (double)k;
-  gw[a.ld] = score;
-#pragma unroll 5
-  for (int f = 0; f < kCoalF; ++f) gw[(2 + f) * a.ld] = s.p[f * 64];
-  gw[(kCoalW - 1) * a.ld] = 0.0;
+  g[0] = (double)k;
+  g[a.ld] = score;
+#pragma unroll
+  for (int f = 0; f < kCoalWin; ++f) g[(2 + f) * a.ld] = s.p[f * 64];
+#pragma unroll
+  for (int f = 0; f <= kCoalWin; ++f) g[(2 + kCoalKMax + f) * a.ld] = s.p[(kCoalWin + f) * 64];
+  g[(kCoalW - 1) * a.ld] = 0.0;
   for (int m = 0; m < 3; ++m) a.accepts[cl * 3 + m] = acc[m];
 }
 

@@ -373,6 +373,10 @@ int gh_coal_step(gh_coal* h, int n_iters, int32_t* accepts, int32_t* khist, doub
    accepts[2] counts the third move's acceptances either way */
 int gh_coal_set_kernel(gh_coal* h, int kernel);
 int gh_coal_read_state(gh_coal* h, double* state);
+/* Resume the chains from given rows ([n_chains][68], the layout of
+   gh_coal_read_state: fields past k / k+1 zero); the next gh_coal_step
+   continues at iteration iter0 + 1 (its draws are those of that iteration). */
+int gh_coal_write_state(gh_coal* h, const double* state, int iter0);
 int gh_coal_destroy(gh_coal* h);
 
 /* ---- diagnostics ------------------------------------------------------------ */

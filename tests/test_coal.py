@@ -125,3 +125,37 @@ def test_gpu_coal_run_stateless_matches_oracle(gh_ctx):
                                acc.ctypes.data_as(POINTER(c_int32)), None, byref(ms)))
     ref2 = O.coal_run(EVENTS, n, 10, seed=5, chain0=3, iter0=25, state=ref[0])
     assert np.array_equal(st, ref2[0]) and np.array_equal(acc, ref2[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("simple", [False, True])
+def test_gpu_coal_many_change_points_bitexact(gh_ctx, simple):
+    """Chains resumed from states with more change points than the kernel's LDS
+    window (k_coal keeps cp 1..15, h 1..16 in LDS; the rest of a row is read
+    and written in place in HBM): synthetic rows with k = 14..32 (the window's
+    edge, the k = 31 kind of test_coal_pins.py, the capacity) run 30
+    iterations of either MCMC kernel bit-exact against the oracle — births
+    past the window, deaths back into it, regenerated k' across it."""
+    from gen_amd.coal import CoalChains
+
+    ev = np.sort(np.asarray(EVENTS, dtype=np.float64))
+    T = float(ev[-1])
+    rng = np.random.default_rng(21)
+    rows = []
+    for i in range(320):
+        k = int([14, 15, 16, 17, 24, 31, 32, 3][i % 8])
+        r = np.zeros(68)
+        r[0] = k
+        r[2 : 2 + k] = np.sort(rng.uniform(0, T, k))
+        r[34 : 34 + k + 1] = rng.gamma(1.0, 1.0 / 200.0, k + 1) + 1e-4
+        r[1] = O.coal_score(r, ev)
+        rows.append(r)
+    st = np.array(rows)
+    ref = O.coal_run(ev, len(rows), 30, seed=8, chain0=11, iter0=4, state=st, simple=simple)
+    ch = CoalChains(ev, len(rows), seed=8, chain0=11, ctx=gh_ctx,
+                    kernel="simple_mcmc_step" if simple else "mcmc_step")
+    ch.load_state(st, 4)
+    ch.run(30)
+    assert np.array_equal(ch.state, ref[0]) and np.array_equal(ch.accepts, ref[1])
+    assert (ref[0][:, 0] > 15).sum() > 20  # chains past the window at the end too
+    ch.close()

@@ -1,5 +1,9 @@
-# round-4 GPU check: new multi-rank paths first, then the whole GPU suite and the bench
+# round-4 GPU check: new multi-rank paths first, then the whole GPU suite, the bench, C3 window variants
 mkdir -p gpurun_out/r4a
-timeout -k 10 600 python -u -m pytest tests/test_multirank.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r4a/mr.log 2>&1 && \
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4a/gputest.log 2>&1 && \
-timeout -k 10 300 python bench.py > gpurun_out/r4a/bench.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_multirank.py tests/test_coal.py tests/test_unfold_kats_device.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r4a/mr.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4a/gputest.log 2>&1 && \
+timeout -k 10 400 python bench.py > gpurun_out/r4a/bench.log 2>&1 && \
+for v in base coal_w10 coal_w7; do
+  lib=gen_amd/libgen_hip.so; [ $v != base ] && lib=gen_amd/variants/$v.so
+  GEN_HIP_LIB=$lib timeout -k 10 120 python tools/bench_coal.py --steps 300 > gpurun_out/r4a/coal_$v.json 2>&1 || exit 1
+done

@@ -16,6 +16,8 @@ VARIANTS = {
     "occ6": ["GH_LG10_WAVES=6"],
     "philox1": ["GH_PHILOX_ROUNDS=1"],
     "philox7": ["GH_PHILOX_ROUNDS=7"],
+    "coal_w10": ["GH_COAL_WIN=10"],
+    "coal_w7": ["GH_COAL_WIN=7"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
