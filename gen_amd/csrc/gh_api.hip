@@ -739,6 +739,7 @@ struct gh_pf {
   // MH moves already applied at this step (their draw windows)
   StepObs last_obs{};
   std::vector<StepObs> obs_hist;  // every step's observation (prior form), index t-1: trace scores
+  std::vector<std::vector<double>> raw_obs;  // every step's observation as given (index t-1; empty: none)
   uint32_t rejuv_moves = 0;
   unsigned long long* acc_count = nullptr;
   // the Gaussian custom proposal's last arguments (alpha, beta, gamma, sigma_q)
@@ -756,6 +757,8 @@ struct gh_pf {
 };
 
 static int64_t split_lo(int64_t n, int r, int R) { return (n * r) / R; }
+
+static void log_raw_obs(gh_pf* pf, int t, const gh_obs* obs);
 
 // Tile size of the one-launch resample kernels: the smallest 1024 x IT tile
 // whose grid fits the co-resident capacity (their grid barrier needs every
@@ -1348,11 +1351,20 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->t = 1;
   pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
   pf->obs_hist.assign(1, o_prior);
+  log_raw_obs(pf, 1, obs);
   *out = pf;
   return GH_OK;
 }
 
 static int grow_for_step(gh_pf* pf, int t) { return ensure_capacity(pf, t + 1); }
+
+// the observation of step t as given (rebuilt under other parameters: gh_pf_step_params)
+static void log_raw_obs(gh_pf* pf, int t, const gh_obs* obs) {
+  if ((int)pf->raw_obs.size() < t) pf->raw_obs.resize(t);
+  auto& r = pf->raw_obs[t - 1];
+  r.clear();
+  if (obs && obs->present && obs->values && obs->n_values > 0) r.assign(obs->values, obs->values + obs->n_values);
+}
 
 static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double* pin_ref);
 
@@ -1438,6 +1450,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
   if ((int)pf->obs_hist.size() < t) pf->obs_hist.resize(t);
   pf->obs_hist[t - 1] = o_prior;
+  log_raw_obs(pf, t, obs);
   pf->rejuv_moves = 0;
   return GH_OK;
 }
@@ -2012,41 +2025,33 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
 
 // Trace score columns (gh_scores.h): per particle and step the latent's and
 // the observation's score, and the trace's total (get_score).
-extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
-  if (!pf || !total) return set_err(GH_E_INVAL, "null argument");
-  CHECK(materialize_marks(pf));
+// The trace score columns of every current particle (k_scores: the genealogy
+// walk) under model m and the steps' observations obs[0..T): dtot[n] and the
+// per-step scratch/output dper[T][2][n], device buffers, on the filter's stream.
+static int scores_dev(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& obs, double* dtot, double* dper) {
   const int T = pf->t;
-  if (T < 1) return set_err(GH_E_STATE, "gh_pf_get_scores before init");
-  if (!pf->opts.record_history && T > 1) return set_err(GH_E_STATE, "gh_pf_get_scores needs record_history");
-  if (mr(pf->ctx) && T > 1)
-    return set_err(GH_E_STATE, "multi-rank: the genealogy before the current step is not materialised");
-  if ((int)pf->obs_hist.size() < T) return set_err(GH_E_STATE, "internal: observation history");
   const int64_t n = pf->n;
-  if (n == 0) return GH_OK;
-  double *dtot = nullptr, *dper = nullptr;
   const double** dxs = nullptr;
   const int32_t** dancs = nullptr;
   StepObs* dobs = nullptr;
-  auto cleanup = [&]() { hipFree(dtot); hipFree(dper); hipFree(dxs); hipFree(dancs); hipFree(dobs); };
+  auto cleanup = [&]() { hipFree(dxs); hipFree(dancs); hipFree(dobs); };
   std::vector<const double*> hx(T);
   std::vector<const int32_t*> ha(T);
   for (int s = 1; s <= T; ++s) {
     hx[s - 1] = slot_x(pf, s);
     ha[s - 1] = anc_for_step(pf, s);
   }
-  if (hipMalloc(&dtot, sizeof(double) * n) != hipSuccess ||
-      hipMalloc(&dper, sizeof(double) * 2 * (size_t)T * n) != hipSuccess ||
-      hipMalloc(&dxs, sizeof(double*) * T) != hipSuccess || hipMalloc(&dancs, sizeof(int32_t*) * T) != hipSuccess ||
+  if (hipMalloc(&dxs, sizeof(double*) * T) != hipSuccess || hipMalloc(&dancs, sizeof(int32_t*) * T) != hipSuccess ||
       hipMalloc(&dobs, sizeof(StepObs) * T) != hipSuccess) {
     cleanup();
-    return set_err(GH_E_NOMEM, "gh_pf_get_scores: %d steps x %lld particles", T, (long long)n);
+    return set_err(GH_E_NOMEM, "scores: %d steps", T);
   }
   int rc = GH_OK;
   do {
     if (hipMemcpyAsync(dxs, hx.data(), sizeof(double*) * T, hipMemcpyHostToDevice, pf->s) != hipSuccess ||
         hipMemcpyAsync(dancs, ha.data(), sizeof(int32_t*) * T, hipMemcpyHostToDevice, pf->s) != hipSuccess ||
-        hipMemcpyAsync(dobs, pf->obs_hist.data(), sizeof(StepObs) * T, hipMemcpyHostToDevice, pf->s) != hipSuccess) {
-      rc = set_err(GH_E_HIP, "gh_pf_get_scores: upload");
+        hipMemcpyAsync(dobs, obs.data(), sizeof(StepObs) * T, hipMemcpyHostToDevice, pf->s) != hipSuccess) {
+      rc = set_err(GH_E_HIP, "scores: upload");
       break;
     }
     ScoreArgs sa{};
@@ -2062,21 +2067,112 @@ extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
     sa.total = dtot;
     const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
     // the model's own densities, whatever proposal made the particles
-    rc = with_model(pf->m, [&](auto model, const auto& p) {
-      hipLaunchKernelGGL(k_scores<decltype(model)>, grid, dim3(kBlock), 0, pf->s, (const double*)pf->m->dparams, p, sa,
+    rc = with_model(m, [&](auto model, const auto& p) {
+      hipLaunchKernelGGL(k_scores<decltype(model)>, grid, dim3(kBlock), 0, pf->s, (const double*)m->dparams, p, sa,
                          (const DevScalars*)pf->dev);
     });
     if (rc) break;
-    if (hipGetLastError() != hipSuccess) {
-      rc = set_err(GH_E_HIP, "gh_pf_get_scores: launch");
-      break;
-    }
-    if (hipMemcpyAsync(total, dtot, sizeof(double) * n, hipMemcpyDeviceToHost, pf->s) != hipSuccess ||
-        (per_step && hipMemcpyAsync(per_step, dper, sizeof(double) * 2 * (size_t)T * n, hipMemcpyDeviceToHost, pf->s) !=
-                         hipSuccess) ||
-        hipStreamSynchronize(pf->s) != hipSuccess)
-      rc = set_err(GH_E_HIP, "gh_pf_get_scores: download");
+    if (hipGetLastError() != hipSuccess) rc = set_err(GH_E_HIP, "scores: launch");
+    // the argument arrays are freed below: wait for the kernel
+    if (!rc && hipStreamSynchronize(pf->s) != hipSuccess) rc = set_err(GH_E_HIP, "scores: sync");
   } while (0);
+  cleanup();
+  return rc;
+}
+
+static int scores_ready(gh_pf* pf, const char* who) {
+  CHECK(materialize_marks(pf));
+  const int T = pf->t;
+  if (T < 1) return set_err(GH_E_STATE, "%s before init", who);
+  if (!pf->opts.record_history && T > 1) return set_err(GH_E_STATE, "%s needs record_history", who);
+  if (mr(pf->ctx) && T > 1)
+    return set_err(GH_E_STATE, "multi-rank: the genealogy before the current step is not materialised");
+  if ((int)pf->obs_hist.size() < T) return set_err(GH_E_STATE, "internal: observation history");
+  return GH_OK;
+}
+
+extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
+  if (!pf || !total) return set_err(GH_E_INVAL, "null argument");
+  CHECK(scores_ready(pf, "gh_pf_get_scores"));
+  const int T = pf->t;
+  const int64_t n = pf->n;
+  if (n == 0) return GH_OK;
+  double *dtot = nullptr, *dper = nullptr;
+  if (hipMalloc(&dtot, sizeof(double) * n) != hipSuccess ||
+      hipMalloc(&dper, sizeof(double) * 2 * (size_t)T * n) != hipSuccess) {
+    hipFree(dtot);
+    hipFree(dper);
+    return set_err(GH_E_NOMEM, "gh_pf_get_scores: %d steps x %lld particles", T, (long long)n);
+  }
+  int rc = scores_dev(pf, pf->m, pf->obs_hist, dtot, dper);
+  if (!rc && (hipMemcpyAsync(total, dtot, sizeof(double) * n, hipMemcpyDeviceToHost, pf->s) != hipSuccess ||
+              (per_step && hipMemcpyAsync(per_step, dper, sizeof(double) * 2 * (size_t)T * n, hipMemcpyDeviceToHost,
+                                          pf->s) != hipSuccess) ||
+              hipStreamSynchronize(pf->s) != hipSuccess))
+    rc = set_err(GH_E_HIP, "gh_pf_get_scores: download");
+  hipFree(dtot);
+  hipFree(dper);
+  return rc;
+}
+
+// particle_filter_step!(state, (t, params'...), (UnknownChange(), UnknownChange()...), obs)
+// (particle_filter.jl:162-180) with the Unfold's parameters changed to those of
+// nm: the Unfold's update re-visits every retained kernel application
+// (unfold/generic_update.jl:9-16), each contributing new score - old score
+// (no new constraints on them), then generates the new application under the
+// new parameters.  Delta_j = get_score under nm - under the old model along
+// particle j's trajectory (k_scores twice; the past observations rebuilt under
+// nm), the step under nm, then logw_j += Delta_j and the block partials again
+// (k_add_delta).  One rank, history kept, same family and dimensions.
+extern "C" int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm) {
+  if (!pf || !nm) return set_err(GH_E_INVAL, "gh_pf_step_params: null argument");
+  if (pf->cond) return set_err(GH_E_STATE, "gh_pf_step_params: a conditional filter keeps its model");
+  if (mr(pf->ctx)) return set_err(GH_E_STATE, "gh_pf_step_params: one rank (the re-scoring walks the genealogy)");
+  if (!pf->opts.record_history) return set_err(GH_E_STATE, "gh_pf_step_params needs record_history");
+  const gh_model* m = pf->m;
+  if (nm->ctx != m->ctx || nm->family != m->family || nm->d != m->d || nm->dy != m->dy || nm->k != m->k ||
+      nm->v != m->v)
+    return set_err(GH_E_INVAL, "gh_pf_step_params: the new parameters must be of the same family and dimensions");
+  if (!proposal_ok(nm, proposal)) return set_err(GH_E_INVAL, "gh_pf_step_params: proposal %d not available", proposal);
+  CHECK(set_qargs(pf->qargs, &pf->has_q, proposal, nullptr, 0));
+  CHECK(scores_ready(pf, "gh_pf_step_params"));
+  const int T = pf->t;
+  const int64_t n = pf->n;
+  std::vector<StepObs> rebuilt(T);
+  for (int s = 1; s <= T; ++s) {
+    const auto& r = pf->raw_obs[s - 1];
+    const gh_obs in{r.empty() ? nullptr : r.data(), (int32_t)r.size(), r.empty() ? 0 : 1};
+    CHECK(make_obs(nm, s, &in, &rebuilt[s - 1]));
+  }
+  double *dold = nullptr, *dnew = nullptr, *dper = nullptr;
+  auto cleanup = [&]() { hipFree(dold); hipFree(dnew); hipFree(dper); };
+  const size_t nn = (size_t)(n > 0 ? n : 1);
+  if (hipMalloc(&dold, sizeof(double) * nn) != hipSuccess || hipMalloc(&dnew, sizeof(double) * nn) != hipSuccess ||
+      hipMalloc(&dper, sizeof(double) * 2 * (size_t)T * nn) != hipSuccess) {
+    cleanup();
+    return set_err(GH_E_NOMEM, "gh_pf_step_params: re-scoring buffers (%d steps)", T);
+  }
+  int rc = GH_OK;
+  if (n > 0) {
+    rc = scores_dev(pf, m, pf->obs_hist, dold, dper);
+    if (!rc) rc = scores_dev(pf, nm, rebuilt, dnew, dper);
+  }
+  if (rc) {
+    cleanup();
+    return rc;
+  }
+  pf->m = nm;
+  pf->obs_hist = rebuilt;
+  rc = pf_step_impl(pf, obs, proposal, nullptr);
+  if (!rc && n > 0) {
+    hipLaunchKernelGGL(k_add_delta, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, pf->logw,
+                       (const double*)dnew, (const double*)dold, n, pf->pm, pf->ps, pf->ps2);
+    if (hipGetLastError() != hipSuccess) rc = set_err(GH_E_HIP, "gh_pf_step_params: launch");
+    pf->nb_part = pf->nb_step;
+    pf->last_pairs = false;
+    pf->stats_valid = false;
+  }
+  if (hipStreamSynchronize(pf->s) != hipSuccess && !rc) rc = set_err(GH_E_HIP, "gh_pf_step_params: sync");
   cleanup();
   return rc;
 }

@@ -63,4 +63,20 @@ __global__ __launch_bounds__(kBlock) void k_scores(const double* __restrict__ pr
   a.total[j] = tot;
 }
 
+// gh_pf_step_params: after the step under the new parameters, every particle's
+// weight gains its trajectory's re-scoring, logw += new - old, and the step
+// kernel's block partials are taken again from the new weights (256-particle
+// blocks, block_partial's arithmetic) for the next fold / resample.
+static __global__ __launch_bounds__(kBlock) void k_add_delta(double* logw, const double* snew, const double* sold,
+                                                             int64_t n, double* pm, double* ps, double* ps2) {
+  __shared__ double sm[3][4];
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double lw = -INFINITY;
+  if (j < n) {
+    lw = logw[j] + (snew[j] - sold[j]);
+    logw[j] = lw;
+  }
+  block_partial(lw, sm, pm + blockIdx.x, ps + blockIdx.x, ps2 + blockIdx.x);
+}
+
 }  // namespace gh

@@ -461,11 +461,36 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
 
 def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: tuple, observations,
                          proposal=None, proposal_args: tuple = ()) -> None:
+    """particle_filter_step!(state, new_args, argdiffs, observations[, proposal,
+    proposal_args]) (particle_filter.jl:139-180).  new_args = (t,) extends the
+    Unfold by one step; new_args = (t, model') also changes the Unfold's
+    parameters to those of model' (the same family and dimensions) with an
+    UnknownChange() argdiff for them: every retained kernel application is
+    re-scored (gh_pf_step_params), as the Unfold's update does."""
     t = state.t + 1
-    if tuple(new_args)[:1] != (t,):
-        raise _lib.GenHipError(1, f"new_args must extend the Unfold by one step: expected ({t},), got {new_args}")
+    new_args = tuple(new_args)
+    argdiffs = tuple(argdiffs)
+    if new_args[:1] != (t,):
+        raise _lib.GenHipError(1, f"new_args must extend the Unfold by one step: expected ({t}, ...), got {new_args}")
     if argdiffs and not isinstance(argdiffs[0], UnknownChange):
         raise _lib.GenHipError(1, "the length argument changes: its argdiff must be UnknownChange()")
+    if len(new_args) > 2:
+        raise _lib.GenHipError(1, "new_args = (t,) or (t, model with the new parameters)")
+    new_model = new_args[1] if len(new_args) == 2 else None
+    if new_model is not None and new_model is not state.model:
+        diff = argdiffs[1] if len(argdiffs) > 1 else UnknownChange()
+        if isinstance(diff, NoChange):
+            raise _lib.GenHipError(1, "the parameters differ from the filter's but their argdiff is NoChange()")
+        if type(new_model) is not type(state.model):
+            raise _lib.GenHipError(1, "new parameters of another model family")
+        obs, keep = _step_obs(new_model, t, observations)
+        if proposal_args:
+            raise _lib.GenHipError(1, "a parameter change takes the proposal's stored arguments")
+        mh = state.ctx.model_handle(new_model)
+        _lib.check(_lib.load().gh_pf_step_params(state.h, byref(obs), _proposal_code(proposal), mh))
+        state.model = new_model
+        state._log_obs(t, keep)
+        return
     obs, keep = _step_obs(state.model, t, observations)
     qa, nq = _qargs(proposal, proposal_args)
     _lib.check(_lib.load().gh_pf_step_q(state.h, byref(obs), _proposal_code(proposal),

@@ -243,6 +243,15 @@ int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal);
 int gh_pf_init_q(gh_model* m, const gh_obs* obs, int proposal, const double* proposal_args, int n_proposal_args,
                  int64_t n_particles, uint64_t seed, const gh_pf_opts* opts, gh_pf** out);
 int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const double* proposal_args, int n_proposal_args);
+/* particle_filter_step!(state, (t, params'...), (UnknownChange(), UnknownChange()...),
+   observations) (particle_filter.jl:162-180) with the Unfold's parameters
+   changed to those of new_model (same family and dimensions, same context):
+   the Unfold's update re-visits every retained kernel application
+   (unfold/generic_update.jl:9-16), so every particle's weight gains its
+   trajectory's score under the new parameters minus under the old ones, and
+   the new step is generated under the new parameters, which the filter keeps
+   from then on (new_model must outlive it).  One rank, record_history. */
+int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* new_model);
 /* ess_threshold NaN means the reference's default N/2; any other value >= 0 is
    the threshold as given (resample iff ESS < ess_threshold, so 0 never
    resamples, as in Gen); a negative threshold is GH_E_INVAL (before round 3,

@@ -476,13 +476,18 @@ typedef struct {
   /* LGSSM optimal proposal: t = 1: mean mu1 (g) and constant weight w0;
      t >= 2: g = F b + K (y - c), vt = L_S^{-1}(y - c) - L_S^{-1} H b */
   double g[64], vt[64], w0;
+  double raw[64]; /* the observation as given (rebuilt under other parameters: orc_pf_step_params) */
+  int nraw;
 } obs_t;
 
 static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* o) {
   o->present = has;
   o->ct = 0.0;
+  o->nraw = 0;
   if (m->family == ORC_KITAGAWA) o->ct = 8.0 * orc_cos(1.2 * (double)t);
   if (!has) return;
+  o->nraw = (m->family == ORC_LGSSM || m->family == ORC_REGRESSION) ? m->dy : 1;
+  for (int i = 0; i < o->nraw; ++i) o->raw[i] = y[i];
   if (m->family == ORC_LGSSM) {
     double r[64];
     for (int i = 0; i < m->dy; ++i) r[i] = y[i] - m->c[i];
@@ -1226,7 +1231,9 @@ static void model_score(const model_t* m, const obs_t* o, int t, const double* x
 
 /* get_score of every current particle's trace along its genealogy, with the
    per-step latent / observation scores (per_step [t][2][n], nullable) */
-int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step) {
+/* the trace score columns of every particle under model m and the steps'
+   observations obs[0..T) (the filter's own, or rebuilt for other parameters) */
+static int scores_with(orc_pf* pf, const model_t* m, const obs_t* obs, double* total, double* per_step) {
   if (pf->t < 1 || (!pf->record_history && pf->t > 1) || pf->lo != 0 || pf->n != pf->n_global) return -1;
   const int T = pf->t, D = pf->m.d;
   const int64_t n = pf->n;
@@ -1242,9 +1249,9 @@ int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step) {
         if (pf->hres[s - 1]) parent = pf->hanc[s - 1][idx];
         for (int k = 0; k < D; ++k) xp[k] = pf->hx[s - 2][(size_t)k * n + parent];
       }
-      const obs_t* o = pf->record_history ? &pf->hobs[s - 1] : &pf->obs;
+      const obs_t* o = &obs[s - 1];
       double lat, ob;
-      model_score(&pf->m, o, s, xp, x, &lat, &ob);
+      model_score(m, o, s, xp, x, &lat, &ob);
       ps[((size_t)(s - 1) * 2) * n + j] = lat;
       ps[((size_t)(s - 1) * 2 + 1) * n + j] = ob;
       for (int k = 0; k < D; ++k) x[k] = xp[k];
@@ -1256,6 +1263,52 @@ int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step) {
   }
   if (!per_step) free(ps);
   return 0;
+}
+
+int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step) {
+  if (pf->t < 1) return -1;
+  return scores_with(pf, &pf->m, pf->record_history ? pf->hobs : &pf->obs, total, per_step);
+}
+
+/* particle_filter_step!(state, (t, params'...), (UnknownChange(), UnknownChange()...), obs)
+   (particle_filter.jl:162-180): the Unfold's parameters change, so its update
+   visits every retained kernel application (unfold/generic_update.jl:9-16);
+   with no new constraints on them each contributes its new score - old score
+   (static_ir/update.jl), then the new application is generated under the new
+   parameters.  Here: Delta_j = get_score under the new parameters - under the
+   old ones along particle j's trajectory (time-ordered sums), the step under
+   the new model, then logw_j += Delta_j.  Same family and dimensions; needs
+   the history (one shard). */
+int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const double* obs, int has_obs, int proposal) {
+  if (pf->cond || pf->t < 1 || !pf->record_history || pf->lo != 0 || pf->n != pf->n_global) return -1;
+  model_t m2;
+  const model_t* m = &pf->m;
+  if (model_build(&m2, m->family, m->d, m->dy, m->k, m->v, params, np)) {
+    model_free(&m2);
+    return -1;
+  }
+  if (!proposal_ok(&m2, proposal)) {
+    model_free(&m2);
+    return -1;
+  }
+  const int T = pf->t;
+  const int64_t n = pf->n;
+  obs_t* o2 = malloc(sizeof(obs_t) * (size_t)T);
+  for (int s = 1; s <= T; ++s) obs_build(&m2, s, pf->hobs[s - 1].raw, pf->hobs[s - 1].present, &o2[s - 1]);
+  double* old_tot = malloc(sizeof(double) * (size_t)(n ? n : 1));
+  double* new_tot = malloc(sizeof(double) * (size_t)(n ? n : 1));
+  scores_with(pf, &pf->m, pf->hobs, old_tot, NULL);
+  scores_with(pf, &m2, o2, new_tot, NULL);
+  model_free(&pf->m);
+  pf->m = m2;
+  memcpy(pf->hobs, o2, sizeof(obs_t) * (size_t)T);
+  free(o2);
+  int rc = step_impl(pf, obs, has_obs, proposal, NULL);
+  if (!rc)
+    for (int64_t j = 0; j < n; ++j) pf->logw[j] += new_tot[j] - old_tot[j];
+  free(old_tot);
+  free(new_tot);
+  return rc;
 }
 
 /* simulate(model, (T,)) for n traces (static_ir/simulate.jl:23-34, 50-83;

@@ -87,6 +87,9 @@ int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* 
    latent / observation choice scores (per_step [t][2][n], nullable); one shard */
 int orc_pf_mh_drift(orc_pf* pf, uint32_t mask, const double* sd, int n_moves, int64_t* accepted);
 int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step);
+/* a step whose Unfold parameters change (new_args with UnknownChange on them):
+   every retained application re-scored, weight += new - old score (see .c) */
+int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const double* obs, int has_obs, int proposal);
 double orc_log1p(double y);
 double orc_lgamma(double x);
 int orc_dist_logpdf(int dist, int dim, int np, int stride, const double* params, int64_t n, const double* x,

@@ -89,6 +89,7 @@ def _load(path):
             "orc_pf_num_steps": (I, [V]),
             "orc_pf_get_history": (I, [V, I, D, POINTER(c_int32), POINTER(c_int)]),
             "orc_pf_get_scores": (I, [V, D, D]),
+            "orc_pf_step_params": (I, [V, D, I64, D, I, I]),
             "orc_lgamma": (c_double, [c_double]),
             "orc_log1p": (c_double, [c_double]),
             "orc_dist_logpdf": (I, [I, I, I, I, D, I64, D, D]),
@@ -195,6 +196,17 @@ class OraclePF:
         a, has = self._obs(y)
         if self.L.orc_pf_step(self.h, _d(a), has, proposal):
             raise ValueError("oracle: this filter does not take plain steps")
+
+    def step_params(self, model, y, proposal=DEFAULT):
+        """particle_filter_step! with the Unfold's parameters changed to `model`'s
+        (same family and dimensions): every particle's weight gains its
+        trajectory's score under the new parameters minus under the old ones."""
+        fam, d, dy, k, v, p = model_args(model)
+        a, has = self._obs(y)
+        self._p = p
+        if self.L.orc_pf_step_params(self.h, _d(p), p.size, _d(a), has, proposal):
+            raise ValueError("oracle: parameter change needs one shard with its history, a matching model")
+        self.model = model
 
     def init_conditional(self, y, ref):
         a, has = self._obs(y)
