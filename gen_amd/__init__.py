@@ -11,6 +11,7 @@ from .pf import (
     Context,
     NoChange,
     GaussianProposal,
+    LinearGaussianProposal,
     OptimalProposal,
     conditional_particle_filter_step,
     conditional_smc,

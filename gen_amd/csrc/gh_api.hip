@@ -627,6 +627,13 @@ static int make_obs_gauss(const gh_model* m, int t, const gh_obs* in, const doub
 // The optimal proposal's per-step vectors (LGOptModel): t = 1: o.v[0, d) =
 // mu_1 = mu0 + K_1 (y - c - H mu0), o.ct = log N(y; H mu0 + c, S_1); t >= 2:
 // o.v[0, d) = g_t = F b + K (y - c), o.v[d, d + dy) = L_S^-1 (y - c) - L_S^-1 H b.
+// the observation with u_t of the linear proposal behind it (o.v[dy + i])
+static int make_obs_lin(const gh_model* m, int t, const gh_obs* in, const double* u, StepObs* o) {
+  CHECK(make_obs(m, t, in, o));
+  for (int i = 0; i < m->d; ++i) o->v[m->dy + i] = u[i];
+  return GH_OK;
+}
+
 static int make_obs_opt(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
   CHECK(make_obs(m, t, in, o));
   if (!o->present) return GH_OK;
@@ -665,6 +672,7 @@ static int make_obs_opt(const gh_model* m, int t, const gh_obs* in, StepObs* o) 
 static bool proposal_ok(const gh_model* m, int proposal) {
   if (proposal == GH_PROPOSAL_DEFAULT) return true;
   if (proposal == GH_PROPOSAL_GAUSSIAN) return m->family == GH_FAMILY_KITAGAWA;
+  if (proposal == GH_PROPOSAL_LINEAR) return m->family == GH_FAMILY_LGSSM && m->d + m->dy <= kMaxObs;
   if (proposal != GH_PROPOSAL_OPTIMAL) return false;
   return m->family == GH_FAMILY_HMM || (m->family == GH_FAMILY_LGSSM && m->lg_opt);
 }
@@ -745,6 +753,11 @@ struct gh_pf {
   // the Gaussian custom proposal's last arguments (alpha, beta, gamma, sigma_q)
   double qargs[4] = {0, 0, 0, 0};
   bool has_q = false;
+  // the LGSSM's linear-Gaussian custom proposal (GH_PROPOSAL_LINEAR): device P | chol(Sigma_q)
+  double* qlin = nullptr;
+  double cstq = 0.0;
+  bool has_qlin = false;
+  std::vector<double> qlin_u;     // u_t of the next steps
   // conditional SMC (gh_csmc.h): particle 0 is pinned to a given trajectory
   bool cond = false;
   double* pin = nullptr;          // [D] this step's distinguished state, [D] its new log weight
@@ -883,7 +896,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
   hipFree(pf->acc_count); hipFree(pf->pin); hipFree(pf->amax);
-  hipFree(pf->amax_all); hipFree(pf->rec); hipFree(pf->recs_all);
+  hipFree(pf->amax_all); hipFree(pf->rec); hipFree(pf->recs_all); hipFree(pf->qlin);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
   if (pf->ev_plan) hipEventDestroy(pf->ev_plan);
@@ -1020,6 +1033,23 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
     return set_err(GH_E_INVAL, "the regression model has no time steps");
   if (a.proposal == GH_PROPOSAL_GAUSSIAN) {  // Kitagawa only (proposal_ok); its own functor
     launch_step_t<KitGaussModel>(pf, pf->m->kit, o, a, init, e0, e1);
+    HIP_TRY(hipGetLastError());
+    return GH_OK;
+  }
+  if (a.proposal == GH_PROPOSAL_LINEAR) {  // LGSSM only (proposal_ok); P and chol(Sigma_q) in the filter's buffer
+    LGParams p = pf->m->lg;
+    p.QP = pf->qlin;
+    p.QL = pf->qlin + pf->D * pf->D;
+    p.cstq = pf->cstq;
+    switch (pf->m->d) {
+#define GH_LGL_CASE(DD) \
+  case DD: launch_step_t<LGLinModel<DD>>(pf, p, o, a, init, e0, e1); break;
+      GH_LGL_CASE(1) GH_LGL_CASE(2) GH_LGL_CASE(3) GH_LGL_CASE(4) GH_LGL_CASE(5) GH_LGL_CASE(6)
+      GH_LGL_CASE(7) GH_LGL_CASE(8) GH_LGL_CASE(9) GH_LGL_CASE(10) GH_LGL_CASE(11) GH_LGL_CASE(12)
+      GH_LGL_CASE(13) GH_LGL_CASE(14) GH_LGL_CASE(15) GH_LGL_CASE(16)
+#undef GH_LGL_CASE
+      default: return set_err(GH_E_INVAL, "LGSSM d=%d not instantiated", pf->m->d);
+    }
     HIP_TRY(hipGetLastError());
     return GH_OK;
   }
@@ -1191,6 +1221,40 @@ static int set_qargs(double* dst, bool* has, int proposal, const double* q, int 
   return GH_OK;
 }
 
+// GH_PROPOSAL_LINEAR's arguments: P[d*d] Sigma_q[d*d] u[d] (P and chol(Sigma_q)
+// to the filter's device buffer), or u[d] alone, or none (keep everything)
+static int set_qlin(gh_pf* pf, const double* q, int nq) {
+  const int d = pf->D;
+  if (!q || nq == 0) {
+    if (!pf->has_qlin)
+      return set_err(GH_E_INVAL, "the linear proposal needs (P[d*d], Sigma_q[d*d], u[d]) first");
+    return GH_OK;
+  }
+  if (nq == d) {
+    if (!pf->has_qlin) return set_err(GH_E_INVAL, "the linear proposal needs (P[d*d], Sigma_q[d*d], u[d]) first");
+    pf->qlin_u.assign(q, q + d);
+    return GH_OK;
+  }
+  if (nq != 2 * d * d + d)
+    return set_err(GH_E_INVAL, "linear proposal arguments: P[d*d] Sigma_q[d*d] u[d] (%d values) or u[d] (%d), got %d",
+                   2 * d * d + d, d, nq);
+  std::vector<double> buf(2 * d * d);
+  for (int i = 0; i < d * d; ++i) buf[i] = q[i];
+  if (chol(d, q + d * d, buf.data() + d * d))
+    return set_err(GH_E_INVAL, "linear proposal: Sigma_q is not positive definite");
+  for (int i = 0; i < 2 * d * d; ++i)
+    if (!std::isfinite(buf[i])) return set_err(GH_E_INVAL, "linear proposal: non-finite P or Sigma_q");
+  if (!pf->qlin && hipMalloc(&pf->qlin, sizeof(double) * 2 * d * d) != hipSuccess)
+    return set_err(GH_E_NOMEM, "linear proposal buffer");
+  // ordered on the filter's stream; synchronous so that buf may go (off the hot path)
+  HIP_TRY(hipMemcpyAsync(pf->qlin, buf.data(), sizeof(double) * 2 * d * d, hipMemcpyHostToDevice, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  pf->cstq = gauss_cst(d, buf.data() + d * d);
+  pf->qlin_u.assign(q + 2 * d * d, q + 2 * d * d + d);
+  pf->has_qlin = true;
+  return GH_OK;
+}
+
 extern "C" int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_particles, uint64_t seed,
                                       const gh_pf_opts* opts, const double* ref_x1, gh_pf** out) {
   if (!m || !ref_x1 || !out) return set_err(GH_E_INVAL, "gh_pf_init_conditional: null argument");
@@ -1206,7 +1270,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (!m || !out) return set_err(GH_E_INVAL, "gh_pf_init: null argument");
   double q0[4] = {0, 0, 0, 0};
   bool has_q = false;
-  CHECK(set_qargs(q0, &has_q, proposal, qargs, nq));
+  if (proposal != GH_PROPOSAL_LINEAR) CHECK(set_qargs(q0, &has_q, proposal, qargs, nq));
   if (n_particles < 1 || n_particles > 0x7fffffffLL)
     return set_err(GH_E_INVAL, "gh_pf_init: num_particles must be in 1..2^31-1");
   if (!proposal_ok(m, proposal))
@@ -1317,10 +1381,12 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   }
   StepObs o, o_prior;
   int rc = make_obs(m, 1, obs, &o_prior);
+  if (!rc && proposal == GH_PROPOSAL_LINEAR) rc = set_qlin(pf, qargs, nq);
   if (!rc) {
     o = o_prior;
     if (proposal == GH_PROPOSAL_OPTIMAL && m->family == GH_FAMILY_LGSSM) rc = make_obs_opt(m, 1, obs, &o);
     if (proposal == GH_PROPOSAL_GAUSSIAN) rc = make_obs_gauss(m, 1, obs, pf->qargs, &o);
+    if (proposal == GH_PROPOSAL_LINEAR) rc = make_obs_lin(m, 1, obs, pf->qlin_u.data(), &o);
   }
   if (rc) return fail(rc);
   StepArgs a{};
@@ -1368,9 +1434,15 @@ static void log_raw_obs(gh_pf* pf, int t, const gh_obs* obs) {
 
 static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double* pin_ref);
 
+// a step's proposal arguments: the Gaussian (nonlinear SSM) or linear (LGSSM) custom proposal's
+static int step_qargs(gh_pf* pf, int proposal, const double* q, int nq) {
+  if (proposal == GH_PROPOSAL_LINEAR) return proposal_ok(pf->m, proposal) ? set_qlin(pf, q, nq) : GH_OK;
+  return set_qargs(pf->qargs, &pf->has_q, proposal, q, nq);
+}
+
 extern "C" int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal) {
   if (pf && pf->cond) return set_err(GH_E_STATE, "a conditional filter steps with gh_pf_step_conditional");
-  if (pf) CHECK(set_qargs(pf->qargs, &pf->has_q, proposal, nullptr, 0));
+  if (pf) CHECK(step_qargs(pf, proposal, nullptr, 0));
   return pf_step_impl(pf, obs, proposal, nullptr);
 }
 
@@ -1378,7 +1450,7 @@ extern "C" int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const do
                             int n_proposal_args) {
   if (!pf) return set_err(GH_E_INVAL, "null pf");
   if (pf->cond) return set_err(GH_E_STATE, "a conditional filter steps with gh_pf_step_conditional");
-  CHECK(set_qargs(pf->qargs, &pf->has_q, proposal, proposal_args, n_proposal_args));
+  CHECK(step_qargs(pf, proposal, proposal_args, n_proposal_args));
   return pf_step_impl(pf, obs, proposal, nullptr);
 }
 
@@ -1402,6 +1474,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   o = o_prior;
   if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family == GH_FAMILY_LGSSM) CHECK(make_obs_opt(pf->m, t, obs, &o));
   if (proposal == GH_PROPOSAL_GAUSSIAN) CHECK(make_obs_gauss(pf->m, t, obs, pf->qargs, &o));
+  if (proposal == GH_PROPOSAL_LINEAR) CHECK(make_obs_lin(pf->m, t, obs, pf->qlin_u.data(), &o));
   StepArgs a{};
   a.xprev = slot_x(pf, t - 1);
   a.anc = anc_for_step(pf, t);
@@ -2134,7 +2207,7 @@ extern "C" int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_
       nm->v != m->v)
     return set_err(GH_E_INVAL, "gh_pf_step_params: the new parameters must be of the same family and dimensions");
   if (!proposal_ok(nm, proposal)) return set_err(GH_E_INVAL, "gh_pf_step_params: proposal %d not available", proposal);
-  CHECK(set_qargs(pf->qargs, &pf->has_q, proposal, nullptr, 0));
+  CHECK(step_qargs(pf, proposal, nullptr, 0));
   CHECK(scores_ready(pf, "gh_pf_step_params"));
   const int T = pf->t;
   const int64_t n = pf->n;

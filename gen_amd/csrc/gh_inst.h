@@ -30,7 +30,9 @@
 
 #define GH_LGO_KERNELS(X, D)                                                                                   \
   X __global__ void gh::k_step<gh::LGOptModel<D>, true>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
-  X __global__ void gh::k_step<gh::LGOptModel<D>, false>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs);
+  X __global__ void gh::k_step<gh::LGOptModel<D>, false>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::LGLinModel<D>, true>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::LGLinModel<D>, false>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs);
 
 #define GH_LG_DIM(X, D)      \
   GH_LG_KERNELS(X, D, 0)     \

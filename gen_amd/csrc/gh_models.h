@@ -67,6 +67,11 @@ struct LGParams {
   const double* H;    // dy*d  observation matrix  (simulate: y = H x + c + L_R z)
   const double* cv;   // dy    observation offset c
   const double* LR;   // dy*dy lower Cholesky factor of R
+  // user-parameterised linear-Gaussian proposal (LGLinModel): the filter's own
+  // buffer, absolute pointers (not rebased): QP d*d, QL d*d chol(Sigma_q)
+  const double* QP = nullptr;
+  const double* QL = nullptr;
+  double cstq = 0.0;  // -0.5 (d log 2pi + log det Sigma_q)
   int dy;
   double cstR;        // -0.5 (dy log 2pi + log det R)
   double cstS;        // -0.5 (dy log 2pi + log det S)
@@ -291,6 +296,79 @@ struct LGOptModel {
       quad = fma(u, u, quad);
     }
     return p.cstS - 0.5 * quad;
+  }
+};
+
+// --------------------------------- LGSSM, user-parameterised linear proposal
+// A custom proposal in Gen's sense (particle_filter.jl:79-91,139-154 via the
+// SimpleExtendingTraceTranslator, trace_translators.jl:775-802) whose
+// arguments the caller supplies: q(x_t | x_{t-1}) = N(P x_{t-1} + u_t, Sigma_q)
+// (t = 1: N(u_1, Sigma_q)), P and chol(Sigma_q) in the filter's buffer, u_t
+// per step in o.v[dy + i] (after the observation's L_R^{-1}(y - c)).  The
+// weight is the translator's model weight - proposal score:
+//   log p(x_t | x_{t-1}) + log p(y_t | x_t) - log q(x_t)
+// with the model's densities as the trace's score columns compute them
+// (LGModel<D, 0>::score) and q's logpdf of the drawn value by forward
+// substitution.
+template <int D>
+struct LGLinModel {
+  static constexpr int kD = D;
+  static constexpr int kMinWaves = (D <= 4) ? 8 : (D <= 8 ? 5 : (D <= 14 ? 4 : 3));
+  using Params = LGParams;
+  using Prior = LGModel<D, 0>;
+
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return Prior::loglik(p, o, x); }
+
+  // x = mean + L_q z with mean = u (+ P xp); returns log q(x) recomputing the
+  // mean in the same order (the logpdf of the value, as mvnormal.jl:14 scores it)
+  __device__ static double draw(const Params& p, const StepObs& o, const double* xp, const double* z, double* x) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = o.v[p.dy + i];
+      if (xp) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc = fma(p.QP[i * D + k], xp[k], acc);
+      }
+#pragma unroll
+      for (int k = 0; k <= i; ++k) acc = fma(p.QL[i * D + k], z[k], acc);
+      x[i] = acc;
+    }
+    double w[D];
+    double quad = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double mean = o.v[p.dy + i];
+      if (xp) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) mean = fma(p.QP[i * D + k], xp[k], mean);
+      }
+      double r = x[i] - mean;
+#pragma unroll
+      for (int k = 0; k < i; ++k) r = fma(-p.QL[i * D + k], w[k], r);
+      w[i] = r / p.QL[i * D + i];
+      quad = fma(w[i], w[i], quad);
+    }
+    return p.cstq - 0.5 * quad;
+  }
+
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, int /*proposal*/,
+                                double* x, Draw dr = {STREAM_INIT, 0}) {
+    double z[D + 1];
+    normals_n<D>(seed, pid, 1, dr.stream, dr.base, z, dr.tab);
+    const double lq = draw(p, o, nullptr, z, x);
+    double lat, ob;
+    Prior::score(p, o, 1, x, x, &lat, &ob);
+    return (lat + ob) - lq;
+  }
+
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, uint32_t t,
+                                int /*proposal*/, const double* xp, double* x, Draw dr = {STREAM_STEP, 0}) {
+    double z[D + 1];
+    normals_n<D>(seed, pid, t, dr.stream, dr.base, z, dr.tab);
+    const double lq = draw(p, o, xp, z, x);
+    double lat, ob;
+    Prior::score(p, o, t, xp, x, &lat, &ob);
+    return (lat + ob) - lq;
   }
 };
 

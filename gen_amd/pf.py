@@ -54,7 +54,25 @@ class GaussianProposal:
     (trace_translators.jl:775-802)."""
 
 
+class LinearGaussianProposal:
+    """The LG-SSM's user-parameterised custom proposal (the same translator):
+
+        @gen function linear_proposal(trace, P, Sigma_q, u)
+            x_prev = trace[:chain => t - 1 => :x]          # absent at t = 1
+            @trace(mvnormal(P * x_prev + u, Sigma_q), :chain => t => :x)
+
+    proposal_args = (P, Sigma_q, u) — or (u,) alone to keep P and Sigma_q
+    (e.g. a data-driven mean offset per step).  weight = model score of the
+    new choices - proposal score."""
+
+
 def _qargs(proposal, proposal_args):
+    if proposal is LinearGaussianProposal or isinstance(proposal, LinearGaussianProposal):
+        if not proposal_args:
+            return None, 0
+        parts = [np.asarray(a, dtype=np.float64).ravel() for a in proposal_args]
+        a = np.ascontiguousarray(np.concatenate(parts))
+        return a, a.size
     if not (proposal is GaussianProposal or isinstance(proposal, GaussianProposal)):
         return None, 0
     a = np.ascontiguousarray(proposal_args, dtype=np.float64)
@@ -175,6 +193,8 @@ def _proposal_code(proposal) -> int:
         return _lib.PROPOSAL_OPTIMAL
     if proposal is GaussianProposal or isinstance(proposal, GaussianProposal):
         return _lib.PROPOSAL_GAUSSIAN
+    if proposal is LinearGaussianProposal or isinstance(proposal, LinearGaussianProposal):
+        return _lib.PROPOSAL_LINEAR
     raise _lib.GenHipError(1, f"unsupported proposal {proposal!r}: the engine lowers the model's default "
                               "proposal and the locally optimal proposal")
 

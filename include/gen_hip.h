@@ -107,6 +107,12 @@ typedef enum {
                               775-802): x_t ~ normal(alpha m + beta y_t + gamma, sigma_q),
                               m the prior mean; proposal_args = (alpha, beta, gamma, sigma_q)
                               through gh_pf_init_q / gh_pf_step_q; weight log p(x_t|x_{t-1})
+                              + log p(y_t|x_t) - log q(x_t) */,
+  GH_PROPOSAL_LINEAR = 3  /* user-parameterised custom proposal of the LGSSM (the same
+                              translator): x_t ~ mvnormal(P x_{t-1} + u_t, Sigma_q) (t = 1:
+                              mvnormal(u_1, Sigma_q)); proposal_args = P[d*d] Sigma_q[d*d] u[d]
+                              (required at gh_pf_init_q), or u[d] alone to keep P and Sigma_q
+                              (none: keep u too); d + dy <= 32; weight log p(x_t|x_{t-1})
                               + log p(y_t|x_t) - log q(x_t) */
 } gh_proposal;
 

@@ -331,12 +331,17 @@ typedef struct {
      1/(2 sigma_q^2), -0.5 log(2 pi sigma_q^2) */
   double mu1, s1, sx, sy, inv2vy, csty, inv2vx, cstx, inv2v1, cst1;
   double qa[6];
+  /* LGSSM, the user-parameterised linear-Gaussian proposal N(P x_{t-1} + u, Sigma_q):
+     P, chol(Sigma_q), its log-normaliser, the next steps' u (orc_pf_set_proposal_args) */
+  int qlin;
+  double *QP, *QL, cstq, qu[64];
   /* regression (quickstart.jl:3-9): priors, 1/(2 sigma^2), -0.5 log(2 pi sigma^2), xs */
   double mu_s, sd_s, mu_i, sd_i, sigma, inv2v, cst, inv2s, csts, inv2i, csti;
   double xs[32];
 } model_t;
 
 static void model_free(model_t* m) {
+  free(m->QP); free(m->QL);
   free(m->A); free(m->b); free(m->LQ); free(m->M); free(m->LR); free(m->c); free(m->mu0);
   free(m->L0); free(m->prior); free(m->T); free(m->E); free(m->logE);
   free(m->H); free(m->LS); free(m->Kt); free(m->FA); free(m->Fb); free(m->LSig); free(m->WA); free(m->Wb);
@@ -608,6 +613,33 @@ static double kit_z(uint64_t seed, uint64_t pid, uint32_t t, uint32_t stream, ui
   return ((pid >> 6) & 1) ? z1 : z0;
 }
 
+static void model_score(const model_t* m, const obs_t* o, int t, const double* xp, const double* x, double* lat,
+                        double* ob);
+
+/* The linear proposal's draw x = u (+ P xp) + L_q z and its logpdf at x (the
+   mean recomputed in the same order, forward substitution with L_q) */
+static double lin_draw(const model_t* m, const double* xp, const double* z, double* x) {
+  const int d = m->d;
+  for (int i = 0; i < d; ++i) {
+    double acc = m->qu[i];
+    if (xp)
+      for (int k = 0; k < d; ++k) acc = fma(m->QP[i * d + k], xp[k], acc);
+    for (int k = 0; k <= i; ++k) acc = fma(m->QL[i * d + k], z[k], acc);
+    x[i] = acc;
+  }
+  double w[64], quad = 0.0;
+  for (int i = 0; i < d; ++i) {
+    double mean = m->qu[i];
+    if (xp)
+      for (int k = 0; k < d; ++k) mean = fma(m->QP[i * d + k], xp[k], mean);
+    double r = x[i] - mean;
+    for (int k = 0; k < i; ++k) r = fma(-m->QL[i * d + k], w[k], r);
+    w[i] = r / m->QL[i * d + i];
+    quad = fma(w[i], w[i], quad);
+  }
+  return m->cstq - 0.5 * quad;
+}
+
 static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
                             int proposal, double* x, uint32_t stream, uint32_t base) {
   if (m->family == ORC_REGRESSION) {
@@ -620,6 +652,12 @@ static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const
   if (m->family == ORC_LGSSM) {
     double z[64];
     normals_at(seed, pid, 1, stream, base, m->d, z);
+    if (proposal == ORC_PROPOSAL_LINEAR) {  /* custom proposal: model weight - proposal score */
+      const double lq = lin_draw(m, NULL, z, x);
+      double lat, ob;
+      model_score(m, o, 1, x, x, &lat, &ob);
+      return (lat + ob) - lq;
+    }
     if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
       /* x ~ N(mu1, (I - K1 H) P0); weight log N(y; H mu0 + c, H P0 H^T + R) */
       for (int i = 0; i < m->d; ++i) {
@@ -669,6 +707,12 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
     double z[64];
     normals_at(seed, pid, t, stream, base, m->d, z);
     int d = m->d;
+    if (proposal == ORC_PROPOSAL_LINEAR) {
+      const double lq = lin_draw(m, xp, z, x);
+      double lat, ob;
+      model_score(m, o, (int)t, xp, x, &lat, &ob);
+      return (lat + ob) - lq;
+    }
     if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
       /* x ~ N(F A xp + g, Sigma); weight log p(y | xp) = log N(y; H (A xp + b) + c, S) */
       for (int i = 0; i < d; ++i) {
@@ -821,9 +865,29 @@ static int init_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
 static int proposal_ok(const model_t* m, int proposal) {
   if (proposal == 0) return 1;
   if (proposal == ORC_PROPOSAL_GAUSSIAN) return m->family == ORC_KITAGAWA && m->qa[3] > 0.0;
+  if (proposal == ORC_PROPOSAL_LINEAR) return m->family == ORC_LGSSM && m->qlin && m->d + m->dy <= 32;
   return proposal == ORC_PROPOSAL_OPTIMAL && (m->family == ORC_HMM || (m->family == ORC_LGSSM && m->opt));
 }
 int orc_pf_set_proposal_args(orc_pf* pf, const double* args, int n) {
+  model_t* m = &pf->m;
+  if (m->family == ORC_LGSSM) {  /* the linear proposal: P Sigma_q u, or u alone */
+    const int d = m->d;
+    if (n == d && m->qlin) {
+      for (int i = 0; i < d; ++i) m->qu[i] = args[i];
+      return 0;
+    }
+    if (n != 2 * d * d + d) return -1;
+    double* L = malloc(sizeof(double) * d * d);
+    if (chol(d, args + d * d, L)) { free(L); return -1; }
+    free(m->QP); free(m->QL);
+    m->QP = malloc(sizeof(double) * d * d);
+    for (int i = 0; i < d * d; ++i) m->QP[i] = args[i];
+    m->QL = L;
+    m->cstq = gauss_cst(d, L);
+    for (int i = 0; i < d; ++i) m->qu[i] = args[2 * d * d + i];
+    m->qlin = 1;
+    return 0;
+  }
   if (n != 4 || !(args[3] > 0.0)) return -1;
   double v = args[3] * args[3];
   pf->m.qa[0] = args[0]; pf->m.qa[1] = args[1]; pf->m.qa[2] = args[2]; pf->m.qa[3] = args[3];
@@ -1281,13 +1345,14 @@ int orc_pf_get_scores(orc_pf* pf, double* total, double* per_step) {
    the history (one shard). */
 int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const double* obs, int has_obs, int proposal) {
   if (pf->cond || pf->t < 1 || !pf->record_history || pf->lo != 0 || pf->n != pf->n_global) return -1;
+  if (proposal == ORC_PROPOSAL_LINEAR && !pf->m.qlin) return -1;
   model_t m2;
   const model_t* m = &pf->m;
   if (model_build(&m2, m->family, m->d, m->dy, m->k, m->v, params, np)) {
     model_free(&m2);
     return -1;
   }
-  if (!proposal_ok(&m2, proposal)) {
+  if (proposal != ORC_PROPOSAL_LINEAR && !proposal_ok(&m2, proposal)) {  /* (the linear one: the filter's args) */
     model_free(&m2);
     return -1;
   }
@@ -1299,6 +1364,14 @@ int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const doubl
   double* new_tot = malloc(sizeof(double) * (size_t)(n ? n : 1));
   scores_with(pf, &pf->m, pf->hobs, old_tot, NULL);
   scores_with(pf, &m2, o2, new_tot, NULL);
+  /* the proposal arguments are the filter's: they carry over */
+  memcpy(m2.qa, pf->m.qa, sizeof m2.qa);
+  m2.qlin = pf->m.qlin;
+  m2.QP = pf->m.QP;
+  m2.QL = pf->m.QL;
+  m2.cstq = pf->m.cstq;
+  memcpy(m2.qu, pf->m.qu, sizeof m2.qu);
+  pf->m.QP = pf->m.QL = NULL;
   model_free(&pf->m);
   pf->m = m2;
   memcpy(pf->hobs, o2, sizeof(obs_t) * (size_t)T);

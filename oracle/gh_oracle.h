@@ -39,7 +39,7 @@ extern "C" {
 
 enum { ORC_LGSSM = 1, ORC_HMM = 2, ORC_KITAGAWA = 3, ORC_REGRESSION = 4 };
 enum { ORC_SYSTEMATIC = 0, ORC_MULTINOMIAL = 1 };
-enum { ORC_PROPOSAL_DEFAULT = 0, ORC_PROPOSAL_OPTIMAL = 1, ORC_PROPOSAL_GAUSSIAN = 2 };
+enum { ORC_PROPOSAL_DEFAULT = 0, ORC_PROPOSAL_OPTIMAL = 1, ORC_PROPOSAL_GAUSSIAN = 2, ORC_PROPOSAL_LINEAR = 3 };
 
 typedef struct orc_pf orc_pf;
 

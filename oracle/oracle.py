@@ -20,7 +20,7 @@ OMP_PATH = os.path.join(HERE, "liboracle_omp.so")  # the same oracle on every ho
 
 LGSSM, HMM, KITAGAWA, REGRESSION = 1, 2, 3, 4
 SYSTEMATIC, MULTINOMIAL = 0, 1
-DEFAULT, OPTIMAL, GAUSSIAN = 0, 1, 2
+DEFAULT, OPTIMAL, GAUSSIAN, LINEAR = 0, 1, 2, 3
 
 _lib = None
 _libs = {}
