@@ -6,8 +6,8 @@ weight log p(x_t | x_{t-1}) + log p(y_t | x_t) - log q(x_t)
 
 CPU: the oracle's weights against scipy's multivariate-normal densities, its
 draws are q's (whitened residuals standard normal), the proposal equal to the
-prior reproduces the bootstrap filter's states and weights.  GPU: bit-exact against the oracle with arguments changing
-between steps (full and u-only forms), a step without observation, a
+prior reproduces the bootstrap filter's states and weights.
+GPU: bit-exact against the oracle with arguments changing between steps (full and u-only forms), a step without observation, a
 parameter change on top, argument errors."""
 import numpy as np
 import pytest
@@ -120,6 +120,14 @@ def test_gpu_linear_proposal_bitexact(gh_ctx, name):
     assert abs(a - b) <= 1e-9 * abs(b)
     # the trace scores are the model's, whatever proposal made the particles
     assert np.array_equal(gen.get_traces(st).scores().view(np.uint64), orc.scores().view(np.uint64))
+    # a parameter change on top: the filter keeps its proposal arguments
+    m2 = gen.LinearGaussianSSM(0.8 * m.A, 1.5 * m.Q, m.H, 0.7 * m.R, m.mu0, m.P0, b=m.b, c=m.c)
+    t = len(ys) + 1
+    gen.particle_filter_step(st, (t, m2), (gen.UnknownChange(), gen.UnknownChange()), {m.obs_address(t): ys[1]},
+                             gen.LinearGaussianProposal)
+    orc.step_params(m2, ys[1], O.LINEAR)
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
     st.close()
 
 
