@@ -59,7 +59,8 @@ class PFOpts(ctypes.Structure):
         ("history_capacity", c_int32),
         ("block_size", c_int32),
         ("time_kernels", c_int32),
-        ("reserved", c_int32 * 3),
+        ("exact_quantisation", c_int32),
+        ("reserved", c_int32 * 2),
     ]
 
 
