@@ -1,6 +1,6 @@
 # round-4 GPU check: new multi-rank paths first, then the whole GPU suite, the bench, C3 window variants
 mkdir -p gpurun_out/r4a
-timeout -k 10 600 python -u -m pytest tests/test_multirank.py tests/test_coal.py tests/test_unfold_kats_device.py tests/test_step_params.py tests/test_lg_linear_proposal.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r4a/mr.log 2>&1 && \
+timeout -k 10 600 python -u -m pytest tests/test_coal.py tests/test_unfold_kats_device.py tests/test_step_params.py tests/test_lg_linear_proposal.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r4a/mr.log 2>&1 && \
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r4a/gputest.log 2>&1 && \
 timeout -k 10 400 python bench.py > gpurun_out/r4a/bench.log 2>&1 && \
 for v in base coal_w10 coal_w7; do
