@@ -144,9 +144,11 @@ def test_gpu_outlier_observations_fall_back(gh_ctx):
 @pytest.mark.gpu
 def test_gpu_bound_path_across_block_sizes(gh_ctx):
     """Particle counts at and around the pairs kernel's and k_step's block
-    boundaries, and the first-step bound (no earlier weights)."""
+    boundaries, and the first-step bound (no earlier weights).  One particle
+    never takes the bound path (its total reaches 2^shift only if its weight
+    equals U), so there the test is the exact path's parity alone."""
     m = KitagawaSSM(10.0, 1.0)
     _, ys = m.simulate(5, np.random.default_rng(9))
     ys = [float(y) for y in ys]
     for n in (1, 63, 512, 513, 4096, 65537):
-        assert _gpu_vs_oracle(m, ys, n, 2, O.SYSTEMATIC, False, n + 1) >= 3
+        assert _gpu_vs_oracle(m, ys, n, 2, O.SYSTEMATIC, False, n + 1) >= (0 if n == 1 else 3)
