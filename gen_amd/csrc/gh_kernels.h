@@ -1173,9 +1173,10 @@ struct Resample1Args {
   uint32_t t;
 };
 
-// The bound path quantises against U when every weight is at most U and the
-// total against U is at least 2^shift (the floor then misallocates at most
-// n 2^-shift of the mass, as the exact path at worst); otherwise against M.
+// The bound path's gap: the reference U may exceed the weights' max M by up to
+// 20 ln 2 (the heaviest particle keeps >= 2^(shift - 20) quantisation levels);
+// past that, or when a weight exceeded U, the resample quantises against M.
+constexpr double kUGap = 0x1.bb9d3beb8c86bp+3;  // 20 ln 2
 constexpr int64_t kBoundMaxN = (int64_t)1 << 22;  // particles per rank of the bound path (its tiles co-resident)
 
 // 1024-thread block reductions (16 waves), result broadcast; LDS-only
@@ -1503,9 +1504,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     if (threadIdx.x == 0) {
       sfire = m_ok && ((S1 * S1) / S2 < r.d.thr);
       // the bound path (uniform: every block folds the same totals): every
-      // weight at most U and the integer total at least 2^shift, so the
-      // floor's misallocated mass n / total is no larger than the exact
-      // path's worst case (its maximum alone quantises to 2^shift)
+      // weight at most U, U within kUGap of the max, some weight quantised
       int up = 0;
       if (r.btot) {
         uint64_t ta = 0, tb = 0;
@@ -1517,7 +1516,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
           inv = inv || sbt[2][k] != 0;
         }
         const double U = sU;
-        up = !inv && m_ok && U < INFINITY && M <= U && ta >= ((uint64_t)1 << r.shift);
+        up = !inv && m_ok && U < INFINITY && M <= U && M - U >= -kUGap && ta > 0;
         sua = ta;
         sub = tb;
       }

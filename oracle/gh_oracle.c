@@ -780,6 +780,9 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
 }
 
 /* ---------------------------------------------------------- PF state */
+/* the bound path's gap: U within 20 ln 2 of the weights' maximum */
+#define ORC_UGAP 0x1.bb9d3beb8c86bp+3
+
 struct orc_pf {
   model_t m;
   int64_t n_global, lo, n;
@@ -794,8 +797,7 @@ struct orc_pf {
   int pending;          /* resampled since the last step */
   /* the bound path of the resample: one shard of at most 2^22
      particles quantises against U, the step's a-priori weight bound, when
-     every weight is at most U and the total quantised against U is at least
-     2^shift */
+     every weight is at most U and U is within 20 ln 2 of the maximum */
   int bound_on;
   double U;             /* this step's bound (+inf: none) */
   int decided;          /* a maybe_resample since the last step */
@@ -1275,16 +1277,13 @@ int orc_pf_maybe_resample(orc_pf* pf, double thr, double* ess_out) {
   /* the quantisation reference: U on the bound path, else the maximum */
   double R = M;
   const double U = pf->U;
-  /* (the engine's k_resample1: every weight at most U and the total quantised
-     against U at least 2^shift, so the floor misallocates at most n / 2^shift
-     of the mass, the exact path's worst case) */
-  if (first && !pf->pending && U > -INFINITY && U < INFINITY && M <= U) {
+  if (first && !pf->pending && U > -INFINITY && U < INFINITY && M <= U && M - U >= -ORC_UGAP) {
     int ok = 1;
     for (int64_t i = 0; i < pf->n && ok; ++i) {
       const double w = pf->logw[i];
       if (w > -INFINITY && !(w - U <= 0.0)) ok = 0;
     }
-    if (ok && orc_pf_local_qtotal(pf, U) >= (1ull << qshift((uint64_t)pf->n_global))) { R = U; pf->bound_uses++; }
+    if (ok && orc_pf_local_qtotal(pf, U) > 0) { R = U; pf->bound_uses++; }
   }
   M = R;
   uint64_t tot = orc_pf_local_qtotal(pf, M);

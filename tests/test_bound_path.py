@@ -3,17 +3,15 @@
 A one-rank filter quantises the weights against the a-priori bound
 U = (the last decision's maximum, or 0 after a resample) + the step's weight
 bound (the observation density's maximum) instead of their maximum M, when
-every weight is <= U and the integer total against U is at least 2^shift
-(so the floor misallocates at most n 2^-shift of the mass, the exact path's
-worst case): then k_step's per-block integer totals are the resample's, and
-k_resample1 runs without its grid barrier.  Otherwise (an outlier
-observation, a proposal without a bound, a second decision on the same
-weights, N > 2^22) it quantises against M as before.
+every weight is <= U and M - U >= -20 ln 2: then k_step's per-block integer
+totals are the resample's, and k_resample1 runs without its grid barrier.
+Otherwise (an outlier observation, a proposal without a bound, a second
+decision on the same weights, N > 2^22) it quantises against M as before.
 
 The bound path changes which uniform falls in which particle only at the
-quantisation's rounding, so its parents equal the exact path's except at
-such ties, and the filter's law is the exact path's (log-ML over seeds); the
-fall-back cases are bit-identical to the exact path.  CPU: the oracle's two rules.  GPU: the engine bit-exact against
+quantisation's rounding (relative 2^-32 at worst), so its parents equal the
+exact path's except at such ties; the fall-back cases are bit-identical to the
+exact path.  CPU: the oracle's two rules.  GPU: the engine bit-exact against
 the oracle under both rules (gh_pf_opts.exact_quantisation).
 """
 import numpy as np
