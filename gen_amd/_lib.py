@@ -59,8 +59,7 @@ class PFOpts(ctypes.Structure):
         ("history_capacity", c_int32),
         ("block_size", c_int32),
         ("time_kernels", c_int32),
-        ("exact_quantisation", c_int32),
-        ("reserved", c_int32 * 2),
+        ("reserved", c_int32 * 3),
     ]
 
 

@@ -369,7 +369,6 @@ struct gh_model {
   double* dparams = nullptr;  // device copy of the derived parameters
   // host copies needed per step
   std::vector<double> LR, c;  // LGSSM: chol(R), offset c
-  std::vector<double> logEmax; // HMM: max_z log E[x | z] per symbol x (the weight bound, StepObs.ub)
   // LGSSM locally optimal proposal (LGOptModel): host halves
   bool lg_opt = false;        // derivable (S, Sigma positive definite, d + dy <= kMaxObs)
   std::vector<double> LS, Kt, Fb, Wb;       // chol(S), K^T (dy x d), F b, L_S^-1 H b
@@ -498,9 +497,6 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->d = 1;
     h.insert(h.end(), p, p + K + K * K + V * K);  // prior | T | E
     for (int i = 0; i < V * K; ++i) h.push_back(gh_log(p[K + K * K + i]));  // logE
-    m->logEmax.assign(V, -INFINITY);
-    for (int x = 0; x < V; ++x)
-      for (int z = 0; z < K; ++z) m->logEmax[x] = std::max(m->logEmax[x], h[K + K * K + V * K + x * K + z]);
     m->hmm.k = K;
     m->hmm.v = V;
   } else if (desc->family == GH_FAMILY_KITAGAWA) {
@@ -590,18 +586,11 @@ extern "C" int gh_model_state_dim(const gh_model* m, int* d) {
 }
 
 // host preprocessing of one step's observation
-// The prior-form observation of step t.  o->ub bounds the model's own weight
-// increment log p(y_t | x_t) from above (0 without an observation): LGSSM
-// cst_R (the quadratic form is >= 0), the nonlinear SSM its normal's constant,
-// the HMM max_z log E[y_t | z]; the regression has no steps (+inf: no bound).
 static int make_obs(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
   memset(o, 0, sizeof(*o));
   o->present = (in && in->present && in->values) ? 1 : 0;
-  o->ub = m->family == GH_FAMILY_REGRESSION ? INFINITY : 0.0;
   if (m->family == GH_FAMILY_KITAGAWA) o->ct = 8.0 * gh_cos(1.2 * (double)t);
   if (!o->present) return GH_OK;
-  if (m->family == GH_FAMILY_LGSSM) o->ub = m->lg.cstR;
-  if (m->family == GH_FAMILY_KITAGAWA) o->ub = m->kit.csty;
   if (m->family == GH_FAMILY_LGSSM) {
     if (in->n_values != m->dy) return set_err(GH_E_INVAL, "observation has %d values, dy = %d", in->n_values, m->dy);
     double r[kMaxObs];
@@ -616,7 +605,6 @@ static int make_obs(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
       return set_err(GH_E_INVAL, "HMM observation %g is not a symbol in 0..%d", s, m->v - 1);
     o->v[0] = s;
     o->sym = (int)s;
-    o->ub = m->logEmax[o->sym];
   } else {
     o->v[0] = in->values[0];
   }
@@ -639,21 +627,6 @@ static int make_obs_gauss(const gh_model* m, int t, const gh_obs* in, const doub
 // The optimal proposal's per-step vectors (LGOptModel): t = 1: o.v[0, d) =
 // mu_1 = mu0 + K_1 (y - c - H mu0), o.ct = log N(y; H mu0 + c, S_1); t >= 2:
 // o.v[0, d) = g_t = F b + K (y - c), o.v[d, d + dy) = L_S^-1 (y - c) - L_S^-1 H b.
-// o.ub for the step's proposal (make_obs set the model's own bound): the
-// locally optimal proposals' weights log p(y_t | x_{t-1}) are bounded by cst_S
-// (t = 1: the constant weight itself) for the LGSSM and by max_z log E[y_t | z]
-// for the HMM (its sum over z in floating point may exceed that by an ulp: a
-// relative slack of 1e-12); the custom proposals' weights have no bound.  The
-// oracle's step_ub is the same function.
-static double step_ub(const gh_model* m, const StepObs& o, int proposal, int t) {
-  if (proposal == GH_PROPOSAL_GAUSSIAN || proposal == GH_PROPOSAL_LINEAR) return INFINITY;
-  if (proposal == GH_PROPOSAL_OPTIMAL && o.present) {
-    if (m->family == GH_FAMILY_LGSSM) return t == 1 ? o.ct : m->lg.cstS;
-    if (m->family == GH_FAMILY_HMM) return o.ub + 1e-12 * std::max(1.0, std::fabs(o.ub));
-  }
-  return o.ub;
-}
-
 // the observation with u_t of the linear proposal behind it (o.v[dy + i])
 static int make_obs_lin(const gh_model* m, int t, const gh_obs* in, const double* u, StepObs* o) {
   CHECK(make_obs(m, t, in, o));
@@ -741,10 +714,6 @@ struct gh_pf {
   int64_t nb_part = 0;             // block partials the last step kernel wrote (pair kernels: n / 512)
   bool pairs = false;             // the default step runs the pair kernel (512 particles per block)
   bool last_pairs = false;        // the last step kernel was the pair kernel
-  // the bound path of the one-rank resample: the step kernel's
-  // per-block totals of the weights quantised against its bound U
-  uint64_t* btot = nullptr;       // [nb_step] (nullptr: exact quantisation only)
-  bool btot_valid = false;        // the last step kernel wrote them for the current weights
   double *pm = nullptr, *ps = nullptr, *ps2 = nullptr;
   DevScalars* dev = nullptr;
   double* stats_all = nullptr;    // [3*world]
@@ -928,7 +897,6 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
   hipFree(pf->acc_count); hipFree(pf->pin); hipFree(pf->amax);
   hipFree(pf->amax_all); hipFree(pf->rec); hipFree(pf->recs_all); hipFree(pf->qlin);
-  hipFree(pf->btot);
   if (pf->aux) hipStreamDestroy(pf->aux);
   if (pf->ev_tot) hipEventDestroy(pf->ev_tot);
   if (pf->ev_plan) hipEventDestroy(pf->ev_plan);
@@ -1359,10 +1327,6 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   ALLOC(pf->tsum, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles));
   pick_resample_tiles(pf, n);
   ALLOC(pf->amax, sizeof(uint64_t) * 2 * kAmaxShards * kAmaxStride);
-  // the bound path: one rank, not conditional, up to kBoundMaxN particles (the
-  // one-launch resample's co-resident tiles cover them; the oracle's rule)
-  if (!mr(ctx) && !pin_ref && !pf->opts.exact_quantisation && pf->n <= kBoundMaxN && pf->n > 0)
-    ALLOC(pf->btot, sizeof(uint64_t) * pf->nb_step);
   if (mr(ctx)) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
@@ -1423,7 +1387,6 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     if (proposal == GH_PROPOSAL_OPTIMAL && m->family == GH_FAMILY_LGSSM) rc = make_obs_opt(m, 1, obs, &o);
     if (proposal == GH_PROPOSAL_GAUSSIAN) rc = make_obs_gauss(m, 1, obs, pf->qargs, &o);
     if (proposal == GH_PROPOSAL_LINEAR) rc = make_obs_lin(m, 1, obs, pf->qlin_u.data(), &o);
-    o.ub = step_ub(m, o, proposal, 1);
   }
   if (rc) return fail(rc);
   StepArgs a{};
@@ -1440,10 +1403,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   a.ps2 = pf->ps2;
   a.stats_out = !mr(ctx) ? pf->stats_all : pf->dev->stats;
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
-  a.btot = pf->btot;
-  a.shift = quant_shift((uint64_t)pf->n_global);
   rc = timed_step(pf, o, a, true);
-  pf->btot_valid = pf->btot != nullptr && pf->rs_grid > 0;
   if (rc) return fail(rc);
   if (pin_ref) {
     pf->cond = true;
@@ -1515,7 +1475,6 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   if (proposal == GH_PROPOSAL_OPTIMAL && pf->m->family == GH_FAMILY_LGSSM) CHECK(make_obs_opt(pf->m, t, obs, &o));
   if (proposal == GH_PROPOSAL_GAUSSIAN) CHECK(make_obs_gauss(pf->m, t, obs, pf->qargs, &o));
   if (proposal == GH_PROPOSAL_LINEAR) CHECK(make_obs_lin(pf->m, t, obs, pf->qlin_u.data(), &o));
-  o.ub = step_ub(pf->m, o, proposal, t);
   StepArgs a{};
   a.xprev = slot_x(pf, t - 1);
   a.anc = anc_for_step(pf, t);
@@ -1540,10 +1499,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   const bool multi = mr(pf->ctx);
   // multi-rank: a max-only step needs the shards (the rank maximum has no other fold)
-  // (one rank with the bound path: full partials, the resample folds them)
-  a.max_only = pf->step_max_only && !pin_ref && (!multi || pf->amax_armed) && !pf->btot ? 1 : 0;
-  a.btot = pin_ref ? nullptr : pf->btot;
-  a.shift = quant_shift((uint64_t)pf->n_global);
+  a.max_only = pf->step_max_only && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
   // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
   // short step more than the fold they save, measured)
   a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
@@ -1558,7 +1514,6 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   CHECK(timed_step(pf, o, a, false));
   if (pin_ref) CHECK(pin_launch(pf, o, false, false));
   if (!a.max_only) CHECK(share_stats(pf));  // (max-only: the resample's own all-gathers)
-  pf->btot_valid = a.btot != nullptr && pf->rs_grid > 0;
   pf->t = t;
   pf->max_only = a.max_only != 0;
   pf->amax_valid = a.amax != nullptr;
@@ -1869,8 +1824,6 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     ra.C = pf->C;
     ra.seed = pf->seed;
     ra.t = (uint32_t)t;
-    ra.btot = pf->btot_valid && !pf->max_only ? pf->btot : nullptr;
-    ra.btot_span = pf->last_pairs ? 2 * kBlock : kBlock;
     if (pf->amax) {  // the step's own max fold (when it wrote one); the next step's shards emptied
       ra.amax_in = pf->max_only && pf->amax_valid ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride : nullptr;
       ra.amax_reset = pf->amax + ((t + 1) & 1) * kAmaxShards * kAmaxStride;
@@ -2291,7 +2244,6 @@ extern "C" int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_
     pf->nb_part = pf->nb_step;
     pf->last_pairs = false;
     pf->stats_valid = false;
-    pf->btot_valid = false;  // the weights moved by Delta: the next resample quantises against the max
   }
   if (hipStreamSynchronize(pf->s) != hipSuccess && !rc) rc = set_err(GH_E_HIP, "gh_pf_step_params: sync");
   cleanup();

@@ -67,7 +67,6 @@ struct DevScalars {
   int cfire, cerr;
   unsigned bar_gen;    // k_resample1 / k_rank_a grid barriers completed
   int64_t ra, rb;      // multi-rank: local slots [0, ra) and [rb, n) take received rows
-  double U;            // the last step's weight bound (the quantisation reference of the bound path)
 
 };
 
@@ -109,16 +108,7 @@ struct StepArgs {
   // gets every per-slot pointer advanced by j0 slots (j0 = 0 otherwise).
   int part;              // host only: 0 one launch; 1, 2 the halves of a split step
   int64_t j0;            // slot offset of this launch (the received-row index only)
-  // the bound path of the next resample: every particle's weight
-  // quantised against U = (weights kept ? the last decision's max : 0) + o.ub,
-  // q = floor(exp(w - U) 2^shift), summed per block into btot[block]
-  // (kBtotInvalid when a weight exceeds U or U is not finite); nullptr: off
-  uint64_t* btot;
-  int shift;
 };
-
-constexpr uint64_t kBtotInvalid = ~0ull;
-
 
 // ------------------------------------------------------------ reductions
 // Wave-level reductions and scans on DPP lane moves (quad_perm, row_shr,
@@ -265,50 +255,6 @@ __device__ __forceinline__ void buf_st_f64x2(const double* in, __amdgpu_buffer_r
 // release fence would emit vmcnt(0) and expose every store's latency.)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// (uint64)x for 0 <= x <= 2^52 in three instructions: floor, then the integer
-// read off the mantissa of floor(x) + 2^52 (exact below 2^53); the generic
-// f64 -> u64 conversion is a dozen
-__device__ __forceinline__ uint64_t f64_to_u52(double x) {
-  return as_u64(floor(x) + 0x1p52) - 0x4330000000000000ull;
-}
-
-// U of this step (uniform): the increment bound on top of the weights' max
-// (0 after a resample or at init); +inf when no decision since the last step
-// tells that max
-__device__ __forceinline__ double step_bound(bool init, int pend, int resampled, double Mprev, double ub) {
-  if (init || pend) return ub;
-  return resampled ? Mprev + ub : INFINITY;
-}
-
-// one particle's quantised weight against U (0 for -inf / NaN weights); *bad:
-// the weight exceeds U (the bound failed: the resample takes the exact path)
-__device__ __forceinline__ uint64_t bound_q(double lw, double U, double qscale, bool* bad) {
-  if (!(lw > -INFINITY)) return 0;
-  const double x = lw - U;
-  const bool b = !(x <= 0.0);
-  *bad = *bad || b;
-  return b ? 0 : f64_to_u52(gh_exp_nonpos(x) * qscale);
-}
-
-// the block's q total (thread 0 stores it): wave sums, then 4 waves in order
-__device__ __forceinline__ void block_qtotal(uint64_t q, bool bad, uint64_t* smq, uint64_t* out) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t s = wave_sum_u64(q);
-  const bool anybad = __builtin_amdgcn_ballot_w64(bad) != 0;
-  if (lane == 0) smq[w] = anybad ? kBtotInvalid : s;
-  lds_barrier();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    bool inv = false;
-#pragma unroll
-    for (int k = 0; k < kBlock / 64; ++k) {
-      inv = inv || smq[k] == kBtotInvalid;
-      t += smq[k];
-    }
-    *out = inv ? kBtotInvalid : t;
-  }
-}
-
 // Block partial of the step kernel: the block max first (wave DPP max, then
 // the 4 waves through LDS), then every lane's e = exp(lw - max) and the wave
 // sums of e and e^2 — partial sums on one reference, so the 4 waves add
@@ -401,11 +347,9 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   // would be waited for right here)
   uint64_t mv = 0, cv = 0;
   int pending = 0, fire = 0;
-  double Mprev = 0.0;
   if (!INIT && a.resampled) {
     pending = a.dev->pending;
     fire = a.dev->fire;
-    if (a.btot) Mprev = a.dev->M;
     if (a.mark_mode) {
       const int64_t last = a.n > 0 ? a.n - 1 : 0;
       mv = a.mark[j < last ? j : last];
@@ -476,18 +420,6 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   }
   if (a.max_only) block_max_partial(lw, sm, a.pm + vb, a.amax, vb);
   else block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
-  if (a.btot) {  // the bound path's quantised weights (uniform branches)
-    __shared__ uint64_t smq[kBlock / 64];
-    const double U = step_bound(INIT, pending | fire, a.resampled, Mprev, o.ub);
-    if (vb == 0 && threadIdx.x == 0) a.dev->U = U;
-    if (U > -INFINITY && U < INFINITY) {
-      bool bad = false;
-      const uint64_t q = bound_q(lw, U, as_f64((uint64_t)(a.shift + 1023) << 52), &bad);
-      block_qtotal(q, bad, smq, a.btot + vb);
-    } else if (threadIdx.x == 0) {
-      a.btot[vb] = kBtotInvalid;
-    }
-  }
 }
 
 // k_step for one-dimensional models whose particles p, p + 64 share their
@@ -537,11 +469,9 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
   const int64_t j0 = tile0 * 64 + lane, j1 = j0 + 64;
   uint64_t mv0 = 0, mv1 = 0, cv0 = 0, cv1 = 0;
   int pending = 0, fire = 0;
-  double Mprev = 0.0;
   if (!INIT && a.resampled) {
     pending = a.dev->pending;
     fire = a.dev->fire;
-    if (a.btot) Mprev = a.dev->M;
     if (a.mark_mode) {
       const int64_t last = a.n > 0 ? a.n - 1 : 0, lt = last >> 6;
       mv0 = a.mark[j0 < last ? j0 : last];
@@ -619,19 +549,6 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
   }
   if (a.max_only) block_max_partial(fmax(lw0, lw1), sm, a.pm + vb, a.amax, vb);
   else block_partial2(lw0, lw1, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
-  if (a.btot) {  // the bound path (one total per 512-particle block)
-    __shared__ uint64_t smq[kBlock / 64];
-    const double U = step_bound(INIT, pending | fire, a.resampled, Mprev, o.ub);
-    if (vb == 0 && threadIdx.x == 0) a.dev->U = U;
-    if (U > -INFINITY && U < INFINITY) {
-      bool bad = false;
-      const double qs = as_f64((uint64_t)(a.shift + 1023) << 52);
-      const uint64_t q = bound_q(lw0, U, qs, &bad) + bound_q(lw1, U, qs, &bad);
-      block_qtotal(q, bad, smq, a.btot + vb);
-    } else if (threadIdx.x == 0) {
-      a.btot[vb] = kBtotInvalid;
-    }
-  }
 }
 
 // --------------------------------------------------------------- decision
@@ -1167,17 +1084,9 @@ struct Resample1Args {
   uint64_t* C;
   const uint64_t* amax_in; // the step's atomic-max shards (sums-in-pass only; nullptr: fold pm)
   uint64_t* amax_reset;    // the other parity's shards, emptied for the next step
-  const uint64_t* btot;    // the bound path: the step's per-block q totals against dev->U (nullptr: off)
-  int btot_span;           //   particles per total (256, or 512 for the pair kernel)
   uint64_t seed;
   uint32_t t;
 };
-
-// The bound path's gap: the reference U may exceed the weights' max M by up to
-// 20 ln 2 (the heaviest particle keeps >= 2^(shift - 20) quantisation levels);
-// past that, or when a weight exceeded U, the resample quantises against M.
-constexpr double kUGap = 0x1.bb9d3beb8c86bp+3;  // 20 ln 2
-constexpr int64_t kBoundMaxN = (int64_t)1 << 22;  // particles per rank of the bound path (its tiles co-resident)
 
 // 1024-thread block reductions (16 waves), result broadcast; LDS-only
 // barriers (outstanding global loads/stores are not waited for)
@@ -1330,6 +1239,12 @@ __device__ __forceinline__ double blk16_max1(double v, double* sm) {
   return sm[16];
 }
 
+// (uint64)x for 0 <= x <= 2^52 in three instructions: floor, then the integer
+// read off the mantissa of floor(x) + 2^52 (exact below 2^53); the generic
+// f64 -> u64 conversion is a dozen
+__device__ __forceinline__ uint64_t f64_to_u52(double x) {
+  return as_u64(floor(x) + 0x1p52) - 0x4330000000000000ull;
+}
 
 // timing-only variants (results wrong): GH_RS_EXIT=k leaves k_resample1 after
 // phase k (0 start, 1 fold, 2 quantise + scan, 3 grid barrier), to price the
@@ -1357,16 +1272,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   __shared__ uint64_t sbase;
   __shared__ unsigned sgen;
   __shared__ int sfail;  // the barrier wait timed out: write nothing
-  __shared__ double sU;  // the bound path's reference (the step's U)
-  __shared__ uint64_t sbt[3][16];  // the bound path: wave totals (all, before this tile, any invalid)
-  __shared__ int supath;
   GH_RS_STAMP(0);
   GH_RS_EXIT_AT(0);
   // barrier generation of this launch: read before this block publishes
   if (threadIdx.x == 0) {
     sgen = r.dev->bar_gen + 1;
     sfail = 0;
-    sU = r.btot ? r.dev->U : INFINITY;
   }
   // ---- fold the step partials (same order in every block: same result)
   // this tile's log-weights are loaded up front, beside the partials
@@ -1390,7 +1301,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     GH_RS_STAMP(7);
   } else if (IT <= 8 && r.nb_part <= KP * kRsBlock) {  // uniform; always true at IT <= kRsPart (host-checked)
     double pmv[KP], psv[kSumsEarly ? KP : 1], ps2v[kSumsEarly ? KP : 1];
-    uint64_t btv[KP];
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
       const int b = threadIdx.x + k * kRsBlock;
@@ -1400,29 +1310,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
         psv[k] = ok && !sums ? r.ps[b] : 0.0;
         ps2v[k] = ok && !sums ? r.ps2[b] : 0.0;
       }
-      btv[k] = ok && r.btot ? r.btot[b] : 0ull;
-    }
-    if (!sums && r.btot) {  // the bound path's totals: all tiles, those before this tile, any invalid
-      const int64_t first = ((int64_t)blockIdx.x * (kRsBlock * IT)) / r.btot_span;
-      uint64_t ta = 0, tb = 0;
-      bool inv = false;
-#pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        const int b = threadIdx.x + k * kRsBlock;
-        inv = inv || btv[k] == kBtotInvalid;
-        ta += btv[k];
-        tb += b < first ? btv[k] : 0ull;
-      }
-      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-      ta = wave_sum_u64(ta);
-      tb = wave_sum_u64(tb);
-      const bool winv = __builtin_amdgcn_ballot_w64(inv) != 0;
-      if (lane == 0) {
-        sbt[0][w] = ta;
-        sbt[1][w] = tb;
-        sbt[2][w] = winv ? 1ull : 0ull;
-      }
-      // (read after the next LDS barrier, in blk16_max1)
     }
     double m = pmv[0];
 #pragma unroll
@@ -1457,26 +1344,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   } else {  // larger sets: max pass, then a sum pass over the (cache-hot) partials
     double m = -INFINITY;
     for (int b = threadIdx.x; b < r.nb_part; b += kRsBlock) m = fmax(m, r.pm[b]);
-    if (!sums && r.btot) {  // the bound path's totals (as in the register path above)
-      const int64_t first = ((int64_t)blockIdx.x * (kRsBlock * IT)) / r.btot_span;
-      uint64_t ta = 0, tb = 0;
-      bool inv = false;
-      for (int b = threadIdx.x; b < r.nb_part; b += kRsBlock) {
-        const uint64_t v = r.btot[b];
-        inv = inv || v == kBtotInvalid;
-        ta += v;
-        tb += b < first ? v : 0ull;
-      }
-      const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-      ta = wave_sum_u64(ta);
-      tb = wave_sum_u64(tb);
-      const bool winv = __builtin_amdgcn_ballot_w64(inv) != 0;
-      if (lane == 0) {
-        sbt[0][w] = ta;
-        sbt[1][w] = tb;
-        sbt[2][w] = winv ? 1ull : 0ull;
-      }
-    }
     M = blk16_max(m, smd);
     if (!sums && M > -INFINITY)
       for (int b = threadIdx.x; b < r.nb_part; b += kRsBlock) {
@@ -1496,35 +1363,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // follows the grid barrier.
   __shared__ int sfire;
   __shared__ double sS[2];
-  __shared__ uint64_t sua, sub;  // the bound path: integer total, total before this tile
   if (!sums) {
     blk16_sum2(&s1, &s2, smd);
     S1 = s1;
     S2 = s2;
-    if (threadIdx.x == 0) {
-      sfire = m_ok && ((S1 * S1) / S2 < r.d.thr);
-      // the bound path (uniform: every block folds the same totals): every
-      // weight at most U, U within kUGap of the max, some weight quantised
-      int up = 0;
-      if (r.btot) {
-        uint64_t ta = 0, tb = 0;
-        bool inv = false;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          ta += sbt[0][k];
-          tb += sbt[1][k];
-          inv = inv || sbt[2][k] != 0;
-        }
-        const double U = sU;
-        up = !inv && m_ok && U < INFINITY && M <= U && M - U >= -kUGap && ta > 0;
-        sua = ta;
-        sub = tb;
-      }
-      supath = up;
-    }
+    if (threadIdx.x == 0) sfire = m_ok && ((S1 * S1) / S2 < r.d.thr);
     lds_barrier();
-  } else if (threadIdx.x == 0) {
-    supath = 0;
   }
   GH_RS_STAMP(1);
   auto commit = [&]() {
@@ -1545,11 +1389,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     commit();
     return;
   }
-  if (sums) lds_barrier();  // (supath)
-  const bool upath = supath != 0;
-  // the quantisation reference: U on the bound path (no grid barrier: the
-  // step's block totals give every tile its offset), else the max
-  const double Mq = upath ? sU : M;
+  const double Mq = M;
   // ---- quantise this block's tile (IT consecutive particles per thread);
   // sums_in_pass: the same e = exp(w - M) also feed this tile's sums
   const double qscale = as_f64((uint64_t)(r.shift + 1023) << 52);
@@ -1583,8 +1423,8 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // this pass), so each of the three words alternates its tag strictly and a
   // matching tag always means this generation's value: a poller can never
   // pair a fresh tile total with sums left over from two generations back.
-  if (!upath && threadIdx.x == kRsBlock - 1) st_sc1(&r.tsum[blockIdx.x], incl | par);
-  if (!upath && threadIdx.x == 0) {
+  if (threadIdx.x == kRsBlock - 1) st_sc1(&r.tsum[blockIdx.x], incl | par);
+  if (threadIdx.x == 0) {
     st_sc1(&r.ts1[blockIdx.x], (as_u64(s1) & ~kTag) | par);
     st_sc1(&r.ts2[blockIdx.x], (as_u64(s2) & ~kTag) | par);
   }
@@ -1602,7 +1442,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       const u32x4 wr = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);  // independent of the totals
       su53 = u53_bits(wr.x, wr.y);
     }
-    if (w < 8 && !upath) {  // (the bound path has its totals already: no grid barrier)
+    if (w < 8) {
       const unsigned b = (unsigned)(w * 64 + lane);
       const bool mine = b < gridDim.x;
       // the totals alone while the grid publishes, then the tile sums
@@ -1659,17 +1499,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   if (threadIdx.x == 0) {
     uint64_t all = 0, before = 0;
     double g1 = 0.0, g2 = 0.0;
-    if (upath) {
-      all = sua;
-      before = sub;
-    } else {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        all += spa[k];
-        before += spb[k];
-        g1 += spg[0][k];
-        g2 += spg[1][k];
-      }
+    for (int k = 0; k < 8; ++k) {
+      all += spa[k];
+      before += spb[k];
+      g1 += spg[0][k];
+      g2 += spg[1][k];
     }
     if (sums) {
       sS[0] = g1;
@@ -1687,7 +1522,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     sd.invS = recip_est((double)all);
     sbase = before;
     if (blockIdx.x == 0) {
-      if (!upath) r.dev->bar_gen = sgen;  // every block has published, so has read the old value
+      r.dev->bar_gen = sgen;  // every block has published, so has read the old value
       r.dev->S = sd.S;
       r.dev->base = 0;
       r.dev->local = sd.local;

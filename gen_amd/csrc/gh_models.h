@@ -36,8 +36,6 @@ struct Draw {
 struct StepObs {
   double v[kMaxObs];  // LGSSM: L_R^{-1}(y - c); Kitagawa: y; HMM: symbol
   double ct;          // Kitagawa: 8 cos(1.2 t); LGSSM optimal proposal at t = 1: the (constant) weight
-  double ub;          // an upper bound of every particle's weight increment at this step (the
-                      // resample's quantisation reference); +inf: none known
   int present;
   int sym;            // HMM symbol (integer copy of v[0])
 };

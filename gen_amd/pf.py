@@ -433,11 +433,9 @@ def _normal_lp(x, mu, sd) -> float:
 
 
 # --------------------------------------------------------------- the API
-def _opts(resampler: str, record_history: bool, history_capacity: int, time_kernels: int,
-          exact_quantisation: bool = False) -> _lib.PFOpts:
+def _opts(resampler: str, record_history: bool, history_capacity: int, time_kernels: int) -> _lib.PFOpts:
     o = _lib.PFOpts()
     _lib.load().gh_pf_opts_default(byref(o))
-    o.exact_quantisation = int(exact_quantisation)
     o.resampler = {"systematic": _lib.RESAMPLE_SYSTEMATIC, "multinomial": _lib.RESAMPLE_MULTINOMIAL}[resampler]
     o.record_history = int(record_history)
     o.history_capacity = int(history_capacity)
@@ -448,7 +446,6 @@ def _opts(resampler: str, record_history: bool, history_capacity: int, time_kern
 def initialize_particle_filter(model: Model, model_args: tuple, observations, *args, seed: int = 0,
                                resampler: str = "systematic", record_history: bool = True,
                                history_capacity: int = 0, time_kernels: int = 0,
-                               exact_quantisation: bool = False,
                                ctx: Context | None = None) -> ParticleFilterState:
     """initialize_particle_filter(model, model_args, observations, num_particles)
     initialize_particle_filter(model, model_args, observations, proposal, proposal_args, num_particles)
@@ -472,7 +469,7 @@ def initialize_particle_filter(model: Model, model_args: tuple, observations, *a
     mh = ctx.model_handle(model)
     obs, keep = _step_obs(model, 1, observations)
     h = c_void_p()
-    opts = _opts(resampler, record_history, history_capacity, time_kernels, exact_quantisation)
+    opts = _opts(resampler, record_history, history_capacity, time_kernels)
     qa, nq = _qargs(proposal, proposal_args)
     _lib.check(_lib.load().gh_pf_init_q(mh, byref(obs), _proposal_code(proposal),
                                         _lib.dptr(qa) if qa is not None else None, nq, int(num_particles),

@@ -144,11 +144,7 @@ typedef struct {
   int32_t history_capacity; /* steps to preallocate when record_history (0 = grow) */
   int32_t block_size;     /* 0 = default (256) */
   int32_t time_kernels;   /* k > 0: time every k-th step kernel with hipEvents (gh_pf_kernel_time) */
-  int32_t exact_quantisation; /* 1: every resample quantises against the weights' maximum (DESIGN.md
-                                 §6); 0 (default): a one-rank filter of at most 2^22 particles
-                                 quantises against the step's a-priori weight bound when it is
-                                 within 20 ln 2 of the maximum (no grid barrier) */
-  int32_t reserved[2];
+  int32_t reserved[3];
 } gh_pf_opts;
 
 /* ---- context ------------------------------------------------------------ */

@@ -483,28 +483,16 @@ typedef struct {
   double g[64], vt[64], w0;
   double raw[64]; /* the observation as given (rebuilt under other parameters: orc_pf_step_params) */
   int nraw;
-  double ub;      /* an upper bound of the step's weight increment (+inf: none): the model's own
-                     (obs_build), the proposal's (step_ub) */
 } obs_t;
 
 static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* o) {
   o->present = has;
   o->ct = 0.0;
   o->nraw = 0;
-  o->ub = m->family == ORC_REGRESSION ? INFINITY : 0.0;
   if (m->family == ORC_KITAGAWA) o->ct = 8.0 * orc_cos(1.2 * (double)t);
   if (!has) return;
   o->nraw = (m->family == ORC_LGSSM || m->family == ORC_REGRESSION) ? m->dy : 1;
   for (int i = 0; i < o->nraw; ++i) o->raw[i] = y[i];
-  /* the model's increment log p(y | x) <= its normalising constant (LGSSM,
-     nonlinear SSM) or max_z log E[y | z] (HMM) */
-  if (m->family == ORC_LGSSM) o->ub = m->cstR;
-  if (m->family == ORC_KITAGAWA) o->ub = m->csty;
-  if (m->family == ORC_HMM) {
-    double mx = -INFINITY;
-    for (int z = 0; z < m->k; ++z) mx = fmax(mx, m->logE[(int)y[0] * m->k + z]);
-    o->ub = mx;
-  }
   if (m->family == ORC_LGSSM) {
     double r[64];
     for (int i = 0; i < m->dy; ++i) r[i] = y[i] - m->c[i];
@@ -780,9 +768,6 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
 }
 
 /* ---------------------------------------------------------- PF state */
-/* the bound path's gap: U within 20 ln 2 of the weights' maximum */
-#define ORC_UGAP 0x1.bb9d3beb8c86bp+3
-
 struct orc_pf {
   model_t m;
   int64_t n_global, lo, n;
@@ -795,14 +780,6 @@ struct orc_pf {
   int64_t* anc;         /* pending ancestors (global ids) */
   double* anc_state;    /* [d][n] ancestor states after a (distributed) resample */
   int pending;          /* resampled since the last step */
-  /* the bound path of the resample: one shard of at most 2^22
-     particles quantises against U, the step's a-priori weight bound, when
-     every weight is at most U and U is within 20 ln 2 of the maximum */
-  int bound_on;
-  double U;             /* this step's bound (+inf: none) */
-  int decided;          /* a maybe_resample since the last step */
-  double lastM;         /* the last decision's maximum */
-  int64_t bound_uses;   /* resamples that quantised against U (tests) */
   double log_ml_est;
   obs_t obs;            /* observation of the current step (rejuvenation) */
   int cond;             /* conditional SMC: particle 0 is pinned (smc.jl:100-151) */
@@ -822,8 +799,6 @@ orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* par
   if (model_build(&pf->m, family, d, dy, k, v, params, np)) { model_free(&pf->m); free(pf); return NULL; }
   pf->n_global = n_global; pf->lo = lo; pf->n = n_local; pf->seed = seed;
   pf->resampler = resampler; pf->record_history = record_history;
-  pf->bound_on = lo == 0 && n_local == n_global && n_global <= ((int64_t)1 << 22);
-  pf->U = INFINITY;
   int D = pf->m.d;
   pf->x = calloc((size_t)D * n_local, sizeof(double));
   pf->xprev = calloc((size_t)D * n_local, sizeof(double));
@@ -831,12 +806,6 @@ orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* par
   pf->logw = calloc((size_t)n_local, sizeof(double));
   pf->anc = calloc((size_t)n_local, sizeof(int64_t));
   return pf;
-}
-
-/* 1: every resample quantises against the weights' maximum (the engine's
-   gh_pf_opts.exact_quantisation; multi-shard oracles always do) */
-void orc_pf_set_exact_quantisation(orc_pf* pf, int on) {
-  pf->bound_on = !on && pf->lo == 0 && pf->n == pf->n_global && pf->n_global <= ((int64_t)1 << 22);
 }
 
 void orc_pf_destroy(orc_pf* pf) {
@@ -869,23 +838,9 @@ static void record(orc_pf* pf) {
 
 static double model_loglik(const model_t* m, const obs_t* o, const double* x);
 
-/* the proposal's weight bound (the engine's step_ub) */
-static double step_ub(const model_t* m, const obs_t* o, int proposal, int t) {
-  if (proposal == ORC_PROPOSAL_GAUSSIAN || proposal == ORC_PROPOSAL_LINEAR) return INFINITY;
-  if (proposal == ORC_PROPOSAL_OPTIMAL && o->present) {
-    if (m->family == ORC_LGSSM) return t == 1 ? o->w0 : m->cstS;
-    if (m->family == ORC_HMM) return o->ub + 1e-12 * fmax(1.0, fabs(o->ub));
-  }
-  return o->ub;
-}
-
 static int init_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, const double* ref) {
   obs_t o;
   obs_build(&pf->m, 1, obs, has_obs, &o);
-  o.ub = step_ub(&pf->m, &o, proposal, 1);
-  /* the bound path's reference: no earlier weights */
-  pf->U = pf->bound_on && !ref ? o.ub : INFINITY;
-  pf->decided = 0;
   int D = pf->m.d;
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < pf->n; ++i) {
@@ -954,14 +909,6 @@ static int step_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
   uint32_t t = (uint32_t)(pf->t + 1);
   obs_t o;
   obs_build(&pf->m, (int)t, obs, has_obs, &o);
-  o.ub = step_ub(&pf->m, &o, proposal, (int)t);
-  /* U = (weights reset ? 0 : the last decision's max) + the step's bound; +inf
-     without a decision since the last step (the engine's step_bound) */
-  if (pf->bound_on && !ref && !pf->cond)
-    pf->U = pf->pending ? o.ub : (pf->decided ? pf->lastM + o.ub : INFINITY);
-  else
-    pf->U = INFINITY;
-  pf->decided = 0;
   int D = pf->m.d;
   int64_t n = pf->n;
   double* src = pf->pending ? pf->anc_state : pf->x;
@@ -1268,24 +1215,9 @@ int orc_pf_maybe_resample(orc_pf* pf, double thr, double* ess_out) {
   double st[3], L, ess, M;
   orc_pf_local_stats(pf, st);
   int dec = orc_combine_stats(st, 1, pf->n_global, thr, &L, &ess, &M);
-  const int first = !pf->decided;  /* (a second call resamples the uniform weights exactly) */
-  pf->decided = 1;
-  pf->lastM = M;
   if (ess_out) *ess_out = ess;
   if (dec < 0) return -1;
   if (!dec) return 0;
-  /* the quantisation reference: U on the bound path, else the maximum */
-  double R = M;
-  const double U = pf->U;
-  if (first && !pf->pending && U > -INFINITY && U < INFINITY && M <= U && M - U >= -ORC_UGAP) {
-    int ok = 1;
-    for (int64_t i = 0; i < pf->n && ok; ++i) {
-      const double w = pf->logw[i];
-      if (w > -INFINITY && !(w - U <= 0.0)) ok = 0;
-    }
-    if (ok && orc_pf_local_qtotal(pf, U) > 0) { R = U; pf->bound_uses++; }
-  }
-  M = R;
   uint64_t tot = orc_pf_local_qtotal(pf, M);
   int64_t n = pf->n;
   int D = pf->m.d;
@@ -1314,7 +1246,6 @@ void orc_pf_get_state(orc_pf* pf, double* out) {
 }
 void orc_pf_get_parents(orc_pf* pf, int64_t* out) { memcpy(out, pf->anc, sizeof(int64_t) * pf->n); }
 int orc_pf_num_steps(orc_pf* pf) { return pf->t; }
-int64_t orc_pf_bound_uses(orc_pf* pf) { return pf->bound_uses; }
 
 /* The scores of one step's choices under the model (the per-choice score
    fields of src/static_ir/trace.jl:91-129): the latent x_t | x_{t-1} (t = 1:
@@ -1448,7 +1379,6 @@ int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const doubl
   int rc = step_impl(pf, obs, has_obs, proposal, NULL);
   if (!rc)
     for (int64_t j = 0; j < n; ++j) pf->logw[j] += new_tot[j] - old_tot[j];
-  pf->U = INFINITY;  /* the weights moved by Delta: the next resample quantises against the max */
   free(old_tot);
   free(new_tot);
   return rc;

@@ -59,7 +59,6 @@ orc_pf* orc_pf_create(int family, int d, int dy, int k, int v, const double* par
                       int64_t n_global, int64_t lo, int64_t n_local, uint64_t seed, int resampler,
                       int record_history);
 void orc_pf_destroy(orc_pf* pf);
-void orc_pf_set_exact_quantisation(orc_pf* pf, int on);
 int orc_pf_init(orc_pf* pf, const double* obs, int has_obs, int proposal);
 int orc_pf_step(orc_pf* pf, const double* obs, int has_obs, int proposal);
 /* arguments of the Gaussian custom proposal (alpha, beta, gamma, sigma_q), used
@@ -83,7 +82,6 @@ void orc_pf_get_log_weights(orc_pf* pf, double* out);     /* n_local */
 void orc_pf_get_state(orc_pf* pf, double* out);           /* [d][n_local] */
 void orc_pf_get_parents(orc_pf* pf, int64_t* out);        /* n_local, global ids */
 int orc_pf_num_steps(orc_pf* pf);
-int64_t orc_pf_bound_uses(orc_pf* pf); /* resamples quantised against the bound U */
 int orc_pf_get_history(orc_pf* pf, int t, double* x_out, int32_t* anc_out, int* resampled);
 /* get_score of every current particle's trace (total [n]) and the per-step
    latent / observation choice scores (per_step [t][2][n], nullable); one shard */

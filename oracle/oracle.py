@@ -90,8 +90,6 @@ def _load(path):
             "orc_pf_get_history": (I, [V, I, D, POINTER(c_int32), POINTER(c_int)]),
             "orc_pf_get_scores": (I, [V, D, D]),
             "orc_pf_step_params": (I, [V, D, I64, D, I, I]),
-            "orc_pf_set_exact_quantisation": (None, [V, I]),
-            "orc_pf_bound_uses": (I64, [V]),
             "orc_lgamma": (c_double, [c_double]),
             "orc_log1p": (c_double, [c_double]),
             "orc_dist_logpdf": (I, [I, I, I, I, D, I64, D, D]),
@@ -157,12 +155,7 @@ def model_args(model):
 class OraclePF:
     """CPU restatement of ParticleFilterState over particles [lo, lo+n_local)."""
 
-    def __init__(self, model, n_global, seed, resampler=SYSTEMATIC, lo=0, n_local=None, record_history=True,
-                 exact_quantisation=False):
-        """exact_quantisation: every resample quantises against the weights'
-        maximum (the engine's gh_pf_opts.exact_quantisation; the multi-rank
-        filter's rule); otherwise a one-shard filter takes the bound path
-         as the engine's one-rank filter does."""
+    def __init__(self, model, n_global, seed, resampler=SYSTEMATIC, lo=0, n_local=None, record_history=True):
         fam, d, dy, k, v, p = model_args(model)
         self.L = lib()
         self._p = p
@@ -174,8 +167,6 @@ class OraclePF:
                                      int(record_history))
         if not self.h:
             raise ValueError("oracle: bad model parameters")
-        if exact_quantisation:
-            self.L.orc_pf_set_exact_quantisation(self.h, 1)
         self.model = model
 
     def __del__(self):
@@ -271,10 +262,6 @@ class OraclePF:
         o = np.empty((self.d, self.n))
         self.L.orc_pf_get_state(self.h, _d(o))
         return o
-
-    def bound_uses(self):
-        """resamples that quantised against the bound U (the bound path)"""
-        return int(self.L.orc_pf_bound_uses(self.h))
 
     def parents(self):
         o = np.empty(self.n, dtype=np.int64)
@@ -399,10 +386,9 @@ def dist_random(name, params, n, seed, dim=1, per_value=False):
     return out
 
 
-def run_pf(model, ys, n, seed, thr=None, resampler=SYSTEMATIC, proposal=DEFAULT, record_history=True,
-           exact_quantisation=False):
+def run_pf(model, ys, n, seed, thr=None, resampler=SYSTEMATIC, proposal=DEFAULT, record_history=True):
     """The reference caller loop (test/inference/particle_filter.jl:152-162)."""
-    pf = OraclePF(model, n, seed, resampler, record_history=record_history, exact_quantisation=exact_quantisation)
+    pf = OraclePF(model, n, seed, resampler, record_history=record_history)
     pf.init(ys[0], proposal)
     for y in ys[1:]:
         pf.maybe_resample(thr)

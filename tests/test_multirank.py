@@ -267,7 +267,7 @@ def test_gloo_sharded_oracle_with_product_plan(tmp_path, R):
         os.environ.pop("GH_OUT", None)
     m = LinearGaussianSSM.benchmark(4)
     _, ys = m.simulate(8, np.random.default_rng(5))
-    ref = O.run_pf(m, ys, 3001, 9, thr=3001, exact_quantisation=True)  # (the multi-rank rule)
+    ref = O.run_pf(m, ys, 3001, 9, thr=3001)
     parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
     assert np.array_equal(np.concatenate([p["states"] for p in parts], axis=1), ref.state())
     assert np.array_equal(np.concatenate([p["parents"] for p in parts]), ref.parents())
@@ -296,7 +296,7 @@ def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr
                   *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--out", out], R, timeout=400)
     m = build_model(model)
     _, ys = m.simulate(T, np.random.default_rng(5))
-    ref = O.run_pf(m, ys, n, seed, thr=thr, exact_quantisation=True)  # (multi-rank: exact quantisation)
+    ref = O.run_pf(m, ys, n, seed, thr=thr)
     parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
     states = np.concatenate([p["states"] for p in parts], axis=0)  # [n, d]
     assert np.array_equal(states.T, ref.state())
@@ -313,7 +313,7 @@ def _check_against_oracle(out, model, R, n, T, seed, thr):
 
     m = build_model(model)
     _, ys = m.simulate(T, np.random.default_rng(5))
-    ref = O.run_pf(m, ys, n, seed, thr=thr, exact_quantisation=True)  # (multi-rank: exact quantisation)
+    ref = O.run_pf(m, ys, n, seed, thr=thr)
     parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
     states = np.concatenate([p["states"] for p in parts], axis=0)  # [n, d]
     assert np.array_equal(states.T, ref.state())

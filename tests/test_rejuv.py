@@ -144,7 +144,7 @@ def test_gpu_rejuvenation_multirank_host_transport(tmp_path):
                   "--thr", "1e9", "--seed", str(seed), "--rejuv", "2", "--out", out], R, timeout=400)
     m = build_model("lg4")
     _, ys = m.simulate(T, np.random.default_rng(5))
-    orc = O.OraclePF(m, n, seed, exact_quantisation=True)  # (the multi-rank rule)
+    orc = O.OraclePF(m, n, seed)
     orc.init(ys[0])
     orc.rejuvenate(2)
     for t in range(2, T + 1):
