@@ -68,8 +68,6 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=1.5, help="seconds per CPU repetition (5 per baseline)")
     p.add_argument("--no-secondary", action="store_true", help="skip the C3 / C4 / C5 measurements")
     p.add_argument("--no-history", action="store_true")
-    p.add_argument("--exact-quantisation", action="store_true",
-                   help="quantise every resample against the weights' maximum (no bound path, DESIGN.md §6)")
     p.add_argument("--ess-threshold", type=float, default=None, help="default N/2 (the reference's default)")
     p.add_argument("--no-kernel-timing", action="store_true", help="no hipEvents around the step kernel")
     p.add_argument("--transport", default="rccl", choices=["rccl", "gloo"],
@@ -220,7 +218,7 @@ def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn):
     st = gen.initialize_particle_filter(
         model, (1,), {("chain", 1, "y"): ys[0]}, *init_args, seed=42, resampler=a.resampler,
         record_history=not a.no_history, history_capacity=T + 2, time_kernels=0 if a.no_kernel_timing else a.time_every,
-        exact_quantisation=a.exact_quantisation, ctx=ctx,
+        ctx=ctx,
     )
     gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold, proposal=prop)
     ctx.synchronize()

@@ -1,6 +1,6 @@
 """Print per-kernel register/occupancy usage of libgen_hip's device code.
 
-python tools/regs.py [substring-filter ...]
+python tools/regs.py [substring-filter ...]   (GH_REGS_SRC=gh_inst_lg2.hip: another unit)
 """
 import re
 import subprocess
@@ -8,7 +8,7 @@ import sys
 
 ROOT = __file__.rsplit("/tools/", 1)[0]
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-       f"-I{ROOT}/include", "--cuda-device-only", "-c", f"{ROOT}/gen_amd/csrc/gh_api.hip", "-o", "/tmp/_regs.o",
+       f"-I{ROOT}/include", "--cuda-device-only", "-c", f"{ROOT}/gen_amd/csrc/" + __import__("os").environ.get("GH_REGS_SRC", "gh_api.hip"), "-o", "/tmp/_regs.o",
        "-Rpass-analysis=kernel-resource-usage", "-mllvm", "-disable-machine-licm"] + [x for a in sys.argv[1:] if a.startswith("-mllvm=") for x in ("-mllvm", a[7:])] + [a for a in sys.argv[1:] if a.startswith("-D")]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 filt = [a for a in sys.argv[1:] if not a.startswith(("-D", "-mllvm="))]
