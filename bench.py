@@ -69,6 +69,8 @@ def parse(argv=None):
     p.add_argument("--no-secondary", action="store_true", help="skip the C3 / C4 / C5 measurements")
     p.add_argument("--no-history", action="store_true")
     p.add_argument("--ess-threshold", type=float, default=None, help="default N/2 (the reference's default)")
+    p.add_argument("--force-multirank", action="store_true",
+                   help="one GPU on the multi-rank code path (a one-rank RCCL communicator; profiling)")
     p.add_argument("--no-kernel-timing", action="store_true", help="no hipEvents around the step kernel")
     p.add_argument("--transport", default="rccl", choices=["rccl", "gloo"],
                    help="multi-GPU collectives: RCCL (default) or the host-staged gloo transport "
@@ -435,7 +437,7 @@ def main(argv=None):
             dist.broadcast_object_list(uid, src=0)
             ctx = gen.Context(device=local, rank=rank, world=world, unique_id=uid[0])
     else:
-        ctx = gen.Context(device=0)
+        ctx = gen.Context(device=0, force_multirank=a.force_multirank)
     gen.set_default_context(ctx)
 
     if a.model == "lgssm":

@@ -157,5 +157,7 @@ def test_gpu_coal_many_change_points_bitexact(gh_ctx, simple):
     ch.load_state(st, 4)
     ch.run(30)
     assert np.array_equal(ch.state, ref[0]) and np.array_equal(ch.accepts, ref[1])
-    assert (ref[0][:, 0] > 15).sum() > 20  # chains past the window at the end too
+    # chains past the window at the end too (the simple kernel regenerates k
+    # from its prior, so most of its chains are back inside it by then)
+    assert (ref[0][:, 0] > 15).sum() > (3 if simple else 20)
     ch.close()

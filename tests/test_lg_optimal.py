@@ -117,11 +117,20 @@ def test_gpu_optimal_proposal_bitexact(gh_ctx, name):
 
 @pytest.mark.gpu
 def test_gpu_optimal_proposal_log_ml_near_kalman(gh_ctx):
-    """2^20 particles on the C2 model: the optimal-proposal filter's log-ML is
-    within 0.01 of the exact Kalman value over 30 steps."""
+    """2^20 particles on the C2 model over 30 steps: the optimal-proposal
+    filter's log-ML estimate around the exact Kalman value.  Its spread is
+    ~0.26 at 2^15 particles (60 oracle seeds), so ~0.046 at 2^20: the mean of
+    8 seeds (sd ~0.016) is within 0.07 and each run within 0.25 (> 5 sd)."""
     m = gen.LinearGaussianSSM.benchmark(10)
     _, ys = m.simulate(30, np.random.default_rng(8))
     n = 1 << 20
-    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, gen.OptimalProposal, (), n, seed=3)
-    gen.run_particle_filter(st, list(ys[1:]), None, proposal=gen.OptimalProposal)
-    assert abs(gen.log_ml_estimate(st) - m.kalman_log_marginal(ys)) < 0.01
+    k = m.kalman_log_marginal(ys)
+    errs = []
+    for seed in range(3, 11):
+        st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, gen.OptimalProposal, (), n,
+                                            seed=seed)
+        gen.run_particle_filter(st, list(ys[1:]), None, proposal=gen.OptimalProposal)
+        errs.append(gen.log_ml_estimate(st) - k)
+        st.close()
+    assert abs(np.mean(errs)) < 0.07, errs
+    assert max(abs(e) for e in errs) < 0.25, errs

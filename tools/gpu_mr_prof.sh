@@ -1,0 +1,11 @@
+# GPU suite, default bench line, and kernel traces of the one-rank and forced multi-rank paths (C2, C4)
+set -e
+O=gpurun_out/mr
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
+export TMPDIR=/tmp
+for v in "c2|" "c2mr|--force-multirank" "c4|--model kitagawa --particles 2097152" "c4mr|--model kitagawa --particles 2097152 --force-multirank"; do
+  name=${v%%|*}; args=${v#*|}
+  GH_PROF_STEPS=20 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/$name -o run --output-format csv -- python3 tools/profile_run.py $args > $O/$name.log 2>&1
+done
