@@ -25,7 +25,7 @@ STATUS = {
 
 FAMILY_LGSSM, FAMILY_HMM, FAMILY_KITAGAWA, FAMILY_REGRESSION = 1, 2, 3, 4
 RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = 0, 1
-PROPOSAL_DEFAULT, PROPOSAL_OPTIMAL, PROPOSAL_GAUSSIAN = 0, 1, 2
+PROPOSAL_DEFAULT, PROPOSAL_OPTIMAL, PROPOSAL_GAUSSIAN, PROPOSAL_LINEAR = 0, 1, 2, 3
 
 
 class GenHipError(RuntimeError):
