@@ -353,9 +353,10 @@ def secondary_c3(gen, ctx, a):
                      "hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch") if pmc else None,
                      "valu_frac": pmc.get("valu_frac") if pmc else None,
                      "source": pmc.get("source") if pmc else None,
-                     "note": ("state in LDS for the launch: HBM = one read + one write of the 544-byte rows; "
-                              "VALU busy ~30 %: the chains wait on dependent LDS reads (event-count scans, "
-                              "per-move segment lookups), neither HBM nor VALU saturates")},
+                     "note": ("a 15-change-point window of each chain in LDS for the launch (two waves per "
+                              "SIMD), the rest of a longer chain's row in place in HBM; the chains wait on "
+                              "dependent LDS reads (event-count scans, per-move segment lookups): neither HBM "
+                              "nor VALU saturates (valu_frac from the PMC profile in source)")},
     }
     if not a.no_cpu_baseline:
         def make(threads):

@@ -792,6 +792,9 @@ template <int IT>
 static int rank_cap(int cus) {  // multi-rank: k_rank_a's (k_rank_b has no grid barrier)
   return occ_blocks(k_rank_a<IT>) * cus;
 }
+#ifndef GH_RS_MIN_IT
+#define GH_RS_MIN_IT 4  // the smallest resample tile considered (particles per thread); variants time larger ones
+#endif
 static void pick_resample_tiles(gh_pf* pf, int64_t n) {
   const int cus = pf->ctx->cus;
   pf->rs_grid = 0;
@@ -814,6 +817,7 @@ static void pick_resample_tiles(gh_pf* pf, int64_t n) {
     cands = {{4, rank_cap<4>(cus)}, {8, rank_cap<8>(cus)}, {16, rank_cap<16>(cus)}};
   }
   for (const Cand& c : cands) {
+    if (c.it < GH_RS_MIN_IT) continue;
     if (c.it <= kRsPart && pf->nb_part > (int64_t)kRsPart * kRsBlock) continue;
     const int64_t g = grid_of(c.it);
     if (g <= std::min<int64_t>(gmax, c.cap)) {

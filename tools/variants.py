@@ -18,6 +18,7 @@ VARIANTS = {
     "philox7": ["GH_PHILOX_ROUNDS=7"],
     "coal_w10": ["GH_COAL_WIN=10"],
     "coal_w7": ["GH_COAL_WIN=7"],
+    "rsit8": ["GH_RS_MIN_IT=8"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
