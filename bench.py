@@ -349,14 +349,13 @@ def secondary_c3(gen, ctx, a):
                    "chains": chains, "steps": steps},
         "kernel_ms": kms,
         "k_posterior": [round(float(x), 4) for x in ks],
-        "roofline": {"bound": "latency", "kernel": "k_coal",
+        "roofline": {"bound": "valu", "kernel": "k_coal",
                      "hbm_bytes_per_launch": pmc.get("hbm_bytes_per_launch") if pmc else None,
                      "valu_frac": pmc.get("valu_frac") if pmc else None,
                      "source": pmc.get("source") if pmc else None,
-                     "note": ("a 15-change-point window of each chain in LDS for the launch (two waves per "
-                              "SIMD), the rest of a longer chain's row in place in HBM; the chains wait on "
-                              "dependent LDS reads (event-count scans, per-move segment lookups): neither HBM "
-                              "nor VALU saturates (valu_frac from the PMC profile in source)")},
+                     "note": ("an 8-change-point window of each chain in LDS for the launch (four waves per "
+                              "SIMD), the rest of a longer chain's row in place in HBM; VALU-bound "
+                              "(valu_frac from the PMC profile in source); HBM is one pass over the windows")},
     }
     if not a.no_cpu_baseline:
         def make(threads):

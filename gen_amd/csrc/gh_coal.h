@@ -28,10 +28,12 @@
 // 1..kCoalWin, h 1..kCoalWin+1) lives in LDS for the whole launch
 // ([field][lane] per wave: conflict-free for any per-lane index), k and the
 // score in registers; the fields past the window (a chain with more than
-// kCoalWin change points: the posterior puts < 0.1 % of its mass there) are
+// kCoalWin change points: the posterior puts ~0.4 % of its mass above k = 8) are
 // read and written in place in the chain's HBM row.  The window keeps a
-// chain's LDS at 31 fields instead of 65, so twice the waves fit a CU (the
-// kernel waits on dependent LDS reads; more resident waves hide them).  HBM:
+// chain's LDS at 17 fields instead of 65, so four waves per SIMD fit instead
+// of one (the kernel waits on dependent LDS reads; more resident waves hide
+// them; measured: window 15 / 10 / 8 / 7 / 6 with 128- or 256-thread blocks,
+// DESIGN.md §7c).  HBM:
 // the window read once and written once per launch.  Event counts come from the sorted event times in LDS through a
 // bucket table (start index) and a short scan.  The oracle
 // (oracle/gh_oracle.c, orc_coal_run) restates the same arithmetic.
@@ -45,11 +47,14 @@ constexpr int kCoalW = 2 + kCoalKMax + (kCoalKMax + 1) + 1;  // 68: k, score, cp
 constexpr int kCoalF = kCoalKMax + (kCoalKMax + 1);          // 65 LDS fields per chain: cp[32], h[33]
 constexpr int kCoalMaxEvents = 4096;
 #ifndef GH_COAL_WIN
-#define GH_COAL_WIN 15
+#define GH_COAL_WIN 8
 #endif
 constexpr int kCoalWin = GH_COAL_WIN;                        // change points in LDS (rates: kCoalWin + 1)
 constexpr int kCoalLF = 2 * kCoalWin + 1;                    // LDS fields per chain
-constexpr int kCoalBlock = 128;                              // two waves: 4 blocks (31.8 KB window each + tables) per CU
+#ifndef GH_COAL_BLOCK
+#define GH_COAL_BLOCK 256
+#endif
+constexpr int kCoalBlock = GH_COAL_BLOCK;                    // four waves: 4 blocks (34.8 KB window each + tables) per CU
 constexpr int kCoalBuckets = 256;                            // event-count start table
 constexpr double kCoalRate = 200.0;                          // gamma(1, 1/200) rate prior: 1 / theta (coal.jl:56-58)
 

@@ -101,6 +101,8 @@ def main():
                      os.path.join(src, "c5.pmc*", "run_counter_collection.csv"), lambda k: k.startswith("gh::k_pmmh("),
                      "profiles/pmc_k_pmmh.json", "tools/bench_pmmh.py (C5: 2^16 chains x 256 inner particles)"))
     for tag, stats, pmc_glob, match, out_json, config in jobs:
+        if not os.path.exists(stats):  # (a partial profile run: that configuration only)
+            continue
         shutil.copy(stats, f"{prefix}{tag}_kernel_stats.csv")
         agg = counters(pmc_glob)
         write_pmc_txt(agg, f"{prefix}{tag}_pmc.txt")

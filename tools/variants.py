@@ -18,6 +18,16 @@ VARIANTS = {
     "philox7": ["GH_PHILOX_ROUNDS=7"],
     "coal_w10": ["GH_COAL_WIN=10"],
     "coal_w7": ["GH_COAL_WIN=7"],
+    "coal_w6": ["GH_COAL_WIN=6"],
+    "coal_w5": ["GH_COAL_WIN=5"],
+    "coal_w4": ["GH_COAL_WIN=4"],
+    "coal_b64": ["GH_COAL_BLOCK=64"],
+    "coal_b256w7": ["GH_COAL_BLOCK=256", "GH_COAL_WIN=7"],
+    "coal_b256w6": ["GH_COAL_BLOCK=256", "GH_COAL_WIN=6"],
+    "coal_b256w8": ["GH_COAL_BLOCK=256", "GH_COAL_WIN=8"],
+    "coal_b512w6": ["GH_COAL_BLOCK=512", "GH_COAL_WIN=6"],
+    "coal_b512w7": ["GH_COAL_BLOCK=512", "GH_COAL_WIN=7"],
+    "coal_b64w10": ["GH_COAL_BLOCK=64", "GH_COAL_WIN=10"],
     "rsit8": ["GH_RS_MIN_IT=8"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
