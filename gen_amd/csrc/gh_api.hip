@@ -1634,6 +1634,8 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
     ra.dev = pf->dev;
     ra.d = d;
     ra.tsum = pf->tsum;
+    ra.ts1 = pf->tsum + pf->n_tiles;
+    ra.ts2 = pf->tsum + 2 * pf->n_tiles;
     switch (pf->rs_it) {
       case 4: hipLaunchKernelGGL(k_rank_a<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
       case 8: hipLaunchKernelGGL(k_rank_a<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;

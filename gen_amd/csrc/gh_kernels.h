@@ -1605,6 +1605,8 @@ struct RankAArgs {
   DevScalars* dev;
   DecideArgs d;      // stats_all = the R all-gathered triples
   uint64_t* tsum;    // [grid] tile totals (bit 63: generation parity)
+  uint64_t* ts1;     // [grid] the tile-sum words k_rank_a2 and k_resample1 poll: published here
+  uint64_t* ts2;     //   too (0, tagged), so each word's tag alternates with every generation
 };
 
 template <int IT>
@@ -1633,7 +1635,13 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
   const uint64_t tot = blk16_sum_u64(tsum, smu);
   const uint64_t kTag = 1ull << 63;
   const uint64_t par = (sgen & 1u) ? kTag : 0ull;
-  if (threadIdx.x == 0) st_sc1(&r.tsum[blockIdx.x], tot | par);
+  if (threadIdx.x == 0) {
+    st_sc1(&r.tsum[blockIdx.x], tot | par);
+    // (a generation that skipped these would leave them one parity behind:
+    // the next k_rank_a2 would take a tile's sums from two generations back)
+    st_sc1(&r.ts1[blockIdx.x], par);
+    st_sc1(&r.ts2[blockIdx.x], par);
+  }
   uint64_t all = 0;
   unsigned failed = 0;
   for (int b = threadIdx.x; b < (int)gridDim.x; b += kRsBlock) {
@@ -1917,8 +1925,6 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
   __shared__ int64_t sown_lo, sown_hi, sra, srb, ssend;
   __shared__ uint64_t sbase;
-  __shared__ int32_t se[(kRsBlock * IT)];
-  __shared__ int64_t sfirst;
   const int R = r.R, q = r.rank;
   const uint64_t N = (uint64_t)r.mk.n_global;
   // tile offset within the rank
@@ -1979,39 +1985,43 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   const int64_t own_lo = sown_lo, own_hi = sown_hi;
   auto clamp_own = [&](int64_t s) { return s < own_lo ? own_lo : (s > own_hi ? own_hi : s); };
   int64_t s0 = sys_count(&sd, N, run);
-  if (threadIdx.x == 0) sfirst = clamp_own(s0) - own_lo;
   // more rows than the bounded send buffer holds (this rank carries most of
   // the weight): keep the CDF, the host regrows the buffer and k_rows_fill
   // writes every row from it (rare; the hot path only tests the flag)
   const bool spill = ssend > r.rows_cap;
+  // particle i's slots [s0, s1) (global); the part this rank owns, [l0, l1)
+  // in local slots, gets a tagged mark at l0 and the carry of every 64-slot
+  // group starting inside it — a lane writes up to two carries, a longer
+  // range gets them from its whole wave (as k_resample1's marks phase: no
+  // LDS copy of the range ends, no block barrier)
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     run += qv[k];
     const int64_t i = i0 + k;
-    const int64_t s1 = (i < r.n && qv[k]) ? sys_count(&sd, N, run) : s0;
-    const int64_t l0 = clamp_own(s0), l1 = clamp_own(s1);
-    se[threadIdx.x * IT + k] = (int32_t)(l1 - own_lo);
-    if (l1 > l0) r.mk.mark[l0 - own_lo] = (r.mk.epoch << 32) | (uint64_t)i;
+    // (a particle past n or of zero weight leaves run, hence the count, unchanged)
+    const int64_t s1 = sys_count_w(&sd, N, run);
+    const int64_t l0 = clamp_own(s0) - own_lo, l1 = clamp_own(s1) - own_lo;
+    const uint64_t tagged = (r.mk.epoch << 32) | (uint64_t)i;
+    if (l1 > l0) r.mk.mark[l0] = tagged;
+    const int64_t g0 = (l0 + 63) >> 6, g1 = (l1 + 63) >> 6;  // local groups g with 64 g in [l0, l1)
+    const bool many = g1 - g0 > 2;
+    if (!many) {
+      if (g1 > g0) r.mk.cmark[g0] = tagged;
+      if (g1 > g0 + 1) r.mk.cmark[g0 + 1] = tagged;
+    }
+    uint64_t bm = __builtin_amdgcn_ballot_w64(many);
+    while (bm) {
+      const int L = __builtin_ctzll(bm);
+      bm &= bm - 1;
+      const int32_t a0 = __builtin_amdgcn_readlane((int32_t)g0, L), a1 = __builtin_amdgcn_readlane((int32_t)g1, L);
+      const uint64_t tg = (r.mk.epoch << 32) | (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)i, L);
+      for (int32_t g = a0 + (threadIdx.x & 63); g < a1; g += 64) r.mk.cmark[g] = tg;
+    }
     if (spill && i < r.n) r.C[i] = run;
     // slots of other ranks: state rows, by destination then slot
     if (!spill)
       send_rows(s0, s1, i, own_lo, own_hi, R, N, sdst_lo, sseg_lo, ssoff, r.rows_cap, r.rows, r.xprev, r.D, r.lo);
     s0 = s1;
-  }
-  __syncthreads();
-  // carries of the 64-slot groups (local slot space) starting in this tile's
-  // own-slot span
-  const int64_t s_lo = sfirst, s_hi = se[(kRsBlock * IT) - 1];
-  const int64_t pbase = (int64_t)blockIdx.x * (kRsBlock * IT);
-  for (int64_t g = (s_lo + 63) / 64 + threadIdx.x; g * 64 < s_hi; g += kRsBlock) {
-    const int32_t slot = (int32_t)(g * 64);
-    int lo = 0, hi = (kRsBlock * IT) - 1;  // first particle p with se[p] > slot
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (se[mid] > slot) hi = mid;
-      else lo = mid + 1;
-    }
-    r.mk.cmark[g] = (r.mk.epoch << 32) | (uint64_t)(pbase + lo);
   }
 }
 

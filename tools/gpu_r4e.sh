@@ -1,0 +1,7 @@
+# multi-rank GPU tests twice (host transport 2..4 ranks on one GPU, forced RCCL world 1), then the bench line
+set -e
+O=gpurun_out/r4e
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests/test_multirank.py -m gpu -q --timeout 300 --timeout-method thread > $O/mr_tests1.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_multirank.py -m gpu -q --timeout 300 --timeout-method thread > $O/mr_tests2.log 2>&1
+timeout -k 10 400 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err
