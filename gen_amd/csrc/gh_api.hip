@@ -11,12 +11,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <string>
 #include <type_traits>
+#include <chrono>
 #include <vector>
 
 #include "../../include/gen_hip.h"
@@ -734,6 +736,8 @@ struct gh_pf {
   hipEvent_t ev_rb = nullptr;     //   k_rank_b packed the rows
   hipEvent_t ev_x = nullptr;      //   rows exchanged
   uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]] (k_rank_a) or the R rank records (k_rank_a2)
+  uint64_t* h_mail = nullptr;     // pinned, coherent: [tag, R rank records] written by k_rank_b (batched loop)
+  uint64_t mail_seq = 0;          //   the tag of the last plan posted there
   bool plan_recs = false;         // the pending plan is k_rank_a2's records (the host takes the decision)
   double plan_thr = 0.0;          //   at this threshold
   uint64_t* amax_all = nullptr;   // multi-rank: [R][kAmaxShards * kAmaxStride] all-gathered shard words
@@ -907,6 +911,7 @@ static void pf_free(gh_pf* pf) {
   if (pf->ev_rb) hipEventDestroy(pf->ev_rb);
   if (pf->ev_x) hipEventDestroy(pf->ev_x);
   if (pf->h_plan) hipHostFree(pf->h_plan);
+  if (pf->h_mail) hipHostFree(pf->h_mail);
   if (!pf->opts.record_history) {
     for (auto p : pf->xs) hipFree(p);
     for (auto p : pf->ancs) hipFree(p);
@@ -1346,6 +1351,8 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
         hipEventCreateWithFlags(&pf->ev_plan, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&pf->ev_rb, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&pf->ev_x, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void**)&pf->h_mail, sizeof(uint64_t) * (1 + kRecWords * ctx->world),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostMalloc((void**)&pf->h_plan, sizeof(uint64_t) * std::max(ctx->world + 1, kRecWords * ctx->world),
                       hipHostMallocDefault) != hipSuccess)
       return fail(set_err(GH_E_NOMEM, "multi-rank plan buffers"));
@@ -1643,8 +1650,8 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
     }
     HIP_TRY(hipGetLastError());
     CHECK(comm_allgather(c, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
+    HIP_TRY(hipEventRecord(pf->ev_tot, pf->s));
   }
-  HIP_TRY(hipEventRecord(pf->ev_tot, pf->s));
   RankBArgs rb{};
   rb.logw = pf->logw;
   rb.n = pf->n;
@@ -1654,6 +1661,10 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.totals = sums ? pf->recs_all : pf->totals_all;
   rb.tot_stride = sums ? kRecWords : 1;
   rb.recs = sums ? pf->recs_all : nullptr;
+  if (sums) {  // the plan comes back through the host-mapped mailbox (no event, no copy, no stream wait)
+    rb.hplan = pf->h_mail;
+    rb.htag = ++pf->mail_seq;
+  }
   rb.d = d;
   rb.R = R;
   rb.rank = q;
@@ -1673,17 +1684,14 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.C = pf->C;
   launch_rank_b(pf, rb);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
-  // the decision and the totals, read on the side stream while k_rank_b runs
-  HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_tot, 0));
-  if (sums) {  // the host takes the decision from the records itself (decide_records)
-    HIP_TRY(hipMemcpyAsync(pf->h_plan, pf->recs_all, sizeof(uint64_t) * kRecWords * R, hipMemcpyDeviceToHost,
-                           pf->aux));
-  } else {
+  // the row exchange (R > 1) starts on the side stream once k_rank_b packed the rows
+  if (R > 1) HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
+  if (!sums) {  // the decision and the totals, read on the side stream while k_rank_b runs
+    HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_tot, 0));
     HIP_TRY(hipMemcpyAsync(pf->h_plan, &pf->dev->fire, sizeof(int), hipMemcpyDeviceToHost, pf->aux));
     HIP_TRY(hipMemcpyAsync(pf->h_plan + 1, pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->aux));
+    HIP_TRY(hipEventRecord(pf->ev_plan, pf->aux));
   }
-  HIP_TRY(hipEventRecord(pf->ev_plan, pf->aux));
   pf->plan_recs = sums;
   pf->plan_thr = d.thr;
   pf->mark_mode = 2;
@@ -1697,6 +1705,29 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
 // the row exchange on the side stream and make the filter's stream wait for
 // it (work already enqueued on the filter's stream — the local half of the
 // next step — runs meanwhile).  Sets the received-row slot ranges.
+// The batched loop's plan: k_rank_b's block 0 writes the R records and then
+// the launch's tag into pinned, coherent host memory.  The host spins on the
+// tag (the records were copied before it, behind a system-scope release).  A
+// kernel that never writes it (a fault) ends the wait through the stream's
+// error after a bounded spin.
+static int wait_mailbox(gh_pf* pf) {
+  volatile uint64_t* tag = pf->h_mail;
+  const uint64_t want = pf->mail_seq;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spins = 0; __atomic_load_n(tag, __ATOMIC_ACQUIRE) != want; ++spins) {
+    if ((spins & 0xfffff) == 0xfffff) {  // every ~1M polls: is the stream still alive?
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+        return set_err(GH_E_STATE, "plan wait: no plan from k_rank_b after 60 s");
+      const hipError_t e = hipStreamQuery(pf->s);
+      if (e != hipSuccess && e != hipErrorNotReady) return set_err(GH_E_HIP, "plan wait: %s", hipGetErrorString(e));
+      if (e == hipSuccess && __atomic_load_n(tag, __ATOMIC_ACQUIRE) != want)
+        return set_err(GH_E_STATE, "plan wait: the stream drained without the plan (tag %llu, want %llu)",
+                       (unsigned long long)*tag, (unsigned long long)want);
+    }
+  }
+  return GH_OK;
+}
+
 static int finish_plan(gh_pf* pf) {
   if (!pf->plan_pending) return GH_OK;
   pf->plan_pending = false;
@@ -1704,13 +1735,15 @@ static int finish_plan(gh_pf* pf) {
   const int R = c->world, q = c->rank;
   const int D = pf->D;
   const int t = pf->t;
-  HIP_TRY(hipEventSynchronize(pf->ev_plan));
   int fire = 0;
   std::vector<uint64_t> totv(R);
   if (pf->plan_recs) {  // k_rank_b takes the same decision from the same records
-    fire = decide_records(pf->h_plan, R, pf->plan_thr).fire;
-    for (int r = 0; r < R; ++r) totv[r] = pf->h_plan[kRecWords * r];
+    CHECK(wait_mailbox(pf));
+    const uint64_t* recs = pf->h_mail + 1;
+    fire = decide_records(recs, R, pf->plan_thr).fire;
+    for (int r = 0; r < R; ++r) totv[r] = recs[kRecWords * r];
   } else {
+    HIP_TRY(hipEventSynchronize(pf->ev_plan));
     memcpy(&fire, pf->h_plan, sizeof(int));
     for (int r = 0; r < R; ++r) totv[r] = pf->h_plan[1 + r];
   }

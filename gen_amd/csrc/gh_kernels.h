@@ -1843,6 +1843,8 @@ struct RankBArgs {
   const uint64_t* totals; // all-gathered rank totals, rank k's at totals[k * tot_stride]
   int tot_stride;         // 1: k_rank_a's totals; kRecWords: k_rank_a2's records
   const uint64_t* recs;   // k_rank_a2's records: this launch takes (and block 0 commits) the decision
+  uint64_t* hplan;        // (with recs) host-mapped plan mailbox: block 0 copies the R records to
+  uint64_t htag;          //   hplan[1..] and then writes htag to hplan[0] (the host polls it)
   DecideArgs d;           //   (with recs) the decision's threshold and histories
   int R, rank;
   int64_t lo;             // global id of this rank's first particle
@@ -1904,6 +1906,14 @@ template <int IT>
 __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ int sfire;
   __shared__ double sMq;
+  // this tile's log-weights and the tile totals before it are loaded first,
+  // so their round trip overlaps the decision's and thread 0's plan
+  const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
+  double lw[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : 0.0;
+  uint64_t before = 0;  // tile offset within the rank
+  for (int b = threadIdx.x; b < (int)blockIdx.x; b += kRsBlock) before += r.tsum[b] & ~(1ull << 63);
   if (threadIdx.x == 0) {
     if (r.recs) {  // the decision from the R rank records (every block the same)
       const Decision dec = decide_records(r.recs, r.R, r.d.thr);
@@ -1912,6 +1922,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
       if (blockIdx.x == 0) {
         r.dev->pending = 0;
         commit_decision(r.d, dec, r.dev, 0);
+        if (r.hplan) {  // the host's copy of the records, then the tag behind a system-scope release
+          for (int w = 0; w < r.R * kRecWords; ++w) r.hplan[1 + w] = r.recs[w];
+          __threadfence_system();
+          __hip_atomic_store(&r.hplan[0], r.htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
       }
     } else {  // k_rank_a decided
       sfire = r.dev->fire;
@@ -1927,9 +1942,6 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ uint64_t sbase;
   const int R = r.R, q = r.rank;
   const uint64_t N = (uint64_t)r.mk.n_global;
-  // tile offset within the rank
-  uint64_t before = 0;
-  for (int b = threadIdx.x; b < (int)blockIdx.x; b += kRsBlock) before += r.tsum[b] & ~(1ull << 63);
   before = blk16_sum_u64(before, smu);
   if (threadIdx.x == 0) {
     uint64_t S = 0, base = 0;
@@ -1972,12 +1984,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   }
   __syncthreads();
   const double M = sMq;
-  const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
   uint64_t qv[IT];
   uint64_t tsum = 0;
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
-    qv[k] = (i0 + k < r.n) ? quantize_weight(r.logw[i0 + k], M, r.shift) : 0;
+    qv[k] = (i0 + k < r.n) ? quantize_weight(lw[k], M, r.shift) : 0;
     tsum += qv[k];
   }
   const uint64_t incl = blk16_incl_u64(tsum, smu);
