@@ -133,11 +133,6 @@ __device__ __forceinline__ uint64_t readfirstlane_u64(uint64_t v) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int L) {  // L wave-uniform
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, L);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), L);
-  return ((uint64_t)hi << 32) | lo;
-}
 __device__ __forceinline__ uint64_t readlane63_u64(uint64_t v) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
@@ -1948,60 +1943,43 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   const int R = r.R, q = r.rank;
   const uint64_t N = (uint64_t)r.mk.n_global;
   before = blk16_sum_u64(before, smu);
-  // the plan of this resample, taken by wave 0 with the per-rank work
-  // data-parallel over its lanes (lane k: rank k's total, destination block
-  // and send offset; lanes 0 and 1: the two coverage counts) instead of one
-  // thread walking the ranks with 128-bit divisions
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const uint64_t tk = lane < R ? r.totals[lane * r.tot_stride] : 0ull;
-    DevScalars loc;
-    loc.S = wave_sum_u64(tk);
-    loc.base = wave_sum_u64(lane < q ? tk : 0ull);
-    loc.local = readlane_u64(tk, q);
-    const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
-    loc.o = scale_u53(u53_bits(w.x, w.y), loc.S);
-    loc.invN = r.d.inv_n;
-    loc.Qs = udiv_n(loc.S, N, loc.invN);
-    loc.Rs = loc.S - loc.Qs * N;
-    loc.invS = recip_est((double)loc.S);
-    // this rank's particles cover the global slots [cov_lo, cov_hi)
-    const int64_t cov = sys_count_exact(&loc, N, lane == 0 ? loc.base : loc.base + loc.local);
-    const int64_t cov_lo = (int64_t)readlane_u64((uint64_t)cov, 0), cov_hi = (int64_t)readlane_u64((uint64_t)cov, 1);
-    // rank k owns [dlo_k, dhi_k); the rows for rank k != q start at soff_k,
-    // in slot order (as send_tables / gh_sys_plan)
-    const int64_t dlo = (int64_t)(((__int128)N * lane) / R), dhi = (int64_t)(((__int128)N * (lane + 1)) / R);
-    const int64_t sa = cov_lo > dlo ? cov_lo : dlo, sb = cov_hi < dhi ? cov_hi : dhi;
-    const uint64_t len = (lane < R && lane != q && sb > sa) ? (uint64_t)(sb - sa) : 0ull;
-    const uint64_t soff = wave_incl_sum_u64(len) - len;
-    const uint64_t send_total = wave_sum_u64(len);
-    if (lane < R) {
-      sdst_lo[lane] = dlo;
-      sseg_lo[lane] = sa;
-      ssoff[lane] = (int64_t)soff;
+  if (threadIdx.x == 0) {
+    uint64_t S = 0, base = 0;
+    for (int k = 0; k < R; ++k) {
+      if (k < q) base += r.totals[k * r.tot_stride];
+      S += r.totals[k * r.tot_stride];
     }
-    if (lane == 0) {
-      sd = loc;
-      ssend = (int64_t)send_total;
-      const int64_t own_lo = r.lo, own_hi = r.lo + r.n;
-      sown_lo = own_lo;
-      sown_hi = own_hi;
-      const int64_t ca = cov_lo < own_lo ? own_lo : (cov_lo > own_hi ? own_hi : cov_lo);
-      const int64_t cb = cov_hi < own_lo ? own_lo : (cov_hi > own_hi ? own_hi : cov_hi);
-      sra = ca - own_lo;
-      srb = cb - own_lo;
-      sbase = loc.base + before;
-      if (blockIdx.x == 0) {
-        r.dev->S = loc.S;
-        r.dev->base = loc.base;
-        r.dev->o = loc.o;
-        r.dev->Qs = loc.Qs;
-        r.dev->Rs = loc.Rs;
-        r.dev->invN = loc.invN;
-        r.dev->invS = loc.invS;
-        r.dev->ra = sra;
-        r.dev->rb = srb;
-      }
+    sd.S = S;
+    sd.base = base;
+    sd.local = r.totals[q * r.tot_stride];
+    const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
+    sd.o = scale_u53(u53_bits(w.x, w.y), S);
+    sd.invN = 1.0 / (double)N;
+    sd.Qs = udiv_n(S, N, sd.invN);
+    sd.Rs = S - sd.Qs * N;
+    sd.invS = 1.0 / (double)S;
+    const int64_t own_lo = r.lo, own_hi = r.lo + r.n;
+    // rows this rank sends: destination blocks in rank order (lower ranks,
+    // then higher ranks), each the part of [cov_lo, cov_hi) it owns
+    int64_t cov_lo, cov_hi;
+    ssend = send_tables(&sd, N, R, q, sd.local, sdst_lo, sseg_lo, ssoff, &cov_lo, &cov_hi);
+    sown_lo = own_lo;
+    sown_hi = own_hi;
+    const int64_t ca = cov_lo < own_lo ? own_lo : (cov_lo > own_hi ? own_hi : cov_lo);
+    const int64_t cb = cov_hi < own_lo ? own_lo : (cov_hi > own_hi ? own_hi : cov_hi);
+    sra = ca - own_lo;
+    srb = cb - own_lo;
+    sbase = base + before;
+    if (blockIdx.x == 0) {
+      r.dev->S = S;
+      r.dev->base = base;
+      r.dev->o = sd.o;
+      r.dev->Qs = sd.Qs;
+      r.dev->Rs = sd.Rs;
+      r.dev->invN = sd.invN;
+      r.dev->invS = sd.invS;
+      r.dev->ra = sra;
+      r.dev->rb = srb;
     }
   }
   __syncthreads();
