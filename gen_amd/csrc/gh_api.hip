@@ -796,6 +796,9 @@ template <int IT>
 static int rank_cap(int cus) {  // multi-rank: k_rank_a's (k_rank_b has no grid barrier)
   return occ_blocks(k_rank_a<IT>) * cus;
 }
+#ifndef GH_PAIRS_SHARDS
+#define GH_PAIRS_SHARDS 0  // 1: the one-rank pair kernel also folds its maxima into the shards (variant timing)
+#endif
 #ifndef GH_RS_MIN_IT
 #define GH_RS_MIN_IT 4  // the smallest resample tile considered (particles per thread); variants time larger ones
 #endif
@@ -1513,7 +1516,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.max_only = pf->step_max_only && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
   // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
   // short step more than the fold they save, measured)
-  a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
+  a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step || GH_PAIRS_SHARDS)
                ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride
                : nullptr;
   // multi-rank after a resample: the local half now, the rest once the rows arrive

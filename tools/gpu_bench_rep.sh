@@ -22,7 +22,8 @@ out, reps, variants = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
 for i, v in enumerate(variants, 1):
     us = []
     for r in range(1, reps + 1):
-        d = json.load(open(f"{out}/{i}_{r}.json"))
+        s = open(f"{out}/{i}_{r}.json").read()
+        d = json.loads(s[s.index('{"metric"'):])  # (RCCL prints a banner first on the forced multi-rank path)
         us.append(d["ms_per_step"] * 1e3)
     print(f"{v!r:60s} us/step " + " ".join(f"{u:.2f}" for u in us) + f"  kernel_ms {d['roofline']['kernel_avg_ms']}")
 EOF
