@@ -796,12 +796,6 @@ template <int IT>
 static int rank_cap(int cus) {  // multi-rank: k_rank_a's (k_rank_b has no grid barrier)
   return occ_blocks(k_rank_a<IT>) * cus;
 }
-#ifndef GH_PAIRS_SHARDS
-#define GH_PAIRS_SHARDS 0  // 1: the one-rank pair kernel also folds its maxima into the shards (variant timing)
-#endif
-#ifndef GH_RS_MIN_IT
-#define GH_RS_MIN_IT 4  // the smallest resample tile considered (particles per thread); variants time larger ones
-#endif
 static void pick_resample_tiles(gh_pf* pf, int64_t n) {
   const int cus = pf->ctx->cus;
   pf->rs_grid = 0;
@@ -824,7 +818,6 @@ static void pick_resample_tiles(gh_pf* pf, int64_t n) {
     cands = {{4, rank_cap<4>(cus)}, {8, rank_cap<8>(cus)}, {16, rank_cap<16>(cus)}};
   }
   for (const Cand& c : cands) {
-    if (c.it < GH_RS_MIN_IT) continue;
     if (c.it <= kRsPart && pf->nb_part > (int64_t)kRsPart * kRsBlock) continue;
     const int64_t g = grid_of(c.it);
     if (g <= std::min<int64_t>(gmax, c.cap)) {
@@ -1516,7 +1509,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.max_only = pf->step_max_only && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
   // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
   // short step more than the fold they save, measured)
-  a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step || GH_PAIRS_SHARDS)
+  a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
                ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride
                : nullptr;
   // multi-rank after a resample: the local half now, the rest once the rows arrive
@@ -1718,6 +1711,7 @@ static int wait_mailbox(gh_pf* pf) {
   const uint64_t want = pf->mail_seq;
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spins = 0; __atomic_load_n(tag, __ATOMIC_ACQUIRE) != want; ++spins) {
+    __builtin_ia32_pause();
     if ((spins & 0xfffff) == 0xfffff) {  // every ~1M polls: is the stream still alive?
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
         return set_err(GH_E_STATE, "plan wait: no plan from k_rank_b after 60 s");
