@@ -737,6 +737,7 @@ struct gh_pf {
   hipEvent_t ev_x = nullptr;      //   rows exchanged
   uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]] (k_rank_a) or the R rank records (k_rank_a2)
   uint64_t* h_mail = nullptr;     // pinned, coherent: [tag, R rank records] written by k_rank_b (batched loop)
+  int64_t* dlo = nullptr;         // [R + 1] floor(N k / R): the ranks' first global slots
   uint64_t mail_seq = 0;          //   the tag of the last plan posted there
   bool plan_recs = false;         // the pending plan is k_rank_a2's records (the host takes the decision)
   double plan_thr = 0.0;          //   at this threshold
@@ -908,6 +909,7 @@ static void pf_free(gh_pf* pf) {
   if (pf->ev_x) hipEventDestroy(pf->ev_x);
   if (pf->h_plan) hipHostFree(pf->h_plan);
   if (pf->h_mail) hipHostFree(pf->h_mail);
+  hipFree(pf->dlo);
   if (!pf->opts.record_history) {
     for (auto p : pf->xs) hipFree(p);
     for (auto p : pf->ancs) hipFree(p);
@@ -1340,6 +1342,13 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     ALLOC(pf->amax_all, sizeof(uint64_t) * kAmaxShards * kAmaxStride * ctx->world);
     ALLOC(pf->rec, sizeof(uint64_t) * kRecWords);
     ALLOC(pf->recs_all, sizeof(uint64_t) * kRecWords * ctx->world);
+    ALLOC(pf->dlo, sizeof(int64_t) * (ctx->world + 1));
+    {
+      std::vector<int64_t> t(ctx->world + 1);
+      for (int k = 0; k <= ctx->world; ++k) t[k] = (int64_t)(((__int128)pf->n_global * k) / ctx->world);
+      if (hipMemcpy(pf->dlo, t.data(), sizeof(int64_t) * t.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return fail(set_err(GH_E_HIP, "rank slot table"));
+    }
     // the shards are empty between uses: k_rank_a2 empties what it consumed
     pf->amax_armed = true;
     if (hipStreamCreateWithFlags(&pf->aux, hipStreamNonBlocking) != hipSuccess ||
@@ -1678,6 +1687,7 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.rows = pf->rows_send;
   rb.rows_cap = pf->send_cap;
   rb.C = pf->C;
+  rb.dlo = pf->dlo;
   launch_rank_b(pf, rb);
   HIP_TRY(hipGetLastError());
   // the row exchange (R > 1) starts on the side stream once k_rank_b packed the rows
@@ -1791,6 +1801,7 @@ static int finish_plan(gh_pf* pf) {
     fa.D = D;
     fa.rows = pf->rows_send;
     fa.rows_cap = pf->send_cap;
+    fa.dlo = pf->dlo;
     hipLaunchKernelGGL(k_rows_fill, dim3((unsigned)((pf->n + 255) / 256)), dim3(256), 0, pf->s, fa);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));

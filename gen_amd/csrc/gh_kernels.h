@@ -862,7 +862,7 @@ __device__ __forceinline__ uint64_t sys_target(const DevScalars* dev, uint64_t N
 __device__ __forceinline__ int64_t sys_count_exact(const DevScalars* dev, uint64_t N, uint64_t X) {
   if (X == 0) return 0;
   if (X >= dev->S) return (int64_t)N;
-  const double est = ((double)X * (double)N - (double)dev->o) / (double)dev->S;
+  const double est = ((double)X * (double)N - (double)dev->o) * dev->invS;  // (a start only: corrected below)
   int64_t j = est <= 0.0 ? 0 : (est >= (double)N ? (int64_t)N : (int64_t)est);
   while (j > 0 && sys_target(dev, N, (uint64_t)(j - 1)) >= X) --j;
   while (j < (int64_t)N && sys_target(dev, N, (uint64_t)j) < X) ++j;
@@ -1843,6 +1843,7 @@ struct RankBArgs {
   const uint64_t* totals; // all-gathered rank totals, rank k's at totals[k * tot_stride]
   int tot_stride;         // 1: k_rank_a's totals; kRecWords: k_rank_a2's records
   const uint64_t* recs;   // k_rank_a2's records: this launch takes (and block 0 commits) the decision
+  const int64_t* dlo;     // [R + 1] floor(N k / R): rank k's first global slot (host table)
   uint64_t* hplan;        // (with recs) host-mapped plan mailbox: block 0 copies the R records to
   uint64_t htag;          //   hplan[1..] and then writes htag to hplan[0] (the host polls it)
   DecideArgs d;           //   (with recs) the decision's threshold and histories
@@ -1862,13 +1863,13 @@ struct RankBArgs {
 // owns global slots [dlo_k, dhi_k); this rank's particles cover [cov_lo,
 // cov_hi); the rows for rank k != rank start at soff_k, in slot order.
 __device__ __forceinline__ int64_t send_tables(const DevScalars* sd, uint64_t N, int R, int q, uint64_t local,
-                                               int64_t* dst_lo, int64_t* seg_lo, int64_t* soffs, int64_t* cov_lo_out,
-                                               int64_t* cov_hi_out) {
+                                               const int64_t* dlo_tab, int64_t* dst_lo, int64_t* seg_lo,
+                                               int64_t* soffs, int64_t* cov_lo_out, int64_t* cov_hi_out) {
   const int64_t cov_lo = sys_count_exact(sd, N, sd->base);
   const int64_t cov_hi = sys_count_exact(sd, N, sd->base + local);
   int64_t soff = 0;
   for (int k = 0; k < R; ++k) {
-    const int64_t dlo = (int64_t)(((__int128)N * k) / R), dhi = (int64_t)(((__int128)N * (k + 1)) / R);
+    const int64_t dlo = dlo_tab[k], dhi = dlo_tab[k + 1];  // floor(N k / R), from the host
     const int64_t a = cov_lo > dlo ? cov_lo : dlo, b = cov_hi < dhi ? cov_hi : dhi;
     dst_lo[k] = dlo;
     seg_lo[k] = a;
@@ -1914,6 +1915,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : 0.0;
   uint64_t before = 0;  // tile offset within the rank
   for (int b = threadIdx.x; b < (int)blockIdx.x; b += kRsBlock) before += r.tsum[b] & ~(1ull << 63);
+  __shared__ uint64_t su53;
+  if (threadIdx.x == 64) {  // another wave draws the systematic offset's uniform meanwhile (independent of the totals)
+    const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
+    su53 = u53_bits(w.x, w.y);
+  }
   if (threadIdx.x == 0) {
     if (r.recs) {  // the decision from the R rank records (every block the same)
       const Decision dec = decide_records(r.recs, r.R, r.d.thr);
@@ -1952,17 +1958,16 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     sd.S = S;
     sd.base = base;
     sd.local = r.totals[q * r.tot_stride];
-    const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
-    sd.o = scale_u53(u53_bits(w.x, w.y), S);
-    sd.invN = 1.0 / (double)N;
+    sd.o = scale_u53(su53, S);
+    sd.invN = r.d.inv_n;
     sd.Qs = udiv_n(S, N, sd.invN);
     sd.Rs = S - sd.Qs * N;
-    sd.invS = 1.0 / (double)S;
+    sd.invS = recip_est((double)S);
     const int64_t own_lo = r.lo, own_hi = r.lo + r.n;
     // rows this rank sends: destination blocks in rank order (lower ranks,
     // then higher ranks), each the part of [cov_lo, cov_hi) it owns
     int64_t cov_lo, cov_hi;
-    ssend = send_tables(&sd, N, R, q, sd.local, sdst_lo, sseg_lo, ssoff, &cov_lo, &cov_hi);
+    ssend = send_tables(&sd, N, R, q, sd.local, r.dlo, sdst_lo, sseg_lo, ssoff, &cov_lo, &cov_hi);
     sown_lo = own_lo;
     sown_hi = own_hi;
     const int64_t ca = cov_lo < own_lo ? own_lo : (cov_lo > own_hi ? own_hi : cov_lo);
@@ -2051,6 +2056,7 @@ struct RowsFillArgs {
   int D;
   double* rows;
   int64_t rows_cap;
+  const int64_t* dlo;      // [R + 1] floor(N k / R), from the host
 };
 
 static __global__ __launch_bounds__(256) void k_rows_fill(RowsFillArgs r) {
@@ -2060,7 +2066,7 @@ static __global__ __launch_bounds__(256) void k_rows_fill(RowsFillArgs r) {
   if (threadIdx.x == 0) {
     sd = *r.dev;
     int64_t a, b;
-    send_tables(&sd, N, r.R, r.rank, r.totals[r.rank * r.tot_stride], sdst_lo, sseg_lo, ssoff, &a, &b);
+    send_tables(&sd, N, r.R, r.rank, r.totals[r.rank * r.tot_stride], r.dlo, sdst_lo, sseg_lo, ssoff, &a, &b);
   }
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
