@@ -1939,8 +1939,6 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
       sMq = r.dev->M;
     }
   }
-  __syncthreads();
-  if (!sfire) return;
   __shared__ uint64_t smu[16];
   __shared__ DevScalars sd;
   __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
@@ -1948,7 +1946,9 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ uint64_t sbase;
   const int R = r.R, q = r.rank;
   const uint64_t N = (uint64_t)r.mk.n_global;
+  // (the block sum's LDS barriers also publish the decision)
   before = blk16_sum_u64(before, smu);
+  if (!sfire) return;
   if (threadIdx.x == 0) {
     uint64_t S = 0, base = 0;
     for (int k = 0; k < R; ++k) {
