@@ -5,7 +5,7 @@ set -e
 OUT=${1:-gpurun_out/prof}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-export GH_PROF_STEPS=${GH_PROF_STEPS:-20}
+export GH_PROF_STEPS=${GH_PROF_STEPS:-100}  # the bench line's steps (and warm-up): kernel averages comparable
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 tools/profile_run.py > "$OUT/trace.log" 2>&1
 i=0
 for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \

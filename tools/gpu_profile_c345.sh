@@ -13,7 +13,7 @@ C5="tools/bench_pmmh.py --cpu-chains 1 --iters 1"
 i=0
 for w in c4 c3 c5; do
   case $w in c4) cmd=$C4;; c3) cmd=$C3;; c5) cmd=$C5;; esac
-  GH_PROF_STEPS=20 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$w.trace" -o run --output-format csv -- python3 $cmd > "$OUT/$w.trace.log" 2>&1
+  GH_PROF_STEPS=100 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$w.trace" -o run --output-format csv -- python3 $cmd > "$OUT/$w.trace.log" 2>&1
   for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
               "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_INSTS_SALU" \
               "FETCH_SIZE" "WRITE_SIZE"; do

@@ -8,7 +8,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.argv = [sys.argv[0], "--steps", os.environ.get("GH_PROF_STEPS", "20"), "--warmup", "5", "--no-cpu-baseline", "--no-secondary"] + sys.argv[1:]
+# (defaults = bench.py's own: the same history length, hence the same memory footprint, as the bench line)
+sys.argv = [sys.argv[0], "--steps", os.environ.get("GH_PROF_STEPS", "100"), "--warmup", os.environ.get("GH_PROF_WARMUP", "10"),
+            "--no-cpu-baseline", "--no-secondary"] + sys.argv[1:]
 import bench  # noqa: E402
 
 bench.main()
