@@ -953,7 +953,8 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
   a.nvb = (a.n + kBlock - 1) / kBlock;
   if constexpr (has_pairs<Model>::value) {
     if (use_pairs<Model>(pf)) {
-      const dim3 grid((unsigned)((a.n + 2 * kBlock - 1) / (2 * kBlock))), block(kBlock);
+      const dim3 grid((unsigned)(a.grid_blocks > 0 ? a.grid_blocks : (a.n + 2 * kBlock - 1) / (2 * kBlock))),
+          block(kBlock);
       if (a.part != 2) {
         pf->nb_part = grid.x;
         pf->last_pairs = true;
@@ -971,7 +972,7 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
     pf->nb_part = pf->nb_step;
     pf->last_pairs = false;
   }
-  const dim3 grid((unsigned)(a.part == 2 ? a.nvb : pf->nb_step)), block(kBlock);
+  const dim3 grid((unsigned)(a.grid_blocks > 0 ? a.grid_blocks : (a.part == 2 ? a.nvb : pf->nb_step))), block(kBlock);
   // the timed launch records its events at the kernel's own start and end
   if (init)
     hipExtLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, e0, e1, 0, (const double*)pf->m->dparams,
@@ -1102,27 +1103,12 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
         tA = nb;
         tB = nb;
       }
-      if (tA > 0) {
+      if (tA > 0 || tB < nb) {  // one launch: blocks [0, tA) and, remapped, [tB, nb)
         StepArgs b = a;
         b.part = 2;
-        b.n = std::min<int64_t>(n, tA * kb);
-        CHECK(launch_step(pf, o, b, init));
-      }
-      if (tB < nb) {  // every per-slot pointer advanced to tile tB
-        const int64_t off = tB * kb;
-        StepArgs b = a;
-        b.part = 2;
-        b.j0 = off;
-        b.n = n - off;
-        b.lo = a.lo + off;
-        b.anc = a.anc + off;
-        b.mark = a.mark + off;
-        b.carry = a.carry + off / 64;
-        b.xout = a.xout + tbase(off, pf->D);  // off is a whole number of tiles
-        b.logw = a.logw + off;
-        b.pm = a.pm + tB;
-        b.ps = a.ps + tB;
-        b.ps2 = a.ps2 + tB;
+        b.vb_split = tA;
+        b.vb_skip = tB - tA;
+        b.grid_blocks = tA + (nb - tB);
         CHECK(launch_step(pf, o, b, init));
       }
     }

@@ -108,6 +108,11 @@ struct StepArgs {
   // gets every per-slot pointer advanced by j0 slots (j0 = 0 otherwise).
   int part;              // host only: 0 one launch; 1, 2 the halves of a split step
   int64_t j0;            // slot offset of this launch (the received-row index only)
+  // part 2 as ONE launch over the block ranges [0, vb_split) and
+  // [vb_split + vb_skip, ...): block b >= vb_split steps block b + vb_skip
+  // (vb_skip = 0: every block its own)
+  int64_t vb_split, vb_skip;
+  int64_t grid_blocks;   // host only: the launch's blocks when nonzero
 };
 
 // ------------------------------------------------------------ reductions
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   __shared__ double sm[3][4];
   __shared__ double logtab[kMathTabDoubles];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t vb = blockIdx.x;
+  const int64_t vb = blockIdx.x + (blockIdx.x >= a.vb_split ? a.vb_skip : 0);
   const int64_t tile = vb * (kBlock / 64) + w;
   const int64_t j = tile * 64 + lane;
   // The device flags and this slot's range mark + carry are loaded before the
@@ -464,7 +469,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
   __shared__ double sm[3][4];
   __shared__ double logtab[kMathTabDoubles];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t vb = blockIdx.x;
+  const int64_t vb = blockIdx.x + (blockIdx.x >= a.vb_split ? a.vb_skip : 0);
   const int64_t tile0 = (vb * (kBlock / 64) + w) * 2;
   const int64_t j0 = tile0 * 64 + lane, j1 = j0 + 64;
   uint64_t mv0 = 0, mv1 = 0, cv0 = 0, cv1 = 0;
