@@ -1347,6 +1347,8 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
         hipHostMalloc((void**)&pf->h_plan, sizeof(uint64_t) * std::max(ctx->world + 1, kRecWords * ctx->world),
                       hipHostMallocDefault) != hipSuccess)
       return fail(set_err(GH_E_NOMEM, "multi-rank plan buffers"));
+    // tags count from 1: a reused pinned page must not hold one already
+    memset(pf->h_mail, 0, sizeof(uint64_t) * (1 + kRecWords * ctx->world));
   }
   if (!pf->opts.record_history) {
     for (int i = 0; i < 2; ++i) {
