@@ -208,9 +208,13 @@ def pmc_profile(name):
 
 
 # --------------------------------------------------------------- PF runs
-def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn):
+def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn, loop="run"):
     """One filter: init, warm-up steps, then the timed region over K steps
-    (barrier + device sync on both sides, max over ranks)."""
+    (barrier + device sync on both sides, max over ranks).  loop: "run" =
+    gh_pf_run (the batched loop); "cbc" = the reference caller loop, one
+    gh_pf_maybe_resample(did, ess) + gh_pf_step per step through the C ABI as
+    a Julia ccall shim issues them (test/inference/particle_filter.jl:130-137);
+    "cbc_async" = the same with the decision not asked for (NULL did / ess)."""
     T = a.warmup + a.steps + 1
     seed_data = 2 if isinstance(model, gen.LinearGaussianSSM) else 3
     _, ys = model.simulate(T, np.random.default_rng(seed_data))
@@ -234,9 +238,26 @@ def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn):
         if dist is not None:
             dist.barrier()
 
+    if loop != "run":
+        import ctypes
+
+        from gen_amd import _lib
+
+        lib = _lib.load()
+        thr = float(n_global / 2 if a.ess_threshold is None else a.ess_threshold)
+        did, ess = ctypes.c_int(), ctypes.c_double()
+        pd, pe = (ctypes.byref(did), ctypes.byref(ess)) if loop == "cbc" else (None, None)
+        obs = [ctypes.byref(batch.arr[i]) for i in range(a.steps)]
+        mr_fn, step_fn, h = lib.gh_pf_maybe_resample, lib.gh_pf_step, st.h
     barrier()
     t0 = time.perf_counter()
-    gen.run_particle_filter(st, batch, a.ess_threshold, proposal=prop)
+    if loop == "run":
+        gen.run_particle_filter(st, batch, a.ess_threshold, proposal=prop)
+    else:
+        for i in range(a.steps):
+            rc = mr_fn(h, thr, pd, pe) or step_fn(h, obs[i], 0)
+            if rc:
+                _lib.check(rc)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -319,6 +340,24 @@ def secondary_multirank_path(gen, a, c2_ms, c4_ms):
         ctx.close()
     out["note"] = ("world = 1 on the multi-rank path over RCCL: the collectives are one-rank copies and no rows "
                    "move, so the extra time is the path's launches, host plan and all-gather kernels, not xGMI")
+    return out
+
+
+def secondary_call_by_call(gen, ctx, a, c2_ms):
+    """C2 through the reference's own caller loop instead of gh_pf_run: per
+    step gh_pf_maybe_resample then gh_pf_step, each one C-ABI call from the
+    host (ctypes here, a ccall in the Julia shim).  "with_decision" asks for
+    the Bool that maybe_resample! returns (the host waits for k_resample1 to
+    post it to a host-mapped mailbox, not for the stream); "no_decision"
+    passes NULL."""
+    model = gen.LinearGaussianSSM.benchmark(a.d)
+    out = {}
+    for name, loop in (("with_decision", "cbc"), ("no_decision", "cbc_async")):
+        r = pf_run(gen, ctx, None, 1, a, model, a.particles, "", lambda n_res: 16 * a.d + 16, loop=loop)
+        ms = r["dt"] * 1e3 / a.steps
+        out[name] = {"ms_per_step": ms, "vs_gh_pf_run": None if not c2_ms else round(ms / c2_ms, 4),
+                     "resample_steps_timed": r["n_res"], "log_ml": r["lml"]}
+    out["gh_pf_run_ms_per_step"] = c2_ms
     return out
 
 
@@ -415,7 +454,7 @@ def secondary_c5(gen, ctx, a):
 def main(argv=None):
     a = parse(argv)
     if a.time_every is None:
-        a.time_every = 1  # every step-kernel launch (measured: no change in ms_per_step against 2 or none)
+        a.time_every = 10  # every 10th step-kernel launch (A/B at 20 steps: events on every launch cost 1.0 us per step)
     import gen_amd as gen
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -509,6 +548,8 @@ def main(argv=None):
     if rank == 0 and world == 1 and not a.no_secondary and a.model == "lgssm":
         c4 = secondary_c4(gen, ctx, a)
         out["secondary"] = {"C4": c4, "C3": secondary_c3(gen, ctx, a), "C5": secondary_c5(gen, ctx, a)}
+        if a.proposal == "default":
+            out["secondary"]["call_by_call"] = secondary_call_by_call(gen, ctx, a, out["ms_per_step"])
         if a.proposal == "default" and a.transport == "rccl":
             out["secondary"]["multirank_path"] = secondary_multirank_path(gen, a, out["ms_per_step"],
                                                                           c4["ms_per_step"])

@@ -72,6 +72,7 @@ SIGNATURES = {
     "gh_ctx_destroy": (c_int, [c_void_p]),
     "gh_ctx_force_multirank": (c_int, [c_void_p]),
     "gh_pf_step_params": (c_int, [c_void_p, POINTER(Obs), c_int, c_void_p]),
+    "gh_pf_step_params_conditional": (c_int, [c_void_p, POINTER(Obs), c_void_p, POINTER(c_double)]),
     "gh_ctx_rank": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
     "gh_ctx_stream": (c_int, [c_void_p, POINTER(c_void_p)]),
     "gh_ctx_synchronize": (c_int, [c_void_p]),

@@ -45,6 +45,10 @@ def compile_cmd(src: str, obj: str, extra: list[str] | None = None) -> list[str]
     return [HIPCC, *FLAGS, *(extra or []), "-c", src, "-o", obj]
 
 
+def _sources(csrc: str) -> list[str]:
+    return [os.path.join(csrc, "gh_api.hip")] + sorted(glob.glob(os.path.join(csrc, "gh_inst_lg*.hip")))
+
+
 def link_cmd(objs: list[str], out: str) -> list[str]:
     return [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-o", out, "-L/opt/rocm/lib", "-lrccl",
             "-Wl,-rpath,/opt/rocm/lib"]
@@ -57,11 +61,12 @@ def hipcc_cmd(out: str = LIB, extra: list[str] | None = None) -> list[str]:
             "-Wl,-rpath,/opt/rocm/lib"]
 
 
-def _compile_all(out: str, obj_dir: str, extra: list[str] | None, verbose: bool) -> None:
+def _compile_all(out: str, obj_dir: str, extra: list[str] | None, verbose: bool, sources: list[str] | None = None) -> None:
     """Every translation unit to an object in parallel, then one link."""
     os.makedirs(obj_dir, exist_ok=True)
-    objs = [os.path.join(obj_dir, os.path.basename(s).replace(".hip", ".o")) for s in SOURCES]
-    cmds = [compile_cmd(s, o, extra) for s, o in zip(SOURCES, objs)]
+    sources = sources or SOURCES
+    objs = [os.path.join(obj_dir, os.path.basename(s).replace(".hip", ".o")) for s in sources]
+    cmds = [compile_cmd(s, o, extra) for s, o in zip(sources, objs)]
     if verbose:
         print(" ".join(cmds[0]), f"(+{len(cmds) - 1} units, {JOBS} jobs)", flush=True)
     from concurrent.futures import ThreadPoolExecutor
@@ -98,13 +103,24 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return LIB
 
 
-def build_variant(name: str, defines: list[str]) -> str:
+def build_variant(name: str, defines: list[str], patch: str | None = None) -> str:
     """Timing-only variant (e.g. -DGH_PHILOX_ROUNDS=7) at gen_amd/variants/<name>.so;
-    never the product, never used by the parity tests."""
+    never the product, never used by the parity tests.  `patch`: a unified
+    diff against gen_amd/csrc (e.g. tools/rs_stamps.patch, the resample's
+    phase clocks), applied to a copy of the sources for this build only."""
     out_dir = os.path.join(HERE, "variants")
     os.makedirs(out_dir, exist_ok=True)
     out = os.path.join(out_dir, f"{name}.so")
-    _compile_all(out, os.path.join(out_dir, f"obj_{name}"), [f"-D{d}" for d in defines], True)
+    sources = None
+    if patch:
+        src = os.path.join(out_dir, f"src_{name}")
+        shutil.rmtree(src, ignore_errors=True)
+        shutil.copytree(CSRC, os.path.join(src, "gen_amd", "csrc"))
+        shutil.copytree(os.path.join(ROOT, "include"), os.path.join(src, "include"))
+        with open(patch) as f:
+            subprocess.run(["patch", "-s", "-p1", "-d", os.path.join(src, "gen_amd", "csrc")], stdin=f, check=True)
+        sources = _sources(os.path.join(src, "gen_amd", "csrc"))
+    _compile_all(out, os.path.join(out_dir, f"obj_{name}"), [f"-D{d}" for d in defines], True, sources)
     return out
 
 

@@ -18,7 +18,6 @@
 #include <cstring>
 #include <string>
 #include <type_traits>
-#include <chrono>
 #include <vector>
 
 #include "../../include/gen_hip.h"
@@ -104,6 +103,7 @@ struct gh_ctx {
   // gh_ctx_force_multirank: filters take the multi-rank path even at world 1
   // (a one-rank RCCL communicator; tests and timing on a one-GPU box)
   bool force_multi = false;
+  int n_filters = 0;  // live filters (their buffers follow the path chosen at their creation)
 };
 
 // the filter's multi-rank path (collectives, split steps) is in use
@@ -179,6 +179,10 @@ extern "C" int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_
 extern "C" int gh_ctx_force_multirank(gh_ctx* c) {
   if (!c) return set_err(GH_E_INVAL, "null ctx");
   if (c->force_multi) return GH_OK;
+  // a live filter allocated the one-rank path's buffers only; switching it
+  // would run the multi-rank kernels and collectives on missing buffers
+  if (c->n_filters > 0)
+    return set_err(GH_E_STATE, "gh_ctx_force_multirank: %d filter(s) exist on this context", c->n_filters);
   if (c->world == 1 && !c->host_comm && !c->comm) {  // a one-rank RCCL communicator
     ncclUniqueId u;
     NCCL_TRY(ncclGetUniqueId(&u));
@@ -737,6 +741,15 @@ struct gh_pf {
   hipEvent_t ev_x = nullptr;      //   rows exchanged
   uint64_t* h_plan = nullptr;     // pinned: [fire, totals[R]] (k_rank_a) or the R rank records (k_rank_a2)
   uint64_t* h_mail = nullptr;     // pinned, coherent: [tag, R rank records] written by k_rank_b (batched loop)
+  uint64_t* d_mail = nullptr;     //   its device alias (the kernels' pointer)
+  // maybe_resample!'s decision for the host (one rank): pinned, coherent [tag,
+  // fire | err << 32, ess] posted by k_resample1's block 0 (no stream sync)
+  uint64_t* h_dec = nullptr;
+  uint64_t* d_dec = nullptr;
+  uint64_t dec_seq = 0;           // the tag of the last decision posted there
+  bool dec_posted = false;        // the last maybe_resample! posts its decision to h_dec
+  bool no_max_only = false;       // gh_pf_step_params: the step writes full partials
+  bool mr_stale = false;          // multi-rank: the last step left its weight sums to the next resample
   int64_t* dlo = nullptr;         // [R + 1] floor(N k / R): the ranks' first global slots
   uint64_t mail_seq = 0;          //   the tag of the last plan posted there
   bool plan_recs = false;         // the pending plan is k_rank_a2's records (the host takes the decision)
@@ -801,6 +814,11 @@ static void pick_resample_tiles(gh_pf* pf, int64_t n) {
   const int cus = pf->ctx->cus;
   pf->rs_grid = 0;
   pf->rs_it = 0;
+  // multi-rank: the choice (tile size, usable or not) is made for the largest
+  // shard, ceil(N / R), so that every rank takes the same resample path and
+  // posts the same collectives; each rank's grid covers its own particles
+  const int64_t n_own = n;
+  if (mr(pf->ctx)) n = (pf->n_global + pf->ctx->world - 1) / pf->ctx->world;
   // the polling waves read at most 64 * kRsPoll tile words
   const int64_t gmax = 64 * kRsPoll;
   auto grid_of = [&](int it) { return (n + (int64_t)it * kRsBlock - 1) / ((int64_t)it * kRsBlock); };
@@ -819,11 +837,12 @@ static void pick_resample_tiles(gh_pf* pf, int64_t n) {
     cands = {{4, rank_cap<4>(cus)}, {8, rank_cap<8>(cus)}, {16, rank_cap<16>(cus)}};
   }
   for (const Cand& c : cands) {
-    if (c.it <= kRsPart && pf->nb_part > (int64_t)kRsPart * kRsBlock) continue;
+    const int64_t nb_part = (n + (pf->pairs ? 2 : 1) * kBlock - 1) / ((pf->pairs ? 2 : 1) * kBlock);
+    if (c.it <= kRsPart && nb_part > (int64_t)kRsPart * kRsBlock) continue;
     const int64_t g = grid_of(c.it);
     if (g <= std::min<int64_t>(gmax, c.cap)) {
       pf->rs_it = c.it;
-      pf->rs_grid = (int)g;
+      pf->rs_grid = (int)std::max<int64_t>(1, (n_own + (int64_t)c.it * kRsBlock - 1) / ((int64_t)c.it * kRsBlock));
       return;
     }
   }
@@ -909,11 +928,13 @@ static void pf_free(gh_pf* pf) {
   if (pf->ev_x) hipEventDestroy(pf->ev_x);
   if (pf->h_plan) hipHostFree(pf->h_plan);
   if (pf->h_mail) hipHostFree(pf->h_mail);
+  if (pf->h_dec) hipHostFree(pf->h_dec);
   hipFree(pf->dlo);
   if (!pf->opts.record_history) {
     for (auto p : pf->xs) hipFree(p);
     for (auto p : pf->ancs) hipFree(p);
   }
+  pf->ctx->n_filters--;
   delete pf;
 }
 
@@ -962,6 +983,9 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
       if (init)
         hipExtLaunchKernelGGL((k_step_pairs<Model, true>), grid, block, 0, pf->s, e0, e1, 0,
                               (const double*)pf->m->dparams, p, o, a);
+      else if (a.part == 2)
+        hipExtLaunchKernelGGL((k_step_pairs<Model, false, true>), grid, block, 0, pf->s, e0, e1, 0,
+                              (const double*)pf->m->dparams, p, o, a);
       else
         hipExtLaunchKernelGGL((k_step_pairs<Model, false>), grid, block, 0, pf->s, e0, e1, 0,
                               (const double*)pf->m->dparams, p, o, a);
@@ -977,6 +1001,9 @@ static void launch_step_t(gh_pf* pf, const typename Model::Params& p, const Step
   if (init)
     hipExtLaunchKernelGGL((k_step<Model, true>), grid, block, 0, pf->s, e0, e1, 0, (const double*)pf->m->dparams,
                           p, o, a);
+  else if (a.part == 2)  // one launch over two block ranges (the block remap's own instantiation)
+    hipExtLaunchKernelGGL((k_step<Model, false, true>), grid, block, 0, pf->s, e0, e1, 0,
+                          (const double*)pf->m->dparams, p, o, a);
   else
     hipExtLaunchKernelGGL((k_step<Model, false>), grid, block, 0, pf->s, e0, e1, 0, (const double*)pf->m->dparams,
                           p, o, a);
@@ -988,11 +1015,26 @@ static void launch_fold(gh_pf* pf, const StepArgs& a, bool init, int64_t nb) {
                      init ? 0 : 1, 0.0, pf->n_global);
 }
 
-// one rank: make stats_all current (the fold is otherwise done by k_resample1)
+// one rank: make stats_all current (the fold is otherwise done by k_resample1).
+// After a max-only step the block sums are recomputed first (k_block_sums:
+// the values a full-partials step would have written).
 static int ensure_stats(gh_pf* pf) {
-  if (mr(pf->ctx) || pf->stats_valid) return GH_OK;
-  if (pf->max_only)  // cannot happen: a max-only step is always followed by the fused resample
-    return set_err(GH_E_STATE, "internal: step partials hold block maxima only");
+  if (mr(pf->ctx)) {
+    // (recomputing them here would be a collective only this caller enters)
+    if (pf->mr_stale)
+      return set_err(GH_E_STATE, "multi-rank: the last step left its weight sums to the next maybe_resample "
+                                 "(a gh_pf_run that stopped early); step again first");
+    return GH_OK;
+  }
+  if (pf->stats_valid) return GH_OK;
+  if (pf->max_only && pf->n > 0) {
+    if (pf->last_pairs)
+      hipLaunchKernelGGL(k_block_sums<true>, dim3((unsigned)pf->nb_part), dim3(kBlock), 0, pf->s,
+                         (const double*)pf->logw, pf->n, (const double*)pf->pm, pf->ps, pf->ps2);
+    else
+      hipLaunchKernelGGL(k_block_sums<false>, dim3((unsigned)pf->nb_part), dim3(kBlock), 0, pf->s,
+                         (const double*)pf->logw, pf->n, (const double*)pf->pm, pf->ps, pf->ps2);
+  }
   hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_part,
                      pf->stats_all, pf->dev, 0, 0.0, pf->n_global);
   HIP_TRY(hipGetLastError());
@@ -1271,10 +1313,17 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
                                "HMM, and LGSSM with d + dy <= %d; the Gaussian proposal: the nonlinear SSM)",
                    proposal, kMaxObs);
   gh_ctx* ctx = m->ctx;
+  // every rank holds at least one particle, so each rank takes the same path
+  // through every collective (a rank with none would skip kernels whose
+  // all-gathers the others post)
+  if (mr(ctx) && n_particles < ctx->world)
+    return set_err(GH_E_INVAL, "gh_pf_init: %lld particles for %d ranks (at least one per rank)",
+                   (long long)n_particles, ctx->world);
   HIP_TRY(hipSetDevice(ctx->device));
   gh_pf* pf = new gh_pf();
   pf->m = m;
   pf->ctx = ctx;
+  ctx->n_filters++;  // (pf_free undoes it on every failure below)
   pf->s = ctx->stream;
   pf->D = m->d;
   pf->cond = pin_ref != nullptr;  // before the first step kernel (use_pairs)
@@ -1283,8 +1332,10 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (opts) pf->opts = *opts;
   else gh_pf_opts_default(&pf->opts);
   if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC && pf->opts.resampler != GH_RESAMPLE_MULTINOMIAL) {
+    const int r = pf->opts.resampler;
+    pf->ctx->n_filters--;
     delete pf;
-    return set_err(GH_E_INVAL, "unknown resampler %d", pf->opts.resampler);
+    return set_err(GH_E_INVAL, "unknown resampler %d", r);
   }
   pf->n_global = n_particles;
   pf->lo = split_lo(n_particles, ctx->rank, ctx->world);
@@ -1349,7 +1400,14 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
       return fail(set_err(GH_E_NOMEM, "multi-rank plan buffers"));
     // tags count from 1: a reused pinned page must not hold one already
     memset(pf->h_mail, 0, sizeof(uint64_t) * (1 + kRecWords * ctx->world));
+    if (hipHostGetDevicePointer((void**)&pf->d_mail, pf->h_mail, 0) != hipSuccess)
+      return fail(set_err(GH_E_HIP, "plan mailbox: device alias"));
   }
+  if (hipHostMalloc((void**)&pf->h_dec, sizeof(uint64_t) * 4, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void**)&pf->d_dec, pf->h_dec, 0) != hipSuccess)
+    return fail(set_err(GH_E_NOMEM, "decision mailbox"));
+  memset(pf->h_dec, 0, sizeof(uint64_t) * 4);
   if (!pf->opts.record_history) {
     for (int i = 0; i < 2; ++i) {
       double* x = nullptr;
@@ -1502,8 +1560,13 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.stats_out = !mr(pf->ctx) ? pf->stats_all : pf->dev->stats;
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   const bool multi = mr(pf->ctx);
-  // multi-rank: a max-only step needs the shards (the rank maximum has no other fold)
-  a.max_only = pf->step_max_only && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
+  // One rank: every step writes block maxima only — the next maybe_resample!
+  // sums the weights in its own pass, any other reader recomputes the sums
+  // (ensure_stats) — so a caller's maybe_resample! + particle_filter_step!
+  // loop runs what gh_pf_run runs.  Multi-rank: gh_pf_run's steps, which
+  // need the shards (the rank maximum has no other fold).
+  const bool lazy = !multi && pf->rs_grid > 0 && !pf->cond && pf->n > 0 && !pf->no_max_only;
+  a.max_only = (pf->step_max_only || lazy) && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
   // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
   // short step more than the fold they save, measured)
   a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
@@ -1520,6 +1583,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   if (!a.max_only) CHECK(share_stats(pf));  // (max-only: the resample's own all-gathers)
   pf->t = t;
   pf->max_only = a.max_only != 0;
+  pf->mr_stale = multi && a.max_only;
   pf->amax_valid = a.amax != nullptr;
   if (!multi) pf->amax_armed = false;
   pf->resample_calls = 0;
@@ -1655,7 +1719,7 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.tot_stride = sums ? kRecWords : 1;
   rb.recs = sums ? pf->recs_all : nullptr;
   if (sums) {  // the plan comes back through the host-mapped mailbox (no event, no copy, no stream wait)
-    rb.hplan = pf->h_mail;
+    rb.hplan = pf->d_mail;
     rb.htag = ++pf->mail_seq;
   }
   rb.d = d;
@@ -1704,24 +1768,24 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
 // tag (the records were copied before it, behind a system-scope release).  A
 // kernel that never writes it (a fault) ends the wait through the stream's
 // error after a bounded spin.
-static int wait_mailbox(gh_pf* pf) {
-  volatile uint64_t* tag = pf->h_mail;
-  const uint64_t want = pf->mail_seq;
+static int wait_tag(gh_pf* pf, volatile uint64_t* tag, uint64_t want, const char* what) {
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t spins = 0; __atomic_load_n(tag, __ATOMIC_ACQUIRE) != want; ++spins) {
     __builtin_ia32_pause();
     if ((spins & 0xfffff) == 0xfffff) {  // every ~1M polls: is the stream still alive?
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
-        return set_err(GH_E_STATE, "plan wait: no plan from k_rank_b after 60 s");
+        return set_err(GH_E_STATE, "%s wait: nothing posted after 60 s", what);
       const hipError_t e = hipStreamQuery(pf->s);
-      if (e != hipSuccess && e != hipErrorNotReady) return set_err(GH_E_HIP, "plan wait: %s", hipGetErrorString(e));
+      if (e != hipSuccess && e != hipErrorNotReady) return set_err(GH_E_HIP, "%s wait: %s", what, hipGetErrorString(e));
       if (e == hipSuccess && __atomic_load_n(tag, __ATOMIC_ACQUIRE) != want)
-        return set_err(GH_E_STATE, "plan wait: the stream drained without the plan (tag %llu, want %llu)",
+        return set_err(GH_E_STATE, "%s wait: the stream drained without it (tag %llu, want %llu)", what,
                        (unsigned long long)*tag, (unsigned long long)want);
     }
   }
   return GH_OK;
 }
+static int wait_mailbox(gh_pf* pf) { return wait_tag(pf, pf->h_mail, pf->mail_seq, "plan"); }
+static int wait_decision(gh_pf* pf) { return wait_tag(pf, pf->h_dec, pf->dec_seq, "decision"); }
 
 static int finish_plan(gh_pf* pf) {
   if (!pf->plan_pending) return GH_OK;
@@ -1811,6 +1875,7 @@ static int finish_plan(gh_pf* pf) {
 static int resample_enqueue(gh_pf* pf, double thr) {
   const int t = pf->t;
   CHECK(grow_for_step(pf, t + 1));
+  pf->dec_posted = false;
   const int R = pf->ctx->world;
   const bool multi = mr(pf->ctx);
   const int64_t n = pf->n;
@@ -1859,6 +1924,8 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     ra.C = pf->C;
     ra.seed = pf->seed;
     ra.t = (uint32_t)t;
+    ra.hdec = pf->d_dec;
+    ra.htag = ++pf->dec_seq;
     if (pf->amax) {  // the step's own max fold (when it wrote one); the next step's shards emptied
       ra.amax_in = pf->max_only && pf->amax_valid ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride : nullptr;
       ra.amax_reset = pf->amax + ((t + 1) & 1) * kAmaxShards * kAmaxStride;
@@ -1882,6 +1949,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     }
 #undef GH_RS1
     pf->stats_valid = true;
+    pf->dec_posted = true;
     if (sys) {
       pf->marks_pending = true;
     } else {
@@ -1993,6 +2061,21 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
   // the ancestor array is only read if the resample fired
   if (pf->cond) HIP_TRY(hipMemsetAsync(anc_for_step(pf, pf->t + 1), 0, sizeof(int32_t), pf->s));
   if (did || ess) {
+    // the fused one-rank resample posts its decision to the host mailbox as
+    // soon as it is taken: wait for that, not for the stream (the caller's
+    // next particle_filter_step! is enqueued while the marks are written)
+    if (pf->dec_posted) {
+      const int rc = wait_decision(pf);
+      if (rc == GH_OK) {
+        const uint64_t w = __atomic_load_n(&pf->h_dec[1], __ATOMIC_ACQUIRE);
+        const int err = (int)(uint32_t)(w >> 32);
+        if (err) return set_err(err, dev_error_msg(err));
+        if (did) *did = (int)(uint32_t)w;
+        if (ess) *ess = as_f64(__atomic_load_n(&pf->h_dec[2], __ATOMIC_ACQUIRE));
+        return GH_OK;
+      }
+      if (rc != GH_E_STATE) return rc;  // (drained without a post: the device error below)
+    }
     DevScalars h;
     HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
     HIP_TRY(hipStreamSynchronize(pf->s));
@@ -2232,9 +2315,26 @@ extern "C" int gh_pf_get_scores(gh_pf* pf, double* total, double* per_step) {
 // particle j's trajectory (k_scores twice; the past observations rebuilt under
 // nm), the step under nm, then logw_j += Delta_j and the block partials again
 // (k_add_delta).  One rank, history kept, same family and dimensions.
+static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm, const double* pin_ref);
+
 extern "C" int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm) {
   if (!pf || !nm) return set_err(GH_E_INVAL, "gh_pf_step_params: null argument");
-  if (pf->cond) return set_err(GH_E_STATE, "gh_pf_step_params: a conditional filter keeps its model");
+  if (pf->cond)
+    return set_err(GH_E_STATE, "gh_pf_step_params: a conditional filter steps with gh_pf_step_params_conditional");
+  return step_params_impl(pf, obs, proposal, nm, nullptr);
+}
+
+// conditional SMC with changed parameters (particle Gibbs with parameter
+// moves): the re-scoring of gh_pf_step_params, then the conditional step
+// pinning the distinguished particle to ref_xt
+extern "C" int gh_pf_step_params_conditional(gh_pf* pf, const gh_obs* obs, gh_model* nm, const double* ref_xt) {
+  if (!pf || !nm || !ref_xt) return set_err(GH_E_INVAL, "gh_pf_step_params_conditional: null argument");
+  if (!pf->cond)
+    return set_err(GH_E_STATE, "gh_pf_step_params_conditional on a filter not made by gh_pf_init_conditional");
+  return step_params_impl(pf, obs, GH_PROPOSAL_DEFAULT, nm, ref_xt);
+}
+
+static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm, const double* pin_ref) {
   if (mr(pf->ctx)) return set_err(GH_E_STATE, "gh_pf_step_params: one rank (the re-scoring walks the genealogy)");
   if (!pf->opts.record_history) return set_err(GH_E_STATE, "gh_pf_step_params needs record_history");
   const gh_model* m = pf->m;
@@ -2269,9 +2369,25 @@ extern "C" int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_
     cleanup();
     return rc;
   }
+  {  // the new step's observation under the new parameters, checked before anything changes
+    StepObs probe;
+    rc = make_obs(nm, T + 1, obs, &probe);
+    if (rc) {
+      cleanup();
+      return rc;
+    }
+  }
+  const gh_model* m_old = pf->m;
+  std::vector<StepObs> hist_old = pf->obs_hist;
   pf->m = nm;
   pf->obs_hist = rebuilt;
-  rc = pf_step_impl(pf, obs, proposal, nullptr);
+  pf->no_max_only = true;  // k_add_delta rewrites full partials of the changed weights
+  rc = pf_step_impl(pf, obs, proposal, pin_ref);
+  pf->no_max_only = false;
+  if (rc && pf->t == T) {  // no step was taken: the filter keeps its model and history
+    pf->m = const_cast<gh_model*>(m_old);
+    pf->obs_hist = hist_old;
+  }
   if (!rc && n > 0) {
     hipLaunchKernelGGL(k_add_delta, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, pf->logw,
                        (const double*)dnew, (const double*)dold, n, pf->pm, pf->ps, pf->ps2);
@@ -2279,6 +2395,8 @@ extern "C" int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_
     pf->nb_part = pf->nb_step;
     pf->last_pairs = false;
     pf->stats_valid = false;
+    pf->max_only = false;
+    pf->amax_valid = false;
   }
   if (hipStreamSynchronize(pf->s) != hipSuccess && !rc) rc = set_err(GH_E_HIP, "gh_pf_step_params: sync");
   cleanup();
@@ -2972,14 +3090,6 @@ extern "C" int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n
   gh_pf_destroy(pf);
   return rc;
 }
-
-#if defined(GH_RS_STAMPS)
-extern "C" int gh_debug_rs_stamps(uint64_t* out, int n) {
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rs_stamps), sizeof(uint64_t) * (size_t)n));
-  return GH_OK;
-}
-#endif
 
 // ------------------------------------------------------------------ PMMH
 extern "C" int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T,

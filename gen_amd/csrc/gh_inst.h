@@ -15,6 +15,8 @@
 #define GH_LG_KERNELS(X, D, S)                                                                               \
   X __global__ void gh::k_step<gh::LGModel<D, S>, true>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
   X __global__ void gh::k_step<gh::LGModel<D, S>, false>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::LGModel<D, S>, false, true>(const double*, gh::LGParams, gh::StepObs,         \
+                                                               gh::StepArgs);                                    \
   X __global__ void gh::k_rejuv<gh::LGModel<D, S>, true>(const double*, gh::LGParams, gh::StepObs, gh::RejuvArgs); \
   X __global__ void gh::k_rejuv<gh::LGModel<D, S>, false>(const double*, gh::LGParams, gh::StepObs,              \
                                                           gh::RejuvArgs);                                        \
@@ -31,8 +33,12 @@
 #define GH_LGO_KERNELS(X, D)                                                                                   \
   X __global__ void gh::k_step<gh::LGOptModel<D>, true>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
   X __global__ void gh::k_step<gh::LGOptModel<D>, false>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::LGOptModel<D>, false, true>(const double*, gh::LGParams, gh::StepObs,           \
+                                                               gh::StepArgs);                                      \
   X __global__ void gh::k_step<gh::LGLinModel<D>, true>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
-  X __global__ void gh::k_step<gh::LGLinModel<D>, false>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs);
+  X __global__ void gh::k_step<gh::LGLinModel<D>, false>(const double*, gh::LGParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::LGLinModel<D>, false, true>(const double*, gh::LGParams, gh::StepObs,           \
+                                                               gh::StepArgs);
 
 #define GH_LG_DIM(X, D)      \
   GH_LG_KERNELS(X, D, 0)     \

@@ -225,6 +225,17 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
   return (sm[0] + sm[1]) + (sm[2] + sm[3]);
 }
 
+// agent-scope relaxed accesses: global_load/store ... sc1 (L1 bypassed; the
+// store writes through and drops the line from the XCD's L2)
+template <class T>
+__device__ __forceinline__ T ld_sc1(T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------- buffer accesses
 // A buffer descriptor (wave-uniform, from kernel arguments) + a 32-bit
 // per-lane byte offset + a uniform SGPR offset per state component: one
@@ -333,7 +344,7 @@ __device__ __forceinline__ void block_max_partial(double lw, double (*sm)[4], do
 // launch (a per-block ticket would serialise ~4k atomics per 1M particles at
 // the memory side), and the block barrier waits for LDS only, so a block's
 // state stores are not waited for before it retires.
-template <class Model, bool INIT>
+template <class Model, bool INIT, bool SPLIT = false>
 __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double* __restrict__ prm,
                                                                     typename Model::Params p0, StepObs o,
                                                                     StepArgs a) {
@@ -342,7 +353,10 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   __shared__ double sm[3][4];
   __shared__ double logtab[kMathTabDoubles];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t vb = blockIdx.x + (blockIdx.x >= a.vb_split ? a.vb_skip : 0);
+  // (the remap lives in its own instantiation: the compare on two kernel
+  // arguments made every other launch's waves wait for them before their
+  // first loads — k_step 35.6 -> 37.5 us, A/B on one box)
+  const int64_t vb = SPLIT ? (int64_t)blockIdx.x + (blockIdx.x >= a.vb_split ? a.vb_skip : 0) : (int64_t)blockIdx.x;
   const int64_t tile = vb * (kBlock / 64) + w;
   const int64_t j = tile * 64 + lane;
   // The device flags and this slot's range mark + carry are loaded before the
@@ -410,6 +424,11 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
         const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x, dr_step);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
       }
+#if defined(GH_LOGW_SC1)  // timing variant: write-through log-weights
+#define GH_LOGW_STORE(p, v) st_sc1(p, v)
+#else
+#define GH_LOGW_STORE(p, v) (*(p) = (v))
+#endif
       if (a.buf) {
         const __amdgpu_buffer_rsrc_t ro = gh_rsrc(a.xout);
         const uint32_t tb = (uint32_t)tile * (uint32_t)(kTileP * D * 8);
@@ -420,7 +439,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
 #pragma unroll
         for (int k = 0; k < D; ++k) a.xout[xidx(j, k, D)] = x[k];
       }
-      a.logw[j] = lw;
+      GH_LOGW_STORE(&a.logw[j], lw);
     }
   }
   if (a.max_only) block_max_partial(lw, sm, a.pm + vb, a.amax, vb);
@@ -460,7 +479,7 @@ __device__ __forceinline__ void block_partial2(double lw0, double lw1, double (*
   }
 }
 
-template <class Model, bool INIT>
+template <class Model, bool INIT, bool SPLIT = false>
 __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const double* __restrict__ prm,
                                                                           typename Model::Params p0, StepObs o,
                                                                           StepArgs a) {
@@ -469,7 +488,10 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
   __shared__ double sm[3][4];
   __shared__ double logtab[kMathTabDoubles];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t vb = blockIdx.x + (blockIdx.x >= a.vb_split ? a.vb_skip : 0);
+  // (the remap lives in its own instantiation: the compare on two kernel
+  // arguments made every other launch's waves wait for them before their
+  // first loads — k_step 35.6 -> 37.5 us, A/B on one box)
+  const int64_t vb = SPLIT ? (int64_t)blockIdx.x + (blockIdx.x >= a.vb_split ? a.vb_skip : 0) : (int64_t)blockIdx.x;
   const int64_t tile0 = (vb * (kBlock / 64) + w) * 2;
   const int64_t j0 = tile0 * 64 + lane, j1 = j0 + 64;
   uint64_t mv0 = 0, mv1 = 0, cv0 = 0, cv1 = 0;
@@ -554,6 +576,51 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
   }
   if (a.max_only) block_max_partial(fmax(lw0, lw1), sm, a.pm + vb, a.amax, vb);
   else block_partial2(lw0, lw1, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
+}
+
+// The weight sums of a max-only step, recomputed when something other than
+// the next maybe_resample! asks for them (log_ml_estimate, the ESS readers, a
+// second maybe_resample! without a step).  Same block geometry, block maxima
+// (the step kernel's pm) and reduction order as block_partial (PAIRS:
+// block_partial2), so ps / ps2 are exactly what a full-partials step would
+// have written.  One rank: every step writes maxima only, so a caller loop of
+// maybe_resample! + particle_filter_step! runs the batched loop's kernels.
+template <bool PAIRS>
+__global__ __launch_bounds__(kBlock) void k_block_sums(const double* __restrict__ logw, int64_t n,
+                                                        const double* __restrict__ pm, double* ps, double* ps2) {
+  __shared__ double sm[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t vb = blockIdx.x;
+  const double mb = pm[vb];
+  double sw, s2w;
+  if (!PAIRS) {
+    const int64_t j = (vb * (kBlock / 64) + w) * 64 + lane;
+    const double lw = j < n ? logw[j] : -INFINITY;
+    double e = 0.0;
+    if (lw > -INFINITY) e = gh_exp_nonpos(lw - mb);
+    if (lw != lw) e = lw;
+    sw = wave_sum(e);
+    s2w = wave_sum(e * e);
+  } else {
+    const int64_t j0 = (vb * (kBlock / 64) + w) * 2 * 64 + lane, j1 = j0 + 64;
+    const double lw0 = j0 < n ? logw[j0] : -INFINITY, lw1 = j1 < n ? logw[j1] : -INFINITY;
+    double e0 = 0.0, e1 = 0.0;
+    if (lw0 > -INFINITY) e0 = gh_exp_nonpos(lw0 - mb);
+    if (lw1 > -INFINITY) e1 = gh_exp_nonpos(lw1 - mb);
+    if (lw0 != lw0) e0 = lw0;
+    if (lw1 != lw1) e1 = lw1;
+    sw = wave_sum(e0 + e1);
+    s2w = wave_sum(e0 * e0 + e1 * e1);
+  }
+  if (lane == 0) {
+    sm[0][w] = sw;
+    sm[1][w] = s2w;
+  }
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    ps[vb] = (sm[0][0] + sm[0][1]) + (sm[0][2] + sm[0][3]);
+    ps2[vb] = (sm[1][0] + sm[1][1]) + (sm[1][2] + sm[1][3]);
+  }
 }
 
 // --------------------------------------------------------------- decision
@@ -770,14 +837,6 @@ __device__ __forceinline__ bool last_block(unsigned* ticket, int* sm_flag) {
   return last;
 }
 
-template <class T>
-__device__ __forceinline__ T ld_sc1(T* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <class T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Integer block sums of the quantised weights.  With `fused` the launch also
 // takes the maybe_resample! decision: every block evaluates it from the same
@@ -1091,7 +1150,20 @@ struct Resample1Args {
   uint64_t* amax_reset;    // the other parity's shards, emptied for the next step
   uint64_t seed;
   uint32_t t;
+  uint64_t* hdec;          // host-mapped decision mailbox [tag, fire | err << 32, ess] (nullptr: none);
+  uint64_t htag;           //   block 0 posts the decision as soon as it is known, then this tag
 };
+
+// maybe_resample!'s return value for the host (block 0, thread 0): the
+// decision words, a system-scope release, then the tag the host polls
+// (gh_pf_maybe_resample with did / ess: no stream synchronisation)
+__device__ __forceinline__ void post_decision(uint64_t* hdec, uint64_t htag, const Decision& dec) {
+  if (!hdec) return;
+  hdec[1] = (uint64_t)(uint32_t)dec.fire | ((uint64_t)(uint32_t)dec.err << 32);
+  hdec[2] = as_u64(dec.ess);
+  __threadfence_system();
+  __hip_atomic_store(&hdec[0], htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // 1024-thread block reductions (16 waves), result broadcast; LDS-only
 // barriers (outstanding global loads/stores are not waited for)
@@ -1251,24 +1323,6 @@ __device__ __forceinline__ uint64_t f64_to_u52(double x) {
   return as_u64(floor(x) + 0x1p52) - 0x4330000000000000ull;
 }
 
-// timing-only variants (results wrong): GH_RS_EXIT=k leaves k_resample1 after
-// phase k (0 start, 1 fold, 2 quantise + scan, 3 grid barrier), to price the
-// phases including the launch
-#if defined(GH_RS_EXIT)
-#define GH_RS_EXIT_AT(k) \
-  if (GH_RS_EXIT == (k)) return;
-#else
-#define GH_RS_EXIT_AT(k)
-#endif
-
-#if defined(GH_RS_STAMPS)  // timing-only variant: per-block phase clocks
-static __device__ uint64_t g_rs_stamps[1024 * 8];
-#define GH_RS_STAMP(k) \
-  if (threadIdx.x == 0 && blockIdx.x < 1024) g_rs_stamps[blockIdx.x * 8 + (k)] = wall_clock64();
-#else
-#define GH_RS_STAMP(k)
-#endif
-
 template <bool MARKS, int IT, bool SUMS>
 __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resample1Args r) {
   __shared__ double smd[32];
@@ -1277,8 +1331,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   __shared__ uint64_t sbase;
   __shared__ unsigned sgen;
   __shared__ int sfail;  // the barrier wait timed out: write nothing
-  GH_RS_STAMP(0);
-  GH_RS_EXIT_AT(0);
   // barrier generation of this launch: read before this block publishes
   if (threadIdx.x == 0) {
     sgen = r.dev->bar_gen + 1;
@@ -1303,7 +1355,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     uint64_t key = lane < kAmaxShards ? r.amax_in[lane * kAmaxStride] : 0ull;
     key = wave_incl_max_u64(key);
     M = amax_value(readlane63_u64(key));
-    GH_RS_STAMP(7);
   } else if (IT <= 8 && r.nb_part <= KP * kRsBlock) {  // uniform; always true at IT <= kRsPart (host-checked)
     double pmv[KP], psv[kSumsEarly ? KP : 1], ps2v[kSumsEarly ? KP : 1];
 #pragma unroll
@@ -1320,8 +1371,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
 #pragma unroll
     for (int k = 1; k < KP; ++k) m = fmax(m, pmv[k]);
     M = blk16_max1(m, smd);
-    GH_RS_STAMP(7);
-    GH_RS_EXIT_AT(1);
     if (!sums && M > -INFINITY) {
       double a1[KP], a2[KP];
 #pragma unroll
@@ -1368,26 +1417,38 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // follows the grid barrier.
   __shared__ int sfire;
   __shared__ double sS[2];
+  // block 0 posts the decision to the host as soon as it is taken (before the
+  // marks), and commits it to the device scalars at its end
+  bool posted = false;
+  auto decision = [&]() {
+    double st[3] = {M, S1, S2};
+    DecideArgs d = r.d;
+    d.stats_all = st;
+    d.R = 1;
+    return decide(d, false);
+  };
   if (!sums) {
     blk16_sum2(&s1, &s2, smd);
     S1 = s1;
     S2 = s2;
-    if (threadIdx.x == 0) sfire = m_ok && ((S1 * S1) / S2 < r.d.thr);
+    if (threadIdx.x == 0) {
+      sfire = m_ok && ((S1 * S1) / S2 < r.d.thr);
+      if (blockIdx.x == 0) {
+        post_decision(r.hdec, r.htag, decision());
+        posted = true;
+      }
+    }
     lds_barrier();
   }
-  GH_RS_STAMP(1);
   auto commit = [&]() {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      double st[3] = {M, S1, S2};
-      DecideArgs d = r.d;
-      d.stats_all = st;
-      d.R = 1;
-      const Decision dec = decide(d, false);
+      const Decision dec = decision();
       r.stats_out[0] = M;
       r.stats_out[1] = S1;
       r.stats_out[2] = S2;
       r.dev->pending = 0;
       commit_decision(r.d, dec, r.dev, 0);
+      if (!posted) post_decision(r.hdec, r.htag, dec);
     }
   };
   if (sums ? !m_ok : !sfire) {  // uniform over the grid: nobody publishes
@@ -1415,8 +1476,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
   }
   const uint64_t incl = sums ? blk16_scan<true>(tsum, &s1, &s2, smu, smd) : blk16_scan<false>(tsum, &s1, &s2, smu, smd);
-  GH_RS_STAMP(2);
-  GH_RS_EXIT_AT(2);
   // ---- grid barrier: each tile total (< 2^62) is published as ONE 8-byte
   // agent-scope store tagged in bit 63 with the generation's parity, and read
   // back with agent-scope loads until every tag matches (the payload is its
@@ -1500,7 +1559,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
   }
   lds_barrier();
-  GH_RS_STAMP(3);
   if (threadIdx.x == 0) {
     uint64_t all = 0, before = 0;
     double g1 = 0.0, g2 = 0.0;
@@ -1515,6 +1573,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       sS[0] = g1;
       sS[1] = g2;
       sfire = (g1 * g1) / g2 < r.d.thr;
+      if (blockIdx.x == 0 && !sfail) {
+        S1 = g1;
+        S2 = g2;
+        post_decision(r.hdec, r.htag, decision());
+        posted = true;
+      }
     }
     const uint64_t N = (uint64_t)r.d.n_global;
     sd.S = all;
@@ -1543,7 +1607,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // grid never started): the totals are partial.  The block leaves without
   // marks or decision; the error surfaces as GH_E_STATE at the next sync.
   if (sfail) return;
-  GH_RS_EXIT_AT(3);
   if (sums) {
     S1 = sS[0];
     S2 = sS[1];
@@ -1552,7 +1615,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       return;
     }
   }
-  GH_RS_STAMP(4);
   uint64_t run = sbase + incl - tsum;
   if (!MARKS) {
 #pragma unroll
@@ -1576,7 +1638,11 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     // (a particle past n or of zero weight leaves run, hence the count, unchanged)
     const int64_t e_i = sys_count_w(&sd, N, run);
     const uint64_t tagged = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
+#if defined(GH_MARK_SC1)  // timing variant: write-through marks (nothing dirty in L2 at the kernel's end)
+    if (e_i > s_i) st_sc1(&r.mk.mark[s_i], tagged);
+#else
     if (e_i > s_i) r.mk.mark[s_i] = tagged;
+#endif
     const int64_t g0 = (s_i + 63) >> 6, g1 = (e_i + 63) >> 6;  // groups g with 64 g in [s_i, e_i)
     const bool many = g1 - g0 > 2;
     if (!many) {
@@ -1593,9 +1659,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     s_i = e_i;
   }
-  GH_RS_STAMP(5);
   commit();
-  GH_RS_STAMP(6);
 }
 
 // ------------------------------------------------ multi-rank resample (R > 1)

@@ -722,10 +722,25 @@ def initialize_conditional_particle_filter(model: Model, model_args: tuple, obse
 def conditional_particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: tuple, observations,
                                      reference_xt) -> None:
     """One step of conditional_smc (smc.jl:138-147): the distinguished particle
-    takes reference_xt, its own parent, weight += log p(y_t | x_t)."""
+    takes reference_xt, its own parent, weight += log p(y_t | x_t).  new_args =
+    (t, model') also changes the Unfold's parameters (every retained kernel
+    application re-scored, as particle_filter_step does)."""
     t = state.t + 1
-    if tuple(new_args)[:1] != (t,):
-        raise _lib.GenHipError(1, f"new_args must extend the Unfold by one step: expected ({t},), got {new_args}")
+    new_args = tuple(new_args)
+    if new_args[:1] != (t,) or len(new_args) > 2:
+        raise _lib.GenHipError(1, f"new_args must extend the Unfold by one step: expected ({t},) or ({t}, model'), "
+                                  f"got {new_args}")
+    new_model = new_args[1] if len(new_args) == 2 else None
+    if new_model is not None and new_model is not state.model:
+        if type(new_model) is not type(state.model):
+            raise _lib.GenHipError(1, "new parameters of another model family")
+        obs, keep = _step_obs(new_model, t, observations)
+        ref = _ref_state(new_model, reference_xt)
+        mh = state.ctx.model_handle(new_model)
+        _lib.check(_lib.load().gh_pf_step_params_conditional(state.h, byref(obs), mh, _lib.dptr(ref)))
+        state.model = new_model
+        state._log_obs(t, keep)
+        return
     obs, keep = _step_obs(state.model, t, observations)
     ref = _ref_state(state.model, reference_xt)
     _lib.check(_lib.load().gh_pf_step_conditional(state.h, byref(obs), _lib.dptr(ref)))

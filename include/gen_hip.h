@@ -172,7 +172,9 @@ int gh_ctx_destroy(gh_ctx* ctx);
    multi-rank code path (collectives, split step after a resample, k_rank_a/b)
    even at world 1 — over a one-rank RCCL communicator for a gh_ctx_create /
    gh_ctx_create_dist context, over the user's functions for a host-comm one.
-   Results are the same filter's (bit-exact against the one-rank path). */
+   Results are the same filter's (bit-exact against the one-rank path).
+   GH_E_STATE while a filter exists on the context (its buffers were
+   allocated for the path chosen when it was created). */
 int gh_ctx_force_multirank(gh_ctx* ctx);
 int gh_ctx_rank(const gh_ctx* ctx, int* rank, int* world);
 int gh_ctx_stream(const gh_ctx* ctx, void** hip_stream);
@@ -258,6 +260,13 @@ int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const double* propo
    the new step is generated under the new parameters, which the filter keeps
    from then on (new_model must outlive it).  One rank, record_history. */
 int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* new_model);
+/* The same for a conditional filter (gh_pf_init_conditional): the re-scoring,
+   then the conditional step of gh_pf_step_conditional with the distinguished
+   particle pinned to ref_xt[d] (particle Gibbs with a parameter move between
+   sweeps, examples/pmmh/smc.jl:138-147).  The reference's Unfold update KAT
+   with changed parameters (test/modeling_library/unfold.jl:303-326) is driven
+   through this entry: tests/test_step_params.py. */
+int gh_pf_step_params_conditional(gh_pf* pf, const gh_obs* obs, gh_model* new_model, const double* ref_xt);
 /* ess_threshold NaN means the reference's default N/2; any other value >= 0 is
    the threshold as given (resample iff ESS < ess_threshold, so 0 never
    resamples, as in Gen); a negative threshold is GH_E_INVAL (before round 3,

@@ -174,3 +174,44 @@ def test_gpu_step_params_refusals(gh_ctx):
         gen.particle_filter_step(st, (2, LinearGaussianSSM.benchmark(3, seed=5)), (gen.UnknownChange(), gen.NoChange()),
                                  {("chain", 2, "y"): ys[1]})
     st.close()
+
+
+@pytest.mark.gpu
+def test_gpu_step_params_matches_reference_update_params_kat(gh_ctx):
+    """The reference's own update_params KAT (test/modeling_library/unfold.jl
+    :303-326; numbers in tests/golden/unfold_kats.json) through
+    gh_pf_step_params itself: the Unfold x ~ normal(alpha x_prev + beta, 1)
+    (unfold.jl:5-8) is the LG-SSM at d = 1, its literal trajectory (x1 1.1,
+    x2 1.2 from x_init 0.1) the distinguished particle of a conditional
+    filter, no observations (weights 0).  Changing alpha 0.2 -> 0.5 re-scores
+    both retained applications: particle 0's weight gains exactly the KAT's
+    weight (0.1929) and its score columns of steps 1, 2 sum to the KAT's new
+    score; the new step 3 (pinned to 1.4) is scored under alpha 0.5."""
+    import json
+    import os
+
+    from gen_amd import dists as D
+
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "unfold_kats.json")))
+    a, want = g["args"], g["cases"]["update_params"]
+    xi, al, be, x1, x2 = a["x_init"], a["alpha"], a["beta"], a["x1"], a["x2"]
+    an, x3 = 0.5, 1.4
+
+    def unfold(alpha):
+        return gen.LinearGaussianSSM([[alpha]], [[1.0]], [[1.0]], [[1.0]], [alpha * xi + be], [[1.0]], b=[be])
+
+    m_old, m_new = unfold(al), unfold(an)
+    st = gen.initialize_conditional_particle_filter(m_old, (1,), None, 64, [x1], seed=5)
+    gen.conditional_particle_filter_step(st, (2,), (gen.UnknownChange(),), None, [x2])
+    w_before = gen.get_log_weights(st)[0]
+    assert w_before == 0.0
+    gen.conditional_particle_filter_step(st, (3, m_new), (gen.UnknownChange(), gen.UnknownChange()), None, [x3])
+    w = gen.get_log_weights(st)[0]
+    assert abs(w - want["weight"]) <= 1e-12 * max(1.0, abs(want["weight"])), (w, want)
+    tr = gen.get_traces(st)
+    assert [tr.step_states(t)[0, 0] for t in (1, 2, 3)] == [x1, x2, x3]
+    _, ps = tr.scores(per_step=True)
+    lat = ps[:, 0, 0]
+    assert abs(lat[0] + lat[1] - want["score"]) <= 1e-13 * max(1.0, abs(want["score"])), (lat, want)
+    assert abs(lat[2] - D.normal.logpdf(x3, an * x2 + be, 1.0)) <= 1e-13
+    st.close()

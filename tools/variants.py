@@ -28,10 +28,14 @@ VARIANTS = {
     "coal_b512w6": ["GH_COAL_BLOCK=512", "GH_COAL_WIN=6"],
     "coal_b512w7": ["GH_COAL_BLOCK=512", "GH_COAL_WIN=7"],
     "coal_b64w10": ["GH_COAL_BLOCK=64", "GH_COAL_WIN=10"],
+    "mark_sc1": ["GH_MARK_SC1"],
+    "logw_sc1": ["GH_LOGW_SC1"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
 EXTRA = {"rs_stamps": ["GH_RS_STAMPS"]}
+# variants whose hooks are not in the product sources: a patch applied to a copy
+PATCHES = {"rs_stamps": os.path.join(ROOT, "tools", "rs_stamps.patch")}
 BENCH_ARGS = os.environ.get("GH_VARIANT_ARGS", "--steps 50").split()
 # GH_VARIANT_SCRIPT=tools/bench_pmmh.py times another workload with the same variants
 BENCH_SCRIPT = os.environ.get("GH_VARIANT_SCRIPT", "bench.py")
@@ -44,7 +48,7 @@ def main():
         for name, defs in {**VARIANTS, **EXTRA}.items():
             if len(sys.argv) > 2 and name not in sys.argv[2:]:
                 continue
-            gb.build_variant(name, defs)
+            gb.build_variant(name, defs, PATCHES.get(name))
             print("built", name, flush=True)
     else:
         out = {}
