@@ -69,6 +69,7 @@ SIGNATURES = {
     "gh_comm_unique_id": (c_int, [POINTER(c_uint8)]),
     "gh_ctx_create_dist": (c_int, [c_int, c_int, c_int, POINTER(c_uint8), c_void_p, POINTER(c_void_p)]),
     "gh_ctx_create_hostcomm": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, POINTER(c_void_p)]),
+    "gh_ctx_create_peer": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, POINTER(c_void_p)]),
     "gh_ctx_destroy": (c_int, [c_void_p]),
     "gh_ctx_force_multirank": (c_int, [c_void_p]),
     "gh_pf_step_params": (c_int, [c_void_p, POINTER(Obs), c_int, c_void_p]),

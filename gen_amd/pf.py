@@ -86,20 +86,25 @@ class Context:
     """One GPU (and, for multi-GPU, one rank of an RCCL communicator)."""
 
     def __init__(self, device: int | None = None, rank: int = 0, world: int = 1, unique_id: bytes | None = None,
-                 transport=None, force_multirank: bool = False):
+                 transport=None, force_multirank: bool = False, peer: bool = False):
         """`unique_id`: RCCL communicator id (Context.unique_id() on rank 0,
         broadcast to the others).  `transport`: a host-staged transport
         (gen_amd.transport.GlooTransport) used instead of RCCL.
         `force_multirank`: filters take the multi-rank path even at world 1
         (a one-rank RCCL communicator; gh_ctx_force_multirank, for tests and
-        timing on one GPU)."""
+        timing on one GPU).  `peer`: with a `transport`, the ranks exchange
+        through each other's mapped device memory (gh_ctx_create_peer); the
+        transport only swaps the IPC handles."""
         lib = _lib.load()
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         self.device = device
         self.transport = transport
         h = c_void_p()
-        if transport is not None:
+        if transport is not None and peer:
+            rank, world = transport.rank, transport.world
+            _lib.check(lib.gh_ctx_create_peer(device, rank, world, byref(transport.struct), None, byref(h)))
+        elif transport is not None:
             rank, world = transport.rank, transport.world
             _lib.check(lib.gh_ctx_create_hostcomm(device, rank, world, byref(transport.struct), None, byref(h)))
         elif world > 1:
@@ -602,7 +607,9 @@ def sample_unweighted_traces(state: ParticleFilterState, num_samples: int, seed:
     _lib.check(_lib.load().gh_pf_sample_unweighted(state.h, int(num_samples), int(seed) & 0xFFFFFFFFFFFFFFFF,
                                                    idx.ctypes.data_as(ctypes.POINTER(c_int64))))
     tr = get_traces(state)
-    return [tr[i] for i in idx], idx
+    # (on R ranks the indices are global: this rank's views of its own ones)
+    lo, nl = state.first, state.n_local
+    return [tr[i - lo] if lo <= i < lo + nl else None for i in idx], idx
 
 
 def rejuvenate(state: ParticleFilterState, n_moves: int = 1) -> int:

@@ -409,26 +409,6 @@ static int comm_exchange(gh_ctx* c, const std::vector<CommMsg>& sends, const std
   return GH_OK;
 }
 
-// All-gather of a large buffer for the genealogy queries (off the step
-// path): RCCL, or staged through host memory and the user's all-gather (the
-// host and peer transports).  Synchronous.
-static int bulk_allgather(gh_ctx* c, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
-  if (c->comm) {
-    NCCL_TRY(ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    return GH_OK;
-  }
-  if (!c->hc.allgather) return set_err(GH_E_STATE, "no transport for the genealogy all-gather");
-  std::vector<uint8_t> hs(bytes), hr(bytes * (size_t)c->world);
-  HIP_TRY(hipMemcpyAsync(hs.data(), dsend, bytes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  if (c->hc.allgather(c->hc.user, hs.data(), hr.data(), bytes))
-    return set_err(GH_E_RCCL, "genealogy all-gather failed");
-  HIP_TRY(hipMemcpyAsync(drecv, hr.data(), hr.size(), hipMemcpyHostToDevice, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  return GH_OK;
-}
-
 extern "C" int gh_ctx_synchronize(gh_ctx* c) {
   if (!c) return set_err(GH_E_INVAL, "null ctx");
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -874,12 +854,6 @@ struct gh_pf {
   double* prow[kPeerMaxRanks] = {};
   uint64_t* ptag[kPeerMaxRanks] = {};
   uint64_t row_use = 0;
-  // multi-rank genealogy (record_history): per step, the rows received for
-  // it (the parents on other ranks; D + 1 doubles each, row-indexed), kept by
-  // the step's part-2 launch; chunked device storage
-  std::vector<double*> rh_step;   // index t-1 (nullptr: none received)
-  std::vector<char*> rh_chunks;
-  size_t rh_used = 0, rh_cap = 0;
   int64_t* dlo = nullptr;         // [R + 1] floor(N k / R): the ranks' first global slots
   uint64_t mail_seq = 0;          //   the tag of the last plan posted there
   bool plan_recs = false;         // the pending plan is k_rank_a2's records (the host takes the decision)
@@ -1059,7 +1033,6 @@ static void pf_free(gh_pf* pf) {
   if (pf->h_plan) hipHostFree(pf->h_plan);
   if (pf->h_mail) hipHostFree(pf->h_mail);
   if (pf->h_dec) hipHostFree(pf->h_dec);
-  for (auto c : pf->rh_chunks) hipFree(c);
   if (pf->ctx->peer) ipc_close(pf->ctx, (void**)pf->prow);
   hipFree(pf->dlo);
   if (!pf->opts.record_history) {
@@ -1259,28 +1232,6 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
 
 static int finish_plan(gh_pf* pf);
 
-// The genealogy record of step t's received rows (count of them): chunked
-// device storage, released with the filter.
-static int rhist_reserve(gh_pf* pf, int t, int64_t count, double** out) {
-  *out = nullptr;
-  if ((int)pf->rh_step.size() < t) pf->rh_step.resize(t, nullptr);
-  pf->rh_step[t - 1] = nullptr;
-  if (count <= 0) return GH_OK;
-  const size_t bytes = (sizeof(double) * (size_t)(pf->D + 1) * (size_t)count + 255) & ~(size_t)255;
-  if (pf->rh_used + bytes > pf->rh_cap) {
-    const size_t cap = std::max(bytes, (size_t)64 << 20);
-    char* c = nullptr;
-    if (hipMalloc(&c, cap) != hipSuccess) return set_err(GH_E_NOMEM, "genealogy rows (%zu bytes)", cap);
-    pf->rh_chunks.push_back(c);
-    pf->rh_used = 0;
-    pf->rh_cap = cap;
-  }
-  *out = (double*)(pf->rh_chunks.back() + pf->rh_used);
-  pf->rh_used += bytes;
-  pf->rh_step[t - 1] = *out;
-  return GH_OK;
-}
-
 // Multi-rank, after the step kernel: when the step followed a resample it was
 // enqueued before the host read the plan (part 1); now the plan is read, the
 // rows exchanged and the tiles holding slots that take received rows run
@@ -1305,7 +1256,6 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
         b.vb_split = tA;
         b.vb_skip = tB - tA;
         b.grid_blocks = tA + (nb - tB);
-        if (pf->opts.record_history) CHECK(rhist_reserve(pf, (int)a.t, ra + (n - rb), &b.rhist));
         CHECK(launch_step(pf, o, b, init));
       }
     }
@@ -1740,11 +1690,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.max_only = (pf->step_max_only || lazy) && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
   // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
   // short step more than the fold they save, measured)
-#if defined(GH_PAIRS_SHARDS)  // timing variant: the pair kernel folds its maxima into the shards too
-  a.amax = a.max_only && pf->amax_armed
-#else
   a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
-#endif
                ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride
                : nullptr;
   // multi-rank after a resample: the local half now, the rest once the rows arrive
@@ -2387,151 +2333,16 @@ extern "C" int gh_pf_get_log_weights(gh_pf* pf, double* out) {
   return GH_OK;
 }
 
-// ------------------------------------------- multi-rank genealogy queries
-// (kernels in gh_kernels.h "multi-rank genealogy").  Collective:
-// every rank calls the same query.  Cursors = the global ids of this rank's
-// particles' ancestors at the step the walk has reached.
-struct DBuf {
-  void* p = nullptr;
-  ~DBuf() {
-    if (p) hipFree(p);
-  }
-  template <class T>
-  T* as() const {
-    return (T*)p;
-  }
-};
-static int dalloc(DBuf& b, size_t bytes) {
-  if (hipMalloc(&b.p, bytes ? bytes : 8) != hipSuccess) return set_err(GH_E_NOMEM, "genealogy query: %zu bytes", bytes);
-  return GH_OK;
-}
-
-struct MrWalk {
-  gh_pf* pf = nullptr;
-  int64_t n = 0, N = 0, pad = 0;
-  int R = 1;
-  std::vector<int32_t> res;  // res[s]: a resample preceded step s
-  DBuf cur, gp, gp_all;
-};
-
-static const double* rh_of(const gh_pf* pf, int s) {
-  return s >= 1 && s - 1 < (int)pf->rh_step.size() ? pf->rh_step[s - 1] : nullptr;
-}
-
-static int mr_walk_begin(gh_pf* pf, MrWalk& w) {
-  CHECK(materialize_marks(pf));
-  w.pf = pf;
-  w.n = pf->n;
-  w.N = pf->n_global;
-  w.R = pf->ctx->world;
-  w.pad = (w.N + w.R - 1) / w.R;
-  w.res.assign(pf->cap + 2, 0);
-  CHECK(d2h(pf, w.res.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2)));
-  DevScalars h;
-  CHECK(d2h(pf, &h, pf->dev, sizeof h));
-  if (h.error) return set_err(h.error, dev_error_msg(h.error));
-  CHECK(dalloc(w.cur, sizeof(int64_t) * (size_t)w.n));
-  CHECK(dalloc(w.gp, sizeof(int64_t) * (size_t)w.pad));
-  CHECK(dalloc(w.gp_all, sizeof(int64_t) * (size_t)w.pad * w.R));
-  const dim3 grid((unsigned)((w.n + kBlock - 1) / kBlock));
-  if (flags_live(pf) && (h.pending | h.fire) && pf->cap >= pf->t + 1) {
-    // a resample pending after the last step: the particles are its copies,
-    // slot j's parent (local, or a row received for the next step)
-    hipLaunchKernelGGL(k_mr_gparents, grid, dim3(kBlock), 0, pf->s, (const int32_t*)anc_for_step(pf, pf->t + 1), w.n,
-                       pf->lo, (const double*)pf->rows_recv, pf->D, w.cur.as<int64_t>());
-  } else {
-    hipLaunchKernelGGL(k_iota64, grid, dim3(kBlock), 0, pf->s, w.cur.as<int64_t>(), w.n, pf->lo);
-  }
-  HIP_TRY(hipGetLastError());
-  return GH_OK;
-}
-
-// every cursor from step s back to step s - 1
-static int mr_walk_back(MrWalk& w, int s) {
-  gh_pf* pf = w.pf;
-  if (!w.res[s]) return GH_OK;
-  const dim3 grid((unsigned)((w.n + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_mr_gparents, grid, dim3(kBlock), 0, pf->s, (const int32_t*)anc_for_step(pf, s), w.n, pf->lo,
-                     rh_of(pf, s), pf->D, w.gp.as<int64_t>());
-  HIP_TRY(hipGetLastError());
-  CHECK(bulk_allgather(pf->ctx, w.gp.p, w.gp_all.p, sizeof(int64_t) * (size_t)w.pad, pf->s));
-  hipLaunchKernelGGL(k_mr_back, grid, dim3(kBlock), 0, pf->s, w.cur.as<int64_t>(), w.n,
-                     (const int64_t*)w.gp_all.as<int64_t>(), (const int64_t*)pf->dlo, w.R, w.N, w.pad);
-  HIP_TRY(hipGetLastError());
-  return GH_OK;
-}
-
-// get_traces at step t on R ranks: the states of this rank's particles' ancestors, [D][n] on the device
-static int mr_trajectory(gh_pf* pf, int t, double* dout) {
-  MrWalk w;
-  CHECK(mr_walk_begin(pf, w));
-  for (int s = pf->t; s > t; --s) CHECK(mr_walk_back(w, s));
-  const int64_t pad_d = slot_doubles(w.pad, pf->D);
-  DBuf send, slab;
-  CHECK(dalloc(send, sizeof(double) * (size_t)pad_d));
-  CHECK(dalloc(slab, sizeof(double) * (size_t)pad_d * w.R));
-  HIP_TRY(hipMemsetAsync(send.p, 0, sizeof(double) * (size_t)pad_d, pf->s));
-  HIP_TRY(hipMemcpyAsync(send.p, slot_x(pf, t), sizeof(double) * (size_t)slot_doubles(w.n, pf->D),
-                         hipMemcpyDeviceToDevice, pf->s));
-  CHECK(bulk_allgather(pf->ctx, send.p, slab.p, sizeof(double) * (size_t)pad_d, pf->s));
-  hipLaunchKernelGGL(k_mr_states, dim3((unsigned)((w.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s,
-                     (const int64_t*)w.cur.as<int64_t>(), w.n, (const double*)slab.as<double>(), pad_d,
-                     (const int64_t*)pf->dlo, w.R, w.N, pf->D, dout);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(pf->s));
-  return GH_OK;
-}
-
-// the score columns on R ranks (k_scores' values): per step, every rank
-// scores its own slots, the ranks all-gather them, each cursor takes its
-// slot's pair, then the cursors step back
-static int mr_scores(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& obs, double* dtot, double* dper) {
-  MrWalk w;
-  CHECK(mr_walk_begin(pf, w));
-  const int T = pf->t;
-  const int64_t n = w.n;
-  DBuf sc, sc_all;
-  CHECK(dalloc(sc, sizeof(double) * 2 * (size_t)w.pad));
-  CHECK(dalloc(sc_all, sizeof(double) * 2 * (size_t)w.pad * w.R));
-  HIP_TRY(hipMemsetAsync(sc.p, 0, sizeof(double) * 2 * (size_t)w.pad, pf->s));
-  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
-  for (int s = T; s >= 1; --s) {
-    const int32_t* anc = s > 1 && w.res[s] ? anc_for_step(pf, s) : nullptr;
-    CHECK(with_model(m, [&](auto model, const auto& p) {
-      hipLaunchKernelGGL(k_mr_slot_scores<decltype(model)>, grid, dim3(kBlock), 0, pf->s, (const double*)m->dparams,
-                         p, obs[s - 1], s, (const double*)slot_x(pf, s),
-                         (const double*)(s > 1 ? slot_x(pf, s - 1) : nullptr), anc, rh_of(pf, s), n, w.pad,
-                         sc.as<double>());
-    }));
-    HIP_TRY(hipGetLastError());
-    CHECK(bulk_allgather(pf->ctx, sc.p, sc_all.p, sizeof(double) * 2 * (size_t)w.pad, pf->s));
-    hipLaunchKernelGGL(k_mr_take_scores, grid, dim3(kBlock), 0, pf->s, (const int64_t*)w.cur.as<int64_t>(), n,
-                       (const double*)sc_all.as<double>(), (const int64_t*)pf->dlo, w.R, w.N, w.pad,
-                       dper + (int64_t)(s - 1) * 2 * n, dper + ((int64_t)(s - 1) * 2 + 1) * n);
-    HIP_TRY(hipGetLastError());
-    if (s > 1) CHECK(mr_walk_back(w, s));
-  }
-  hipLaunchKernelGGL(k_score_total, grid, dim3(kBlock), 0, pf->s, (const double*)dper, T, n, dtot);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(pf->s));
-  return GH_OK;
-}
-
 extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
   CHECK(materialize_marks(pf));
   if (t < 1 || t > pf->t) return set_err(GH_E_INVAL, "step %d outside 1..%d", t, pf->t);
   if (!pf->opts.record_history && t != pf->t)
     return set_err(GH_E_STATE, "record_history is off: only the current step is kept");
+  if (mr(pf->ctx) && t != pf->t)
+    return set_err(GH_E_STATE, "multi-rank: trajectories before the current step are not materialised");
   const int64_t n = pf->n;
   if (n == 0) return GH_OK;
-  if (mr(pf->ctx)) {  // collective: the walk crosses ranks
-    DBuf d;
-    CHECK(dalloc(d, sizeof(double) * pf->D * (size_t)n));
-    CHECK(mr_trajectory(pf, t, d.as<double>()));
-    HIP_TRY(hipMemcpy(out, d.p, sizeof(double) * pf->D * (size_t)n, hipMemcpyDeviceToHost));
-    return GH_OK;
-  }
   double* dout = nullptr;
   const double** dxs = nullptr;
   const int32_t** dancs = nullptr;
@@ -2573,10 +2384,7 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
 // The trace score columns of every current particle (k_scores: the genealogy
 // walk) under model m and the steps' observations obs[0..T): dtot[n] and the
 // per-step scratch/output dper[T][2][n], device buffers, on the filter's stream.
-static int mr_scores(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& obs, double* dtot, double* dper);
-
 static int scores_dev(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& obs, double* dtot, double* dper) {
-  if (mr(pf->ctx)) return mr_scores(pf, m, obs, dtot, dper);
   const int T = pf->t;
   const int64_t n = pf->n;
   const double** dxs = nullptr;
@@ -2633,6 +2441,8 @@ static int scores_ready(gh_pf* pf, const char* who) {
   const int T = pf->t;
   if (T < 1) return set_err(GH_E_STATE, "%s before init", who);
   if (!pf->opts.record_history && T > 1) return set_err(GH_E_STATE, "%s needs record_history", who);
+  if (mr(pf->ctx) && T > 1)
+    return set_err(GH_E_STATE, "multi-rank: the genealogy before the current step is not materialised");
   if ((int)pf->obs_hist.size() < T) return set_err(GH_E_STATE, "internal: observation history");
   return GH_OK;
 }
@@ -3191,86 +3001,52 @@ extern "C" int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int3
 
 extern "C" int gh_pf_sample_unweighted(gh_pf* pf, int64_t ns, uint64_t seed, int64_t* idx) {
   if (!pf || !idx || ns < 0) return set_err(GH_E_INVAL, "bad argument");
+  if (mr(pf->ctx)) return set_err(GH_E_STATE, "sample_unweighted: single rank only");
   if (ns == 0) return GH_OK;
   const int64_t n = pf->n;
-  const bool multi = mr(pf->ctx);
-  const int R = pf->ctx->world;
   CHECK(ensure_stats(pf));
-  hipLaunchKernelGGL(k_prep_sample, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, R, flags_live(pf));
+  hipLaunchKernelGGL(k_prep_sample, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, 1, flags_live(pf));
   GateArgs g;
   g.gate = &pf->dev->one;
   g.M = &pf->dev->sM;
   g.zero_w = &pf->dev->spend;
-  g.shift = quant_shift((uint64_t)pf->n_global);
+  g.shift = quant_shift((uint64_t)n);
   CHECK(materialize_marks(pf));
   DecideArgs d{};
   hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum, 0, d,
                      pf->dev);
-  if (multi) {  // the global integer CDF: every rank's total (one word each)
-    hipLaunchKernelGGL(k_rank_total, dim3(1), dim3(kBlock), 0, pf->s, g.gate, pf->bsum, pf->nb_scan, pf->dev);
-    CHECK(comm_allgather(pf->ctx, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s, &pf->dev->error));
-  }
   MarkArgs mk{};
   CdfArgs ca{};
   ca.bsum = pf->bsum;
   ca.nb = pf->nb_scan;
-  ca.totals = multi ? pf->totals_all : nullptr;
-  ca.R = R;
-  ca.rank = pf->ctx->rank;
-  ca.n_global = pf->n_global;
+  ca.R = 1;
+  ca.n_global = n;
   ca.seed = seed;
   ca.t = (uint32_t)pf->t;
   ca.stream = STREAM_SAMPLE;
   hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, ca, pf->dev, pf->C,
                      mk);
   int32_t* dout = nullptr;
-  HIP_TRY(hipMalloc(&dout, sizeof(int32_t) * (ns + 1)));
+  HIP_TRY(hipMalloc(&dout, sizeof(int32_t) * ns));
   SearchArgs sa{};
   sa.C = pf->C;
   sa.n_cdf = n;
   sa.n_slots = ns;
   sa.slot_lo = 0;
-  sa.n_global = pf->n_global;
+  sa.n_global = n;
   sa.seed = seed;
   sa.t = (uint32_t)pf->t;
   sa.mode = SEARCH_SAMPLE;
   sa.anc_old = nullptr;
   sa.anc_out = dout;
-  sa.own_only = multi ? 1 : 0;  // each target is searched by the rank whose CDF range holds it
   hipLaunchKernelGGL(k_search, dim3((unsigned)((ns + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s, sa, g,
                      pf->dev);
   HIP_TRY(hipGetLastError());
-  if (!multi) {
-    std::vector<int32_t> h(ns);
-    HIP_TRY(hipMemcpyAsync(h.data(), dout, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, pf->s));
-    HIP_TRY(hipStreamSynchronize(pf->s));
-    hipFree(dout);
-    for (int64_t i = 0; i < ns; ++i) idx[i] = h[i];
-    return GH_OK;
-  }
-  // every rank's answers (local index, -1 where another rank's range held the
-  // target), all-gathered: each sample is the global id one rank found
-  const size_t bytes = (sizeof(int32_t) * (size_t)ns + 7) & ~(size_t)7;
-  DBuf all;
-  int rc = dalloc(all, bytes * (size_t)R);
-  if (!rc) rc = bulk_allgather(pf->ctx, dout, all.p, bytes, pf->s);
+  std::vector<int32_t> h(ns);
+  HIP_TRY(hipMemcpyAsync(h.data(), dout, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
   hipFree(dout);
-  CHECK(rc);
-  std::vector<int32_t> h(bytes / sizeof(int32_t) * (size_t)R);
-  HIP_TRY(hipMemcpy(h.data(), all.p, bytes * (size_t)R, hipMemcpyDeviceToHost));
-  DevScalars hs;
-  CHECK(d2h(pf, &hs, pf->dev, sizeof hs));
-  if (hs.error) return set_err(hs.error, dev_error_msg(hs.error));
-  const size_t stride = bytes / sizeof(int32_t);
-  for (int64_t i = 0; i < ns; ++i) {
-    idx[i] = -1;
-    for (int r = 0; r < R; ++r)
-      if (h[(size_t)r * stride + i] >= 0) {
-        idx[i] = split_lo(pf->n_global, r, R) + h[(size_t)r * stride + i];
-        break;
-      }
-    if (idx[i] < 0) return set_err(GH_E_STATE, "sample_unweighted: sample %lld found by no rank", (long long)i);
-  }
+  for (int64_t i = 0; i < ns; ++i) idx[i] = h[i];
   return GH_OK;
 }
 

@@ -113,11 +113,6 @@ struct StepArgs {
   // (vb_skip = 0: every block its own)
   int64_t vb_split, vb_skip;
   int64_t grid_blocks;   // host only: the launch's blocks when nonzero
-  // part 2 (record_history): every received row used here is also kept,
-  // row-indexed (D components + global id), as this step's genealogy record of
-  // the parents that lived on other ranks (rows_recv is overwritten by the
-  // next resample); nullptr: not kept
-  double* rhist;
 };
 
 // ------------------------------------------------------------ reductions
@@ -361,6 +356,9 @@ __device__ __forceinline__ void block_max_partial(double lw, double (*sm)[4], do
 // launch (a per-block ticket would serialise ~4k atomics per 1M particles at
 // the memory side), and the block barrier waits for LDS only, so a block's
 // state stores are not waited for before it retires.
+// timing-only variant: per-block start / end clocks and hardware ids of the
+// step kernel's launches (tools/kstep_stamps.py)
+static __device__ uint64_t g_ks_stamps[1 << 16][4];
 template <class Model, bool INIT, bool SPLIT = false>
 __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double* __restrict__ prm,
                                                                     typename Model::Params p0, StepObs o,
@@ -369,6 +367,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   const typename Model::Params p = p0.rebase(prm);
   __shared__ double sm[3][4];
   __shared__ double logtab[kMathTabDoubles];
+  const uint64_t ks_t0 = wall_clock64();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   // (the remap lives in its own instantiation: the compare on two kernel
   // arguments made every other launch's waves wait for them before their
@@ -437,12 +436,6 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
 #pragma unroll
           for (int k = 0; k < D; ++k)
             xp[k] = loc ? a.xprev[xidx(src, k, D)] : ld_sys(&a.remote[(-1 - src) * a.ld_remote + k]);
-          if (SPLIT && !loc && a.rhist) {  // the parent's row, kept for the genealogy
-            double* h = a.rhist + (-1 - src) * (int64_t)(D + 1);
-#pragma unroll
-            for (int k = 0; k < D; ++k) h[k] = xp[k];
-            h[D] = ld_sys(&a.remote[(-1 - src) * a.ld_remote + D]);
-          }
         }
         const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x, dr_step);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
@@ -467,6 +460,20 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   }
   if (a.max_only) block_max_partial(lw, sm, a.pm + vb, a.amax, vb);
   else block_partial(lw, sm, a.pm + vb, a.ps + vb, a.ps2 + vb);
+  if (!INIT && blockIdx.x < (1u << 16)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      uint64_t* st = g_ks_stamps[blockIdx.x];
+      st[0] = ks_t0;
+      st[1] = wall_clock64();
+      st[2] = hw;
+      st[3] = xcc;
+    }
+  }
 }
 
 // k_step for one-dimensional models whose particles p, p + 64 share their
@@ -577,16 +584,6 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
           skip1 = a.part == 1 && s1 < 0;
           xp0 = s0 >= 0 ? a.xprev[s0] : (skip0 ? 0.0 : ld_sys(&a.remote[(-1 - s0) * a.ld_remote]));
           xp1 = s1 >= 0 ? a.xprev[s1] : (skip1 ? 0.0 : ld_sys(&a.remote[(-1 - s1) * a.ld_remote]));
-          if (SPLIT && a.rhist) {  // received parents' rows, kept for the genealogy
-            if (s0 < 0) {
-              a.rhist[(-1 - s0) * 2] = xp0;
-              a.rhist[(-1 - s0) * 2 + 1] = ld_sys(&a.remote[(-1 - s0) * a.ld_remote + 1]);
-            }
-            if (has1 && s1 < 0) {
-              a.rhist[(-1 - s1) * 2] = xp1;
-              a.rhist[(-1 - s1) * 2 + 1] = ld_sys(&a.remote[(-1 - s1) * a.ld_remote + 1]);
-            }
-          }
         } else {
           xp0 = a.xprev[s0];
           xp1 = a.xprev[s1];
@@ -2369,7 +2366,6 @@ struct SearchArgs {
   int mode;
   const int32_t* anc_old;  // compose when a resample is already pending
   int32_t* anc_out;
-  int own_only;            // multi-rank sampling: only the targets in this rank's CDF range (others: -1)
 };
 
 __device__ __forceinline__ uint64_t slot_target(const SearchArgs& s, const DevScalars* dev,
@@ -2409,9 +2405,7 @@ static __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t jc = j < s.n_slots ? j : s.n_slots - 1;  // clamp: padding lanes mirror the last slot
   const uint64_t base = dev->base;
-  const uint64_t tg = slot_target(s, dev, s.slot_lo + jc);
-  const uint64_t target = tg - base;
-  const bool mine = !s.own_only || (tg >= base && target < dev->local);
+  const uint64_t target = slot_target(s, dev, s.slot_lo + jc) - base;
   const int64_t hi_all = s.n_cdf - 1;
   int64_t a;
   if (s.mode == SEARCH_SYSTEMATIC) {
@@ -2438,7 +2432,7 @@ static __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs
       a = cdf_search(s.C, base, target, a_lo, a_hi);
     }
   } else {
-    a = mine ? cdf_search(s.C, base, target, 0, hi_all) : -1;
+    a = cdf_search(s.C, base, target, 0, hi_all);
   }
   if (j >= s.n_slots) return;
   const int zero = *g.zero_w;
@@ -2499,118 +2493,6 @@ static __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevSca
     if (a.res_before[s]) idx = a.ancs[s - 1][idx];
   const double* x = a.xs[a.t_target - 1];
   for (int k = 0; k < a.D; ++k) a.out[k * a.n + j] = x[xidx(idx, k, a.D)];
-}
-
-// ------------------------------------- multi-rank genealogy (queries only)
-// get_traces / the score columns / sample_unweighted_traces on R ranks
-// (particle_filter.jl:31-34, 62-70): the genealogy is kept where it was made —
-// each rank's per-step ancestors of its own slots (local index, or -1 - row of
-// the rows it received, whose global ids and states the step's part-2 launch
-// kept) — and a query walks it collectively: every step back, each rank turns
-// its slots' ancestors into global parent ids, the ranks all-gather them
-// (padded to `pad` per rank), and every cursor moves to its parent.  The
-// position of global particle c in such an all-gather is its owner's block
-// plus its local index.
-__device__ __forceinline__ int64_t mr_pos(int64_t c, const int64_t* dlo, int R, int64_t N, int64_t pad, int64_t* local) {
-  int r = (int)(((__int128)c * R) / N);
-  while (r + 1 < R && dlo[r + 1] <= c) ++r;
-  while (r > 0 && dlo[r] > c) --r;
-  *local = c - dlo[r];
-  return (int64_t)r * pad;
-}
-
-static __global__ void k_iota64(int64_t* out, int64_t n, int64_t lo) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j < n) out[j] = lo + j;
-}
-
-// global parent ids of this rank's slots at one step (rows: the received rows
-// the slots' negative ancestors index; read at system scope: the peer
-// transport's row buffer is written by other processes)
-static __global__ void k_mr_gparents(const int32_t* anc, int64_t n, int64_t lo, const double* rows, int D,
-                                     int64_t* gp) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  const int32_t a = anc[j];
-  gp[j] = a >= 0 ? lo + a : __double_as_longlong(ld_sys(&rows[(int64_t)(-1 - a) * (D + 1) + D]));
-}
-
-// every cursor one step back: cur = parent of the slot it names
-static __global__ void k_mr_back(int64_t* cur, int64_t n, const int64_t* gp_all, const int64_t* dlo, int R, int64_t N,
-                                 int64_t pad) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  int64_t i;
-  const int64_t b = mr_pos(cur[j], dlo, R, N, pad, &i);
-  cur[j] = gp_all[b + i];
-}
-
-// the cursors' states from an all-gather of every rank's (wave-tiled) slot,
-// rank r's at r * stride doubles: out[k * n + j]
-static __global__ void k_mr_states(const int64_t* cur, int64_t n, const double* slab, int64_t stride,
-                                   const int64_t* dlo, int R, int64_t N, int D, double* out) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  int64_t i;
-  const int64_t r = mr_pos(cur[j], dlo, R, N, 1, &i);
-  for (int k = 0; k < D; ++k) out[k * n + j] = slab[r * stride + xidx(i, k, D)];
-}
-
-// The score columns of this rank's slots at step s, as k_scores evaluates them
-// along a walk through the slot: Model::score of the slot's state given its
-// parent's (a local slot of step s - 1, a received row kept for step s, or the
-// slot itself when no resample preceded s; unused at s = 1).  Into the
-// all-gather's send block: lat at [0, pad), ob at [pad, 2 pad).
-template <class Model>
-__global__ __launch_bounds__(kBlock) void k_mr_slot_scores(const double* __restrict__ prm, typename Model::Params p0,
-                                                           StepObs o, int s, const double* xs, const double* xprev,
-                                                           const int32_t* anc, const double* rows, int64_t n,
-                                                           int64_t pad, double* out) {
-  constexpr int D = Model::kD;
-  const typename Model::Params p = p0.rebase(prm);
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  double x[D], xp[D];
-#pragma unroll
-  for (int k = 0; k < D; ++k) x[k] = xs[xidx(j, k, D)];
-  if (s > 1) {
-    const int64_t a = anc ? anc[j] : j;
-    if (a >= 0) {
-#pragma unroll
-      for (int k = 0; k < D; ++k) xp[k] = xprev[xidx(a, k, D)];
-    } else {
-#pragma unroll
-      for (int k = 0; k < D; ++k) xp[k] = rows[(-1 - a) * (D + 1) + k];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < D; ++k) xp[k] = 0.0;
-  }
-  double lat, ob;
-  Model::score(p, o, (uint32_t)s, xp, x, &lat, &ob);
-  out[j] = lat;
-  out[pad + j] = ob;
-}
-
-// the cursors' step-s columns from the all-gathered slot scores
-static __global__ void k_mr_take_scores(const int64_t* cur, int64_t n, const double* all, const int64_t* dlo, int R,
-                                        int64_t N, int64_t pad, double* lat, double* ob) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  int64_t i;
-  const int64_t b = mr_pos(cur[j], dlo, R, N, 2 * pad, &i);
-  lat[j] = all[b + i];
-  ob[j] = all[b + pad + i];
-}
-
-// get_score: the columns summed in time order (k_scores' order)
-static __global__ void k_score_total(const double* per_step, int T, int64_t n, double* total) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  double tot = 0.0;
-  for (int s = 1; s <= T; ++s)
-    tot += per_step[((int64_t)(s - 1) * 2) * n + j] + per_step[((int64_t)(s - 1) * 2 + 1) * n + j];
-  total[j] = tot;
 }
 
 // sample_unweighted: prepare max / equal-weight flag from the current stats

@@ -167,19 +167,6 @@ typedef struct {
 } gh_host_comm;
 int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_host_comm* comm, void* hip_stream,
                            gh_ctx** out);
-/* Peer transport: the ranks' kernels exchange through device memory they map
-   from each other (a fine-grained mailbox per rank, and every filter's
-   received-row buffer), with tagged words and bounded polls — no collective
-   call and no host round trip on the step path.  The bootstrap's allgather
-   (host buffers) swaps the IPC handles once, at context and filter creation
-   (both collective over the ranks), and at gh_ctx_destroy; sendrecv is not
-   used.  Ranks on one GPU (processes sharing a device) or on GPUs that map
-   each other's memory (xGMI peers of one node).  world <= 64.  Multi-rank
-   filters on it resample systematically through the fused kernels (a
-   configuration that would need another form returns GH_E_STATE); a rank
-   that stops posting makes the others' waits end in GH_E_STATE. */
-int gh_ctx_create_peer(int device, int rank, int world, const gh_host_comm* bootstrap, void* hip_stream,
-                       gh_ctx** out);
 int gh_ctx_destroy(gh_ctx* ctx);
 /* Debug / timing: filters created on this context afterwards take the
    multi-rank code path (collectives, split step after a resample, k_rank_a/b)

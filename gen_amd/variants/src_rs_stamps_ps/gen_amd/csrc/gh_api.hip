@@ -3483,6 +3483,14 @@ extern "C" int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n
   return rc;
 }
 
+#if defined(GH_RS_STAMPS)
+extern "C" int gh_debug_rs_stamps(uint64_t* out, int n) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rs_stamps), sizeof(uint64_t) * (size_t)n));
+  return GH_OK;
+}
+#endif
+
 // ------------------------------------------------------------------ PMMH
 extern "C" int gh_pmmh_run(gh_ctx* ctx, int64_t chain0, int64_t n_chains, int n_inner, const double* ys, int T,
                            int n_iters, int iter0, uint64_t seed, int init, double* lvx, double* lvy, double* lml,

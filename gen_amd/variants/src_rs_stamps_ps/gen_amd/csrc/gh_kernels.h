@@ -1356,6 +1356,24 @@ __device__ __forceinline__ uint64_t f64_to_u52(double x) {
   return as_u64(floor(x) + 0x1p52) - 0x4330000000000000ull;
 }
 
+// timing-only variants (results wrong): GH_RS_EXIT=k leaves k_resample1 after
+// phase k (0 start, 1 fold, 2 quantise + scan, 3 grid barrier), to price the
+// phases including the launch
+#if defined(GH_RS_EXIT)
+#define GH_RS_EXIT_AT(k) \
+  if (GH_RS_EXIT == (k)) return;
+#else
+#define GH_RS_EXIT_AT(k)
+#endif
+
+#if defined(GH_RS_STAMPS)  // timing-only variant: per-block phase clocks
+static __device__ uint64_t g_rs_stamps[1024 * 8];
+#define GH_RS_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_rs_stamps[blockIdx.x * 8 + (k)] = wall_clock64();
+#else
+#define GH_RS_STAMP(k)
+#endif
+
 template <bool MARKS, int IT, bool SUMS>
 __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resample1Args r) {
   __shared__ double smd[32];
@@ -1364,6 +1382,8 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   __shared__ uint64_t sbase;
   __shared__ unsigned sgen;
   __shared__ int sfail;  // the barrier wait timed out: write nothing
+  GH_RS_STAMP(0);
+  GH_RS_EXIT_AT(0);
   // barrier generation of this launch: read before this block publishes
   if (threadIdx.x == 0) {
     sgen = r.dev->bar_gen + 1;
@@ -1388,6 +1408,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     uint64_t key = lane < kAmaxShards ? r.amax_in[lane * kAmaxStride] : 0ull;
     key = wave_incl_max_u64(key);
     M = amax_value(readlane63_u64(key));
+    GH_RS_STAMP(7);
   } else if (IT <= 8 && r.nb_part <= KP * kRsBlock) {  // uniform; always true at IT <= kRsPart (host-checked)
     double pmv[KP], psv[kSumsEarly ? KP : 1], ps2v[kSumsEarly ? KP : 1];
 #pragma unroll
@@ -1404,6 +1425,8 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
 #pragma unroll
     for (int k = 1; k < KP; ++k) m = fmax(m, pmv[k]);
     M = blk16_max1(m, smd);
+    GH_RS_STAMP(7);
+    GH_RS_EXIT_AT(1);
     if (!sums && M > -INFINITY) {
       double a1[KP], a2[KP];
 #pragma unroll
@@ -1473,6 +1496,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     lds_barrier();
   }
+  GH_RS_STAMP(1);
   auto commit = [&]() {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       const Decision dec = decision();
@@ -1509,6 +1533,8 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
   }
   const uint64_t incl = sums ? blk16_scan<true>(tsum, &s1, &s2, smu, smd) : blk16_scan<false>(tsum, &s1, &s2, smu, smd);
+  GH_RS_STAMP(2);
+  GH_RS_EXIT_AT(2);
   // ---- grid barrier: each tile total (< 2^62) is published as ONE 8-byte
   // agent-scope store tagged in bit 63 with the generation's parity, and read
   // back with agent-scope loads until every tag matches (the payload is its
@@ -1592,6 +1618,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
   }
   lds_barrier();
+  GH_RS_STAMP(3);
   if (threadIdx.x == 0) {
     uint64_t all = 0, before = 0;
     double g1 = 0.0, g2 = 0.0;
@@ -1640,6 +1667,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // grid never started): the totals are partial.  The block leaves without
   // marks or decision; the error surfaces as GH_E_STATE at the next sync.
   if (sfail) return;
+  GH_RS_EXIT_AT(3);
   if (sums) {
     S1 = sS[0];
     S2 = sS[1];
@@ -1648,6 +1676,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       return;
     }
   }
+  GH_RS_STAMP(4);
   uint64_t run = sbase + incl - tsum;
   if (!MARKS) {
 #pragma unroll
@@ -1692,7 +1721,9 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     s_i = e_i;
   }
+  GH_RS_STAMP(5);
   commit();
+  GH_RS_STAMP(6);
 }
 
 // ------------------------------------------------ multi-rank resample (R > 1)

@@ -36,12 +36,15 @@ def main():
     p.add_argument("--T", type=int, default=8)
     p.add_argument("--thr", type=float, default=None, help="ESS threshold (default: N/2)")
     p.add_argument("--seed", type=int, default=9)
-    p.add_argument("--transport", default="gloo", help="gloo (host-staged), rccl, or rccl1: one rank forced onto "
-                   "the multi-rank path over a one-rank RCCL communicator (gh_ctx_force_multirank)")
+    p.add_argument("--transport", default="gloo", help="gloo (host-staged), peer (device mailboxes, IPC handles "
+                   "swapped over gloo), rccl, or rccl1: one rank forced onto the multi-rank path over a one-rank "
+                   "RCCL communicator (gh_ctx_force_multirank)")
     p.add_argument("--batched", action="store_true", help="steps 2..T through run_particle_filter (gh_pf_run: "
                    "max-only steps, the resample's sums in k_rank_a2)")
     p.add_argument("--rejuv", type=int, default=0, help="rejuvenation moves after init and every step")
     p.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK)")
+    p.add_argument("--genealogy", action="store_true", help="also save trajectories at t = 1, 5, T, the score "
+                   "columns and 500 sample_unweighted_traces indices (collective queries)")
     p.add_argument("--out", required=True)
     a = p.parse_args()
 
@@ -52,9 +55,9 @@ def main():
 
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    if a.transport == "gloo":
+    if a.transport in ("gloo", "peer"):
         tr = GlooTransport()
-        ctx = gen.Context(device=0, transport=tr)
+        ctx = gen.Context(device=0, transport=tr, peer=a.transport == "peer")
     elif a.transport == "rccl1":
         assert world == 1
         ctx = gen.Context(device=a.device or 0, force_multirank=True)
@@ -79,6 +82,13 @@ def main():
         if a.rejuv:
             gen.rejuvenate(st, a.rejuv)
     lml = gen.log_ml_estimate(st)
+    extra = {}
+    if a.genealogy:
+        for t in sorted({1, min(5, a.T), a.T}):
+            extra[f"traj{t}"] = st.states(t)
+        tot, ps = gen.get_traces(st).scores(per_step=True)
+        extra["score_tot"], extra["score_ps"] = tot, ps
+        _, extra["samp"] = gen.sample_unweighted_traces(st, 500, seed=3)
     np.savez(
         f"{a.out}.rank{rank}.npz",
         states=st.states(),
@@ -87,6 +97,7 @@ def main():
         lml=lml,
         did=np.array(did, dtype=np.int64),
         lo=st.first,
+        **extra,
     )
     st.close()
     dist.barrier()

@@ -358,3 +358,76 @@ def test_gpu_multirank_path_over_rccl_one_rank(tmp_path, model, thr, n, batched)
                   *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--transport", "rccl1",
                   "--device", "0", *(["--batched"] if batched else []), "--out", out], 1, timeout=300)
     _check_against_oracle(out, model, 1, n, T, seed, thr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,R,thr,n,batched", [("lg4", 2, None, 3001, True), ("lg4", 3, 1e9, 20011, True),
+                                                    ("kit", 2, None, 4096, True), ("kit", 4, 1e9, 8192, True),
+                                                    ("kit_sharp", 4, None, 4003, True), ("lg10", 2, 3001.0, 3001, True),
+                                                    ("lg4", 2, None, 3001, False), ("kit", 3, 1e9, 4003, False)])
+def test_gpu_multirank_peer_transport(tmp_path, model, R, thr, n, batched):
+    """The peer transport (gh_ctx_create_peer): R processes share GPU 0, map
+    each other's mailboxes and row buffers by IPC handle (swapped once over
+    gloo), and exchange the rank maxima, the records and the state rows with
+    device stores and tagged words — k_rank_a2 / k_rank_b / k_peer_* inside
+    the step loop, no host collective.  The gathered shards equal the
+    single-rank oracle bit for bit (log-ML 1e-9), batched (gh_pf_run) and
+    call by call (the small all-gathers through k_peer_allgather)."""
+    out = str(tmp_path / "p")
+    T, seed = 8, 9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--transport", "peer",
+                  *(["--batched"] if batched else []), "--out", out], R, timeout=400)
+    _check_against_oracle(out, model, R, n, T, seed, thr)
+
+
+def _check_genealogy(out, model, R, n, T, seed, thr, batched):
+    """Trajectories at t = 1, 5, T and the score columns of the gathered shards
+    equal the single-rank oracle bit for bit; the 500 sample_unweighted_traces
+    indices equal a one-rank GPU filter's (the same global integer CDF)."""
+    import gen_amd as gen
+    from oracle import oracle as O
+    from tests.mr_worker import build_model
+
+    m = build_model(model)
+    _, ys = m.simulate(T, np.random.default_rng(5))
+    ref = O.run_pf(m, ys, n, seed, thr=thr)
+    parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
+    for t in sorted({1, min(5, T), T}):
+        got = np.concatenate([p[f"traj{t}"] for p in parts], axis=0)  # [n, d]
+        assert np.array_equal(got.T.view(np.uint64), ref.trajectory(t).view(np.uint64)), t
+    rtot, rps = ref.scores(per_step=True)
+    assert np.array_equal(np.concatenate([p["score_tot"] for p in parts]).view(np.uint64), rtot.view(np.uint64))
+    assert np.array_equal(np.concatenate([p["score_ps"] for p in parts], axis=2).view(np.uint64), rps.view(np.uint64))
+    # the same filter on one rank of this process's GPU
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=seed)
+    if batched:
+        gen.run_particle_filter(st, list(ys[1:T]), thr)
+    else:
+        for t in range(2, T + 1):
+            gen.maybe_resample(st, thr)
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {m.obs_address(t): ys[t - 1]})
+    _, idx = gen.sample_unweighted_traces(st, 500, seed=3)
+    st.close()
+    for p in parts:
+        assert np.array_equal(p["samp"], idx)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,model,R,thr,n,batched", [
+    ("gloo", "lg4", 2, None, 3001, False), ("gloo", "kit", 3, 1e9, 4003, True), ("gloo", "kit_sharp", 3, None, 4003, True),
+    ("peer", "lg4", 2, 1e9, 3001, True), ("peer", "kit", 3, None, 4096, True), ("peer", "lg10", 2, 3001.0, 3001, False),
+    ("rccl1", "lg4", 1, None, 3001, True)])
+def test_gpu_multirank_genealogy(tmp_path, gh_ctx, transport, model, R, thr, n, batched):
+    """The genealogy across ranks (get_traces at earlier steps, the trace score
+    columns, sample_unweighted_traces; particle_filter.jl:31-34, 62-70): each
+    rank keeps its slots' ancestors and the rows it received, and the queries
+    walk them collectively — against the single-rank oracle bit for bit."""
+    out = str(tmp_path / "gen")
+    T, seed = 8, 9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--transport", transport,
+                  *(["--device", "0"] if transport == "rccl1" else []), *(["--batched"] if batched else []),
+                  "--genealogy", "--out", out], R, timeout=400)
+    _check_against_oracle(out, model, R, n, T, seed, thr)
+    _check_genealogy(out, model, R, n, T, seed, thr, batched)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-5 GPU pass C: GPU tests named in $1, then the resample's phase clocks
+# at C4 with the pair kernel folding its maxima into the shards (variant).
+set -e
+OUT=$PWD/gpurun_out/r5c
+mkdir -p $OUT
+export TMPDIR=/tmp
+if [ -n "$1" ]; then
+  timeout -k 10 1000 python -u -m pytest $1 -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+  tail -3 $OUT/pytest.log
+fi
+GEN_HIP_LIB=$PWD/gen_amd/variants/rs_stamps_ps.so timeout -k 10 120 python tools/rs_stamps.py kit 21 > $OUT/rs_kit_ps.txt 2>&1
+GEN_HIP_LIB=$PWD/gen_amd/variants/rs_stamps.so timeout -k 10 120 python tools/rs_stamps.py kit 21 > $OUT/rs_kit.txt 2>&1
+cat $OUT/rs_kit_ps.txt $OUT/rs_kit.txt
