@@ -326,20 +326,27 @@ def secondary_multirank_path(gen, a, c2_ms, c4_ms):
     ncclAllGather, k_rank_a2, k_rank_b and the split step, against the one-rank
     path's ms_per_step measured above (DESIGN.md §7 projects the 8-GPU step
     from the difference)."""
-    ctx = gen.Context(device=0, force_multirank=True)
+    from gen_amd.transport import LocalTransport
+
     out = {}
-    try:
-        for name, model, n, d, base in (("C2", gen.LinearGaussianSSM.benchmark(a.d), a.particles, a.d, c2_ms),
-                                        ("C4", gen.KitagawaSSM(10.0, 1.0), 1 << 21, 1, c4_ms)):
-            r = pf_run(gen, ctx, None, 1, a, model, n, "", lambda n_res, d=d: 16 * d + 16)
-            ms = r["dt"] * 1e3 / a.steps
-            out[name] = {"ms_per_step": ms, "one_rank_ms_per_step": base,
-                         "extra_us_per_step": None if base is None else round((ms - base) * 1e3, 2),
-                         "resample_steps_timed": r["n_res"], "log_ml": r["lml"]}
-    finally:
-        ctx.close()
-    out["note"] = ("world = 1 on the multi-rank path over RCCL: the collectives are one-rank copies and no rows "
-                   "move, so the extra time is the path's launches, host plan and all-gather kernels, not xGMI")
+    for tname, mk in (("rccl", lambda: gen.Context(device=0, force_multirank=True)),
+                      ("peer", lambda: gen.Context(device=0, transport=LocalTransport(), peer=True))):
+        ctx = mk()
+        try:
+            for name, model, n, d, base in (("C2", gen.LinearGaussianSSM.benchmark(a.d), a.particles, a.d, c2_ms),
+                                            ("C4", gen.KitagawaSSM(10.0, 1.0), 1 << 21, 1, c4_ms)):
+                r = pf_run(gen, ctx, None, 1, a, model, n, "", lambda n_res, d=d: 16 * d + 16)
+                ms = r["dt"] * 1e3 / a.steps
+                out[f"{name}_{tname}" if tname != "rccl" else name] = {
+                    "ms_per_step": ms, "one_rank_ms_per_step": base,
+                    "extra_us_per_step": None if base is None else round((ms - base) * 1e3, 2),
+                    "resample_steps_timed": r["n_res"], "log_ml": r["lml"]}
+        finally:
+            ctx.close()
+    out["note"] = ("world = 1 on the multi-rank path: C2 / C4 over RCCL (the collectives are one-rank copies), "
+                   "C2_peer / C4_peer over the peer transport (the maxima and records through the rank's own "
+                   "mailbox inside k_rank_a2 / k_rank_b, no collective launch); no rows move, so the extra time "
+                   "is the path's launches, host plan and exchanges, not xGMI")
     return out
 
 

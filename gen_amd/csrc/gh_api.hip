@@ -1738,15 +1738,10 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   // need the shards (the rank maximum has no other fold).
   const bool lazy = !multi && pf->rs_grid > 0 && !pf->cond && pf->n > 0 && !pf->no_max_only;
   a.max_only = (pf->step_max_only || lazy) && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
-  // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
-  // short step more than the fold they save, measured)
-#if defined(GH_PAIRS_SHARDS)  // timing variant: the pair kernel folds its maxima into the shards too
-  a.amax = a.max_only && pf->amax_armed
-#else
-  a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
-#endif
-               ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride
-               : nullptr;
+  // The block maxima also go into the atomic-max shards, so the resample
+  // reads 32 words instead of every block's maximum (the pair kernel too:
+  // C4 39.45 -> 39.06 us per step, four runs each on one box, round 5).
+  a.amax = a.max_only && pf->amax_armed ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride : nullptr;
   // multi-rank after a resample: the local half now, the rest once the rows arrive
   a.part = pf->plan_pending && a.mark_mode == 2 ? 1 : 0;
   if (pin_ref) {
@@ -2690,7 +2685,6 @@ extern "C" int gh_pf_step_params_conditional(gh_pf* pf, const gh_obs* obs, gh_mo
 }
 
 static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm, const double* pin_ref) {
-  if (mr(pf->ctx)) return set_err(GH_E_STATE, "gh_pf_step_params: one rank (the re-scoring walks the genealogy)");
   if (!pf->opts.record_history) return set_err(GH_E_STATE, "gh_pf_step_params needs record_history");
   const gh_model* m = pf->m;
   if (nm->ctx != m->ctx || nm->family != m->family || nm->d != m->d || nm->dy != m->dy || nm->k != m->k ||
@@ -2752,6 +2746,11 @@ static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model
     pf->stats_valid = false;
     pf->max_only = false;
     pf->amax_valid = false;
+    if (mr(pf->ctx) && !rc) {  // the rank's (M, S, S2) of the changed weights, shared again
+      hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_part,
+                         pf->dev->stats, pf->dev, 1, 0.0, pf->n_global);
+      rc = share_stats(pf);
+    }
   }
   if (hipStreamSynchronize(pf->s) != hipSuccess && !rc) rc = set_err(GH_E_HIP, "gh_pf_step_params: sync");
   cleanup();

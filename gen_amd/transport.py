@@ -86,3 +86,20 @@ class GlooTransport:
         except Exception as e:
             print(f"GlooTransport.sendrecv failed: {e!r}", flush=True)
             return 1
+
+
+class LocalTransport:
+    """A one-rank transport (world 1): the all-gather is a copy.  With
+    Context(peer=True) it runs the multi-rank code path of the peer transport
+    on one process (the mailboxes are its own), e.g. to time that path."""
+
+    def __init__(self):
+        self.rank, self.world = 0, 1
+        self._ag = ALLGATHER_FN(self._allgather)
+        self._sr = SENDRECV_FN(lambda *a: 0)
+        self.struct = HostComm(None, self._ag, self._sr)
+
+    @staticmethod
+    def _allgather(_user, send, recv, nbytes):
+        ctypes.memmove(recv, send, nbytes)
+        return 0

@@ -30,6 +30,7 @@
 #include "gh_rejuv.h"
 #include "gh_csmc.h"
 #include "gh_inst.h"
+#include "gh_peer.h"
 
 using namespace gh;
 
@@ -104,7 +105,51 @@ struct gh_ctx {
   // (a one-rank RCCL communicator; tests and timing on a one-GPU box)
   bool force_multi = false;
   int n_filters = 0;  // live filters (their buffers follow the path chosen at their creation)
+  // peer transport (gh_ctx_create_peer, gh_peer.h): every rank's mailbox as
+  // mapped here (mpeer[rank] = mbox, the own one, fine-grained), the
+  // bootstrap callbacks (hc; setup only) and each region's use counter
+  bool peer = false;
+  uint64_t* mbox = nullptr;
+  uint64_t* mpeer[kPeerMaxRanks] = {};
+  uint64_t use_sh = 0, use_rec = 0, use_ag = 0;
 };
+
+static PeerBox peer_box(const gh_ctx* c) {
+  PeerBox pb{};
+  for (int r = 0; r < c->world; ++r) pb.peer[r] = c->mpeer[r];
+  pb.R = c->world;
+  pb.rank = c->rank;
+  return pb;
+}
+
+// Bootstrap exchange of IPC handles over the user's host all-gather: map
+// every other rank's buffer (out[rank] = own).
+static int ipc_exchange(gh_ctx* c, void* own, void** out) {
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
+  std::vector<uint8_t> send(64, 0), recv(64 * (size_t)c->world, 0);
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, own));
+  memcpy(send.data(), &h, sizeof h);
+  if (c->hc.allgather(c->hc.user, send.data(), recv.data(), 64))
+    return set_err(GH_E_RCCL, "peer transport: bootstrap allgather failed");
+  for (int r = 0; r < c->world; ++r) {
+    if (r == c->rank) {
+      out[r] = own;
+      continue;
+    }
+    hipIpcMemHandle_t hr;
+    memcpy(&hr, recv.data() + 64 * (size_t)r, sizeof hr);
+    void* p = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&p, hr, hipIpcMemLazyEnablePeerAccess));
+    out[r] = p;
+  }
+  return GH_OK;
+}
+
+static void ipc_close(const gh_ctx* c, void* const* mapped) {
+  for (int r = 0; r < c->world; ++r)
+    if (r != c->rank && mapped[r]) hipIpcCloseMemHandle(mapped[r]);
+}
 
 // the filter's multi-rank path (collectives, split steps) is in use
 static bool mr(const gh_ctx* c) { return c->world > 1 || c->force_multi; }
@@ -176,6 +221,42 @@ extern "C" int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_
   return GH_OK;
 }
 
+extern "C" int gh_ctx_create_peer(int device, int rank, int world, const gh_host_comm* bootstrap, void* hip_stream,
+                                  gh_ctx** out) {
+  if (!out || !bootstrap || !bootstrap->allgather || world < 1 || world > kPeerMaxRanks || rank < 0 || rank >= world)
+    return set_err(GH_E_INVAL, "gh_ctx_create_peer: bad argument (rank/world %d/%d, at most %d ranks)", rank, world,
+                   kPeerMaxRanks);
+  gh_ctx* c = new gh_ctx();
+  int rc = ctx_setup(device, hip_stream, c);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  c->rank = rank;
+  c->world = world;
+  c->peer = true;
+  c->hc = *bootstrap;
+  const size_t bytes = sizeof(uint64_t) * (size_t)mb_words(world);
+  if (hipExtMallocWithFlags((void**)&c->mbox, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+    delete c;
+    return set_err(GH_E_NOMEM, "peer transport: mailbox");
+  }
+  if (hipMemset(c->mbox, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    hipFree(c->mbox);
+    delete c;
+    return set_err(GH_E_HIP, "peer transport: mailbox init");
+  }
+  rc = ipc_exchange(c, c->mbox, (void**)c->mpeer);
+  if (rc) {
+    ipc_close(c, (void**)c->mpeer);
+    hipFree(c->mbox);
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return GH_OK;
+}
+
 extern "C" int gh_ctx_force_multirank(gh_ctx* c) {
   if (!c) return set_err(GH_E_INVAL, "null ctx");
   if (c->force_multi) return GH_OK;
@@ -199,6 +280,14 @@ extern "C" int gh_ctx_destroy(gh_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->stage) hipHostFree(c->stage);
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->peer) {
+    // every rank is done writing into the others' mailboxes before any frees its own
+    uint8_t one = 1;
+    std::vector<uint8_t> all((size_t)c->world);
+    c->hc.allgather(c->hc.user, &one, all.data(), 1);
+    ipc_close(c, (void**)c->mpeer);
+    hipFree(c->mbox);
+  }
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
   return GH_OK;
@@ -245,7 +334,15 @@ static int stage_reserve(gh_ctx* c, size_t bytes) {
   return GH_OK;
 }
 
-static int comm_allgather(gh_ctx* c, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
+static int comm_allgather(gh_ctx* c, const void* dsend, void* drecv, size_t bytes, hipStream_t s, int* derr) {
+  if (c->peer) {  // one wave through the mailboxes (gh_peer.h)
+    if (bytes % 8 || bytes > sizeof(uint64_t) * kAgWords)
+      return set_err(GH_E_INVAL, "peer transport: all-gather of %zu bytes", bytes);
+    hipLaunchKernelGGL(k_peer_allgather, dim3(1), dim3(64), 0, s, (const uint64_t*)dsend, (uint64_t*)drecv,
+                       (int)(bytes / 8), peer_box(c), ++c->use_ag, derr);
+    HIP_TRY(hipGetLastError());
+    return GH_OK;
+  }
   if (!c->host_comm) {
     NCCL_TRY(ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, s));
     return GH_OK;
@@ -264,6 +361,7 @@ static int comm_allgather(gh_ctx* c, const void* dsend, void* drecv, size_t byte
 static int comm_exchange(gh_ctx* c, const std::vector<CommMsg>& sends, const std::vector<CommMsg>& recvs,
                          hipStream_t s) {
   if (sends.empty() && recvs.empty()) return GH_OK;
+  if (c->peer) return set_err(GH_E_STATE, "peer transport: rows move inside the resample kernels only");
   if (!c->host_comm) {
     // an error inside the group still closes it (an open group leaves the
     // communicator unusable); the first error is reported
@@ -307,6 +405,26 @@ static int comm_exchange(gh_ctx* c, const std::vector<CommMsg>& sends, const std
     return set_err(GH_E_RCCL, "host transport: sendrecv failed");
   for (size_t i = 0; i < recvs.size(); ++i)
     HIP_TRY(hipMemcpyAsync(recvs[i].dptr, rb[i], recvs[i].bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return GH_OK;
+}
+
+// All-gather of a large buffer for the genealogy queries (off the step
+// path): RCCL, or staged through host memory and the user's all-gather (the
+// host and peer transports).  Synchronous.
+static int bulk_allgather(gh_ctx* c, const void* dsend, void* drecv, size_t bytes, hipStream_t s) {
+  if (c->comm) {
+    NCCL_TRY(ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return GH_OK;
+  }
+  if (!c->hc.allgather) return set_err(GH_E_STATE, "no transport for the genealogy all-gather");
+  std::vector<uint8_t> hs(bytes), hr(bytes * (size_t)c->world);
+  HIP_TRY(hipMemcpyAsync(hs.data(), dsend, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->hc.allgather(c->hc.user, hs.data(), hr.data(), bytes))
+    return set_err(GH_E_RCCL, "genealogy all-gather failed");
+  HIP_TRY(hipMemcpyAsync(drecv, hr.data(), hr.size(), hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));
   return GH_OK;
 }
@@ -750,6 +868,18 @@ struct gh_pf {
   bool dec_posted = false;        // the last maybe_resample! posts its decision to h_dec
   bool no_max_only = false;       // gh_pf_step_params: the step writes full partials
   bool mr_stale = false;          // multi-rank: the last step left its weight sums to the next resample
+  // peer transport: every rank's row buffer as mapped here (prow[rank] =
+  // rows_recv, fine-grained, followed by R tag words indexed by sender) and
+  // the row exchanges posted so far
+  double* prow[kPeerMaxRanks] = {};
+  uint64_t* ptag[kPeerMaxRanks] = {};
+  uint64_t row_use = 0;
+  // multi-rank genealogy (record_history): per step, the rows received for
+  // it (the parents on other ranks; D + 1 doubles each, row-indexed), kept by
+  // the step's part-2 launch; chunked device storage
+  std::vector<double*> rh_step;   // index t-1 (nullptr: none received)
+  std::vector<char*> rh_chunks;
+  size_t rh_used = 0, rh_cap = 0;
   int64_t* dlo = nullptr;         // [R + 1] floor(N k / R): the ranks' first global slots
   uint64_t mail_seq = 0;          //   the tag of the last plan posted there
   bool plan_recs = false;         // the pending plan is k_rank_a2's records (the host takes the decision)
@@ -929,6 +1059,8 @@ static void pf_free(gh_pf* pf) {
   if (pf->h_plan) hipHostFree(pf->h_plan);
   if (pf->h_mail) hipHostFree(pf->h_mail);
   if (pf->h_dec) hipHostFree(pf->h_dec);
+  for (auto c : pf->rh_chunks) hipFree(c);
+  if (pf->ctx->peer) ipc_close(pf->ctx, (void**)pf->prow);
   hipFree(pf->dlo);
   if (!pf->opts.record_history) {
     for (auto p : pf->xs) hipFree(p);
@@ -1127,6 +1259,28 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
 
 static int finish_plan(gh_pf* pf);
 
+// The genealogy record of step t's received rows (count of them): chunked
+// device storage, released with the filter.
+static int rhist_reserve(gh_pf* pf, int t, int64_t count, double** out) {
+  *out = nullptr;
+  if ((int)pf->rh_step.size() < t) pf->rh_step.resize(t, nullptr);
+  pf->rh_step[t - 1] = nullptr;
+  if (count <= 0) return GH_OK;
+  const size_t bytes = (sizeof(double) * (size_t)(pf->D + 1) * (size_t)count + 255) & ~(size_t)255;
+  if (pf->rh_used + bytes > pf->rh_cap) {
+    const size_t cap = std::max(bytes, (size_t)64 << 20);
+    char* c = nullptr;
+    if (hipMalloc(&c, cap) != hipSuccess) return set_err(GH_E_NOMEM, "genealogy rows (%zu bytes)", cap);
+    pf->rh_chunks.push_back(c);
+    pf->rh_used = 0;
+    pf->rh_cap = cap;
+  }
+  *out = (double*)(pf->rh_chunks.back() + pf->rh_used);
+  pf->rh_used += bytes;
+  pf->rh_step[t - 1] = *out;
+  return GH_OK;
+}
+
 // Multi-rank, after the step kernel: when the step followed a resample it was
 // enqueued before the host read the plan (part 1); now the plan is read, the
 // rows exchanged and the tiles holding slots that take received rows run
@@ -1151,6 +1305,7 @@ static int finish_split(gh_pf* pf, const StepObs& o, const StepArgs& a, bool ini
         b.vb_split = tA;
         b.vb_skip = tB - tA;
         b.grid_blocks = tA + (nb - tB);
+        if (pf->opts.record_history) CHECK(rhist_reserve(pf, (int)a.t, ra + (n - rb), &b.rhist));
         CHECK(launch_step(pf, o, b, init));
       }
     }
@@ -1190,7 +1345,7 @@ static int timed_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init)
 // after the step kernel: share the rank's (M, S, S2) with every rank
 static int share_stats(gh_pf* pf) {
   if (!mr(pf->ctx)) return GH_OK;
-  return comm_allgather(pf->ctx, pf->dev->stats, pf->stats_all, 3 * sizeof(double), pf->s);
+  return comm_allgather(pf->ctx, pf->dev->stats, pf->stats_all, 3 * sizeof(double), pf->s, &pf->dev->error);
 }
 
 // Conditional SMC: pin particle 0 around the step kernel (gh_csmc.h).  pre =
@@ -1374,7 +1529,23 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (mr(ctx)) {
     if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
       return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
-    ALLOC(pf->rows_recv, sizeof(double) * (pf->D + 1) * n);
+    if (!ctx->peer) {
+      ALLOC(pf->rows_recv, sizeof(double) * (pf->D + 1) * n);
+    } else {
+      // the received rows (written by the senders' k_rank_b), then R tag
+      // words; fine-grained, mapped by every rank (bootstrap exchange)
+      const size_t rb = sizeof(double) * (pf->D + 1) * n + sizeof(uint64_t) * ctx->world;
+      if (hipExtMallocWithFlags((void**)&pf->rows_recv, rb, hipDeviceMallocFinegrained) != hipSuccess)
+        return fail(set_err(GH_E_NOMEM, "peer transport: row buffer"));
+      if (hipMemset(pf->rows_recv, 0, rb) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return fail(set_err(GH_E_HIP, "peer transport: row buffer init"));
+      const int rc = ipc_exchange(ctx, pf->rows_recv, (void**)pf->prow);
+      if (rc) return fail(rc);
+      for (int r = 0; r < ctx->world; ++r) {
+        const int64_t nr = std::max<int64_t>(1, split_lo(pf->n_global, r + 1, ctx->world) - split_lo(pf->n_global, r, ctx->world));
+        pf->ptag[r] = (uint64_t*)(pf->prow[r] + (pf->D + 1) * nr);
+      }
+    }
     ALLOC(pf->gparent, sizeof(int64_t) * n);
     ALLOC(pf->amax_all, sizeof(uint64_t) * kAmaxShards * kAmaxStride * ctx->world);
     ALLOC(pf->rec, sizeof(uint64_t) * kRecWords);
@@ -1567,11 +1738,10 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   // need the shards (the rank maximum has no other fold).
   const bool lazy = !multi && pf->rs_grid > 0 && !pf->cond && pf->n > 0 && !pf->no_max_only;
   a.max_only = (pf->step_max_only || lazy) && !pin_ref && (!multi || pf->amax_armed) ? 1 : 0;
-  // (one rank: not for the pair-stepped kernel, whose 4096 atomics cost C4's
-  // short step more than the fold they save, measured)
-  a.amax = a.max_only && pf->amax_armed && (multi || pf->nb_part == pf->nb_step)
-               ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride
-               : nullptr;
+  // The block maxima also go into the atomic-max shards, so the resample
+  // reads 32 words instead of every block's maximum (the pair kernel too:
+  // C4 39.45 -> 39.06 us per step, four runs each on one box, round 5).
+  a.amax = a.max_only && pf->amax_armed ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride : nullptr;
   // multi-rank after a resample: the local half now, the rest once the rows arrive
   a.part = pf->plan_pending && a.mark_mode == 2 ? 1 : 0;
   if (pin_ref) {
@@ -1668,9 +1838,13 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   // (global max, quantisation + sums, rank record), the records' all-gather;
   // otherwise k_rank_a on the all-gathered triples and the totals' all-gather
   const bool sums = pf->max_only && pf->amax_valid;
+  uint64_t* shards = pf->amax + (t & 1) * kAmaxShards * kAmaxStride;
   if (sums) {
-    uint64_t* shards = pf->amax + (t & 1) * kAmaxShards * kAmaxStride;
-    CHECK(comm_allgather(c, shards, pf->amax_all, sizeof(uint64_t) * kAmaxShards * kAmaxStride, pf->s));
+    // peer transport: the shards' and the records' all-gathers happen inside
+    // k_rank_a2 / k_rank_b through the mailboxes
+    if (!c->peer)
+      CHECK(comm_allgather(c, shards, pf->amax_all, sizeof(uint64_t) * kAmaxShards * kAmaxStride, pf->s,
+                           &pf->dev->error));
     RankA2Args a2{};
     a2.logw = pf->logw;
     a2.n = pf->n;
@@ -1683,13 +1857,20 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
     a2.ts1 = pf->tsum + pf->n_tiles;
     a2.ts2 = pf->tsum + 2 * pf->n_tiles;
     a2.rec = pf->rec;
+    if (c->peer) {
+      a2.pb = peer_box(c);
+      a2.amax_own = shards;
+      a2.amax_reset = nullptr;  // (k_rank_b empties them: every block here reads them)
+      a2.use_sh = ++c->use_sh;
+      a2.use_rec = ++c->use_rec;
+    }
     switch (pf->rs_it) {
       case 4: hipLaunchKernelGGL(k_rank_a2<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
       case 8: hipLaunchKernelGGL(k_rank_a2<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
       default: hipLaunchKernelGGL(k_rank_a2<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
     }
     HIP_TRY(hipGetLastError());
-    CHECK(comm_allgather(c, pf->rec, pf->recs_all, sizeof(uint64_t) * kRecWords, pf->s));
+    if (!c->peer) CHECK(comm_allgather(c, pf->rec, pf->recs_all, sizeof(uint64_t) * kRecWords, pf->s, &pf->dev->error));
   } else {
     RankAArgs ra{};
     ra.logw = pf->logw;
@@ -1706,7 +1887,7 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
       default: hipLaunchKernelGGL(k_rank_a<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ra); break;
     }
     HIP_TRY(hipGetLastError());
-    CHECK(comm_allgather(c, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
+    CHECK(comm_allgather(c, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s, &pf->dev->error));
     HIP_TRY(hipEventRecord(pf->ev_tot, pf->s));
   }
   RankBArgs rb{};
@@ -1740,10 +1921,33 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.rows_cap = pf->send_cap;
   rb.C = pf->C;
   rb.dlo = pf->dlo;
+  if (c->peer) {  // records from the mailboxes (sums), rows straight into the receivers' buffers
+    if (sums) {
+      rb.pb = peer_box(c);
+      rb.use_rec = c->use_rec;
+      rb.amax_reset = shards;
+    }
+    rb.peer_rows = 1;
+    for (int r = 0; r < R; ++r) rb.prow[r] = pf->prow[r];
+    rb.rows_cap = INT64_MAX;
+  }
   launch_rank_b(pf, rb);
   HIP_TRY(hipGetLastError());
-  // the row exchange (R > 1) starts on the side stream once k_rank_b packed the rows
-  if (R > 1) HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
+  if (c->peer) {
+    // every rank tags every other rank's row buffer once its rows are in
+    // (fired or not: the tags count the exchanges); finish_plan waits
+    if (R > 1) {
+      PeerRowTags pt{};
+      for (int r = 0; r < R; ++r) pt.tag[r] = pf->ptag[r];
+      pt.R = R;
+      pt.rank = q;
+      hipLaunchKernelGGL(k_peer_signal, dim3(1), dim3(64), 0, pf->s, pt, ++pf->row_use);
+      HIP_TRY(hipGetLastError());
+    }
+  } else if (R > 1) {
+    // the row exchange starts on the side stream once k_rank_b packed the rows
+    HIP_TRY(hipEventRecord(pf->ev_rb, pf->s));
+  }
   if (!sums) {  // the decision and the totals, read on the side stream while k_rank_b runs
     HIP_TRY(hipStreamWaitEvent(pf->aux, pf->ev_tot, 0));
     HIP_TRY(hipMemcpyAsync(pf->h_plan, &pf->dev->fire, sizeof(int), hipMemcpyDeviceToHost, pf->aux));
@@ -1823,6 +2027,16 @@ static int finish_plan(gh_pf* pf) {
   auto clamp_own = [&](int64_t v) { return v < own_lo ? own_lo : (v > own_hi ? own_hi : v); };
   pf->rem_ra = clamp_own(sys_count_host(base, N, S, o)) - own_lo;
   pf->rem_rb = clamp_own(sys_count_host(base + tot[q], N, S, o)) - own_lo;
+  if (c->peer) {
+    // the senders' k_rank_b stored the rows here; part 2 of the step reads
+    // them behind this wait (on the filter's stream, after part 1)
+    if (R > 1) {
+      hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, pf->s, (const uint64_t*)pf->ptag[q], R, q, pf->row_use,
+                         &pf->dev->error);
+      HIP_TRY(hipGetLastError());
+    }
+    return GH_OK;
+  }
   std::vector<int64_t> slo(R), shi(R), rlo(R), rhi(R);
   sys_plan(pf->n_global, R, q, tot, o, slo.data(), shi.data(), rlo.data(), rhi.data());
   int64_t n_send = 0;
@@ -1986,7 +2200,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   if (multi) {
     hipLaunchKernelGGL(k_rank_total, dim3(1), dim3(kBlock), 0, pf->s, g.gate, pf->bsum, n > 0 ? pf->nb_scan : 0,
                        pf->dev);
-    CHECK(comm_allgather(pf->ctx, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s));
+    CHECK(comm_allgather(pf->ctx, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s, &pf->dev->error));
   }
   int32_t* anc_target = anc_for_step(pf, t + 1);
   const bool sys1 = !multi && pf->opts.resampler == GH_RESAMPLE_SYSTEMATIC;
@@ -2168,16 +2382,151 @@ extern "C" int gh_pf_get_log_weights(gh_pf* pf, double* out) {
   return GH_OK;
 }
 
+// ------------------------------------------- multi-rank genealogy queries
+// (kernels in gh_kernels.h "multi-rank genealogy").  Collective:
+// every rank calls the same query.  Cursors = the global ids of this rank's
+// particles' ancestors at the step the walk has reached.
+struct DBuf {
+  void* p = nullptr;
+  ~DBuf() {
+    if (p) hipFree(p);
+  }
+  template <class T>
+  T* as() const {
+    return (T*)p;
+  }
+};
+static int dalloc(DBuf& b, size_t bytes) {
+  if (hipMalloc(&b.p, bytes ? bytes : 8) != hipSuccess) return set_err(GH_E_NOMEM, "genealogy query: %zu bytes", bytes);
+  return GH_OK;
+}
+
+struct MrWalk {
+  gh_pf* pf = nullptr;
+  int64_t n = 0, N = 0, pad = 0;
+  int R = 1;
+  std::vector<int32_t> res;  // res[s]: a resample preceded step s
+  DBuf cur, gp, gp_all;
+};
+
+static const double* rh_of(const gh_pf* pf, int s) {
+  return s >= 1 && s - 1 < (int)pf->rh_step.size() ? pf->rh_step[s - 1] : nullptr;
+}
+
+static int mr_walk_begin(gh_pf* pf, MrWalk& w) {
+  CHECK(materialize_marks(pf));
+  w.pf = pf;
+  w.n = pf->n;
+  w.N = pf->n_global;
+  w.R = pf->ctx->world;
+  w.pad = (w.N + w.R - 1) / w.R;
+  w.res.assign(pf->cap + 2, 0);
+  CHECK(d2h(pf, w.res.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2)));
+  DevScalars h;
+  CHECK(d2h(pf, &h, pf->dev, sizeof h));
+  if (h.error) return set_err(h.error, dev_error_msg(h.error));
+  CHECK(dalloc(w.cur, sizeof(int64_t) * (size_t)w.n));
+  CHECK(dalloc(w.gp, sizeof(int64_t) * (size_t)w.pad));
+  CHECK(dalloc(w.gp_all, sizeof(int64_t) * (size_t)w.pad * w.R));
+  const dim3 grid((unsigned)((w.n + kBlock - 1) / kBlock));
+  if (flags_live(pf) && (h.pending | h.fire) && pf->cap >= pf->t + 1) {
+    // a resample pending after the last step: the particles are its copies,
+    // slot j's parent (local, or a row received for the next step)
+    hipLaunchKernelGGL(k_mr_gparents, grid, dim3(kBlock), 0, pf->s, (const int32_t*)anc_for_step(pf, pf->t + 1), w.n,
+                       pf->lo, (const double*)pf->rows_recv, pf->D, w.cur.as<int64_t>());
+  } else {
+    hipLaunchKernelGGL(k_iota64, grid, dim3(kBlock), 0, pf->s, w.cur.as<int64_t>(), w.n, pf->lo);
+  }
+  HIP_TRY(hipGetLastError());
+  return GH_OK;
+}
+
+// every cursor from step s back to step s - 1
+static int mr_walk_back(MrWalk& w, int s) {
+  gh_pf* pf = w.pf;
+  if (!w.res[s]) return GH_OK;
+  const dim3 grid((unsigned)((w.n + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL(k_mr_gparents, grid, dim3(kBlock), 0, pf->s, (const int32_t*)anc_for_step(pf, s), w.n, pf->lo,
+                     rh_of(pf, s), pf->D, w.gp.as<int64_t>());
+  HIP_TRY(hipGetLastError());
+  CHECK(bulk_allgather(pf->ctx, w.gp.p, w.gp_all.p, sizeof(int64_t) * (size_t)w.pad, pf->s));
+  hipLaunchKernelGGL(k_mr_back, grid, dim3(kBlock), 0, pf->s, w.cur.as<int64_t>(), w.n,
+                     (const int64_t*)w.gp_all.as<int64_t>(), (const int64_t*)pf->dlo, w.R, w.N, w.pad);
+  HIP_TRY(hipGetLastError());
+  return GH_OK;
+}
+
+// get_traces at step t on R ranks: the states of this rank's particles' ancestors, [D][n] on the device
+static int mr_trajectory(gh_pf* pf, int t, double* dout) {
+  MrWalk w;
+  CHECK(mr_walk_begin(pf, w));
+  for (int s = pf->t; s > t; --s) CHECK(mr_walk_back(w, s));
+  const int64_t pad_d = slot_doubles(w.pad, pf->D);
+  DBuf send, slab;
+  CHECK(dalloc(send, sizeof(double) * (size_t)pad_d));
+  CHECK(dalloc(slab, sizeof(double) * (size_t)pad_d * w.R));
+  HIP_TRY(hipMemsetAsync(send.p, 0, sizeof(double) * (size_t)pad_d, pf->s));
+  HIP_TRY(hipMemcpyAsync(send.p, slot_x(pf, t), sizeof(double) * (size_t)slot_doubles(w.n, pf->D),
+                         hipMemcpyDeviceToDevice, pf->s));
+  CHECK(bulk_allgather(pf->ctx, send.p, slab.p, sizeof(double) * (size_t)pad_d, pf->s));
+  hipLaunchKernelGGL(k_mr_states, dim3((unsigned)((w.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s,
+                     (const int64_t*)w.cur.as<int64_t>(), w.n, (const double*)slab.as<double>(), pad_d,
+                     (const int64_t*)pf->dlo, w.R, w.N, pf->D, dout);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  return GH_OK;
+}
+
+// the score columns on R ranks (k_scores' values): per step, every rank
+// scores its own slots, the ranks all-gather them, each cursor takes its
+// slot's pair, then the cursors step back
+static int mr_scores(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& obs, double* dtot, double* dper) {
+  MrWalk w;
+  CHECK(mr_walk_begin(pf, w));
+  const int T = pf->t;
+  const int64_t n = w.n;
+  DBuf sc, sc_all;
+  CHECK(dalloc(sc, sizeof(double) * 2 * (size_t)w.pad));
+  CHECK(dalloc(sc_all, sizeof(double) * 2 * (size_t)w.pad * w.R));
+  HIP_TRY(hipMemsetAsync(sc.p, 0, sizeof(double) * 2 * (size_t)w.pad, pf->s));
+  const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+  for (int s = T; s >= 1; --s) {
+    const int32_t* anc = s > 1 && w.res[s] ? anc_for_step(pf, s) : nullptr;
+    CHECK(with_model(m, [&](auto model, const auto& p) {
+      hipLaunchKernelGGL(k_mr_slot_scores<decltype(model)>, grid, dim3(kBlock), 0, pf->s, (const double*)m->dparams,
+                         p, obs[s - 1], s, (const double*)slot_x(pf, s),
+                         (const double*)(s > 1 ? slot_x(pf, s - 1) : nullptr), anc, rh_of(pf, s), n, w.pad,
+                         sc.as<double>());
+    }));
+    HIP_TRY(hipGetLastError());
+    CHECK(bulk_allgather(pf->ctx, sc.p, sc_all.p, sizeof(double) * 2 * (size_t)w.pad, pf->s));
+    hipLaunchKernelGGL(k_mr_take_scores, grid, dim3(kBlock), 0, pf->s, (const int64_t*)w.cur.as<int64_t>(), n,
+                       (const double*)sc_all.as<double>(), (const int64_t*)pf->dlo, w.R, w.N, w.pad,
+                       dper + (int64_t)(s - 1) * 2 * n, dper + ((int64_t)(s - 1) * 2 + 1) * n);
+    HIP_TRY(hipGetLastError());
+    if (s > 1) CHECK(mr_walk_back(w, s));
+  }
+  hipLaunchKernelGGL(k_score_total, grid, dim3(kBlock), 0, pf->s, (const double*)dper, T, n, dtot);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  return GH_OK;
+}
+
 extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
   if (!pf || !out) return set_err(GH_E_INVAL, "null argument");
   CHECK(materialize_marks(pf));
   if (t < 1 || t > pf->t) return set_err(GH_E_INVAL, "step %d outside 1..%d", t, pf->t);
   if (!pf->opts.record_history && t != pf->t)
     return set_err(GH_E_STATE, "record_history is off: only the current step is kept");
-  if (mr(pf->ctx) && t != pf->t)
-    return set_err(GH_E_STATE, "multi-rank: trajectories before the current step are not materialised");
   const int64_t n = pf->n;
   if (n == 0) return GH_OK;
+  if (mr(pf->ctx)) {  // collective: the walk crosses ranks
+    DBuf d;
+    CHECK(dalloc(d, sizeof(double) * pf->D * (size_t)n));
+    CHECK(mr_trajectory(pf, t, d.as<double>()));
+    HIP_TRY(hipMemcpy(out, d.p, sizeof(double) * pf->D * (size_t)n, hipMemcpyDeviceToHost));
+    return GH_OK;
+  }
   double* dout = nullptr;
   const double** dxs = nullptr;
   const int32_t** dancs = nullptr;
@@ -2219,7 +2568,10 @@ extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
 // The trace score columns of every current particle (k_scores: the genealogy
 // walk) under model m and the steps' observations obs[0..T): dtot[n] and the
 // per-step scratch/output dper[T][2][n], device buffers, on the filter's stream.
+static int mr_scores(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& obs, double* dtot, double* dper);
+
 static int scores_dev(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& obs, double* dtot, double* dper) {
+  if (mr(pf->ctx)) return mr_scores(pf, m, obs, dtot, dper);
   const int T = pf->t;
   const int64_t n = pf->n;
   const double** dxs = nullptr;
@@ -2276,8 +2628,6 @@ static int scores_ready(gh_pf* pf, const char* who) {
   const int T = pf->t;
   if (T < 1) return set_err(GH_E_STATE, "%s before init", who);
   if (!pf->opts.record_history && T > 1) return set_err(GH_E_STATE, "%s needs record_history", who);
-  if (mr(pf->ctx) && T > 1)
-    return set_err(GH_E_STATE, "multi-rank: the genealogy before the current step is not materialised");
   if ((int)pf->obs_hist.size() < T) return set_err(GH_E_STATE, "internal: observation history");
   return GH_OK;
 }
@@ -2335,7 +2685,6 @@ extern "C" int gh_pf_step_params_conditional(gh_pf* pf, const gh_obs* obs, gh_mo
 }
 
 static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm, const double* pin_ref) {
-  if (mr(pf->ctx)) return set_err(GH_E_STATE, "gh_pf_step_params: one rank (the re-scoring walks the genealogy)");
   if (!pf->opts.record_history) return set_err(GH_E_STATE, "gh_pf_step_params needs record_history");
   const gh_model* m = pf->m;
   if (nm->ctx != m->ctx || nm->family != m->family || nm->d != m->d || nm->dy != m->dy || nm->k != m->k ||
@@ -2397,6 +2746,11 @@ static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model
     pf->stats_valid = false;
     pf->max_only = false;
     pf->amax_valid = false;
+    if (mr(pf->ctx) && !rc) {  // the rank's (M, S, S2) of the changed weights, shared again
+      hipLaunchKernelGGL(k_fold, dim3(1), dim3(1024), 0, pf->s, pf->pm, pf->ps, pf->ps2, (int)pf->nb_part,
+                         pf->dev->stats, pf->dev, 1, 0.0, pf->n_global);
+      rc = share_stats(pf);
+    }
   }
   if (hipStreamSynchronize(pf->s) != hipSuccess && !rc) rc = set_err(GH_E_HIP, "gh_pf_step_params: sync");
   cleanup();
@@ -2836,52 +3190,86 @@ extern "C" int gh_pf_get_ess_history(gh_pf* pf, int max_steps, double* ess, int3
 
 extern "C" int gh_pf_sample_unweighted(gh_pf* pf, int64_t ns, uint64_t seed, int64_t* idx) {
   if (!pf || !idx || ns < 0) return set_err(GH_E_INVAL, "bad argument");
-  if (mr(pf->ctx)) return set_err(GH_E_STATE, "sample_unweighted: single rank only");
   if (ns == 0) return GH_OK;
   const int64_t n = pf->n;
+  const bool multi = mr(pf->ctx);
+  const int R = pf->ctx->world;
   CHECK(ensure_stats(pf));
-  hipLaunchKernelGGL(k_prep_sample, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, 1, flags_live(pf));
+  hipLaunchKernelGGL(k_prep_sample, dim3(1), dim3(64), 0, pf->s, pf->dev, pf->stats_all, R, flags_live(pf));
   GateArgs g;
   g.gate = &pf->dev->one;
   g.M = &pf->dev->sM;
   g.zero_w = &pf->dev->spend;
-  g.shift = quant_shift((uint64_t)n);
+  g.shift = quant_shift((uint64_t)pf->n_global);
   CHECK(materialize_marks(pf));
   DecideArgs d{};
   hipLaunchKernelGGL(k_qsum, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, pf->bsum, 0, d,
                      pf->dev);
+  if (multi) {  // the global integer CDF: every rank's total (one word each)
+    hipLaunchKernelGGL(k_rank_total, dim3(1), dim3(kBlock), 0, pf->s, g.gate, pf->bsum, pf->nb_scan, pf->dev);
+    CHECK(comm_allgather(pf->ctx, &pf->dev->local, pf->totals_all, sizeof(uint64_t), pf->s, &pf->dev->error));
+  }
   MarkArgs mk{};
   CdfArgs ca{};
   ca.bsum = pf->bsum;
   ca.nb = pf->nb_scan;
-  ca.R = 1;
-  ca.n_global = n;
+  ca.totals = multi ? pf->totals_all : nullptr;
+  ca.R = R;
+  ca.rank = pf->ctx->rank;
+  ca.n_global = pf->n_global;
   ca.seed = seed;
   ca.t = (uint32_t)pf->t;
   ca.stream = STREAM_SAMPLE;
   hipLaunchKernelGGL(k_cdf, dim3((unsigned)pf->nb_scan), dim3(kBlock), 0, pf->s, pf->logw, n, g, ca, pf->dev, pf->C,
                      mk);
   int32_t* dout = nullptr;
-  HIP_TRY(hipMalloc(&dout, sizeof(int32_t) * ns));
+  HIP_TRY(hipMalloc(&dout, sizeof(int32_t) * (ns + 1)));
   SearchArgs sa{};
   sa.C = pf->C;
   sa.n_cdf = n;
   sa.n_slots = ns;
   sa.slot_lo = 0;
-  sa.n_global = n;
+  sa.n_global = pf->n_global;
   sa.seed = seed;
   sa.t = (uint32_t)pf->t;
   sa.mode = SEARCH_SAMPLE;
   sa.anc_old = nullptr;
   sa.anc_out = dout;
+  sa.own_only = multi ? 1 : 0;  // each target is searched by the rank whose CDF range holds it
   hipLaunchKernelGGL(k_search, dim3((unsigned)((ns + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s, sa, g,
                      pf->dev);
   HIP_TRY(hipGetLastError());
-  std::vector<int32_t> h(ns);
-  HIP_TRY(hipMemcpyAsync(h.data(), dout, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, pf->s));
-  HIP_TRY(hipStreamSynchronize(pf->s));
+  if (!multi) {
+    std::vector<int32_t> h(ns);
+    HIP_TRY(hipMemcpyAsync(h.data(), dout, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, pf->s));
+    HIP_TRY(hipStreamSynchronize(pf->s));
+    hipFree(dout);
+    for (int64_t i = 0; i < ns; ++i) idx[i] = h[i];
+    return GH_OK;
+  }
+  // every rank's answers (local index, -1 where another rank's range held the
+  // target), all-gathered: each sample is the global id one rank found
+  const size_t bytes = (sizeof(int32_t) * (size_t)ns + 7) & ~(size_t)7;
+  DBuf all;
+  int rc = dalloc(all, bytes * (size_t)R);
+  if (!rc) rc = bulk_allgather(pf->ctx, dout, all.p, bytes, pf->s);
   hipFree(dout);
-  for (int64_t i = 0; i < ns; ++i) idx[i] = h[i];
+  CHECK(rc);
+  std::vector<int32_t> h(bytes / sizeof(int32_t) * (size_t)R);
+  HIP_TRY(hipMemcpy(h.data(), all.p, bytes * (size_t)R, hipMemcpyDeviceToHost));
+  DevScalars hs;
+  CHECK(d2h(pf, &hs, pf->dev, sizeof hs));
+  if (hs.error) return set_err(hs.error, dev_error_msg(hs.error));
+  const size_t stride = bytes / sizeof(int32_t);
+  for (int64_t i = 0; i < ns; ++i) {
+    idx[i] = -1;
+    for (int r = 0; r < R; ++r)
+      if (h[(size_t)r * stride + i] >= 0) {
+        idx[i] = split_lo(pf->n_global, r, R) + h[(size_t)r * stride + i];
+        break;
+      }
+    if (idx[i] < 0) return set_err(GH_E_STATE, "sample_unweighted: sample %lld found by no rank", (long long)i);
+  }
   return GH_OK;
 }
 
@@ -2981,6 +3369,9 @@ extern "C" int gh_debug_exchange_lists(int64_t n_global, int world, int rank, co
 }
 
 static int exchange_states(gh_pf* pf, int32_t* anc_out) {
+  if (pf->ctx->peer)
+    return set_err(GH_E_STATE, "peer transport: this resample needs the fused multi-rank kernels (systematic, "
+                               "at most %d ranks, co-resident tiles)", kMaxRanks);
   gh_ctx* c = pf->ctx;
   const int R = c->world, q = c->rank;
   const int D = pf->D;

@@ -113,6 +113,11 @@ struct StepArgs {
   // (vb_skip = 0: every block its own)
   int64_t vb_split, vb_skip;
   int64_t grid_blocks;   // host only: the launch's blocks when nonzero
+  // part 2 (record_history): every received row used here is also kept,
+  // row-indexed (D components + global id), as this step's genealogy record of
+  // the parents that lived on other ranks (rows_recv is overwritten by the
+  // next resample); nullptr: not kept
+  double* rhist;
 };
 
 // ------------------------------------------------------------ reductions
@@ -234,6 +239,18 @@ __device__ __forceinline__ T ld_sc1(T* p) {
 template <class T>
 __device__ __forceinline__ void st_sc1(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// system-scope accesses: the stores write through to memory, the loads
+// bypass the caches (the words may be written by other processes' kernels: the peer
+// transport's mailboxes and received rows)
+template <class T>
+__device__ __forceinline__ T ld_sys(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <class T>
+__device__ __forceinline__ void st_sys(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ------------------------------------------------------- buffer accesses
@@ -419,7 +436,13 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
           const bool loc = src >= 0;
 #pragma unroll
           for (int k = 0; k < D; ++k)
-            xp[k] = loc ? a.xprev[xidx(src, k, D)] : a.remote[(-1 - src) * a.ld_remote + k];
+            xp[k] = loc ? a.xprev[xidx(src, k, D)] : ld_sys(&a.remote[(-1 - src) * a.ld_remote + k]);
+          if (SPLIT && !loc && a.rhist) {  // the parent's row, kept for the genealogy
+            double* h = a.rhist + (-1 - src) * (int64_t)(D + 1);
+#pragma unroll
+            for (int k = 0; k < D; ++k) h[k] = xp[k];
+            h[D] = ld_sys(&a.remote[(-1 - src) * a.ld_remote + D]);
+          }
         }
         const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x, dr_step);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
@@ -552,8 +575,18 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
         if (a.remote) {  // uniform (multi-rank): a negative ancestor is row -1 - s of the receive buffer
           skip0 = a.part == 1 && s0 < 0;
           skip1 = a.part == 1 && s1 < 0;
-          xp0 = s0 >= 0 ? a.xprev[s0] : (skip0 ? 0.0 : a.remote[(-1 - s0) * a.ld_remote]);
-          xp1 = s1 >= 0 ? a.xprev[s1] : (skip1 ? 0.0 : a.remote[(-1 - s1) * a.ld_remote]);
+          xp0 = s0 >= 0 ? a.xprev[s0] : (skip0 ? 0.0 : ld_sys(&a.remote[(-1 - s0) * a.ld_remote]));
+          xp1 = s1 >= 0 ? a.xprev[s1] : (skip1 ? 0.0 : ld_sys(&a.remote[(-1 - s1) * a.ld_remote]));
+          if (SPLIT && a.rhist) {  // received parents' rows, kept for the genealogy
+            if (s0 < 0) {
+              a.rhist[(-1 - s0) * 2] = xp0;
+              a.rhist[(-1 - s0) * 2 + 1] = ld_sys(&a.remote[(-1 - s0) * a.ld_remote + 1]);
+            }
+            if (has1 && s1 < 0) {
+              a.rhist[(-1 - s1) * 2] = xp1;
+              a.rhist[(-1 - s1) * 2 + 1] = ld_sys(&a.remote[(-1 - s1) * a.ld_remote + 1]);
+            }
+          }
         } else {
           xp0 = a.xprev[s0];
           xp1 = a.xprev[s1];
@@ -1778,6 +1811,63 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
 // decision is taken from the R records by k_rank_b (and by the host, the same
 // arithmetic, for the split of the next step).
 constexpr int kRecWords = 4;  // rank record: integer total, S_r, S2_r (f64 bits), M (f64 bits)
+// ---------------------------------------------- peer transport primitives
+// (gh_peer.h: the transport's design; gh_ctx_create_peer)
+constexpr int kAgWords = 8;  // largest small all-gather payload (u64 words)
+constexpr int kPeerMaxRanks = 64;
+
+// mailbox layout (u64 words), for R ranks
+__host__ __device__ __forceinline__ int64_t mb_sh(int R, int par, int r) { return (int64_t)par * R + r; }
+__host__ __device__ __forceinline__ int64_t mb_sh_tag(int R, int par, int r) { return 2LL * R + (int64_t)par * R + r; }
+__host__ __device__ __forceinline__ int64_t mb_rec(int R, int par, int r) {
+  return 4LL * R + ((int64_t)par * R + r) * kRecWords;
+}
+__host__ __device__ __forceinline__ int64_t mb_rec_tag(int R, int par, int r) {
+  return 4LL * R + 2LL * R * kRecWords + (int64_t)par * R + r;
+}
+__host__ __device__ __forceinline__ int64_t mb_ag(int R, int par, int r) {
+  return 6LL * R + 2LL * R * kRecWords + ((int64_t)par * R + r) * kAgWords;
+}
+__host__ __device__ __forceinline__ int64_t mb_ag_tag(int R, int par, int r) {
+  return 6LL * R + 2LL * R * kRecWords + 2LL * R * kAgWords + (int64_t)par * R + r;
+}
+__host__ __device__ __forceinline__ int64_t mb_words(int R) { return 8LL * R + 2LL * R * kRecWords + 2LL * R * kAgWords; }
+
+// every rank's mailbox, as this process maps it (peer[rank] is its own)
+struct PeerBox {
+  uint64_t* peer[kPeerMaxRanks];
+  int R, rank;
+};
+
+
+constexpr unsigned kPeerSpins = 1u << 22;  // ~0.3 s of polling, then GH_E_STATE
+
+// Wave-level poll: lanes r < R wait until word (base + stride * r) of the own
+// mailbox reaches `want` (monotonic tags).  Returns false on timeout.
+__device__ __forceinline__ bool peer_poll(const uint64_t* own, int64_t base, int R, uint64_t want, int skip = -1) {
+  const int lane = threadIdx.x & 63;
+  bool ok = lane >= R || lane == skip;
+  for (unsigned spins = 0;; ++spins) {
+    if (!ok) ok = ld_sys(own + base + lane) >= want;
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) return true;
+    if (spins == kPeerSpins) return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Publish `words` u64 values (lane l holds value l; lanes < words) to slot
+// `slot` of every rank's mailbox, then the tag at `tag` behind a system-scope
+// release.  One whole wave calls it.
+__device__ __forceinline__ void peer_publish(const PeerBox& pb, int64_t slot, int64_t tag, uint64_t lane_val,
+                                             int words, uint64_t use) {
+  const int lane = threadIdx.x & 63;
+  for (int q = 0; q < pb.R; ++q)
+    if (lane < words) st_sys(pb.peer[q] + slot + lane, lane_val);
+  __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane < pb.R) st_sys(pb.peer[lane] + tag, use);
+}
+
 struct RankA2Args {
   const double* logw;
   int64_t n;
@@ -1790,6 +1880,14 @@ struct RankA2Args {
   uint64_t* ts1;             // [grid] tile sums of e, e^2 (tagged bits)
   uint64_t* ts2;
   uint64_t* rec;             // [kRecWords] this rank's record (input of the second all-gather)
+  // peer transport (pb.R > 0): no all-gathers — every block folds this rank's
+  // own shards (amax_own), block 0 publishes the rank maximum to every
+  // mailbox (SH, use_sh), every block polls its own for all R; at the end
+  // block 0 publishes the record (REC, use_rec) for k_rank_b.  The shards are
+  // then emptied by k_rank_b (every block of this launch reads them).
+  PeerBox pb;
+  const uint64_t* amax_own;
+  uint64_t use_sh, use_rec;
 };
 
 template <int IT>
@@ -1808,22 +1906,58 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_a2(RankA2Arg
   double lw[IT];
 #pragma unroll
   for (int k = 0; k < IT; ++k) lw[k] = (i0 + k < r.n) ? r.logw[i0 + k] : -INFINITY;
-  // the global max from every rank's shards (the same keys, the same M in every block)
-  uint64_t key = kAmaxEmpty;
-  for (int idx = threadIdx.x; idx < r.R * kAmaxShards; idx += kRsBlock) {
-    const uint64_t v = r.amax_all[(idx / kAmaxShards) * (kAmaxShards * kAmaxStride) + (idx % kAmaxShards) * kAmaxStride];
-    key = v > key ? v : key;
+  const bool peer = r.pb.R > 0;  // (uniform)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ uint64_t srec[kRecWords];
+  double M;
+  if (!peer) {
+    // the global max from every rank's shards (the same keys, the same M in every block)
+    uint64_t key = kAmaxEmpty;
+    for (int idx = threadIdx.x; idx < r.R * kAmaxShards; idx += kRsBlock) {
+      const uint64_t v = r.amax_all[(idx / kAmaxShards) * (kAmaxShards * kAmaxStride) + (idx % kAmaxShards) * kAmaxStride];
+      key = v > key ? v : key;
+    }
+    M = blk16_max1(amax_value(key), smd);
+    if (blockIdx.x == 0 && threadIdx.x < kAmaxShards) r.amax_reset[threadIdx.x * kAmaxStride] = kAmaxEmpty;
+  } else {
+    // this rank's maximum (every block the same), then the R ranks' through the mailboxes
+    const uint64_t k0 = threadIdx.x < kAmaxShards ? r.amax_own[threadIdx.x * kAmaxStride] : kAmaxEmpty;
+    const double Ml = blk16_max1(amax_value(k0), smd);
+    __shared__ double sM;
+    if (w == 0) {
+      const int par = (int)(r.use_sh & 1);
+      const uint64_t* own = r.pb.peer[r.pb.rank];
+      if (blockIdx.x == 0)
+        peer_publish(r.pb, mb_sh(r.pb.R, par, r.pb.rank), mb_sh_tag(r.pb.R, par, r.pb.rank), amax_key(Ml), 1, r.use_sh);
+      const bool ok = peer_poll(own, mb_sh_tag(r.pb.R, par, 0), r.pb.R, r.use_sh);
+      uint64_t kk = ok && lane < r.pb.R ? ld_sys(own + mb_sh(r.pb.R, par, lane)) : kAmaxEmpty;
+      kk = readlane63_u64(wave_incl_max_u64(kk));
+      if (lane == 0) {
+        sM = ok ? amax_value(kk) : NAN;
+        if (!ok) {
+          sfail = 1;
+          r.dev->error = 7;  // GH_E_STATE: a rank never published
+        }
+      }
+    }
+    lds_barrier();
+    M = sM;
   }
-  const double M = blk16_max1(amax_value(key), smd);
-  if (blockIdx.x == 0 && threadIdx.x < kAmaxShards) r.amax_reset[threadIdx.x * kAmaxStride] = kAmaxEmpty;
   const bool m_ok = M > -INFINITY && M != INFINITY && M == M;
   if (!m_ok) {  // uniform over every rank's grid: no tile publishes; the decision raises GH_E_NUMERIC
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      r.rec[0] = 0;
-      r.rec[1] = 0;
-      r.rec[2] = 0;
-      r.rec[3] = as_u64(M);
-      r.dev->local = 0;
+    if (blockIdx.x == 0) {
+      if (threadIdx.x == 0) {
+        r.rec[0] = 0;
+        r.rec[1] = 0;
+        r.rec[2] = 0;
+        r.rec[3] = as_u64(M);
+        r.dev->local = 0;
+      }
+      if (peer && w == 0) {
+        const int par = (int)(r.use_rec & 1);
+        const uint64_t v = lane == 3 ? as_u64(M) : 0ull;
+        peer_publish(r.pb, mb_rec(r.pb.R, par, r.pb.rank), mb_rec_tag(r.pb.R, par, r.pb.rank), v, kRecWords, r.use_rec);
+      }
     }
     return;
   }
@@ -1849,7 +1983,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_a2(RankA2Arg
   }
   if (blockIdx.x != 0) return;
   // block 0: the rank totals (waves 0..7 poll 64 tiles each, as k_resample1)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (w < 8) {
     const unsigned b = (unsigned)(w * 64 + lane);
     const bool mine = b < gridDim.x;
@@ -1897,8 +2030,20 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_a2(RankA2Arg
     r.rec[1] = as_u64(g1);
     r.rec[2] = as_u64(g2);
     r.rec[3] = as_u64(M);
+    srec[0] = all;
+    srec[1] = as_u64(g1);
+    srec[2] = as_u64(g2);
+    srec[3] = as_u64(M);
     r.dev->local = all;
     r.dev->bar_gen = sgen;  // every block has published, so has read the old value
+  }
+  if (peer) {  // the record to every rank's mailbox (k_rank_b polls for all R)
+    lds_barrier();
+    if (w == 0) {
+      const int par = (int)(r.use_rec & 1);
+      peer_publish(r.pb, mb_rec(r.pb.R, par, r.pb.rank), mb_rec_tag(r.pb.R, par, r.pb.rank),
+                   lane < kRecWords ? srec[lane] : 0ull, kRecWords, r.use_rec);
+    }
   }
 }
 
@@ -1957,6 +2102,15 @@ struct RankBArgs {
   double* rows;           // send rows [(D+1)] per slot
   int64_t rows_cap;
   uint64_t* C;            // more rows than rows_cap: the inclusive CDF, for k_rows_fill
+  // peer transport (pb.R > 0): the records come from the own mailbox (REC,
+  // use_rec; every block polls), the rows go straight into every receiving
+  // rank's row buffer prow[k] at the row its slot takes there, and block 0
+  // empties the shards k_rank_a2 read (amax_reset)
+  PeerBox pb;
+  uint64_t use_rec;
+  int peer_rows;          // the rows go to prow (peer transport, either resample form)
+  double* prow[kPeerMaxRanks];
+  uint64_t* amax_reset;
 };
 
 // The send layout of one rank's resample (as gh_sys_plan): destination rank k
@@ -2003,6 +2157,28 @@ __device__ __forceinline__ void send_rows(int64_t s0, int64_t s1, int64_t i, int
   }
 }
 
+// the same rows written into the receivers' own buffers (peer transport):
+// rank k's slot j (local) takes row j below ra_k and ra_k + j - rb_k from rb_k
+__device__ __forceinline__ void send_rows_peer(int64_t s0, int64_t s1, int64_t i, int64_t own_lo, int64_t own_hi,
+                                               int R, uint64_t N, const int64_t* dst_lo, const int64_t* ra,
+                                               const int64_t* rb, double* const* prow, const double* xprev, int D,
+                                               int64_t lo) {
+  for (int64_t sl = s0; sl < s1; ++sl) {
+    if (sl >= own_lo && sl < own_hi) {
+      sl = own_hi - 1;  // skip the own block
+      continue;
+    }
+    int dst = (int)(((__int128)sl * R) / (int64_t)N);  // owner of global slot sl
+    while (dst + 1 < R && dst_lo[dst + 1] <= sl) ++dst;
+    while (dst > 0 && dst_lo[dst] > sl) --dst;
+    const int64_t j = sl - dst_lo[dst];
+    const int64_t row = j < ra[dst] ? j : ra[dst] + (j - rb[dst]);
+    double* rw = prow[dst] + row * (D + 1);
+    for (int c = 0; c < D; ++c) st_sys(rw + c, xprev[xidx(i, c, D)]);
+    st_sys(rw + D, __longlong_as_double(lo + i));
+  }
+}
+
 template <int IT>
 __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ int sfire;
@@ -2020,16 +2196,36 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     const u32x4 w = rng_block(r.seed, ~0ull, r.t, STREAM_RESAMPLE, 0);
     su53 = u53_bits(w.x, w.y);
   }
+  // peer transport: the R records from the own mailbox (wave 0 polls, LDS copy)
+  const bool peer = r.pb.R > 0;  // (uniform)
+  __shared__ uint64_t srecs[kPeerMaxRanks * kRecWords];
+  const uint64_t* recs = r.recs;
+  const uint64_t* totals = r.totals;
+  if (peer) {
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x & 63, par = (int)(r.use_rec & 1);
+      const uint64_t* own = r.pb.peer[r.pb.rank];
+      const bool ok = peer_poll(own, mb_rec_tag(r.pb.R, par, 0), r.pb.R, r.use_rec);
+      if (lane < r.pb.R)
+        for (int k = 0; k < kRecWords; ++k)
+          srecs[lane * kRecWords + k] = ok ? ld_sys(own + mb_rec(r.pb.R, par, lane) + k) : (k == 3 ? as_u64(NAN) : 0ull);
+      if (!ok && lane == 0) r.dev->error = 7;  // GH_E_STATE: a rank never published its record
+      if (blockIdx.x == 0 && lane < kAmaxShards) r.amax_reset[lane * kAmaxStride] = kAmaxEmpty;
+    }
+    lds_barrier();
+    recs = srecs;
+    totals = srecs;
+  }
   if (threadIdx.x == 0) {
-    if (r.recs) {  // the decision from the R rank records (every block the same)
-      const Decision dec = decide_records(r.recs, r.R, r.d.thr);
+    if (recs) {  // the decision from the R rank records (every block the same)
+      const Decision dec = decide_records(recs, r.R, r.d.thr);
       sfire = dec.fire;
       sMq = dec.M;
       if (blockIdx.x == 0) {
         r.dev->pending = 0;
         commit_decision(r.d, dec, r.dev, 0);
         if (r.hplan) {  // the host's copy of the records, then the tag behind a system-scope release
-          for (int w = 0; w < r.R * kRecWords; ++w) r.hplan[1 + w] = r.recs[w];
+          for (int w = 0; w < r.R * kRecWords; ++w) r.hplan[1 + w] = recs[w];
           __threadfence_system();
           __hip_atomic_store(&r.hplan[0], r.htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -2042,6 +2238,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   __shared__ uint64_t smu[16];
   __shared__ DevScalars sd;
   __shared__ int64_t sdst_lo[kMaxRanks], sseg_lo[kMaxRanks], ssoff[kMaxRanks];
+  __shared__ int64_t sra_all[kMaxRanks], srb_all[kMaxRanks];
   __shared__ int64_t sown_lo, sown_hi, sra, srb, ssend;
   __shared__ uint64_t sbase;
   const int R = r.R, q = r.rank;
@@ -2052,12 +2249,12 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   if (threadIdx.x == 0) {
     uint64_t S = 0, base = 0;
     for (int k = 0; k < R; ++k) {
-      if (k < q) base += r.totals[k * r.tot_stride];
-      S += r.totals[k * r.tot_stride];
+      if (k < q) base += totals[k * r.tot_stride];
+      S += totals[k * r.tot_stride];
     }
     sd.S = S;
     sd.base = base;
-    sd.local = r.totals[q * r.tot_stride];
+    sd.local = totals[q * r.tot_stride];
     sd.o = scale_u53(su53, S);
     sd.invN = r.d.inv_n;
     sd.Qs = udiv_n(S, N, sd.invN);
@@ -2075,6 +2272,17 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     sra = ca - own_lo;
     srb = cb - own_lo;
     sbase = base + before;
+    if (r.peer_rows) {  // every receiving rank's [0, ra) / [rb, n) split (its rows' layout)
+      uint64_t bk = 0;
+      for (int k = 0; k < R; ++k) {
+        const uint64_t tk = totals[k * r.tot_stride];
+        const int64_t dl = r.dlo[k], dh = r.dlo[k + 1];
+        const int64_t lo_k = sys_count_exact(&sd, N, bk), hi_k = sys_count_exact(&sd, N, bk + tk);
+        sra_all[k] = (lo_k < dl ? dl : (lo_k > dh ? dh : lo_k)) - dl;
+        srb_all[k] = (hi_k < dl ? dl : (hi_k > dh ? dh : hi_k)) - dl;
+        bk += tk;
+      }
+    }
     if (blockIdx.x == 0) {
       r.dev->S = S;
       r.dev->base = base;
@@ -2135,7 +2343,9 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     }
     if (spill && i < r.n) r.C[i] = run;
     // slots of other ranks: state rows, by destination then slot
-    if (!spill)
+    if (r.peer_rows)
+      send_rows_peer(s0, s1, i, own_lo, own_hi, R, N, sdst_lo, sra_all, srb_all, r.prow, r.xprev, r.D, r.lo);
+    else if (!spill)
       send_rows(s0, s1, i, own_lo, own_hi, R, N, sdst_lo, sseg_lo, ssoff, r.rows_cap, r.rows, r.xprev, r.D, r.lo);
     s0 = s1;
   }
@@ -2190,6 +2400,7 @@ struct SearchArgs {
   int mode;
   const int32_t* anc_old;  // compose when a resample is already pending
   int32_t* anc_out;
+  int own_only;            // multi-rank sampling: only the targets in this rank's CDF range (others: -1)
 };
 
 __device__ __forceinline__ uint64_t slot_target(const SearchArgs& s, const DevScalars* dev,
@@ -2229,7 +2440,9 @@ static __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t jc = j < s.n_slots ? j : s.n_slots - 1;  // clamp: padding lanes mirror the last slot
   const uint64_t base = dev->base;
-  const uint64_t target = slot_target(s, dev, s.slot_lo + jc) - base;
+  const uint64_t tg = slot_target(s, dev, s.slot_lo + jc);
+  const uint64_t target = tg - base;
+  const bool mine = !s.own_only || (tg >= base && target < dev->local);
   const int64_t hi_all = s.n_cdf - 1;
   int64_t a;
   if (s.mode == SEARCH_SYSTEMATIC) {
@@ -2256,7 +2469,7 @@ static __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs
       a = cdf_search(s.C, base, target, a_lo, a_hi);
     }
   } else {
-    a = cdf_search(s.C, base, target, 0, hi_all);
+    a = mine ? cdf_search(s.C, base, target, 0, hi_all) : -1;
   }
   if (j >= s.n_slots) return;
   const int zero = *g.zero_w;
@@ -2317,6 +2530,118 @@ static __global__ __launch_bounds__(kBlock) void k_traj(TrajArgs a, const DevSca
     if (a.res_before[s]) idx = a.ancs[s - 1][idx];
   const double* x = a.xs[a.t_target - 1];
   for (int k = 0; k < a.D; ++k) a.out[k * a.n + j] = x[xidx(idx, k, a.D)];
+}
+
+// ------------------------------------- multi-rank genealogy (queries only)
+// get_traces / the score columns / sample_unweighted_traces on R ranks
+// (particle_filter.jl:31-34, 62-70): the genealogy is kept where it was made —
+// each rank's per-step ancestors of its own slots (local index, or -1 - row of
+// the rows it received, whose global ids and states the step's part-2 launch
+// kept) — and a query walks it collectively: every step back, each rank turns
+// its slots' ancestors into global parent ids, the ranks all-gather them
+// (padded to `pad` per rank), and every cursor moves to its parent.  The
+// position of global particle c in such an all-gather is its owner's block
+// plus its local index.
+__device__ __forceinline__ int64_t mr_pos(int64_t c, const int64_t* dlo, int R, int64_t N, int64_t pad, int64_t* local) {
+  int r = (int)(((__int128)c * R) / N);
+  while (r + 1 < R && dlo[r + 1] <= c) ++r;
+  while (r > 0 && dlo[r] > c) --r;
+  *local = c - dlo[r];
+  return (int64_t)r * pad;
+}
+
+static __global__ void k_iota64(int64_t* out, int64_t n, int64_t lo) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < n) out[j] = lo + j;
+}
+
+// global parent ids of this rank's slots at one step (rows: the received rows
+// the slots' negative ancestors index; read at system scope: the peer
+// transport's row buffer is written by other processes)
+static __global__ void k_mr_gparents(const int32_t* anc, int64_t n, int64_t lo, const double* rows, int D,
+                                     int64_t* gp) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const int32_t a = anc[j];
+  gp[j] = a >= 0 ? lo + a : __double_as_longlong(ld_sys(&rows[(int64_t)(-1 - a) * (D + 1) + D]));
+}
+
+// every cursor one step back: cur = parent of the slot it names
+static __global__ void k_mr_back(int64_t* cur, int64_t n, const int64_t* gp_all, const int64_t* dlo, int R, int64_t N,
+                                 int64_t pad) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  int64_t i;
+  const int64_t b = mr_pos(cur[j], dlo, R, N, pad, &i);
+  cur[j] = gp_all[b + i];
+}
+
+// the cursors' states from an all-gather of every rank's (wave-tiled) slot,
+// rank r's at r * stride doubles: out[k * n + j]
+static __global__ void k_mr_states(const int64_t* cur, int64_t n, const double* slab, int64_t stride,
+                                   const int64_t* dlo, int R, int64_t N, int D, double* out) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  int64_t i;
+  const int64_t r = mr_pos(cur[j], dlo, R, N, 1, &i);
+  for (int k = 0; k < D; ++k) out[k * n + j] = slab[r * stride + xidx(i, k, D)];
+}
+
+// The score columns of this rank's slots at step s, as k_scores evaluates them
+// along a walk through the slot: Model::score of the slot's state given its
+// parent's (a local slot of step s - 1, a received row kept for step s, or the
+// slot itself when no resample preceded s; unused at s = 1).  Into the
+// all-gather's send block: lat at [0, pad), ob at [pad, 2 pad).
+template <class Model>
+__global__ __launch_bounds__(kBlock) void k_mr_slot_scores(const double* __restrict__ prm, typename Model::Params p0,
+                                                           StepObs o, int s, const double* xs, const double* xprev,
+                                                           const int32_t* anc, const double* rows, int64_t n,
+                                                           int64_t pad, double* out) {
+  constexpr int D = Model::kD;
+  const typename Model::Params p = p0.rebase(prm);
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  double x[D], xp[D];
+#pragma unroll
+  for (int k = 0; k < D; ++k) x[k] = xs[xidx(j, k, D)];
+  if (s > 1) {
+    const int64_t a = anc ? anc[j] : j;
+    if (a >= 0) {
+#pragma unroll
+      for (int k = 0; k < D; ++k) xp[k] = xprev[xidx(a, k, D)];
+    } else {
+#pragma unroll
+      for (int k = 0; k < D; ++k) xp[k] = rows[(-1 - a) * (D + 1) + k];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < D; ++k) xp[k] = 0.0;
+  }
+  double lat, ob;
+  Model::score(p, o, (uint32_t)s, xp, x, &lat, &ob);
+  out[j] = lat;
+  out[pad + j] = ob;
+}
+
+// the cursors' step-s columns from the all-gathered slot scores
+static __global__ void k_mr_take_scores(const int64_t* cur, int64_t n, const double* all, const int64_t* dlo, int R,
+                                        int64_t N, int64_t pad, double* lat, double* ob) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  int64_t i;
+  const int64_t b = mr_pos(cur[j], dlo, R, N, 2 * pad, &i);
+  lat[j] = all[b + i];
+  ob[j] = all[b + pad + i];
+}
+
+// get_score: the columns summed in time order (k_scores' order)
+static __global__ void k_score_total(const double* per_step, int T, int64_t n, double* total) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  double tot = 0.0;
+  for (int s = 1; s <= T; ++s)
+    tot += per_step[((int64_t)(s - 1) * 2) * n + j] + per_step[((int64_t)(s - 1) * 2 + 1) * n + j];
+  total[j] = tot;
 }
 
 // sample_unweighted: prepare max / equal-weight flag from the current stats

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void k_rejuv(const double* __restrict__ prm
         for (int k = 0; k < D; ++k) xp[k] = a.xprev[xidx(src, k, D)];
       } else {
 #pragma unroll
-        for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
+        for (int k = 0; k < D; ++k) xp[k] = ld_sys(&a.remote[(-1 - src) * a.ld_remote + k]);
       }
     }
     double ll = Model::loglik(p, o, x);
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void k_mh_drift(const double* __restrict__ 
         for (int k = 0; k < D; ++k) xp[k] = a.xprev[xidx(src, k, D)];
       } else {
 #pragma unroll
-        for (int k = 0; k < D; ++k) xp[k] = a.remote[(-1 - src) * a.ld_remote + k];
+        for (int k = 0; k < D; ++k) xp[k] = ld_sys(&a.remote[(-1 - src) * a.ld_remote + k]);
       }
     }
     double lat, ob;

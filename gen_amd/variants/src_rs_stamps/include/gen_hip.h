@@ -167,6 +167,19 @@ typedef struct {
 } gh_host_comm;
 int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_host_comm* comm, void* hip_stream,
                            gh_ctx** out);
+/* Peer transport: the ranks' kernels exchange through device memory they map
+   from each other (a fine-grained mailbox per rank, and every filter's
+   received-row buffer), with tagged words and bounded polls — no collective
+   call and no host round trip on the step path.  The bootstrap's allgather
+   (host buffers) swaps the IPC handles once, at context and filter creation
+   (both collective over the ranks), and at gh_ctx_destroy; sendrecv is not
+   used.  Ranks on one GPU (processes sharing a device) or on GPUs that map
+   each other's memory (xGMI peers of one node).  world <= 64.  Multi-rank
+   filters on it resample systematically through the fused kernels (a
+   configuration that would need another form returns GH_E_STATE); a rank
+   that stops posting makes the others' waits end in GH_E_STATE. */
+int gh_ctx_create_peer(int device, int rank, int world, const gh_host_comm* bootstrap, void* hip_stream,
+                       gh_ctx** out);
 int gh_ctx_destroy(gh_ctx* ctx);
 /* Debug / timing: filters created on this context afterwards take the
    multi-rank code path (collectives, split step after a resample, k_rank_a/b)
@@ -258,7 +271,8 @@ int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const double* propo
    (unfold/generic_update.jl:9-16), so every particle's weight gains its
    trajectory's score under the new parameters minus under the old ones, and
    the new step is generated under the new parameters, which the filter keeps
-   from then on (new_model must outlive it).  One rank, record_history. */
+   from then on (new_model must outlive it).  record_history; on R ranks
+   every rank calls it (the re-scoring walks the genealogy across ranks). */
 int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* new_model);
 /* The same for a conditional filter (gh_pf_init_conditional): the re-scoring,
    then the conditional step of gh_pf_step_conditional with the distinguished

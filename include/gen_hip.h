@@ -271,7 +271,8 @@ int gh_pf_step_q(gh_pf* pf, const gh_obs* obs, int proposal, const double* propo
    (unfold/generic_update.jl:9-16), so every particle's weight gains its
    trajectory's score under the new parameters minus under the old ones, and
    the new step is generated under the new parameters, which the filter keeps
-   from then on (new_model must outlive it).  One rank, record_history. */
+   from then on (new_model must outlive it).  record_history; on R ranks
+   every rank calls it (the re-scoring walks the genealogy across ranks). */
 int gh_pf_step_params(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* new_model);
 /* The same for a conditional filter (gh_pf_init_conditional): the re-scoring,
    then the conditional step of gh_pf_step_conditional with the distinguished

@@ -29,6 +29,16 @@ def build_model(name):
     raise ValueError(name)
 
 
+def changed_model(name):
+    """The Unfold of `name` with other parameters (a parameter change, --params-step)."""
+    import gen_amd as gen
+
+    if name.startswith("lg"):
+        m = build_model(name)
+        return gen.LinearGaussianSSM(0.8 * m.A, 1.5 * m.Q, m.H, 0.7 * m.R, m.mu0 + 0.1, m.P0, b=m.b + 0.05, c=m.c - 0.1)
+    return gen.KitagawaSSM(6.0, 2.0)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--model", default="lg4")
@@ -43,6 +53,8 @@ def main():
                    "max-only steps, the resample's sums in k_rank_a2)")
     p.add_argument("--rejuv", type=int, default=0, help="rejuvenation moves after init and every step")
     p.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK)")
+    p.add_argument("--params-step", type=int, default=0, help="step whose particle_filter_step changes the Unfold's "
+                   "parameters (new_args = (t, model'): every particle re-scored along its genealogy)")
     p.add_argument("--genealogy", action="store_true", help="also save trajectories at t = 1, 5, T, the score "
                    "columns and 500 sample_unweighted_traces indices (collective queries)")
     p.add_argument("--out", required=True)
@@ -76,9 +88,13 @@ def main():
     did = []
     if a.batched:
         gen.run_particle_filter(st, list(ys[1 : a.T]), a.thr)
+    m2 = changed_model(a.model) if a.params_step else None
     for t in range(2, a.T + 1) if not a.batched else ():
         did.append(gen.maybe_resample(st, a.thr))
-        gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})
+        if t == a.params_step:
+            gen.particle_filter_step(st, (t, m2), (gen.UnknownChange(), gen.UnknownChange()), {addr(t): ys[t - 1]})
+        else:
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})
         if a.rejuv:
             gen.rejuvenate(st, a.rejuv)
     lml = gen.log_ml_estimate(st)

@@ -431,3 +431,37 @@ def test_gpu_multirank_genealogy(tmp_path, gh_ctx, transport, model, R, thr, n, 
                   "--genealogy", "--out", out], R, timeout=400)
     _check_against_oracle(out, model, R, n, T, seed, thr)
     _check_genealogy(out, model, R, n, T, seed, thr, batched)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,model,R", [("gloo", "lg4", 2), ("peer", "kit", 3)])
+def test_gpu_multirank_step_params(tmp_path, transport, model, R):
+    """particle_filter_step with changed Unfold parameters on R ranks
+    (gh_pf_step_params: every particle re-scored along its genealogy, which
+    crosses ranks) equals the single-rank oracle's orc_pf_step_params run bit
+    for bit, and later steps under the new parameters too."""
+    from oracle import oracle as O
+    from tests.mr_worker import build_model, changed_model
+
+    out = str(tmp_path / "sp")
+    T, seed, n, K = 8, 9, 3001, 5
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  "--seed", str(seed), "--transport", transport, "--params-step", str(K), "--out", out], R,
+                 timeout=400)
+    m, m2 = build_model(model), changed_model(model)
+    _, ys = m.simulate(T, np.random.default_rng(5))
+    orc = O.OraclePF(m, n, seed, O.SYSTEMATIC)
+    orc.init(ys[0])
+    for t in range(2, T + 1):
+        orc.maybe_resample(None)
+        if t == K:
+            orc.step_params(m2, ys[t - 1])
+        else:
+            orc.step(ys[t - 1])
+    parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
+    assert np.array_equal(np.concatenate([p["states"] for p in parts], axis=0).T.view(np.uint64),
+                          orc.state().view(np.uint64))
+    assert np.array_equal(np.concatenate([p["logw"] for p in parts]).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(np.concatenate([p["parents"] for p in parts]), orc.parents())
+    lml = float(parts[0]["lml"])
+    assert abs(lml - orc.log_ml_estimate()) <= 1e-9 * abs(orc.log_ml_estimate())
