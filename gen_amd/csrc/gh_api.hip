@@ -1731,6 +1731,10 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.stats_out = !mr(pf->ctx) ? pf->stats_all : pf->dev->stats;
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   const bool multi = mr(pf->ctx);
+  // multi-rank, a resample whose ancestors were materialised (a genealogy
+  // query between maybe_resample! and this step): they name received rows
+  // (negative), which only the general load path reads
+  if (multi && flags_live(pf) && !pf->marks_pending) a.buf = 0;
   // One rank: every step writes block maxima only — the next maybe_resample!
   // sums the weights in its own pass, any other reader recomputes the sums
   // (ensure_stats) — so a caller's maybe_resample! + particle_filter_step!
@@ -1779,6 +1783,17 @@ static int materialize_marks(gh_pf* pf) {
                      (const DevScalars*)pf->dev, pf->mark_mode);
   HIP_TRY(hipGetLastError());
   pf->marks_pending = false;
+  // multi-rank: the next step reads these ancestors in one launch (no part 2,
+  // which would keep the received rows), so the rows received for it are
+  // kept here as that step's genealogy record
+  if (pf->mark_mode == 2 && pf->rem_fire && pf->opts.record_history) {
+    const int64_t cnt = pf->rem_ra + (pf->n - pf->rem_rb);
+    double* dst = nullptr;
+    CHECK(rhist_reserve(pf, pf->t + 1, cnt, &dst));
+    if (dst)
+      HIP_TRY(hipMemcpyAsync(dst, pf->rows_recv, sizeof(double) * (pf->D + 1) * (size_t)cnt, hipMemcpyDeviceToDevice,
+                             pf->s));
+  }
   return GH_OK;
 }
 

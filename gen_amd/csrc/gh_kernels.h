@@ -447,11 +447,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
         const double inc = Model::step(p, o, a.seed, (uint64_t)(a.lo + j), a.t, a.proposal, xp, x, dr_step);
         lw = (pend ? 0.0 : a.logw[j]) + inc;
       }
-#if defined(GH_LOGW_SC1)  // timing variant: write-through log-weights
-#define GH_LOGW_STORE(p, v) st_sc1(p, v)
-#else
-#define GH_LOGW_STORE(p, v) (*(p) = (v))
-#endif
+
       if (a.buf) {
         const __amdgpu_buffer_rsrc_t ro = gh_rsrc(a.xout);
         const uint32_t tb = (uint32_t)tile * (uint32_t)(kTileP * D * 8);
@@ -462,7 +458,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
 #pragma unroll
         for (int k = 0; k < D; ++k) a.xout[xidx(j, k, D)] = x[k];
       }
-      GH_LOGW_STORE(&a.logw[j], lw);
+      a.logw[j] = lw;
     }
   }
   if (a.max_only) block_max_partial(lw, sm, a.pm + vb, a.amax, vb);
@@ -1161,6 +1157,8 @@ constexpr int kRsItems = 4;
 constexpr int kRsTile = kRsBlock * kRsItems;  // particles per block
 constexpr int kRsPart = 4;                    // step partials per thread (nb_part <= 4096)
 constexpr int kRsPoll = 8;                    // polling waves x 64 tiles: grid <= 512
+constexpr int kHugeGroups = 512;              // marks: a range of more carries is written by the whole block
+constexpr int kHugeList = 64;                 //   (at most N / (64 kHugeGroups) such particles in all)
 
 struct Resample1Args {
   const double* pm;        // step-kernel block partials
@@ -1660,6 +1658,10 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   }
   const uint64_t N = (uint64_t)r.mk.n_global;
   int64_t s_i = sys_count(&sd, N, run);
+  __shared__ int shuge_n;
+  __shared__ int64_t shuge[kHugeList][3];
+  if (threadIdx.x == 0) shuge_n = 0;
+  lds_barrier();
   // particle i owns the slots [s_i, e_i): a tagged mark at s_i, and the carry
   // of every 64-slot group that starts inside the range; a lane writes up to
   // two carries itself, a longer range (a particle with > 64 offspring) gets
@@ -1671,18 +1673,27 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     // (a particle past n or of zero weight leaves run, hence the count, unchanged)
     const int64_t e_i = sys_count_w(&sd, N, run);
     const uint64_t tagged = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
-#if defined(GH_MARK_SC1)  // timing variant: write-through marks (nothing dirty in L2 at the kernel's end)
-    if (e_i > s_i) st_sc1(&r.mk.mark[s_i], tagged);
-#else
     if (e_i > s_i) r.mk.mark[s_i] = tagged;
-#endif
     const int64_t g0 = (s_i + 63) >> 6, g1 = (e_i + 63) >> 6;  // groups g with 64 g in [s_i, e_i)
     const bool many = g1 - g0 > 2;
     if (!many) {
       if (g1 > g0) r.mk.cmark[g0] = tagged;
       if (g1 > g0 + 1) r.mk.cmark[g0 + 1] = tagged;
     }
-    uint64_t bm = __builtin_amdgcn_ballot_w64(many);
+    // a range of more than kHugeGroups groups (peaked weights: one particle
+    // with tens of thousands of offspring) goes to the block's list and gets
+    // its carries from all 16 waves below; other long ranges from their wave
+    bool listed = false;
+    if (g1 - g0 > kHugeGroups) {
+      const int e = atomicAdd(&shuge_n, 1);
+      if (e < kHugeList) {  // (a full list: the wave writes them, as below)
+        shuge[e][0] = g0;
+        shuge[e][1] = g1;
+        shuge[e][2] = (int64_t)tagged;
+        listed = true;
+      }
+    }
+    uint64_t bm = __builtin_amdgcn_ballot_w64(many && !listed);
     while (bm) {
       const int L = __builtin_ctzll(bm);
       bm &= bm - 1;
@@ -1692,6 +1703,10 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     s_i = e_i;
   }
+  lds_barrier();
+  const int nh = shuge_n < kHugeList ? shuge_n : kHugeList;  // (uniform)
+  for (int e = 0; e < nh; ++e)
+    for (int64_t g = shuge[e][0] + threadIdx.x; g < shuge[e][1]; g += kRsBlock) r.mk.cmark[g] = (uint64_t)shuge[e][2];
   commit();
 }
 
@@ -2532,7 +2547,8 @@ static __global__ void k_mr_gparents(const int32_t* anc, int64_t n, int64_t lo, 
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
   const int32_t a = anc[j];
-  gp[j] = a >= 0 ? lo + a : __double_as_longlong(ld_sys(&rows[(int64_t)(-1 - a) * (D + 1) + D]));
+  // (a received row without its record cannot happen; -1 makes the query fail, not fault)
+  gp[j] = a >= 0 ? lo + a : (rows ? __double_as_longlong(ld_sys(&rows[(int64_t)(-1 - a) * (D + 1) + D])) : -1);
 }
 
 // every cursor one step back: cur = parent of the slot it names
@@ -2540,6 +2556,7 @@ static __global__ void k_mr_back(int64_t* cur, int64_t n, const int64_t* gp_all,
                                  int64_t pad) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
+  if (cur[j] < 0 || cur[j] >= N) return;  // (a broken walk stays broken: the query's result is wrong, no fault)
   int64_t i;
   const int64_t b = mr_pos(cur[j], dlo, R, N, pad, &i);
   cur[j] = gp_all[b + i];
@@ -2551,6 +2568,10 @@ static __global__ void k_mr_states(const int64_t* cur, int64_t n, const double* 
                                    const int64_t* dlo, int R, int64_t N, int D, double* out) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
+  if (cur[j] < 0 || cur[j] >= N) {
+    for (int k = 0; k < D; ++k) out[k * n + j] = NAN;
+    return;
+  }
   int64_t i;
   const int64_t r = mr_pos(cur[j], dlo, R, N, 1, &i);
   for (int k = 0; k < D; ++k) out[k * n + j] = slab[r * stride + xidx(i, k, D)];
@@ -2580,7 +2601,7 @@ __global__ __launch_bounds__(kBlock) void k_mr_slot_scores(const double* __restr
       for (int k = 0; k < D; ++k) xp[k] = xprev[xidx(a, k, D)];
     } else {
 #pragma unroll
-      for (int k = 0; k < D; ++k) xp[k] = rows[(-1 - a) * (D + 1) + k];
+      for (int k = 0; k < D; ++k) xp[k] = rows ? rows[(-1 - a) * (D + 1) + k] : NAN;
     }
   } else {
 #pragma unroll
@@ -2597,6 +2618,11 @@ static __global__ void k_mr_take_scores(const int64_t* cur, int64_t n, const dou
                                         int64_t N, int64_t pad, double* lat, double* ob) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
+  if (cur[j] < 0 || cur[j] >= N) {
+    lat[j] = NAN;
+    ob[j] = NAN;
+    return;
+  }
   int64_t i;
   const int64_t b = mr_pos(cur[j], dlo, R, N, 2 * pad, &i);
   lat[j] = all[b + i];

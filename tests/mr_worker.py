@@ -55,6 +55,8 @@ def main():
     p.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK)")
     p.add_argument("--params-step", type=int, default=0, help="step whose particle_filter_step changes the Unfold's "
                    "parameters (new_args = (t, model'): every particle re-scored along its genealogy)")
+    p.add_argument("--mid-query", action="store_true", help="genealogy queries between maybe_resample and the step "
+                   "at t = 4 (the step then reads materialised ancestors naming received rows)")
     p.add_argument("--genealogy", action="store_true", help="also save trajectories at t = 1, 5, T, the score "
                    "columns and 500 sample_unweighted_traces indices (collective queries)")
     p.add_argument("--out", required=True)
@@ -91,6 +93,9 @@ def main():
     m2 = changed_model(a.model) if a.params_step else None
     for t in range(2, a.T + 1) if not a.batched else ():
         did.append(gen.maybe_resample(st, a.thr))
+        if a.mid_query and t == 4:
+            st.states(2)
+            gen.get_traces(st).scores()
         if t == a.params_step:
             gen.particle_filter_step(st, (t, m2), (gen.UnknownChange(), gen.UnknownChange()), {addr(t): ys[t - 1]})
         else:

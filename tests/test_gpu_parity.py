@@ -371,6 +371,20 @@ def test_kitagawa_large_tiles_bitexact(gh_ctx, n):
     assert_lml_close(st, orc)
 
 
+@pytest.mark.parametrize("n", [1 << 20, (1 << 21) + 4097])
+def test_peaked_weights_huge_offspring_bitexact(gh_ctx, n):
+    """var_y = 1e-10 puts nearly all the weight on one particle, with most of
+    the N offspring: its range's carries (more than 512 groups of 64 slots)
+    are written by the whole resample block, not one wave.  States and parents
+    bit-exact against the oracle at every step."""
+    m = gen.KitagawaSSM(10.0, 1e-10)
+    _, ys = m.simulate(4, np.random.default_rng(11))
+    st, orc = run_both(m, ys, n, seed=13, thr=n)
+    counts = np.bincount(st.parents, minlength=n)
+    assert counts.max() > 64 * 512  # the block-wide carry path ran
+    assert_lml_close(st, orc)
+
+
 # ------------------------------------------------------------- edge cases
 def test_single_particle(gh_ctx):
     m = gen.KitagawaSSM()

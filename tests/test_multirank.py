@@ -417,18 +417,22 @@ def _check_genealogy(out, model, R, n, T, seed, thr, batched):
 @pytest.mark.parametrize("transport,model,R,thr,n,batched", [
     ("gloo", "lg4", 2, None, 3001, False), ("gloo", "kit", 3, 1e9, 4003, True), ("gloo", "kit_sharp", 3, None, 4003, True),
     ("peer", "lg4", 2, 1e9, 3001, True), ("peer", "kit", 3, None, 4096, True), ("peer", "lg10", 2, 3001.0, 3001, False),
-    ("rccl1", "lg4", 1, None, 3001, True)])
+    ("rccl1", "lg4", 1, None, 3001, True), ("gloo", "kit", 2, 1e9, 3001, "mid"), ("peer", "lg4", 3, 1e9, 3001, "mid")])
 def test_gpu_multirank_genealogy(tmp_path, gh_ctx, transport, model, R, thr, n, batched):
     """The genealogy across ranks (get_traces at earlier steps, the trace score
     columns, sample_unweighted_traces; particle_filter.jl:31-34, 62-70): each
     rank keeps its slots' ancestors and the rows it received, and the queries
-    walk them collectively — against the single-rank oracle bit for bit."""
+    walk them collectively — against the single-rank oracle bit for bit.
+    "mid": queries between maybe_resample and the step at t = 4 too (that
+    step then reads materialised ancestors that name received rows)."""
     out = str(tmp_path / "gen")
     T, seed = 8, 9
+    mid = batched == "mid"
+    batched = batched is True
     _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
                   *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--transport", transport,
                   *(["--device", "0"] if transport == "rccl1" else []), *(["--batched"] if batched else []),
-                  "--genealogy", "--out", out], R, timeout=400)
+                  *(["--mid-query"] if mid else []), "--genealogy", "--out", out], R, timeout=400)
     _check_against_oracle(out, model, R, n, T, seed, thr)
     _check_genealogy(out, model, R, n, T, seed, thr, batched)
 
