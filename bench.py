@@ -72,9 +72,11 @@ def parse(argv=None):
     p.add_argument("--force-multirank", action="store_true",
                    help="one GPU on the multi-rank code path (a one-rank RCCL communicator; profiling)")
     p.add_argument("--no-kernel-timing", action="store_true", help="no hipEvents around the step kernel")
-    p.add_argument("--transport", default="rccl", choices=["rccl", "gloo"],
-                   help="multi-GPU collectives: RCCL (default) or the host-staged gloo transport "
-                        "(ranks may share a GPU; a correctness rehearsal, not a benchmark)")
+    p.add_argument("--transport", default="peer", choices=["peer", "rccl", "gloo"],
+                   help="multi-GPU exchange: peer (default: the ranks' kernels store into each other's mapped "
+                        "mailboxes and row buffers, IPC handles swapped over gloo; falls back to RCCL if the "
+                        "mapping fails), RCCL collectives, or the host-staged gloo transport (ranks may share a "
+                        "GPU; a correctness rehearsal, not a benchmark)")
     p.add_argument("--time-every", type=int, default=None,
                    help="time every k-th step kernel with launch events (default 1: every launch of the timed "
                         "region, so kernel_avg_ms averages all of them)")
@@ -458,6 +460,9 @@ def secondary_c5(gen, ctx, a):
 
 
 # ------------------------------------------------------------------- main
+_KEEP = []
+
+
 def main(argv=None):
     a = parse(argv)
     if a.time_every is None:
@@ -472,13 +477,34 @@ def main(argv=None):
         import torch.distributed as dist
 
         dist.init_process_group("gloo")
+        ctx = None
         if a.transport == "gloo":
             import torch
 
             from gen_amd.transport import GlooTransport
 
             ctx = gen.Context(device=local % max(1, torch.cuda.device_count()), transport=GlooTransport())
-        else:
+        elif a.transport == "peer":
+            import torch
+
+            from gen_amd.transport import GlooTransport
+
+            try:  # (ranks may share a GPU: the one-GPU rehearsal)
+                ctx = gen.Context(device=local % max(1, torch.cuda.device_count()), transport=GlooTransport(),
+                                  peer=True)
+                ok = 1
+            except Exception as e:  # (no IPC mapping between these GPUs)
+                print(f"rank {rank}: peer transport unavailable ({e}); RCCL instead", file=sys.stderr, flush=True)
+                ok = 0
+            oks = [None] * world
+            dist.all_gather_object(oks, ok)
+            if not all(oks):
+                # (a rank whose peer context exists keeps it open: its destroy
+                # would wait for the ranks that have none)
+                _KEEP.append(ctx)
+                ctx = None
+                a.transport = "rccl"
+        if ctx is None:
             uid = [gen.Context.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             ctx = gen.Context(device=local, rank=rank, world=world, unique_id=uid[0])
@@ -534,6 +560,7 @@ def main(argv=None):
             "d": d,
             "resampler": a.resampler,
             "parallelism": f"particle-dp{world}",
+            "transport": a.transport if world > 1 else "none",
             "resample_steps_timed": r["n_res"],
             "log_ml": lml,
         },
@@ -548,7 +575,9 @@ def main(argv=None):
         out["cpu_baseline"] = pf_cpu_baseline(model, ys, a.cpu_seconds)
         # the headline configuration itself (N = the bench's particles, every
         # step of the run, same seed and observations): GPU vs the CPU restatement
-        par = cpu_parity(model, ys, a.particles, a.resampler, a.proposal)
+        # at least the C2 configuration's T = 100 (BASELINE.json configs[1])
+        ys_par = ys if len(ys) >= 100 else model.simulate(100, np.random.default_rng(2))[1]
+        par = cpu_parity(model, ys_par, a.particles, a.resampler, a.proposal)
         out["cpu_baseline"]["parity"] = par
         if out["log_ml_error"] is not None:
             out["log_ml_error"]["vs_cpu_reference_same_seed"] = {"particles": par["particles"], "rel": par["rel"]}

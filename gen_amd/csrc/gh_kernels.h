@@ -1658,10 +1658,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   }
   const uint64_t N = (uint64_t)r.mk.n_global;
   int64_t s_i = sys_count(&sd, N, run);
+#if !defined(GH_NO_HUGE_CARRIES)
   __shared__ int shuge_n;
   __shared__ int64_t shuge[kHugeList][3];
   if (threadIdx.x == 0) shuge_n = 0;
   lds_barrier();
+#endif
   // particle i owns the slots [s_i, e_i): a tagged mark at s_i, and the carry
   // of every 64-slot group that starts inside the range; a lane writes up to
   // two carries itself, a longer range (a particle with > 64 offspring) gets
@@ -1684,6 +1686,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     // with tens of thousands of offspring) goes to the block's list and gets
     // its carries from all 16 waves below; other long ranges from their wave
     bool listed = false;
+#if !defined(GH_NO_HUGE_CARRIES)
     if (g1 - g0 > kHugeGroups) {
       const int e = atomicAdd(&shuge_n, 1);
       if (e < kHugeList) {  // (a full list: the wave writes them, as below)
@@ -1693,6 +1696,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
         listed = true;
       }
     }
+#endif
     uint64_t bm = __builtin_amdgcn_ballot_w64(many && !listed);
     while (bm) {
       const int L = __builtin_ctzll(bm);
@@ -1703,10 +1707,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     s_i = e_i;
   }
+#if !defined(GH_NO_HUGE_CARRIES)
   lds_barrier();
   const int nh = shuge_n < kHugeList ? shuge_n : kHugeList;  // (uniform)
   for (int e = 0; e < nh; ++e)
     for (int64_t g = shuge[e][0] + threadIdx.x; g < shuge[e][1]; g += kRsBlock) r.mk.cmark[g] = (uint64_t)shuge[e][2];
+#endif
   commit();
 }
 

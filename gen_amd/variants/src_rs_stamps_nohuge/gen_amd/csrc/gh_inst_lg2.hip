@@ -1,0 +1,5 @@
+// gh_inst_lg2.hip — explicit instantiations of LG-SSM kernels (see gh_inst.h)
+#include <hip/hip_runtime.h>
+#include "gh_inst.h"
+
+GH_LG_UNIT2(GH_TEMPLATE)
