@@ -1157,8 +1157,6 @@ constexpr int kRsItems = 4;
 constexpr int kRsTile = kRsBlock * kRsItems;  // particles per block
 constexpr int kRsPart = 4;                    // step partials per thread (nb_part <= 4096)
 constexpr int kRsPoll = 8;                    // polling waves x 64 tiles: grid <= 512
-constexpr int kHugeGroups = 512;              // marks: a range of more carries is written by the whole block
-constexpr int kHugeList = 64;                 //   (at most N / (64 kHugeGroups) such particles in all)
 
 struct Resample1Args {
   const double* pm;        // step-kernel block partials
@@ -1658,12 +1656,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   }
   const uint64_t N = (uint64_t)r.mk.n_global;
   int64_t s_i = sys_count(&sd, N, run);
-#if !defined(GH_NO_HUGE_CARRIES)
-  __shared__ int shuge_n;
-  __shared__ int64_t shuge[kHugeList][3];
-  if (threadIdx.x == 0) shuge_n = 0;
-  lds_barrier();
-#endif
   // particle i owns the slots [s_i, e_i): a tagged mark at s_i, and the carry
   // of every 64-slot group that starts inside the range; a lane writes up to
   // two carries itself, a longer range (a particle with > 64 offspring) gets
@@ -1682,22 +1674,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       if (g1 > g0) r.mk.cmark[g0] = tagged;
       if (g1 > g0 + 1) r.mk.cmark[g0 + 1] = tagged;
     }
-    // a range of more than kHugeGroups groups (peaked weights: one particle
-    // with tens of thousands of offspring) goes to the block's list and gets
-    // its carries from all 16 waves below; other long ranges from their wave
-    bool listed = false;
-#if !defined(GH_NO_HUGE_CARRIES)
-    if (g1 - g0 > kHugeGroups) {
-      const int e = atomicAdd(&shuge_n, 1);
-      if (e < kHugeList) {  // (a full list: the wave writes them, as below)
-        shuge[e][0] = g0;
-        shuge[e][1] = g1;
-        shuge[e][2] = (int64_t)tagged;
-        listed = true;
-      }
-    }
-#endif
-    uint64_t bm = __builtin_amdgcn_ballot_w64(many && !listed);
+    uint64_t bm = __builtin_amdgcn_ballot_w64(many);
     while (bm) {
       const int L = __builtin_ctzll(bm);
       bm &= bm - 1;
@@ -1707,12 +1684,6 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     s_i = e_i;
   }
-#if !defined(GH_NO_HUGE_CARRIES)
-  lds_barrier();
-  const int nh = shuge_n < kHugeList ? shuge_n : kHugeList;  // (uniform)
-  for (int e = 0; e < nh; ++e)
-    for (int64_t g = shuge[e][0] + threadIdx.x; g < shuge[e][1]; g += kRsBlock) r.mk.cmark[g] = (uint64_t)shuge[e][2];
-#endif
   commit();
 }
 

@@ -28,14 +28,12 @@ VARIANTS = {
     "coal_b512w6": ["GH_COAL_BLOCK=512", "GH_COAL_WIN=6"],
     "coal_b512w7": ["GH_COAL_BLOCK=512", "GH_COAL_WIN=7"],
     "coal_b64w10": ["GH_COAL_BLOCK=64", "GH_COAL_WIN=10"],
-    "no_huge": ["GH_NO_HUGE_CARRIES"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
-EXTRA = {"rs_stamps": ["GH_RS_STAMPS"], "kstep_stamps": [], "rs_stamps_nohuge": ["GH_RS_STAMPS", "GH_NO_HUGE_CARRIES"]}
+EXTRA = {"rs_stamps": ["GH_RS_STAMPS"], "kstep_stamps": []}
 # variants whose hooks are not in the product sources: a patch applied to a copy
 PATCHES = {"rs_stamps": os.path.join(ROOT, "tools", "rs_stamps.patch"),
-           "rs_stamps_nohuge": os.path.join(ROOT, "tools", "rs_stamps.patch"),
            "kstep_stamps": os.path.join(ROOT, "tools", "kstep_stamps.patch")}
 BENCH_ARGS = os.environ.get("GH_VARIANT_ARGS", "--steps 50").split()
 # GH_VARIANT_SCRIPT=tools/bench_pmmh.py times another workload with the same variants
