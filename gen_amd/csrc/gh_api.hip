@@ -818,9 +818,10 @@ struct gh_pf {
   int32_t* anc_scratch = nullptr;
   double* logw = nullptr;
   uint64_t* C = nullptr;
-  uint64_t* mark = nullptr;       // systematic: tagged range starts per slot
-  uint64_t* cmark = nullptr;      // systematic: tagged carry per step block
-  uint64_t epoch = 0;             // resample counter for the tags
+  uint32_t* mark = nullptr;       // systematic: tagged range starts per slot
+  uint32_t* cmark = nullptr;      // systematic: tagged carry per 64-slot group
+  uint64_t epoch = 0;             // resample counter for the tags (since the last clear)
+  int mark_bits = 1;              // low bits of a mark word holding the ancestor
   bool marks_pending = false;     // last resample's ancestors only exist as marks
   bool stats_valid = false;       // stats_all holds the last step's (M, S, S2) (one rank)
   uint64_t* tsum = nullptr;       // k_resample1: published tile totals (+ tile sums, 3 x n_tiles)
@@ -1511,8 +1512,9 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return fail(set_err(GH_E_NOMEM, "hipMalloc %s", #ptr));
   ALLOC(pf->logw, sizeof(double) * n);
   ALLOC(pf->C, sizeof(uint64_t) * n);
-  ALLOC(pf->mark, sizeof(uint64_t) * n);
-  ALLOC(pf->cmark, sizeof(uint64_t) * ((n + 63) / 64));
+  ALLOC(pf->mark, sizeof(uint32_t) * n);
+  ALLOC(pf->cmark, sizeof(uint32_t) * ((n + 63) / 64));
+  while (pf->mark_bits < 31 && (1ll << pf->mark_bits) < n) ++pf->mark_bits;
   ALLOC(pf->bsum, sizeof(uint64_t) * pf->nb_scan);
   ALLOC(pf->pm, sizeof(double) * pf->nb_step);
   ALLOC(pf->ps, sizeof(double) * pf->nb_step);
@@ -1596,9 +1598,9 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     z.one = 1;
     if (hipMemcpyAsync(pf->dev, &z, sizeof z, hipMemcpyHostToDevice, pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init scalars"));
-    if (hipMemsetAsync(pf->mark, 0, sizeof(uint64_t) * n, pf->s) != hipSuccess ||
+    if (hipMemsetAsync(pf->mark, 0, sizeof(uint32_t) * n, pf->s) != hipSuccess ||
         hipMemsetAsync(pf->tsum, 0, sizeof(uint64_t) * 3 * std::max<int64_t>(1, pf->n_tiles), pf->s) != hipSuccess ||
-        hipMemsetAsync(pf->cmark, 0, sizeof(uint64_t) * ((n + 63) / 64), pf->s) != hipSuccess)
+        hipMemsetAsync(pf->cmark, 0, sizeof(uint32_t) * ((n + 63) / 64), pf->s) != hipSuccess)
       return fail(set_err(GH_E_HIP, "init marks"));
     if (pf->amax) {
       std::vector<uint64_t> e(2 * kAmaxShards * kAmaxStride, kAmaxEmpty);
@@ -1713,6 +1715,7 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.anc = anc_for_step(pf, t);
   a.mark = pf->mark;
   a.carry = pf->cmark;
+  a.mark_idx = (uint32_t)((1ull << pf->mark_bits) - 1);
   a.mark_mode = pf->marks_pending ? pf->mark_mode : 0;
   a.resampled = flags_live(pf);
   a.remote = pf->rows_recv;
@@ -1774,12 +1777,27 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
 // genealogy reads before the next step, or a second resample).
 static int finish_plan(gh_pf* pf);
 
+// The next resample's epoch tag for the range marks (MarkArgs::tag: the epoch
+// above the mark_bits index bits).  When the epoch field is used up, both mark
+// arrays are cleared on the filter's stream first (every consumer of the old
+// marks is enqueued before), so all older words stay below the new tags.
+static int next_mark_tag(gh_pf* pf, uint32_t* tag) {
+  if (pf->epoch + 1 >= (1ull << (32 - pf->mark_bits))) {
+    HIP_TRY(hipMemsetAsync(pf->mark, 0, sizeof(uint32_t) * pf->n, pf->s));
+    HIP_TRY(hipMemsetAsync(pf->cmark, 0, sizeof(uint32_t) * ((pf->n + 63) / 64), pf->s));
+    pf->epoch = 0;
+  }
+  *tag = (uint32_t)(++pf->epoch << pf->mark_bits);
+  return GH_OK;
+}
+
 static int materialize_marks(gh_pf* pf) {
   CHECK(finish_plan(pf));
   if (!pf->marks_pending) return GH_OK;
   int32_t* anc_target = anc_for_step(pf, pf->t + 1);
   hipLaunchKernelGGL(k_sys_ancestors, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
-                     &pf->dev->pending, pf->mark, pf->cmark, pf->n, (const int32_t*)nullptr, anc_target,
+                     &pf->dev->pending, pf->mark, pf->cmark, (uint32_t)((1ull << pf->mark_bits) - 1), pf->n,
+                     (const int32_t*)nullptr, anc_target,
                      (const DevScalars*)pf->dev, pf->mark_mode);
   HIP_TRY(hipGetLastError());
   pf->marks_pending = false;
@@ -1926,7 +1944,7 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   rb.t = (uint32_t)t;
   rb.mk.mark = pf->mark;
   rb.mk.cmark = pf->cmark;
-  rb.mk.epoch = ++pf->epoch;
+  CHECK(next_mark_tag(pf, &rb.mk.tag));
   rb.mk.n_global = pf->n_global;
   rb.mk.n_groups = (pf->n + 63) / 64;
   rb.mk.enabled = 1;
@@ -2101,7 +2119,10 @@ static int finish_plan(gh_pf* pf) {
   return GH_OK;
 }
 
-static int resample_enqueue(gh_pf* pf, double thr) {
+// want_decision: the caller reads maybe_resample!'s Bool (or the ESS) now, so
+// the fused kernel posts it to the host mailbox; the batched loop does not
+// (block 0 then skips the post and its system-scope fence)
+static int resample_enqueue(gh_pf* pf, double thr, bool want_decision) {
   const int t = pf->t;
   CHECK(grow_for_step(pf, t + 1));
   pf->dec_posted = false;
@@ -2146,15 +2167,15 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     ra.sums_in_pass = pf->max_only ? 1 : 0;
     ra.mk.mark = pf->mark;
     ra.mk.cmark = pf->cmark;
-    ra.mk.epoch = ++pf->epoch;
+    CHECK(next_mark_tag(pf, &ra.mk.tag));
     ra.mk.n_global = pf->n_global;
     ra.mk.n_groups = (n + 63) / 64;
     ra.mk.enabled = sys ? 1 : 0;
     ra.C = pf->C;
     ra.seed = pf->seed;
     ra.t = (uint32_t)t;
-    ra.hdec = pf->d_dec;
-    ra.htag = ++pf->dec_seq;
+    ra.hdec = want_decision ? pf->d_dec : nullptr;
+    ra.htag = want_decision ? ++pf->dec_seq : 0;
     if (pf->amax) {  // the step's own max fold (when it wrote one); the next step's shards emptied
       ra.amax_in = pf->max_only && pf->amax_valid ? pf->amax + (t & 1) * kAmaxShards * kAmaxStride : nullptr;
       ra.amax_reset = pf->amax + ((t + 1) & 1) * kAmaxShards * kAmaxStride;
@@ -2178,7 +2199,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     }
 #undef GH_RS1
     pf->stats_valid = true;
-    pf->dec_posted = true;
+    pf->dec_posted = want_decision;
     if (sys) {
       pf->marks_pending = true;
     } else {
@@ -2222,7 +2243,7 @@ static int resample_enqueue(gh_pf* pf, double thr) {
   MarkArgs mk{};
   mk.mark = pf->mark;
   mk.cmark = pf->cmark;
-  mk.epoch = ++pf->epoch;
+  CHECK(next_mark_tag(pf, &mk.tag));
   mk.n_global = pf->n_global;
   mk.n_groups = (pf->n + 63) / 64;
   mk.enabled = sys1 ? 1 : 0;
@@ -2244,7 +2265,8 @@ static int resample_enqueue(gh_pf* pf, double thr) {
     // kernel expands them (no search, no ancestor array round trip)
     if (second) {
       hipLaunchKernelGGL(k_sys_ancestors, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, g.gate, g.zero_w,
-                         pf->mark, pf->cmark, n, (const int32_t*)anc_target, pf->anc_scratch,
+                         pf->mark, pf->cmark, (uint32_t)((1ull << pf->mark_bits) - 1), n,
+                         (const int32_t*)anc_target, pf->anc_scratch,
                          (const DevScalars*)pf->dev, 1);
       hipLaunchKernelGGL(k_copy_anc, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, &pf->dev->fire,
                          pf->anc_scratch, anc_target, n);
@@ -2285,7 +2307,7 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
   if (thr != thr) thr = (double)pf->n_global / 2.0;
   if (thr < 0.0)
     return set_err(GH_E_INVAL, "ess_threshold %g < 0: pass NaN for the default N/2, 0 to never resample", thr);
-  CHECK(resample_enqueue(pf, thr));
+  CHECK(resample_enqueue(pf, thr, did || ess));
   // conditional SMC: the distinguished particle's parent is itself (smc.jl:139);
   // the ancestor array is only read if the resample fired
   if (pf->cond) HIP_TRY(hipMemsetAsync(anc_for_step(pf, pf->t + 1), 0, sizeof(int32_t), pf->s));
@@ -3362,6 +3384,18 @@ extern "C" int gh_sys_plan(int64_t n_global, int world, int rank, const uint64_t
 
 // The message lists one rank posts for a resample with these totals (host
 // arithmetic only; tests): peers and byte counts, sends then receives.
+extern "C" int gh_debug_mark_bits(gh_pf* pf, int bits) {
+  if (!pf) return set_err(GH_E_INVAL, "gh_debug_mark_bits: null filter");
+  if (pf->marks_pending) return set_err(GH_E_STATE, "gh_debug_mark_bits: a resample's marks are pending");
+  int need = 1;
+  while (need < 31 && (1ll << need) < pf->n) ++need;
+  pf->mark_bits = std::min(31, std::max(need, bits));
+  HIP_TRY(hipMemsetAsync(pf->mark, 0, sizeof(uint32_t) * pf->n, pf->s));
+  HIP_TRY(hipMemsetAsync(pf->cmark, 0, sizeof(uint32_t) * ((pf->n + 63) / 64), pf->s));
+  pf->epoch = 0;
+  return GH_OK;
+}
+
 extern "C" int gh_debug_exchange_lists(int64_t n_global, int world, int rank, const uint64_t* totals, uint64_t offset,
                                        int D, int* n_send, int* send_peer, uint64_t* send_bytes, int* n_recv,
                                        int* recv_peer, uint64_t* recv_bytes) {

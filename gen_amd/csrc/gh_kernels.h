@@ -74,8 +74,9 @@ struct StepArgs {
   const double* xprev;   // wave-tiled states of the previous step (xidx)
   int32_t* anc;          // ancestors for this step (read when a resample is pending;
                          // written here when they come from the systematic marks)
-  const uint64_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode)
-  const uint64_t* carry;
+  const uint32_t* mark;  // systematic range marks + per-64-slot-group carries (mark_mode):
+  const uint32_t* carry; //   (epoch tag | ancestor), the ancestor in the low bits of mark_idx
+  uint32_t mark_idx;
   int mark_mode;          // 1: systematic marks (one rank); 2: marks + received rows (multi-rank)
   int resampled;         // a maybe_resample! was enqueued since the last step
                          // (otherwise the device flags are stale and ignored)
@@ -198,6 +199,21 @@ __device__ __forceinline__ uint64_t wave_incl_sum_u64(uint64_t v) {
   t = dpp_u64<0x118>(v, 0); if (rl >= 8) v += t;   // row_shr:8
   t = dpp_u64<0x142>(v, 0); if ((lane & 31) >= 16) v += t;  // row_bcast:15
   t = dpp_u64<0x143>(v, 0); if (lane >= 32) v += t;         // row_bcast:31
+  return v;
+}
+// lanes without a DPP source (row_shr shifted out, rows outside ROW_MASK) read 0
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp0_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+// inclusive max over the lanes (0 is the identity: no lane conditions)
+__device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t v) {
+  v = max(v, dpp0_u32<0x111>(v));       // row_shr:1
+  v = max(v, dpp0_u32<0x112>(v));       // row_shr:2
+  v = max(v, dpp0_u32<0x114>(v));       // row_shr:4
+  v = max(v, dpp0_u32<0x118>(v));       // row_shr:8
+  v = max(v, dpp0_u32<0x142, 0xa>(v));  // row_bcast:15 into rows 1, 3
+  v = max(v, dpp0_u32<0x143, 0xc>(v));  // row_bcast:31 into rows 2, 3
   return v;
 }
 __device__ __forceinline__ uint64_t wave_incl_max_u64(uint64_t v) {
@@ -381,7 +397,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   // read whenever a resample was enqueued; they are used only if it fired).
   // (clamped indices, no per-lane branch: a value merged at a divergent join
   // would be waited for right here)
-  uint64_t mv = 0, cv = 0;
+  uint32_t mv = 0, cv = 0;
   int pending = 0, fire = 0;
   if (!INIT && a.resampled) {
     pending = a.dev->pending;
@@ -404,10 +420,8 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
   if (tile * 64 < a.n) {  // wave-uniform
     int64_t src = j;
     if (use_marks) {
-      uint64_t v = j < a.n ? mv : 0;
-      const uint64_t c = cv;
-      v = wave_incl_max_u64(v > c ? v : c);
-      src = (int64_t)(uint32_t)v;
+      const uint32_t v = wave_incl_max_u32(max(j < a.n ? mv : 0u, cv));
+      src = (int64_t)(v & a.mark_idx);
       if (a.mark_mode == 2) {  // slots outside [ra, rb) take the received rows in slot order
         const int64_t ra = a.dev->ra, rb = a.dev->rb, js = a.j0 + j;
         if (js < ra) src = -1 - js;
@@ -513,7 +527,7 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
   const int64_t vb = SPLIT ? (int64_t)blockIdx.x + (blockIdx.x >= a.vb_split ? a.vb_skip : 0) : (int64_t)blockIdx.x;
   const int64_t tile0 = (vb * (kBlock / 64) + w) * 2;
   const int64_t j0 = tile0 * 64 + lane, j1 = j0 + 64;
-  uint64_t mv0 = 0, mv1 = 0, cv0 = 0, cv1 = 0;
+  uint32_t mv0 = 0, mv1 = 0, cv0 = 0, cv1 = 0;
   int pending = 0, fire = 0;
   if (!INIT && a.resampled) {
     pending = a.dev->pending;
@@ -537,11 +551,10 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
     const bool has1 = j1 < a.n;
     int64_t s0 = j0, s1 = j1;
     if (use_marks) {  // both tiles: prefix max seeded with the tile's carry
-      uint64_t v0 = j0 < a.n ? mv0 : 0, v1 = has1 ? mv1 : 0;
-      v0 = wave_incl_max_u64(v0 > cv0 ? v0 : cv0);
-      v1 = wave_incl_max_u64(v1 > cv1 ? v1 : cv1);
-      s0 = (int64_t)(uint32_t)v0;
-      s1 = (int64_t)(uint32_t)v1;
+      const uint32_t v0 = wave_incl_max_u32(max(j0 < a.n ? mv0 : 0u, cv0));
+      const uint32_t v1 = wave_incl_max_u32(max(has1 ? mv1 : 0u, cv1));
+      s0 = (int64_t)(v0 & a.mark_idx);
+      s1 = (int64_t)(v1 & a.mark_idx);
       if (a.mark_mode == 2) {  // multi-rank: slots outside [ra, rb) take the received rows in slot order
         const int64_t ra = a.dev->ra, rb = a.dev->rb, js0 = a.j0 + j0, js1 = a.j0 + j1;
         if (js0 < ra) s0 = -1 - js0;
@@ -1001,10 +1014,14 @@ __device__ __forceinline__ int64_t sys_count_w(const DevScalars* dev, uint64_t N
   return j;
 }
 
+// Range marks are 32-bit words: the resample's epoch tag in the high bits and
+// the ancestor (a local particle index) in the low ceil(log2 n) bits, so the
+// newest epoch's words are the largest; the host clears both arrays when the
+// epoch field wraps.
 struct MarkArgs {
-  uint64_t* mark;     // [n slots] tagged (epoch << 32 | ancestor) at each range start
-  uint64_t* cmark;    // [64-slot groups] tagged ancestor of the group's first slot
-  uint64_t epoch;     // resample counter (tags older marks as stale)
+  uint32_t* mark;     // [n slots] tagged ancestor at each range start
+  uint32_t* cmark;    // [64-slot groups] tagged ancestor of the group's first slot
+  uint32_t tag;       // this resample's epoch tag (epoch << index bits)
   int64_t n_global;
   int64_t n_groups;   // 64-slot groups (entries of cmark)
   int enabled;        // systematic single-rank path
@@ -1102,7 +1119,7 @@ static __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64
     run += q[k];
     const int64_t e_i = (i0 + k < n && q[k]) ? sys_count(&sd, N, run) : s_i;
     se[threadIdx.x * kScanItems + k] = (int32_t)e_i;
-    if (e_i > s_i) mk.mark[s_i] = (mk.epoch << 32) | (uint64_t)(i0 + k);
+    if (e_i > s_i) mk.mark[s_i] = mk.tag | (uint32_t)(i0 + k);
     s_i = e_i;
   }
   __syncthreads();
@@ -1117,26 +1134,24 @@ static __global__ __launch_bounds__(kBlock) void k_cdf(const double* logw, int64
       if (se[mid] > slot) hi = mid;
       else lo = mid + 1;
     }
-    mk.cmark[b] = (mk.epoch << 32) | (uint64_t)(pbase + lo);
+    mk.cmark[b] = mk.tag | (uint32_t)(pbase + lo);
   }
 }
 
 // systematic ancestors (materialised outside a step): wave-level prefix max
 // of the slot marks seeded with the carry of the 64-slot group
 static __global__ __launch_bounds__(kBlock) void k_sys_ancestors(const int* gate, const int* zero_w,
-                                                          const uint64_t* mark, const uint64_t* carry,
-                                                          int64_t n, const int32_t* anc_old,
+                                                          const uint32_t* mark, const uint32_t* carry,
+                                                          uint32_t idx, int64_t n, const int32_t* anc_old,
                                                           int32_t* anc_out, const DevScalars* dev, int mode) {
   if (!*gate) return;
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   if ((j & ~63LL) >= n) return;  // whole wave past the end
-  uint64_t v = j < n ? mark[j] : 0;
-  const uint64_t c = carry[j >> 6];
-  v = wave_incl_max_u64(v > c ? v : c);
+  const uint32_t v = wave_incl_max_u32(max(j < n ? mark[j] : 0u, carry[j >> 6]));
   (void)lane;
   if (j >= n) return;
-  int32_t a = (int32_t)(uint32_t)v;
+  int32_t a = (int32_t)(v & idx);
   if (mode == 2) {  // multi-rank: slots outside [ra, rb) take received rows
     if (j < dev->ra) a = (int32_t)(-1 - j);
     else if (j >= dev->rb) a = (int32_t)(-1 - (dev->ra + (j - dev->rb)));
@@ -1666,7 +1681,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     run += q[k];
     // (a particle past n or of zero weight leaves run, hence the count, unchanged)
     const int64_t e_i = sys_count_w(&sd, N, run);
-    const uint64_t tagged = (r.mk.epoch << 32) | (uint64_t)(i0 + k);
+    const uint32_t tagged = r.mk.tag | (uint32_t)(i0 + k);
     if (e_i > s_i) r.mk.mark[s_i] = tagged;
     const int64_t g0 = (s_i + 63) >> 6, g1 = (e_i + 63) >> 6;  // groups g with 64 g in [s_i, e_i)
     const bool many = g1 - g0 > 2;
@@ -1679,7 +1694,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       const int L = __builtin_ctzll(bm);
       bm &= bm - 1;
       const int32_t a0 = __builtin_amdgcn_readlane((int32_t)g0, L), a1 = __builtin_amdgcn_readlane((int32_t)g1, L);
-      const uint64_t tg = (r.mk.epoch << 32) | (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(i0 + k), L);
+      const uint32_t tg = r.mk.tag | (uint32_t)__builtin_amdgcn_readlane((int32_t)(i0 + k), L);
       for (int32_t g = a0 + (threadIdx.x & 63); g < a1; g += 64) r.mk.cmark[g] = tg;
     }
     s_i = e_i;
@@ -2286,7 +2301,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     // (a particle past n or of zero weight leaves run, hence the count, unchanged)
     const int64_t s1 = sys_count_w(&sd, N, run);
     const int64_t l0 = clamp_own(s0) - own_lo, l1 = clamp_own(s1) - own_lo;
-    const uint64_t tagged = (r.mk.epoch << 32) | (uint64_t)i;
+    const uint32_t tagged = r.mk.tag | (uint32_t)i;
     if (l1 > l0) r.mk.mark[l0] = tagged;
     const int64_t g0 = (l0 + 63) >> 6, g1 = (l1 + 63) >> 6;  // local groups g with 64 g in [l0, l1)
     const bool many = g1 - g0 > 2;
@@ -2299,7 +2314,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
       const int L = __builtin_ctzll(bm);
       bm &= bm - 1;
       const int32_t a0 = __builtin_amdgcn_readlane((int32_t)g0, L), a1 = __builtin_amdgcn_readlane((int32_t)g1, L);
-      const uint64_t tg = (r.mk.epoch << 32) | (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)i, L);
+      const uint32_t tg = r.mk.tag | (uint32_t)__builtin_amdgcn_readlane((int32_t)i, L);
       for (int32_t g = a0 + (threadIdx.x & 63); g < a1; g += 64) r.mk.cmark[g] = tg;
     }
     if (spill && i < r.n) r.C[i] = run;

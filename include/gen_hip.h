@@ -364,6 +364,12 @@ int gh_debug_exchange_lists(int64_t n_global, int world, int rank, const uint64_
                             int* n_send, int* send_peer, uint64_t* send_bytes, int* n_recv, int* recv_peer,
                             uint64_t* recv_bytes);
 
+/* test hook: widen the ancestor field of the filter's 32-bit range marks to
+   `bits` (at least what the particle count needs, at most 31), which shortens
+   the epoch field, so that a short run crosses several epoch wraps (the marks
+   are cleared at each).  Only before the first resample is pending. */
+int gh_debug_mark_bits(gh_pf* pf, int bits);
+
 /* ---- importance sampling ---------------------------------------------------- */
 int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t seed,
               double* host_log_norm_weights /* may be NULL */, double* host_states /* may be NULL */,

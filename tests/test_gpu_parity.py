@@ -374,14 +374,47 @@ def test_kitagawa_large_tiles_bitexact(gh_ctx, n):
 @pytest.mark.parametrize("n", [1 << 20, (1 << 21) + 4097])
 def test_peaked_weights_huge_offspring_bitexact(gh_ctx, n):
     """var_y = 1e-10 puts nearly all the weight on one particle, with most of
-    the N offspring: its range's carries (more than 512 groups of 64 slots)
-    are written by the whole resample block, not one wave.  States and parents
-    bit-exact against the oracle at every step."""
+    the N offspring: its range's carries (thousands of 64-slot groups) are
+    written by its wave's store loop.  States and parents bit-exact against
+    the oracle at every step."""
     m = gen.KitagawaSSM(10.0, 1e-10)
     _, ys = m.simulate(4, np.random.default_rng(11))
     st, orc = run_both(m, ys, n, seed=13, thr=n)
     counts = np.bincount(st.parents, minlength=n)
-    assert counts.max() > 64 * 512  # the block-wide carry path ran
+    assert counts.max() > 64 * 512  # one particle's range covers > 512 groups
+    assert_lml_close(st, orc)
+
+
+@pytest.mark.parametrize("model,bits,loop", [("lg4", 30, "cbc"), ("lg4", 31, "cbc"), ("lg4", 30, "run"),
+                                             ("lg4", 31, "run"), ("kit", 30, "run"), ("kit", 31, "cbc")])
+def test_mark_epoch_wraps_bitexact(gh_ctx, model, bits, loop):
+    """The range marks are 32-bit words (epoch tag above the ancestor's index
+    bits); when the epoch field is used up the host clears the marks.  With
+    the index field widened to 30 / 31 bits the epoch field has 2 / 1 bits, so
+    a wrap comes every 3 / every resample: 12 resampling steps, call by call
+    and batched, one-particle and pair kernels, bit-exact against the oracle."""
+    m = gen.LinearGaussianSSM.benchmark(4) if model == "lg4" else gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(13, np.random.default_rng(3))
+    n = 20011
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=5)
+    _lib.check(_lib.load().gh_debug_mark_bits(st.h, bits))
+    orc = O.OraclePF(m, n, 5, O.SYSTEMATIC)
+    orc.init(ys[0])
+    if loop == "run":
+        gen.run_particle_filter(st, list(ys[1:]), n)
+    for t in range(2, len(ys) + 1):
+        if loop == "cbc":
+            assert gen.maybe_resample(st, n)
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {m.obs_address(t): ys[t - 1]})
+        assert orc.maybe_resample(n)[0]
+        orc.step(ys[t - 1])
+        if loop == "cbc":
+            assert np.array_equal(st.parents, orc.parents()), t
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(st.parents, orc.parents())
+    for t in (2, 7, 13):
+        assert np.array_equal(st.states(t).T, orc.trajectory(t)), t
     assert_lml_close(st, orc)
 
 

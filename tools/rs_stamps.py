@@ -36,3 +36,11 @@ rel = (a - t0) * 0.01  # wall_clock64 ticks at 100 MHz -> us
 names = {0: "start", 7: "max", 1: "decided", 2: "quantised", 3: "barrier", 4: "offsets", 5: "marks", 6: "end"}
 for k, nm in names.items():
     print(f"{nm:10s} min {rel[:, k].min():7.2f} med {np.median(rel[:, k]):7.2f} max {rel[:, k].max():7.2f} us")
+# the slowest blocks of the late phases, and each phase's own duration
+for k in (4, 5, 6):
+    top = np.argsort(rel[:, k])[::-1][:4]
+    print(f"{names[k]:10s} latest blocks " + ", ".join(f"{b} ({rel[b, k]:.2f})" for b in top))
+order = [0, 7, 1, 2, 3, 4, 5, 6]
+for a_, b_ in zip(order, order[1:]):
+    d = rel[:, b_] - rel[:, a_]
+    print(f"{names[a_]:>9s}->{names[b_]:10s} med {np.median(d):6.2f} max {d.max():6.2f} (block {int(d.argmax())}) us")
