@@ -15,8 +15,10 @@ the ancestor states on resample steps.
 
 Also reported:
   roofline     achieved HBM GB/s of the dominant kernel (k_step) from its
-               algorithmic bytes (16d+16 per particle-step, +4 on resample
-               steps) / its hipEvent-timed average duration on its stream;
+               algorithmic bytes (16d+16 per particle-step: on a resample
+               step the log-weight is not read, and the 4-byte range mark
+               read and the 4-byte ancestor record take its 8 bytes) / its
+               hipEvent-timed average duration on its stream;
                traffic = PMC HBM bytes per launch from profiles/ when present;
                step_frac = the same bytes per whole step / ms_per_step / peak.
   cpu_baseline the CPU oracle (C restatement of Gen's PF) on a bounded sample
@@ -303,7 +305,7 @@ def secondary_c4(gen, ctx, a):
     model = gen.KitagawaSSM(10.0, 1.0)  # examples/pmmh/run.jl:69 (var_x = 10, var_y = 1)
     n = 1 << 21
     r = pf_run(gen, ctx, None, 1, a, model, n, "k_step_pairs<KitModel,false>",
-               lambda n_res: 16 * 1 + 16 + 4.0 * n_res / max(1, a.steps))
+               lambda n_res: 16 * 1 + 16)
     pmc = pmc_profile("pmc_k_step_kitagawa.json")
     r["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
     out = {
@@ -522,7 +524,7 @@ def main(argv=None):
         # (the pair kernel on every rank whose first particle is a multiple of 128)
         kname = "k_step_pairs<KitModel,false>" if a.particles % 128 == 0 else "k_step<KitModel,false>"
     r = pf_run(gen, ctx, dist, world, a, model, a.particles, kname,
-               lambda n_res: 16 * d + 16 + 4.0 * n_res / max(1, a.steps))
+               lambda n_res: 16 * d + 16)
     # PMC HBM bytes per step-kernel launch of the profiled configs (tools/pmc_json.py)
     pmc = None
     if a.model == "lgssm" and a.d == 10 and a.particles == 1 << 20 and r["prop"] is None:

@@ -151,6 +151,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         )
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
+        if name.startswith("gh_debug_") and not hasattr(lib, name):
+            continue  # (test hooks: an older library built for an A/B run may lack one)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
