@@ -1018,6 +1018,22 @@ __device__ __forceinline__ int64_t sys_count_w(const DevScalars* dev, uint64_t N
 // the ancestor (a local particle index) in the low ceil(log2 n) bits, so the
 // newest epoch's words are the largest; the host clears both arrays when the
 // epoch field wraps.
+// sys_count_w as a 32-bit slot index (N < 2^31, as gh_pf_init enforces): the
+// marks loop's slot and group arithmetic then runs on 32-bit integers
+__device__ __forceinline__ int32_t sys_count_w32(const DevScalars* dev, uint32_t N, uint64_t X) {
+  const double v = fma((double)X, (double)N, -(double)dev->o) * dev->invS;
+  const double fl = floor(v);
+  const double fr = v - fl;
+  int32_t j = (int32_t)fmin(fmax(fl + 1.0, 0.0), (double)N);
+  const bool edge = X == 0 || X >= dev->S;
+  j = X == 0 ? 0 : (X >= dev->S ? (int32_t)N : j);
+  const bool near = !edge && !(fr > 0x1p-16 && fr < 1.0 - 0x1p-16);
+  if (__builtin_amdgcn_ballot_w64(near) != 0) {
+    if (near) j = (int32_t)sys_count_exact(dev, N, X);
+  }
+  return j;
+}
+
 struct MarkArgs {
   uint32_t* mark;     // [n slots] tagged ancestor at each range start
   uint32_t* cmark;    // [64-slot groups] tagged ancestor of the group's first slot
@@ -1669,25 +1685,25 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     commit();
     return;
   }
-  const uint64_t N = (uint64_t)r.mk.n_global;
-  int64_t s_i = sys_count(&sd, N, run);
+  const uint32_t N = (uint32_t)r.mk.n_global;  // < 2^31: 32-bit slots and groups
+  int32_t s_i = (int32_t)sys_count(&sd, N, run);
   // particle i owns the slots [s_i, e_i): a tagged mark at s_i, and the carry
   // of every 64-slot group that starts inside the range; a lane writes up to
-  // two carries itself, a longer range (a particle with > 64 offspring) gets
+  // two carries itself, a longer range (a particle with > 128 offspring) gets
   // its carries from the whole wave (one wave-wide store loop per such
   // particle, no block barrier)
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     run += q[k];
     // (a particle past n or of zero weight leaves run, hence the count, unchanged)
-    const int64_t e_i = sys_count_w(&sd, N, run);
+    const int32_t e_i = sys_count_w32(&sd, N, run);
     const uint32_t tagged = r.mk.tag | (uint32_t)(i0 + k);
     if (e_i > s_i) r.mk.mark[s_i] = tagged;
-    const int64_t g0 = (s_i + 63) >> 6, g1 = (e_i + 63) >> 6;  // groups g with 64 g in [s_i, e_i)
-    const bool many = g1 - g0 > 2;
+    const uint32_t g0 = ((uint32_t)s_i + 63u) >> 6, g1 = ((uint32_t)e_i + 63u) >> 6;  // groups g with 64 g in [s_i, e_i)
+    const bool many = g1 - g0 > 2u;
     if (!many) {
       if (g1 > g0) r.mk.cmark[g0] = tagged;
-      if (g1 > g0 + 1) r.mk.cmark[g0 + 1] = tagged;
+      if (g1 > g0 + 1u) r.mk.cmark[g0 + 1u] = tagged;
     }
     uint64_t bm = __builtin_amdgcn_ballot_w64(many);
     while (bm) {

@@ -25,12 +25,23 @@ st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=
 gen.run_particle_filter(st, list(ys[1:10]))
 ctx.synchronize()
 lib = _lib.load()
-buf = (ctypes.c_uint64 * (1024 * 8))()
+buf = (ctypes.c_uint64 * (1024 * 16))()
 lib.gh_debug_rs_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-_lib.check(lib.gh_debug_rs_stamps(buf, 1024 * 8))
+_lib.check(lib.gh_debug_rs_stamps(buf, 1024 * 16))
 grid = -(-n // (1024 * 4))  # IT = 4 (two blocks per CU at 2^21)
 print(f"{name} n={n} grid={grid}")
-a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 8)[:grid, :8].astype(np.int64)
+raw = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16)[:grid].astype(np.int64)
+a = raw[:, :8]
+waves = None
+if hasattr(lib, "gh_debug_rs_waves"):  # (the probe variants have no per-wave clocks)
+    wbuf = (ctypes.c_uint64 * (1024 * 16 * 4))()
+    lib.gh_debug_rs_waves.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    _lib.check(lib.gh_debug_rs_waves(wbuf, 1024 * 16 * 4))
+    waves = np.frombuffer(wbuf, dtype=np.uint64).reshape(1024, 16, 4)[:grid].astype(np.int64)
+if os.environ.get("GH_STAMPS_SAVE"):  # raw per-block clocks (and per-wave marks clocks) for offline analysis
+    np.save(os.environ["GH_STAMPS_SAVE"], raw)
+    if waves is not None:
+        np.save(os.environ["GH_STAMPS_SAVE"].replace(".npy", "_waves.npy"), waves)
 t0 = a[:, 0].min()
 rel = (a - t0) * 0.01  # wall_clock64 ticks at 100 MHz -> us
 names = {0: "start", 7: "max", 1: "decided", 2: "quantised", 3: "barrier", 4: "offsets", 5: "marks", 6: "end"}

@@ -31,13 +31,11 @@ VARIANTS = {
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
-EXTRA = {"rs_stamps": ["GH_RS_STAMPS"], "kstep_stamps": [],
-         "rs_nomarks": ["GH_RS_STAMPS", "GH_RS_NOMARKS"], "rs_noexact": ["GH_RS_STAMPS", "GH_RS_NOEXACT"]}
+EXTRA = {"rs_stamps": ["GH_RS_STAMPS"], "kstep_stamps": []}
 # variants whose hooks are not in the product sources: a patch applied to a copy
 PATCHES = {"rs_stamps": os.path.join(ROOT, "tools", "rs_stamps.patch"),
            "kstep_stamps": os.path.join(ROOT, "tools", "kstep_stamps.patch"),
-           "rs_nomarks": os.path.join(ROOT, "tools", "rs_probe.patch"),
-           "rs_noexact": os.path.join(ROOT, "tools", "rs_probe.patch")}
+}
 BENCH_ARGS = os.environ.get("GH_VARIANT_ARGS", "--steps 50").split()
 # GH_VARIANT_SCRIPT=tools/bench_pmmh.py times another workload with the same variants
 BENCH_SCRIPT = os.environ.get("GH_VARIANT_SCRIPT", "bench.py")
