@@ -190,15 +190,15 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return readlane63_u64(v);
 }
 // inclusive scans over the 64 lanes (lane order)
+// (lanes without a DPP source — shifted out of their row, or in a row outside
+// ROW_MASK — keep the "old" operand 0, which adds nothing: no lane conditions)
 __device__ __forceinline__ uint64_t wave_incl_sum_u64(uint64_t v) {
-  const int lane = threadIdx.x & 63, rl = lane & 15;
-  uint64_t t;
-  t = dpp_u64<0x111>(v, 0); if (rl >= 1) v += t;   // row_shr:1
-  t = dpp_u64<0x112>(v, 0); if (rl >= 2) v += t;   // row_shr:2
-  t = dpp_u64<0x114>(v, 0); if (rl >= 4) v += t;   // row_shr:4
-  t = dpp_u64<0x118>(v, 0); if (rl >= 8) v += t;   // row_shr:8
-  t = dpp_u64<0x142>(v, 0); if ((lane & 31) >= 16) v += t;  // row_bcast:15
-  t = dpp_u64<0x143>(v, 0); if (lane >= 32) v += t;         // row_bcast:31
+  v += dpp_u64<0x111>(v, 0);        // row_shr:1
+  v += dpp_u64<0x112>(v, 0);        // row_shr:2
+  v += dpp_u64<0x114>(v, 0);        // row_shr:4
+  v += dpp_u64<0x118>(v, 0);        // row_shr:8
+  v += dpp_u64<0x142, 0xa>(v, 0);   // row_bcast:15 into rows 1, 3
+  v += dpp_u64<0x143, 0xc>(v, 0);   // row_bcast:31 into rows 2, 3
   return v;
 }
 // lanes without a DPP source (row_shr shifted out, rows outside ROW_MASK) read 0

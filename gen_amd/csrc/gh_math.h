@@ -95,6 +95,20 @@ GH_HD uint64_t u53_bits(uint32_t a, uint32_t b) {
 GH_HD double u53(uint32_t a, uint32_t b) { return (double)u53_bits(a, b) * 0x1p-53; }
 
 // ------------------------------------------------------------------- exp
+// fma(a, b, c) for a constant c: on the device the constant goes to an SGPR
+// pair operand of one v_fma_f64 (the compiler otherwise writes it into the
+// destination VGPRs with two v_mov_b32 per Horner step and uses v_fmac);
+// the same correctly rounded fused operation either way.
+GH_HD double fma_c(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+#else
+  return fma(a, b, c);
+#endif
+}
+
 // Cody–Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-13 Taylor in r.
 GH_HD double ldexp_exact(double p, int k) {
   // p in [0.5, 2); multiply by 2^k without relying on libm ldexp.
@@ -137,17 +151,16 @@ GH_HD double gh_exp_nonpos(double x) {
   const double k = rint(xc * 0x1.71547652b82fep+0);
   double r = fma(-k, 0x1.62e42fee00000p-1, xc);
   r = fma(-k, 0x1.a39ef35793c76p-33, r);
-  double p = 0x1.6124613a86d09p-33;
-  p = fma(p, r, 0x1.1eed8eff8d898p-29);
-  p = fma(p, r, 0x1.ae64567f544e4p-26);
-  p = fma(p, r, 0x1.27e4fb7789f5cp-22);
-  p = fma(p, r, 0x1.71de3a556c734p-19);
-  p = fma(p, r, 0x1.a01a01a01a01ap-16);
-  p = fma(p, r, 0x1.a01a01a01a01ap-13);
-  p = fma(p, r, 0x1.6c16c16c16c17p-10);
-  p = fma(p, r, 0x1.1111111111111p-7);
-  p = fma(p, r, 0x1.5555555555555p-5);
-  p = fma(p, r, 0x1.5555555555555p-3);
+  double p = fma_c(0x1.6124613a86d09p-33, r, 0x1.1eed8eff8d898p-29);
+  p = fma_c(p, r, 0x1.ae64567f544e4p-26);
+  p = fma_c(p, r, 0x1.27e4fb7789f5cp-22);
+  p = fma_c(p, r, 0x1.71de3a556c734p-19);
+  p = fma_c(p, r, 0x1.a01a01a01a01ap-16);
+  p = fma_c(p, r, 0x1.a01a01a01a01ap-13);
+  p = fma_c(p, r, 0x1.6c16c16c16c17p-10);
+  p = fma_c(p, r, 0x1.1111111111111p-7);
+  p = fma_c(p, r, 0x1.5555555555555p-5);
+  p = fma_c(p, r, 0x1.5555555555555p-3);
   p = fma(p, r, 0x1.0000000000000p-1);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
