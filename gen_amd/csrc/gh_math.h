@@ -335,7 +335,7 @@ GH_HD void sincos_2pi_u32(uint32_t c, double* s, double* co, const double* tab =
   const double d = (double)di * 0x1.921fb54442d18p-30;
   const double d2 = d * d;
   double ps = fma(d2, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7);
-  ps = fma(d2, ps, -0x1.5555555555555p-3);
+  ps = fma_c(d2, ps, -0x1.5555555555555p-3);
   const double sd = fma(d * d2, ps, d);
   double pc = fma(d2, -0x1.6c16c16c16c17p-10, 0x1.5555555555555p-5);
   pc = fma(d2, pc, -0.5);
@@ -375,9 +375,9 @@ GH_HD double gh_log_unit(double x, const double* tab = nullptr) {
   const double r = fma(m, invc, -1.0);
   const double r2 = r * r;
   double q = fma(0x1.2492492492492p-3, r, -0x1.5555555555555p-3);  // 1/7, -1/6
-  q = fma(q, r, 0x1.999999999999ap-3);                            // 1/5
-  q = fma(q, r, -0x1.0p-2);                                       // -1/4
-  q = fma(q, r, 0x1.5555555555555p-2);                            // 1/3
+  q = fma_c(q, r, 0x1.999999999999ap-3);                          // 1/5
+  q = fma_c(q, r, -0x1.0p-2);                                     // -1/4
+  q = fma_c(q, r, 0x1.5555555555555p-2);                          // 1/3
   q = fma(q, r, -0x1.0p-1);                                       // -1/2
   const double kd = (double)k;
   const double h = fma(kd, 0x1.62e42fefa3800p-1, logc);           // ln2 high part: k ln2hi exact
