@@ -588,7 +588,7 @@ def main(argv=None):
         out["secondary"] = {"C4": c4, "C3": secondary_c3(gen, ctx, a), "C5": secondary_c5(gen, ctx, a)}
         if a.proposal == "default":
             out["secondary"]["call_by_call"] = secondary_call_by_call(gen, ctx, a, out["ms_per_step"])
-        if a.proposal == "default" and a.transport == "rccl":
+        if a.proposal == "default":  # (world 1: both transports, whatever --transport says)
             out["secondary"]["multirank_path"] = secondary_multirank_path(gen, a, out["ms_per_step"],
                                                                           c4["ms_per_step"])
     if rank == 0:
