@@ -67,7 +67,7 @@ struct DevScalars {
   int cfire, cerr;
   unsigned bar_gen;    // k_resample1 / k_rank_a grid barriers completed
   int64_t ra, rb;      // multi-rank: local slots [0, ra) and [rb, n) take received rows
-
+  unsigned fire_streak;  // k_resample1: consecutive resamples that fired (its speculation policy)
 };
 
 struct StepArgs {
@@ -1188,6 +1188,11 @@ constexpr int kRsItems = 4;
 constexpr int kRsTile = kRsBlock * kRsItems;  // particles per block
 constexpr int kRsPart = 4;                    // step partials per thread (nb_part <= 4096)
 constexpr int kRsPoll = 8;                    // polling waves x 64 tiles: grid <= 512
+#if defined(GH_SPEC_STREAK)  // A/B only
+constexpr unsigned kSpecStreak = GH_SPEC_STREAK;
+#else
+constexpr unsigned kSpecStreak = 8;           // resamples in a row that fired: speculative marks
+#endif
 
 struct Resample1Args {
   const double* pm;        // step-kernel block partials
@@ -1391,9 +1396,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   __shared__ uint64_t sbase;
   __shared__ unsigned sgen;
   __shared__ int sfail;  // the barrier wait timed out: write nothing
-  // barrier generation of this launch: read before this block publishes
+  __shared__ int sspec;  // speculative marks (see below)
+  // barrier generation of this launch and the fire streak: read before this
+  // block publishes (so before block 0 can commit this launch's decision)
   if (threadIdx.x == 0) {
     sgen = r.dev->bar_gen + 1;
+    sspec = r.dev->fire_streak >= kSpecStreak;
     sfail = 0;
   }
   // ---- fold the step partials (same order in every block: same result)
@@ -1508,6 +1516,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       r.stats_out[2] = S2;
       r.dev->pending = 0;
       commit_decision(r.d, dec, r.dev, 0);
+      r.dev->fire_streak = dec.fire ? r.dev->fire_streak + 1u : 0u;
       if (!posted) post_decision(r.hdec, r.htag, dec);
     }
   };
@@ -1560,6 +1569,11 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   __shared__ uint64_t spa[8], spb[8];
   __shared__ double spg[2][8];
   __shared__ uint64_t su53;
+  // sums_in_pass after a run of resamples that all fired (kSpecStreak): the
+  // blocks write the marks without waiting for the weight sums, and block 0
+  // reads them and takes the decision after its marks; a resample that then
+  // does not fire leaves marks no step reads
+  const bool spec = sums && sspec;  // (grid-uniform)
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (threadIdx.x == 8 * 64) {  // a non-polling wave draws the systematic offset's uniform meanwhile
@@ -1587,7 +1601,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      ok = !mine || !sums || timed_out;  // (a timed-out wave does not wait a second time)
+      ok = !mine || !sums || spec || timed_out;  // (a timed-out wave does not wait a second time)
       for (unsigned spins = 0;; ++spins) {
         if (!ok) {
           v1 = ld_sc1(&r.ts1[b]);
@@ -1633,7 +1647,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       sS[0] = g1;
       sS[1] = g2;
       sfire = (g1 * g1) / g2 < r.d.thr;
-      if (blockIdx.x == 0 && !sfail) {
+      if (blockIdx.x == 0 && !sfail && !spec) {
         S1 = g1;
         S2 = g2;
         post_decision(r.hdec, r.htag, decision());
@@ -1667,7 +1681,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // grid never started): the totals are partial.  The block leaves without
   // marks or decision; the error surfaces as GH_E_STATE at the next sync.
   if (sfail) return;
-  if (sums) {
+  if (sums && !spec) {
     S1 = sS[0];
     S2 = sS[1];
     if (!sfire) {
@@ -1675,6 +1689,49 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       return;
     }
   }
+  // speculative: block 0 reads the tile sums and takes the decision after
+  // its marks or CDF
+  auto decide_late = [&]() {
+    if (!spec || blockIdx.x != 0) return;  // (block-uniform)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (w < 8) {
+      const unsigned b = (unsigned)(w * 64 + lane);
+      const bool mine = b < gridDim.x;
+      uint64_t v1 = ld_sc1(&r.ts1[mine ? b : 0u]);  // (every lane: no merged values)
+      uint64_t v2 = ld_sc1(&r.ts2[mine ? b : 0u]);
+      bool ok = !mine || ((v1 & kTag) == par && (v2 & kTag) == par);
+      for (unsigned spins = 0; __builtin_amdgcn_ballot_w64(!ok) != 0; ++spins) {  // (rarely taken)
+        if (spins == (1u << 22)) {
+          r.dev->error = 7;  // GH_E_STATE
+          sfail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (!ok) {
+          v1 = ld_sc1(&r.ts1[b]);
+          v2 = ld_sc1(&r.ts2[b]);
+        }
+        ok = ok || ((v1 & kTag) == par && (v2 & kTag) == par);
+      }
+      const double g1 = wave_sum(mine ? as_f64(v1 & ~kTag) : 0.0);
+      const double g2 = wave_sum(mine ? as_f64(v2 & ~kTag) : 0.0);
+      if (lane == 0) {
+        spg[0][w] = g1;
+        spg[1][w] = g2;
+      }
+    }
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      double g1 = 0.0, g2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g1 += spg[0][k];
+        g2 += spg[1][k];
+      }
+      S1 = g1;
+      S2 = g2;
+    }
+  };
   uint64_t run = sbase + incl - tsum;
   if (!MARKS) {
 #pragma unroll
@@ -1682,7 +1739,8 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       run += q[k];
       if (i0 + k < r.n) r.C[i0 + k] = run;
     }
-    commit();
+    decide_late();
+    if (!sfail) commit();
     return;
   }
   const uint32_t N = (uint32_t)r.mk.n_global;  // < 2^31: 32-bit slots and groups
@@ -1715,7 +1773,8 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     s_i = e_i;
   }
-  commit();
+  decide_late();
+  if (!sfail) commit();
 }
 
 // ------------------------------------------------ multi-rank resample (R > 1)

@@ -194,6 +194,40 @@ def test_batched_run_chunks_and_thresholds(gh_ctx, model):
     assert_lml_close(st, orc)
 
 
+@pytest.mark.parametrize("model", ["lg4", "kit"])
+def test_speculative_marks_then_no_fire(gh_ctx, model):
+    """After 8 resamples in a row that fired, the batched loop's fused resample
+    writes the marks before it knows the decision (block 0 decides after its
+    marks).  Runs of always-fire steps build that streak, then steps that do
+    not fire (threshold 0) and a low threshold follow while speculating, then
+    more resamples: decisions, states, weights and parents bit-exact against
+    the oracle (a resample that does not fire leaves marks no step reads)."""
+    m = gen.LinearGaussianSSM.benchmark(4) if model == "lg4" else gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(26, np.random.default_rng(21))
+    n = 70001
+    chunks = [(10, n), (2, 0.0), (9, n), (1, n / 20), (3, None)]
+    assert sum(c for c, _ in chunks) == len(ys) - 1
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=31)
+    orc = O.OraclePF(m, n, 31, O.SYSTEMATIC)
+    orc.init(ys[0])
+    t, dids = 2, []
+    for c, thr in chunks:
+        gen.run_particle_filter(st, list(ys[t - 1 : t - 1 + c]), thr)
+        for _ in range(c):
+            dids.append(orc.maybe_resample(thr)[0])
+            orc.step(ys[t - 1])
+            t += 1
+    _, did = st.ess_history()
+    assert list(did[: len(ys) - 1]) == [bool(x) for x in dids]
+    assert not any(dids[10:12]) and all(dids[:10]) and all(dids[12:21])
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(st.parents, orc.parents())
+    for tt in (5, 12, 13, 22, 26):
+        assert np.array_equal(st.states(tt).T, orc.trajectory(tt)), tt
+    assert_lml_close(st, orc)
+
+
 def test_timed_launches_change_nothing(gh_ctx):
     """The bench's kernel timing (start/stop events on the step kernel's own
     launch, created without the system-scope fence) must not change the
