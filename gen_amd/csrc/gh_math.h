@@ -94,6 +94,30 @@ GH_HD uint64_t u53_bits(uint32_t a, uint32_t b) {
 }
 GH_HD double u53(uint32_t a, uint32_t b) { return (double)u53_bits(a, b) * 0x1p-53; }
 
+// ------------------------------------------------------------ a / 20
+// a / 20.0 exactly as IEEE division rounds it: the product with y = RN(1/20)
+// and two FMA corrections — the first leaves the quotient within an ulp, the
+// second (Markstein's theorem: y correctly rounded, q faithful, the residual
+// a - 20 q exact) rounds it correctly — five operations instead of the
+// division's scale / reciprocal / fix-up sequence (the nonlinear SSM's
+// observation mean x^2 / 20).  Outside [2^-1000, 2^1000] in magnitude (where
+// the theorem's range conditions could fail: never for the model's states)
+// and for 0, inf and NaN the division itself.
+GH_HD double div20(double a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double m = fabs(a);
+  if (!(m >= 0x1p-1000 && m <= 0x1p1000)) return a / 20.0;
+  const double y = 0.05;  // RN(1/20)
+  double q = a * y;
+  double r = fma(-20.0, q, a);
+  q = fma(r, y, q);
+  r = fma(-20.0, q, a);
+  return fma(r, y, q);
+#else
+  return a / 20.0;
+#endif
+}
+
 // ------------------------------------------------------------------- exp
 // fma(a, b, c) for a constant c: on the device the constant goes to an SGPR
 // pair operand of one v_fma_f64 (the compiler otherwise writes it into the

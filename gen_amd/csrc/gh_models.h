@@ -509,7 +509,7 @@ struct KitModel {
 
   __device__ static double obs(const Params& p, const StepObs& o, double x) {
     if (!o.present) return 0.0;
-    const double diff = o.v[0] - x * x / 20.0;
+    const double diff = o.v[0] - div20(x * x);
     return -(diff * diff) * p.inv2vy + p.csty;
   }
   __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return obs(p, o, x[0]); }
@@ -532,7 +532,7 @@ struct KitModel {
                                    double* y, int64_t, const double* tab) {
     double z0, z1;
     normal_pair(rng_block(seed, pid, t, STREAM_SIM, kSimObsDraw), &z0, &z1, tab);
-    const double m = x[0] * x[0] / 20.0;
+    const double m = div20(x[0] * x[0]);
     y[0] = m + p.sy * z0;
     const double diff = y[0] - m;
     return -(diff * diff) * p.inv2vy + p.csty;

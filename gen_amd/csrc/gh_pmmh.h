@@ -124,7 +124,7 @@ __device__ double pmmh_filter(const PmmhArgs& a, PmmhShared& sh, uint64_t c, uin
   const double invN = 1.0 / (double)N;
   const int shift = quant_shift((uint64_t)N);
   auto obs = [&](double y, double x) {
-    const double diff = y - x * x / 20.0;
+    const double diff = y - div20(x * x);
     return -(diff * diff) * inv2vy + csty;
   };
   // generate: x_1 ~ normal(0, 5), weight = emission logpdf (pf.jl:23-27)
