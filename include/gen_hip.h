@@ -427,7 +427,8 @@ int gh_coal_destroy(gh_coal* h);
 const char* gh_last_error(void);
 const char* gh_version(void);
 /* device self-test: evaluates gh_exp/gh_log/sqrt/div/normals on n inputs on the
-   GPU so tests can compare them bit-for-bit with the CPU oracle */
+   GPU so tests can compare them bit-for-bit with the CPU oracle (out_div: the
+   even entries in[i] / in[i+1], the odd ones the models' in[i] / 20) */
 int gh_selftest_math(gh_ctx* ctx, int64_t n, const double* in, double* out_exp, double* out_log,
                      double* out_sqrt, double* out_div);
 /* Box–Muller stages for n word triples (a, b, c): out[4i..4i+3] =
