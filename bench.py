@@ -324,6 +324,19 @@ def secondary_c4(gen, ctx, a):
     return out
 
 
+def peer_probe(gen, ctx, world):
+    """A few always-resampling steps of a small filter on the peer transport
+    (rows cross ranks every step); returns the log-ML as an exact hex string."""
+    m = gen.LinearGaussianSSM.benchmark(4)
+    _, ys = m.simulate(5, np.random.default_rng(5))
+    n = 2048 * world
+    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=7, ctx=ctx)
+    gen.run_particle_filter(st, list(ys[1:]), float(n))
+    lml = float(gen.log_ml_estimate(st)).hex()
+    st.close()
+    return lml
+
+
 def secondary_multirank_path(gen, a, c2_ms, c4_ms):
     """The multi-rank code path timed on this one GPU (gh_ctx_force_multirank:
     a one-rank RCCL communicator): per step the shards' and the records'
@@ -500,6 +513,19 @@ def main(argv=None):
                 ok = 0
             oks = [None] * world
             dist.all_gather_object(oks, ok)
+            if all(oks):
+                # a short filter over the mapped mailboxes (every wait on the
+                # device is bounded, so a mapping that does not carry stores
+                # between these GPUs errors out instead of hanging): the ranks
+                # must finish and agree on the log-ML bit for bit
+                probe = None
+                try:
+                    probe = peer_probe(gen, ctx, world)
+                except Exception as e:
+                    print(f"rank {rank}: peer transport probe failed ({e}); RCCL instead", file=sys.stderr, flush=True)
+                probes = [None] * world
+                dist.all_gather_object(probes, probe)
+                oks = [p is not None and p == probes[0] for p in probes]
             if not all(oks):
                 # (a rank whose peer context exists keeps it open: its destroy
                 # would wait for the ranks that have none)
