@@ -851,6 +851,14 @@ struct gh_pf {
   double* rows_send = nullptr;    // [send_cap][D+1] rows this rank sends
   int32_t* xanc = nullptr;        // [send_cap] local ancestors of the sent rows
   int64_t send_cap = 0;
+  // multinomial on R ranks (exchange_states_mn): per global slot its key (the
+  // rank holding its target), its rank among the range's slots with that key
+  // and its local ancestor when the key is this rank; per-block key counts
+  int32_t* mn_key = nullptr;
+  int32_t* mn_pos = nullptr;
+  int32_t* mn_anc = nullptr;
+  int32_t* mn_bcnt = nullptr;
+  int32_t* mn_boff = nullptr;
   int send_grows = 0;              // resamples whose rows overflowed the bounded send buffer
   int64_t* gparent = nullptr;     // [n] global parent ids of the last exchange
   hipStream_t aux = nullptr;      // multi-rank: side stream (the plan's D2H read, the row exchange)
@@ -1050,6 +1058,7 @@ static void pf_free(gh_pf* pf) {
   hipFree(pf->ps2); hipFree(pf->dev); hipFree(pf->tsum); hipFree(pf->stats_all); hipFree(pf->totals_all);
   hipFree(pf->ess_hist); hipFree(pf->res_hist); hipFree(pf->anc_scratch);
   hipFree(pf->rows_recv); hipFree(pf->rows_send); hipFree(pf->xanc); hipFree(pf->gparent);
+  hipFree(pf->mn_key); hipFree(pf->mn_pos); hipFree(pf->mn_anc); hipFree(pf->mn_bcnt); hipFree(pf->mn_boff);
   hipFree(pf->acc_count); hipFree(pf->pin); hipFree(pf->amax);
   hipFree(pf->amax_all); hipFree(pf->rec); hipFree(pf->recs_all); hipFree(pf->qlin);
   if (pf->aux) hipStreamDestroy(pf->aux);
@@ -1529,8 +1538,10 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pick_resample_tiles(pf, n);
   ALLOC(pf->amax, sizeof(uint64_t) * 2 * kAmaxShards * kAmaxStride);
   if (mr(ctx)) {
-    if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC)
-      return fail(set_err(GH_E_INVAL, "multi-rank filters use systematic resampling"));
+    if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC && (ctx->peer || ctx->world > kMaxRanks))
+      return fail(set_err(GH_E_INVAL, "multinomial resampling on R ranks needs the RCCL or host transport and "
+                                      "at most %d ranks (the peer transport's rows move inside the systematic "
+                                      "kernels only)", kMaxRanks));
     if (!ctx->peer) {
       ALLOC(pf->rows_recv, sizeof(double) * (pf->D + 1) * n);
     } else {
@@ -1817,6 +1828,7 @@ static int materialize_marks(gh_pf* pf) {
 
 // multi-rank exchange of ancestor states; defined below
 static int exchange_states(gh_pf* pf, int32_t* anc_out);
+static int exchange_states_mn(gh_pf* pf, int32_t* anc_out);
 
 static void sys_plan(int64_t N, int R, int q, const uint64_t* totals, uint64_t o, int64_t* send_lo,
                      int64_t* send_hi, int64_t* recv_lo, int64_t* recv_hi);
@@ -2291,7 +2303,8 @@ static int resample_enqueue(gh_pf* pf, double thr, bool want_decision) {
                          pf->anc_scratch, anc_target, n);
   } else {
     if (second) return set_err(GH_E_STATE, "multi-rank: maybe_resample twice without a step is not supported");
-    CHECK(exchange_states(pf, anc_target));
+    if (pf->opts.resampler == GH_RESAMPLE_MULTINOMIAL) CHECK(exchange_states_mn(pf, anc_target));
+    else CHECK(exchange_states(pf, anc_target));
   }
   HIP_TRY(hipGetLastError());
   pf->resample_calls++;
@@ -3503,6 +3516,163 @@ static int exchange_states(gh_pf* pf, int32_t* anc_out) {
     hipLaunchKernelGGL(k_global_parents, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, anc_out, pf->n,
                        pf->lo, pf->rows_recv, D, pf->gparent);
   HIP_TRY(hipGetLastError());
+  // the received rows, kept as the next step's genealogy record (as the split
+  // step's part 2 keeps them on the fused path)
+  if (pf->opts.record_history && roff > 0) {
+    double* dst = nullptr;
+    CHECK(rhist_reserve(pf, t + 1, roff, &dst));
+    if (dst) HIP_TRY(hipMemcpyAsync(dst, pf->rows_recv, row_bytes * (size_t)roff, hipMemcpyDeviceToDevice, pf->s));
+  }
+  return GH_OK;
+}
+
+// Multinomial resampling on R ranks.  Every rank evaluates the
+// targets of all N slots (one Philox block each) and their keys; the rank
+// holding a slot's target sends that slot's ancestor row to the slot's owner,
+// both ranks ordering those rows by slot, so no index travels.  One host round
+// trip (the decision, the totals and the per-block key counts), one grouped
+// send/recv of rows.  The same ancestors as k_search on one rank.
+static int exchange_states_mn(gh_pf* pf, int32_t* anc_out) {
+  gh_ctx* c = pf->ctx;
+  const int R = c->world, q = c->rank;
+  const int D = pf->D;
+  const int t = pf->t;
+  const int64_t N = pf->n_global;
+  DevScalars h;
+  std::vector<uint64_t> tot(R);
+  HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipMemcpyAsync(tot.data(), pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  if (h.error) return set_err(h.error, dev_error_msg(h.error));
+  if (!h.fire) return GH_OK;
+  // the slot ranges (= the particle ranges) and their blocks
+  std::vector<int64_t> lo(R + 1), boff0(R + 1);
+  for (int r = 0; r <= R; ++r) lo[r] = split_lo(N, r, R);
+  boff0[0] = 0;
+  for (int r = 0; r < R; ++r) boff0[r + 1] = boff0[r] + (lo[r + 1] - lo[r] + kBlock - 1) / kBlock;
+  const int64_t nb = boff0[R];
+  if (!pf->mn_key) {
+    if (hipMalloc(&pf->mn_key, sizeof(int32_t) * N) != hipSuccess || hipMalloc(&pf->mn_pos, sizeof(int32_t) * N) != hipSuccess ||
+        hipMalloc(&pf->mn_anc, sizeof(int32_t) * N) != hipSuccess ||
+        hipMalloc(&pf->mn_bcnt, sizeof(int32_t) * nb * R) != hipSuccess ||
+        hipMalloc(&pf->mn_boff, sizeof(int32_t) * nb * R) != hipSuccess)
+      return set_err(GH_E_NOMEM, "multinomial exchange: %lld slots", (long long)N);
+  }
+  const int* gate = &pf->dev->fire;
+  for (int r = 0; r < R; ++r) {
+    const int64_t n_r = lo[r + 1] - lo[r];
+    if (n_r <= 0) continue;
+    MnArgs m{};
+    m.slot_lo = lo[r];
+    m.n_slots = n_r;
+    m.seed = pf->seed;
+    m.t = (uint32_t)t;
+    m.totals = pf->totals_all;
+    m.R = R;
+    m.key = pf->mn_key + lo[r];
+    m.bcnt = pf->mn_bcnt + boff0[r] * R;
+    hipLaunchKernelGGL(k_mn_keys, dim3((unsigned)((n_r + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s, m, gate,
+                       (const DevScalars*)pf->dev);
+  }
+  HIP_TRY(hipGetLastError());
+  std::vector<int32_t> cnt((size_t)(nb * R)), off((size_t)(nb * R));
+  HIP_TRY(hipMemcpyAsync(cnt.data(), pf->mn_bcnt, sizeof(int32_t) * nb * R, hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  // per range and key: exclusive scan over the range's blocks; the totals are
+  // the rows rank q sends to range r's owner (key q) and receives (range q)
+  std::vector<int64_t> kcount((size_t)R * R, 0);  // [range][key]
+  for (int r = 0; r < R; ++r)
+    for (int k = 0; k < R; ++k) {
+      int64_t run = 0;
+      for (int64_t b = boff0[r]; b < boff0[r + 1]; ++b) {
+        off[(size_t)(b * R + k)] = (int32_t)run;
+        run += cnt[(size_t)(b * R + k)];
+      }
+      kcount[(size_t)r * R + k] = run;
+    }
+  HIP_TRY(hipMemcpyAsync(pf->mn_boff, off.data(), sizeof(int32_t) * nb * R, hipMemcpyHostToDevice, pf->s));
+  GateArgs g;
+  g.gate = &pf->dev->fire;
+  g.M = &pf->dev->M;
+  g.zero_w = &pf->dev->pending;
+  g.shift = quant_shift((uint64_t)N);
+  SearchArgs sa{};
+  sa.C = pf->C;
+  sa.n_cdf = pf->n;
+  sa.n_global = N;
+  sa.seed = pf->seed;
+  sa.t = (uint32_t)t;
+  sa.mode = SEARCH_MULTINOMIAL;
+  sa.anc_old = nullptr;
+  sa.own_only = 1;
+  int64_t n_send = 0;
+  for (int r = 0; r < R; ++r)
+    if (r != q) n_send += kcount[(size_t)r * R + q];
+  if (n_send > pf->send_cap) {
+    HIP_TRY(hipStreamSynchronize(pf->s));
+    hipFree(pf->rows_send);
+    hipFree(pf->xanc);
+    pf->rows_send = nullptr;
+    pf->xanc = nullptr;
+    pf->send_cap = 0;
+    const int64_t cap = n_send + n_send / 4 + 64;
+    if (hipMalloc(&pf->rows_send, sizeof(double) * (D + 1) * cap) != hipSuccess ||
+        hipMalloc(&pf->xanc, sizeof(int32_t) * cap) != hipSuccess)
+      return set_err(GH_E_NOMEM, "exchange: cannot allocate %lld send rows", (long long)cap);
+    pf->send_cap = cap;
+  }
+  std::vector<CommMsg> sends, recvs;
+  const size_t row_bytes = sizeof(double) * (D + 1);
+  int64_t soff = 0;
+  for (int r = 0; r < R; ++r) {
+    const int64_t n_r = lo[r + 1] - lo[r];
+    if (n_r <= 0) continue;
+    const unsigned grid = (unsigned)((n_r + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_mn_pos, dim3(grid), dim3(kBlock), 0, pf->s, (const int32_t*)pf->mn_key + lo[r], n_r,
+                       (const int32_t*)pf->mn_boff + boff0[r] * R, R, pf->mn_pos + lo[r], gate);
+    sa.slot_lo = lo[r];
+    sa.n_slots = n_r;
+    sa.anc_out = pf->mn_anc + lo[r];
+    hipLaunchKernelGGL(k_search, dim3(grid), dim3(kBlock), 0, pf->s, sa, g, pf->dev);
+    if (r == q) continue;
+    const int64_t s_r = kcount[(size_t)r * R + q];
+    if (s_r > 0) {
+      hipLaunchKernelGGL(k_mn_send, dim3(grid), dim3(kBlock), 0, pf->s, (const int32_t*)pf->mn_anc + lo[r],
+                         (const int32_t*)pf->mn_pos + lo[r], n_r, pf->xanc + soff, gate);
+      sends.push_back({r, pf->rows_send + soff * (D + 1), (size_t)s_r * row_bytes});
+      soff += s_r;
+    }
+  }
+  if (n_send > 0)
+    hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)((n_send + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s,
+                       pf->xanc, n_send, slot_x(pf, t), D, pf->lo, pf->rows_send);
+  MnRecvOff ro{};
+  int64_t n_recv = 0;
+  for (int k = 0; k < R; ++k) {
+    ro.off[k] = (int32_t)n_recv;
+    const int64_t c_k = kcount[(size_t)q * R + k];
+    if (k == q || c_k <= 0) continue;
+    recvs.push_back({k, pf->rows_recv + n_recv * (D + 1), (size_t)c_k * row_bytes});
+    n_recv += c_k;
+  }
+  if (pf->n > 0)
+    hipLaunchKernelGGL(k_mn_recv, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s,
+                       (const int32_t*)pf->mn_anc + pf->lo, (const int32_t*)pf->mn_key + pf->lo,
+                       (const int32_t*)pf->mn_pos + pf->lo, pf->n, ro, anc_out, gate);
+  HIP_TRY(hipGetLastError());
+  CHECK(comm_exchange(c, sends, recvs, pf->s));
+  if (pf->n > 0)
+    hipLaunchKernelGGL(k_global_parents, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s, anc_out, pf->n,
+                       pf->lo, pf->rows_recv, D, pf->gparent);
+  HIP_TRY(hipGetLastError());
+  // the received rows are the next step's parents on other ranks: kept as
+  // that step's genealogy record (rows_recv is overwritten by the next resample)
+  if (pf->opts.record_history && n_recv > 0) {
+    double* dst = nullptr;
+    CHECK(rhist_reserve(pf, t + 1, n_recv, &dst));
+    if (dst)
+      HIP_TRY(hipMemcpyAsync(dst, pf->rows_recv, row_bytes * (size_t)n_recv, hipMemcpyDeviceToDevice, pf->s));
+  }
   return GH_OK;
 }
 

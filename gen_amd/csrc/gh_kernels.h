@@ -2527,6 +2527,95 @@ static __global__ __launch_bounds__(kBlock) void k_search(SearchArgs s, GateArgs
   s.anc_out[j] = (zero && s.anc_old) ? s.anc_old[a] : (int32_t)a;
 }
 
+// ------------------------------------------------- multinomial on R ranks
+// DESIGN.md §7.  Slot j's multinomial target T_j (its own RESAMPLE draw scaled
+// by the global total: k_search's target on one rank) lies in the CDF range of
+// one rank, the slot's key.  k_mn_keys writes the keys of a slot range and, per
+// 256-slot block, how many of the block's slots carry each key; k_mn_pos ranks
+// every slot among the earlier slots of the range with its key (stable, from
+// the per-block offsets the host scans).  The rank that holds a slot's target
+// sends that slot's ancestor row to the rank that owns the slot, in slot order.
+struct MnArgs {
+  int64_t slot_lo;          // global index of the range's first slot
+  int64_t n_slots;
+  uint64_t seed;
+  uint32_t t;
+  const uint64_t* totals;   // the R all-gathered rank totals
+  int R;
+  int32_t* key;             // [n_slots] the rank holding the slot's target
+  int32_t* bcnt;            // [blocks][R] slots per key in each block
+};
+static __global__ __launch_bounds__(kBlock) void k_mn_keys(MnArgs m, const int* gate, const DevScalars* dev) {
+  if (!*gate) return;
+  __shared__ int hist[kMaxRanks];
+  for (int k = threadIdx.x; k < m.R; k += kBlock) hist[k] = 0;
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < m.n_slots) {
+    const u32x4 w = rng_block(m.seed, (uint64_t)(m.slot_lo + j), m.t, STREAM_RESAMPLE, 0);
+    const uint64_t T = scale_u53(u53_bits(w.x, w.y), dev->S);  // < S
+    uint64_t base = 0;
+    int k = 0;
+    for (; k < m.R - 1; ++k) {  // (an empty rank's range holds no target)
+      const uint64_t nb = base + m.totals[k];
+      if (T < nb) break;
+      base = nb;
+    }
+    m.key[j] = k;
+    atomicAdd(&hist[k], 1);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < m.R; k += kBlock) m.bcnt[(int64_t)blockIdx.x * m.R + k] = hist[k];
+}
+// pos[j] = the block's offset for key[j] + the slots of the block before j
+// with that key (per wave: one ballot per distinct key of the wave)
+static __global__ __launch_bounds__(kBlock) void k_mn_pos(const int32_t* key, int64_t n, const int32_t* boff, int R,
+                                                         int32_t* pos, const int* gate) {
+  if (!*gate) return;
+  __shared__ int wcnt[kBlock / 64][kMaxRanks];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < (kBlock / 64) * kMaxRanks; i += kBlock) wcnt[i / kMaxRanks][i % kMaxRanks] = 0;
+  __syncthreads();
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int k = j < n ? key[j] : -1;
+  int rl = 0;
+  uint64_t todo = __builtin_amdgcn_ballot_w64(k >= 0);
+  while (todo) {
+    const int L = __builtin_ctzll(todo);
+    const int kk = __builtin_amdgcn_readlane(k, L);
+    const uint64_t mk = __builtin_amdgcn_ballot_w64(k == kk);
+    if (k == kk) rl = __builtin_popcountll(mk & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[w][kk] = __builtin_popcountll(mk);
+    todo &= ~mk;
+  }
+  __syncthreads();
+  if (k >= 0) {
+    int before = 0;
+    for (int v = 0; v < w; ++v) before += wcnt[v][k];
+    pos[j] = boff[(int64_t)blockIdx.x * R + k] + before + rl;
+  }
+}
+// sender: the slots of a range that take one of this rank's particles, in slot
+// order (pos among them), with their local ancestors (k_search, own_only)
+static __global__ __launch_bounds__(kBlock) void k_mn_send(const int32_t* anc, const int32_t* pos, int64_t n,
+                                                          int32_t* xanc, const int* gate) {
+  if (!*gate) return;
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < n && anc[j] >= 0) xanc[pos[j]] = anc[j];
+}
+struct MnRecvOff {
+  int32_t off[kMaxRanks];  // first received row from each rank (rows_recv in rank order)
+};
+// receiver: this rank's slots take a local ancestor or received row
+// off[key] + pos (the slot's rank among this rank's slots with that key)
+static __global__ __launch_bounds__(kBlock) void k_mn_recv(const int32_t* anc_loc, const int32_t* key,
+                                                          const int32_t* pos, int64_t n, MnRecvOff ro,
+                                                          int32_t* anc_out, const int* gate) {
+  if (!*gate) return;
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j < n) anc_out[j] = anc_loc[j] >= 0 ? anc_loc[j] : -1 - (ro.off[key[j]] + pos[j]);
+}
+
 // ------------------------------------------------- multi-rank exchange
 // Rows sent to other ranks: row j = (x[:, anc[j]], global id of anc[j]).
 static __global__ __launch_bounds__(kBlock) void k_pack_rows(const int32_t* anc, int64_t rows, const double* x,

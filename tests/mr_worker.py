@@ -59,6 +59,7 @@ def main():
                    "at t = 4 (the step then reads materialised ancestors naming received rows)")
     p.add_argument("--genealogy", action="store_true", help="also save trajectories at t = 1, 5, T, the score "
                    "columns and 500 sample_unweighted_traces indices (collective queries)")
+    p.add_argument("--resampler", default="systematic", help="systematic or multinomial")
     p.add_argument("--out", required=True)
     a = p.parse_args()
 
@@ -84,7 +85,7 @@ def main():
     m = build_model(a.model)
     _, ys = m.simulate(a.T, np.random.default_rng(5))
     addr = m.obs_address
-    st = gen.initialize_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, seed=a.seed)
+    st = gen.initialize_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, seed=a.seed, resampler=a.resampler)
     if a.rejuv:
         gen.rejuvenate(st, a.rejuv)
     did = []

@@ -307,13 +307,13 @@ def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr
     assert abs(lml - ref.log_ml_estimate()) <= 1e-9 * abs(ref.log_ml_estimate())
 
 
-def _check_against_oracle(out, model, R, n, T, seed, thr):
+def _check_against_oracle(out, model, R, n, T, seed, thr, resampler="systematic"):
     from oracle import oracle as O
     from tests.mr_worker import build_model
 
     m = build_model(model)
     _, ys = m.simulate(T, np.random.default_rng(5))
-    ref = O.run_pf(m, ys, n, seed, thr=thr)
+    ref = O.run_pf(m, ys, n, seed, thr=thr, resampler=O.MULTINOMIAL if resampler == "multinomial" else O.SYSTEMATIC)
     parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
     states = np.concatenate([p["states"] for p in parts], axis=0)  # [n, d]
     assert np.array_equal(states.T, ref.state())
@@ -381,7 +381,28 @@ def test_gpu_multirank_peer_transport(tmp_path, model, R, thr, n, batched):
     _check_against_oracle(out, model, R, n, T, seed, thr)
 
 
-def _check_genealogy(out, model, R, n, T, seed, thr, batched):
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,model,R,thr,n,batched", [
+    ("gloo", "lg4", 2, None, 3001, False), ("gloo", "kit", 3, 1e9, 4003, False), ("gloo", "kit_sharp", 4, None, 4003, True),
+    ("gloo", "lg10", 2, 3001.0, 3001, True), ("rccl1", "lg4", 1, 1e9, 3001, False)])
+def test_gpu_multirank_multinomial(tmp_path, gh_ctx, transport, model, R, thr, n, batched):
+    """Multinomial resampling (the reference's own resampler, Categorical draws
+    per slot, particle_filter.jl:200) on R ranks: every rank evaluates the
+    targets of all slots, the rank holding a slot's target sends that slot's
+    ancestor row to its owner, both ordering by slot.  States, weights, parents
+    and the genealogy queries equal the single-rank multinomial oracle bit for
+    bit (log-ML 1e-9), call by call and batched."""
+    out = str(tmp_path / "mn")
+    T, seed = 8, 9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--transport", transport,
+                  *(["--device", "0"] if transport == "rccl1" else []), *(["--batched"] if batched else []),
+                  "--resampler", "multinomial", "--genealogy", "--out", out], R, timeout=400)
+    _check_against_oracle(out, model, R, n, T, seed, thr, resampler="multinomial")
+    _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="multinomial")
+
+
+def _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="systematic"):
     """Trajectories at t = 1, 5, T and the score columns of the gathered shards
     equal the single-rank oracle bit for bit; the 500 sample_unweighted_traces
     indices equal a one-rank GPU filter's (the same global integer CDF)."""
@@ -391,7 +412,7 @@ def _check_genealogy(out, model, R, n, T, seed, thr, batched):
 
     m = build_model(model)
     _, ys = m.simulate(T, np.random.default_rng(5))
-    ref = O.run_pf(m, ys, n, seed, thr=thr)
+    ref = O.run_pf(m, ys, n, seed, thr=thr, resampler=O.MULTINOMIAL if resampler == "multinomial" else O.SYSTEMATIC)
     parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
     for t in sorted({1, min(5, T), T}):
         got = np.concatenate([p[f"traj{t}"] for p in parts], axis=0)  # [n, d]
@@ -400,7 +421,7 @@ def _check_genealogy(out, model, R, n, T, seed, thr, batched):
     assert np.array_equal(np.concatenate([p["score_tot"] for p in parts]).view(np.uint64), rtot.view(np.uint64))
     assert np.array_equal(np.concatenate([p["score_ps"] for p in parts], axis=2).view(np.uint64), rps.view(np.uint64))
     # the same filter on one rank of this process's GPU
-    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=seed)
+    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=seed, resampler=resampler)
     if batched:
         gen.run_particle_filter(st, list(ys[1:T]), thr)
     else:
