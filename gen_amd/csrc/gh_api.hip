@@ -1361,6 +1361,7 @@ static int share_stats(gh_pf* pf) {
 // Conditional SMC: pin particle 0 around the step kernel (gh_csmc.h).  pre =
 // before the step (saves the new weight), post = after it.
 static int pin_launch(gh_pf* pf, const StepObs& o, bool init, bool pre) {
+  if (pf->lo != 0) return GH_OK;  // (R ranks: the distinguished particle 0 lives on rank 0)
   PinArgs a{};
   a.ref = pf->pin;
   a.w0 = pf->pin + pf->D;
@@ -1460,7 +1461,8 @@ extern "C" int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_
   if (!m || !ref_x1 || !out) return set_err(GH_E_INVAL, "gh_pf_init_conditional: null argument");
   if (!opts || opts->resampler != GH_RESAMPLE_MULTINOMIAL)
     return set_err(GH_E_INVAL, "conditional SMC uses multinomial resampling (examples/pmmh/smc.jl:132)");
-  if (mr(m->ctx)) return set_err(GH_E_INVAL, "conditional SMC runs on one rank");
+  if (mr(m->ctx) && m->ctx->peer)
+    return set_err(GH_E_INVAL, "conditional SMC on R ranks needs the RCCL or host transport (multinomial rows)");
   if (m->family == GH_FAMILY_REGRESSION) return set_err(GH_E_INVAL, "conditional SMC needs a state-space model");
   return pf_init_impl(m, obs, GH_PROPOSAL_DEFAULT, n_particles, seed, opts, ref_x1, out);
 }
@@ -1657,6 +1659,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     if (!rc) rc = pin_launch(pf, o, true, true);
     if (!rc) rc = pin_launch(pf, o, true, false);
     if (rc) return fail(rc);
+    if (mr(ctx) && pf->lo == 0) launch_fold(pf, a, true, pf->nb_part);  // (the fold, again with particle 0 pinned)
   }
   rc = share_stats(pf);
   if (rc) return fail(rc);
@@ -1767,7 +1770,11 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
     CHECK(pin_launch(pf, o, false, true));
   }
   CHECK(timed_step(pf, o, a, false));
-  if (pin_ref) CHECK(pin_launch(pf, o, false, false));
+  if (pin_ref) {
+    CHECK(pin_launch(pf, o, false, false));
+    // R ranks: the step folded its partials already; again with particle 0 pinned
+    if (multi && pf->lo == 0) launch_fold(pf, a, false, pf->nb_part);
+  }
   if (!a.max_only) CHECK(share_stats(pf));  // (max-only: the resample's own all-gathers)
   pf->t = t;
   pf->max_only = a.max_only != 0;
@@ -2323,7 +2330,7 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
   CHECK(resample_enqueue(pf, thr, did || ess));
   // conditional SMC: the distinguished particle's parent is itself (smc.jl:139);
   // the ancestor array is only read if the resample fired
-  if (pf->cond) HIP_TRY(hipMemsetAsync(anc_for_step(pf, pf->t + 1), 0, sizeof(int32_t), pf->s));
+  if (pf->cond && !mr(pf->ctx)) HIP_TRY(hipMemsetAsync(anc_for_step(pf, pf->t + 1), 0, sizeof(int32_t), pf->s));
   if (did || ess) {
     // the fused one-rank resample posts its decision to the host mailbox as
     // soon as it is taken: wait for that, not for the stream (the caller's
@@ -3659,6 +3666,9 @@ static int exchange_states_mn(gh_pf* pf, int32_t* anc_out) {
     hipLaunchKernelGGL(k_mn_recv, dim3((unsigned)pf->nb_step), dim3(kBlock), 0, pf->s,
                        (const int32_t*)pf->mn_anc + pf->lo, (const int32_t*)pf->mn_key + pf->lo,
                        (const int32_t*)pf->mn_pos + pf->lo, pf->n, ro, anc_out, gate);
+  // conditional SMC: the distinguished particle's parent is itself (smc.jl:139;
+  // the row sent for slot 0, if any, goes unused)
+  if (pf->cond && pf->lo == 0) HIP_TRY(hipMemsetAsync(anc_out, 0, sizeof(int32_t), pf->s));
   HIP_TRY(hipGetLastError());
   CHECK(comm_exchange(c, sends, recvs, pf->s));
   if (pf->n > 0)

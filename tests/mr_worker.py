@@ -60,6 +60,8 @@ def main():
     p.add_argument("--genealogy", action="store_true", help="also save trajectories at t = 1, 5, T, the score "
                    "columns and 500 sample_unweighted_traces indices (collective queries)")
     p.add_argument("--resampler", default="systematic", help="systematic or multinomial")
+    p.add_argument("--csmc", action="store_true", help="conditional SMC (multinomial): particle 0 pinned to the "
+                   "reference trajectory 0.9 x (the simulated latents)")
     p.add_argument("--out", required=True)
     a = p.parse_args()
 
@@ -83,9 +85,13 @@ def main():
         ctx = gen.Context(device=dev, rank=rank, world=world, unique_id=uid[0])
     gen.set_default_context(ctx)
     m = build_model(a.model)
-    _, ys = m.simulate(a.T, np.random.default_rng(5))
+    xs, ys = m.simulate(a.T, np.random.default_rng(5))
     addr = m.obs_address
-    st = gen.initialize_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, seed=a.seed, resampler=a.resampler)
+    ref = np.asarray(xs, dtype=np.float64).reshape(len(ys), -1) * 0.9
+    if a.csmc:
+        st = gen.initialize_conditional_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, ref[0], seed=a.seed)
+    else:
+        st = gen.initialize_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, seed=a.seed, resampler=a.resampler)
     if a.rejuv:
         gen.rejuvenate(st, a.rejuv)
     did = []
@@ -97,7 +103,9 @@ def main():
         if a.mid_query and t == 4:
             st.states(2)
             gen.get_traces(st).scores()
-        if t == a.params_step:
+        if a.csmc:
+            gen.conditional_particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]}, ref[t - 1])
+        elif t == a.params_step:
             gen.particle_filter_step(st, (t, m2), (gen.UnknownChange(), gen.UnknownChange()), {addr(t): ys[t - 1]})
         else:
             gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})

@@ -402,6 +402,40 @@ def test_gpu_multirank_multinomial(tmp_path, gh_ctx, transport, model, R, thr, n
     _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="multinomial")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,model,R,thr,n", [("gloo", "lg4", 2, None, 3001), ("gloo", "kit", 3, 1e9, 4003),
+                                                      ("rccl1", "lg4", 1, 1e9, 3001)])
+def test_gpu_multirank_conditional_smc(tmp_path, transport, model, R, thr, n):
+    """Conditional SMC (examples/pmmh/smc.jl:100-151) on R ranks: particle 0
+    (rank 0's first) is pinned to the reference and is its own parent, the
+    others resample multinomially across ranks; states, weights, parents and
+    the trajectories equal the single-rank oracle's conditional run bit for bit."""
+    from oracle import oracle as O
+    from tests.mr_worker import build_model
+
+    out = str(tmp_path / "cs")
+    T, seed = 8, 9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  *([] if thr is None else ["--thr", str(thr)]), "--seed", str(seed), "--transport", transport,
+                  *(["--device", "0"] if transport == "rccl1" else []), "--csmc", "--genealogy", "--out", out], R,
+                 timeout=400)
+    m = build_model(model)
+    xs, ys = m.simulate(T, np.random.default_rng(5))
+    ref_traj = np.asarray(xs, dtype=np.float64).reshape(len(ys), -1) * 0.9
+    orc = O.run_csmc(m, ys, n, seed, ref_traj, thr=thr)
+    parts = [np.load(f"{out}.rank{r}.npz") for r in range(R)]
+    states = np.concatenate([p["states"] for p in parts], axis=0)
+    assert np.array_equal(states.T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(np.concatenate([p["logw"] for p in parts]).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(np.concatenate([p["parents"] for p in parts]), orc.parents())
+    lml = float(parts[0]["lml"])
+    assert abs(lml - orc.log_ml_estimate()) <= 1e-9 * abs(orc.log_ml_estimate())
+    for t in sorted({1, min(5, T), T}):
+        got = np.concatenate([p[f"traj{t}"] for p in parts], axis=0)
+        assert np.array_equal(got.T.view(np.uint64), orc.trajectory(t).view(np.uint64)), t
+        assert np.array_equal(got[0], ref_traj[t - 1]), t  # the distinguished particle's line is the reference
+
+
 def _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="systematic"):
     """Trajectories at t = 1, 5, T and the score columns of the gathered shards
     equal the single-rank oracle bit for bit; the 500 sample_unweighted_traces
