@@ -1573,7 +1573,9 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // blocks write the marks without waiting for the weight sums, and block 0
   // reads them and takes the decision after its marks; a resample that then
   // does not fire leaves marks no step reads
-  const bool spec = sums && sspec;  // (grid-uniform)
+  // (not when the host waits for the decision: the call-by-call loop with
+  // maybe_resample!'s Bool asked for gets it before the marks, as without)
+  const bool spec = sums && sspec && !r.hdec;  // (grid-uniform)
   {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (threadIdx.x == 8 * 64) {  // a non-polling wave draws the systematic offset's uniform meanwhile
