@@ -975,6 +975,12 @@ __device__ __forceinline__ int64_t sys_count_exact(const DevScalars* dev, uint64
   return j;
 }
 
+// sys_count_exact out of line, for loops that call it rarely (one copy, and
+// the caller's registers are not shaped by its search loops)
+__device__ __noinline__ int32_t sys_count_exact_call(const DevScalars* dev, uint32_t N, uint64_t X) {
+  return (int32_t)sys_count_exact(dev, N, X);
+}
+
 // The same count from v = (X N - o) / S in floating point: count = ceil(v)
 // clamped to [0, N].  With 1/S within 2 ulp (recip_est) the computed v is
 // within 7 N 2^-53 (< 2^-19 for N < 2^31) of the exact quotient, so ceil is
@@ -1017,22 +1023,9 @@ __device__ __forceinline__ int64_t sys_count_w(const DevScalars* dev, uint64_t N
 // Range marks are 32-bit words: the resample's epoch tag in the high bits and
 // the ancestor (a local particle index) in the low ceil(log2 n) bits, so the
 // newest epoch's words are the largest; the host clears both arrays when the
-// epoch field wraps.
-// sys_count_w as a 32-bit slot index (N < 2^31, as gh_pf_init enforces): the
-// marks loop's slot and group arithmetic then runs on 32-bit integers
-__device__ __forceinline__ int32_t sys_count_w32(const DevScalars* dev, uint32_t N, uint64_t X) {
-  const double v = fma((double)X, (double)N, -(double)dev->o) * dev->invS;
-  const double fl = floor(v);
-  const double fr = v - fl;
-  int32_t j = (int32_t)fmin(fmax(fl + 1.0, 0.0), (double)N);
-  const bool edge = X == 0 || X >= dev->S;
-  j = X == 0 ? 0 : (X >= dev->S ? (int32_t)N : j);
-  const bool near = !edge && !(fr > 0x1p-16 && fr < 1.0 - 0x1p-16);
-  if (__builtin_amdgcn_ballot_w64(near) != 0) {
-    if (near) j = (int32_t)sys_count_exact(dev, N, X);
-  }
-  return j;
-}
+// epoch field wraps.  k_resample1's marks loop takes its slot
+// counts incrementally, as 32-bit slot indices (N < 2^31, as gh_pf_init
+// enforces), so its slot and group arithmetic runs on 32-bit integers.
 
 struct MarkArgs {
   uint32_t* mark;     // [n slots] tagged ancestor at each range start
@@ -1387,6 +1380,12 @@ __device__ __forceinline__ double blk16_max1(double v, double* sm) {
 __device__ __forceinline__ uint64_t f64_to_u52(double x) {
   return as_u64(floor(x) + 0x1p52) - 0x4330000000000000ull;
 }
+// and back, (double)q for q <= 2^52: the bits of 2^52 plus q (2^52 + q, exact
+// below 2^53; q = 2^52 carries into the exponent: 2^53), minus 2^52 (two
+// instructions; the generic u64 -> f64 conversion is four)
+__device__ __forceinline__ double u52_to_f64(uint64_t q) {
+  return as_f64(q + 0x4330000000000000ull) - 0x1p52;
+}
 
 template <bool MARKS, int IT, bool SUMS>
 __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resample1Args r) {
@@ -1508,8 +1507,12 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     }
     lds_barrier();
   }
+  // (thread 0 keeps M in LDS for the commit: no registers held through the marks)
+  __shared__ double sMv;
+  if (threadIdx.x == 0) sMv = M;
   auto commit = [&]() {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
+      M = sMv;
       const Decision dec = decision();
       r.stats_out[0] = M;
       r.stats_out[1] = S1;
@@ -1683,13 +1686,18 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // grid never started): the totals are partial.  The block leaves without
   // marks or decision; the error surfaces as GH_E_STATE at the next sync.
   if (sfail) return;
-  if (sums && !spec) {
-    S1 = sS[0];
-    S2 = sS[1];
-    if (!sfire) {
-      commit();
-      return;
+  // (sums_in_pass, not speculative: thread 0 reads the sums from LDS at the
+  // commit, so no registers hold them through the marks)
+  auto sums_from_lds = [&]() {
+    if (sums && !spec) {
+      S1 = sS[0];
+      S2 = sS[1];
     }
+  };
+  if (sums && !spec && !sfire) {
+    sums_from_lds();
+    commit();
+    return;
   }
   // speculative: block 0 reads the tile sums and takes the decision after
   // its marks or CDF
@@ -1742,11 +1750,35 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       if (i0 + k < r.n) r.C[i0 + k] = run;
     }
     decide_late();
+    sums_from_lds();
     if (!sfail) commit();
     return;
   }
   const uint32_t N = (uint32_t)r.mk.n_global;  // < 2^31: 32-bit slots and groups
-  int32_t s_i = (int32_t)sys_count(&sd, N, run);
+  // The slot counts count(X) = ceil(v), v = (X N - o) / S, as sys_count, but
+  // v advances by q N / S per particle (one FMA on the quantised weight, exact
+  // as a double) instead of being re-derived from the 64-bit X.  Error: v_0 is
+  // within 7 N 2^-53 of the exact quotient (sys_count), each step adds at
+  // most N 2^-53 by rounding, and the tile's q N |ns - N/S| (ns within 3 ulp)
+  // at most 3 N 2^-53: |v - v*| < 26 N 2^-53 < 2^-17 for IT <= 16, N < 2^31,
+  // so ceil(v) is exact more than 2^-16 from an integer, and otherwise
+  // (probability ~2^-15) the count is taken exactly.  No clamps or edge
+  // tests: for 0 < X < S, v* lies in (-1, N); X = 0 and X = S give
+  // v* = -o/S and N - o/S, whose ceilings are 0 and N (o = 0: v* is an
+  // integer, so the exact count).
+  const double ns = as_f64(readfirstlane_u64(as_u64((double)N * sd.invS)));  // (uniform: SGPRs)
+  double v = fma((double)run, (double)N, -(double)sd.o) * sd.invS;
+  auto count = [&](uint64_t X) {
+    const double fl = floor(v);
+    const double fr = v - fl;
+    int32_t j = (int32_t)fl + 1;
+    const bool near = !(fr > 0x1p-16 && fr < 1.0 - 0x1p-16);
+    if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)
+      if (near) j = sys_count_exact_call(&sd, N, X);
+    }
+    return j;
+  };
+  int32_t s_i = count(run);
   // particle i owns the slots [s_i, e_i): a tagged mark at s_i, and the carry
   // of every 64-slot group that starts inside the range; a lane writes up to
   // two carries itself, a longer range (a particle with > 128 offspring) gets
@@ -1755,10 +1787,11 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     run += q[k];
-    // (a particle past n or of zero weight leaves run, hence the count, unchanged)
-    const int32_t e_i = sys_count_w32(&sd, N, run);
+    v = fma(u52_to_f64(q[k]), ns, v);
+    // (a particle past n or of zero weight leaves run, v, hence the count, unchanged)
+    const int32_t e_i = count(run);
     const uint32_t tagged = r.mk.tag | (uint32_t)(i0 + k);
-    if (e_i > s_i) r.mk.mark[s_i] = tagged;
+    if (e_i > s_i) r.mk.mark[(uint32_t)s_i] = tagged;
     const uint32_t g0 = ((uint32_t)s_i + 63u) >> 6, g1 = ((uint32_t)e_i + 63u) >> 6;  // groups g with 64 g in [s_i, e_i)
     const bool many = g1 - g0 > 2u;
     if (!many) {
@@ -1776,6 +1809,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     s_i = e_i;
   }
   decide_late();
+  sums_from_lds();
   if (!sfail) commit();
 }
 

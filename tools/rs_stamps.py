@@ -55,3 +55,11 @@ order = [0, 7, 1, 2, 3, 4, 5, 6]
 for a_, b_ in zip(order, order[1:]):
     d = rel[:, b_] - rel[:, a_]
     print(f"{names[a_]:>9s}->{names[b_]:10s} med {np.median(d):6.2f} max {d.max():6.2f} (block {int(d.argmax())}) us")
+if waves is not None:  # the marks phase per wave: the latest blocks against the median block
+    wd = (waves[:, :, 1] - waves[:, :, 0]) * 0.01
+    car = waves[:, :, 3]
+    print(f"marks per wave: median {np.median(wd):.2f} us, carries median {np.median(car):.0f}, "
+          f"blocks with a wave-wide carry loop {int((waves[:, :, 2].sum(axis=1) > 0).sum())} of {grid}")
+    for b in np.argsort(rel[:, 5])[::-1][:4]:
+        print(f"  block {b}: marks waves {' '.join(f'{x:.1f}' for x in wd[b])} us; "
+              f"wave-wide loops {' '.join(str(int(x)) for x in waves[b, :, 2])}; carries {' '.join(str(int(x)) for x in car[b])}")
