@@ -102,6 +102,7 @@ SIGNATURES = {
     "gh_pf_mh_drift": (c_int, [c_void_p, ctypes.c_uint32, POINTER(c_double), c_int, POINTER(c_int64)]),
     "gh_pf_get_scores": (c_int, [c_void_p, POINTER(c_double), POINTER(c_double)]),
     "gh_debug_mark_bits": (c_int, [c_void_p, c_int]),
+    "gh_debug_count_window": (c_int, [c_void_p, c_int]),
     "gh_debug_exchange_lists": (c_int, [c_int64, c_int, c_int, POINTER(c_uint64), c_uint64, c_int, POINTER(c_int),
                                         POINTER(c_int), POINTER(c_uint64), POINTER(c_int), POINTER(c_int),
                                         POINTER(c_uint64)]),

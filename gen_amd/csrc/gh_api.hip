@@ -3416,6 +3416,14 @@ extern "C" int gh_debug_mark_bits(gh_pf* pf, int bits) {
   return GH_OK;
 }
 
+extern "C" int gh_debug_count_window(gh_ctx* ctx, int log2_inv) {
+  if (!ctx || log2_inv < 0 || log2_inv > 40) return set_err(GH_E_INVAL, "gh_debug_count_window: bad argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_count_window_log2), &log2_inv, sizeof(int)));
+  return GH_OK;
+}
+
 extern "C" int gh_debug_exchange_lists(int64_t n_global, int world, int rank, const uint64_t* totals, uint64_t offset,
                                        int D, int* n_send, int* send_peer, uint64_t* send_bytes, int* n_recv,
                                        int* recv_peer, uint64_t* recv_bytes) {

@@ -981,18 +981,36 @@ __device__ __noinline__ int32_t sys_count_exact_call(const DevScalars* dev, uint
   return (int32_t)sys_count_exact(dev, N, X);
 }
 
+// The float slot counts below are taken exactly when v lies within this
+// window of an integer: 2^(ceil(log2 N) + 7 - 53) >= 128 N 2^-53, at least
+// four times the worst-case error of v (8 N 2^-53 + 2^-53 for one
+// evaluation, 31 N 2^-53 + 2^-53 for k_resample1's incremental counts).  So
+// the exact count runs with probability ~2^-24 per count at N = 2^21 (a
+// fixed 2^-16 window made it ~2^-15: a hundred exact counts per C4 resample,
+// each holding its wave ~1.7 us past the others, the launch ending with them).
+// (tests, gh_debug_count_window: k > 0 makes the window 2^-k, so that the
+// exact counts run often)
+static __device__ int g_count_window_log2 = 0;
+__device__ __forceinline__ double count_window(uint64_t N) {
+  const int lg = N <= 1 ? 0 : 64 - __builtin_clzll(N - 1);  // ceil(log2 N)
+  const int k = g_count_window_log2;
+  return as_f64((uint64_t)(k > 0 ? 1023 - k : 1023 + lg + 7 - 53) << 52);
+}
+
 // The same count from v = (X N - o) / S in floating point: count = ceil(v)
 // clamped to [0, N].  With 1/S within 2 ulp (recip_est) the computed v is
-// within 7 N 2^-53 (< 2^-19 for N < 2^31) of the exact quotient, so ceil is
-// exact whenever v is more than 2^-16 away from an integer; otherwise
-// (probability ~2^-15) count exactly.
+// within 8 N 2^-53 + 2^-53 of the exact quotient (the error of X's and o's
+// conversions, of the FMA, of 1/S and of the product), so ceil is exact
+// whenever v is more than count_window(N) away from an integer; otherwise
+// count exactly.
 __device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, uint64_t X) {
   if (X == 0) return 0;
   if (X >= dev->S) return (int64_t)N;
   const double v = fma((double)X, (double)N, -(double)dev->o) * dev->invS;
   const double fl = floor(v);
   const double fr = v - fl;
-  if (fr > 0x1p-16 && fr < 1.0 - 0x1p-16) {
+  const double w = count_window(N);
+  if (fr > w && fr < 1.0 - w) {
     const double j = fl + 1.0;
     if (j <= 0.0) return 0;
     if (j >= (double)N) return (int64_t)N;
@@ -1002,7 +1020,7 @@ __device__ __forceinline__ int64_t sys_count(const DevScalars* dev, uint64_t N, 
 }
 
 // sys_count for whole waves: the estimate and its clamps as selects, and the
-// exact count (probability ~2^-15 per call) behind a wave-uniform branch, so
+// exact count (rare: count_window) behind a wave-uniform branch, so
 // the marks loops run straight-line code instead of nested divergent branches
 // (k_resample1's marks phase: 2.7 us of the C2 resample).  Same results.
 __device__ __forceinline__ int64_t sys_count_w(const DevScalars* dev, uint64_t N, uint64_t X) {
@@ -1013,7 +1031,8 @@ __device__ __forceinline__ int64_t sys_count_w(const DevScalars* dev, uint64_t N
   int64_t j = N < (1ull << 31) ? (int64_t)(int32_t)jd : (int64_t)jd;
   const bool edge = X == 0 || X >= dev->S;
   j = X == 0 ? 0 : (X >= dev->S ? (int64_t)N : j);
-  const bool near = !edge && !(fr > 0x1p-16 && fr < 1.0 - 0x1p-16);
+  const double w = count_window(N);
+  const bool near = !edge && !(fr > w && fr < 1.0 - w);
   if (__builtin_amdgcn_ballot_w64(near) != 0) {
     if (near) j = sys_count_exact(dev, N, X);
   }
@@ -1758,21 +1777,27 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
   // The slot counts count(X) = ceil(v), v = (X N - o) / S, as sys_count, but
   // v advances by q N / S per particle (one FMA on the quantised weight, exact
   // as a double) instead of being re-derived from the 64-bit X.  Error: v_0 is
-  // within 7 N 2^-53 of the exact quotient (sys_count), each step adds at
-  // most N 2^-53 by rounding, and the tile's q N |ns - N/S| (ns within 3 ulp)
-  // at most 3 N 2^-53: |v - v*| < 26 N 2^-53 < 2^-17 for IT <= 16, N < 2^31,
-  // so ceil(v) is exact more than 2^-16 from an integer, and otherwise
-  // (probability ~2^-15) the count is taken exactly.  No clamps or edge
-  // tests: for 0 < X < S, v* lies in (-1, N); X = 0 and X = S give
-  // v* = -o/S and N - o/S, whose ceilings are 0 and N (o = 0: v* is an
-  // integer, so the exact count).
+  // within 8 N 2^-53 + 2^-53 of the exact quotient (sys_count); ns = N / S to
+  // within 6 units of 2^-53 (1/S within 2 ulp, one product), so the tile's
+  // increments q ns add at most 6 N 2^-53 (their exact sum is <= N); each FMA
+  // rounds by at most N 2^-53: |v - v*| <= (14 + IT) N 2^-53 + 2^-53 <=
+  // 31 N 2^-53 + 2^-53 for IT <= 16, a quarter of count_window(N), so ceil(v)
+  // is exact outside the window and the count is taken exactly inside it.  No
+  // clamps or edge tests: for 0 < X < S, v* lies in (-1, N); X = 0 and X = S
+  // give v* = -o/S and N - o/S, whose ceilings are 0 and N (o small: inside
+  // the window, so the exact count).
+  static_assert(IT <= 16, "the error bound of the incremental slot counts");
   const double ns = as_f64(readfirstlane_u64(as_u64((double)N * sd.invS)));  // (uniform: SGPRs)
+  // near the integers: |fr - 1/2| >= 1/2 - w (1/2 - w is a double, so the
+  // rounding of fr - 1/2 never takes a near value out; it may take a value
+  // just outside the window in, which only costs an exact count)
+  const double hw = as_f64(readfirstlane_u64(as_u64(0.5 - count_window(N))));
   double v = fma((double)run, (double)N, -(double)sd.o) * sd.invS;
   auto count = [&](uint64_t X) {
     const double fl = floor(v);
     const double fr = v - fl;
     int32_t j = (int32_t)fl + 1;
-    const bool near = !(fr > 0x1p-16 && fr < 1.0 - 0x1p-16);
+    const bool near = fabs(fr - 0.5) >= hw;
     if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)
       if (near) j = sys_count_exact_call(&sd, N, X);
     }

@@ -370,6 +370,13 @@ int gh_debug_exchange_lists(int64_t n_global, int world, int rank, const uint64_
    are cleared at each).  Only before the first resample is pending. */
 int gh_debug_mark_bits(gh_pf* pf, int bits);
 
+/* test hook: the systematic slot counts are taken in floating point and
+   recounted exactly when within a window of an integer (2^(ceil(log2 N) + 7 - 53)
+   by default, so rarely); log2_inv > 0 sets the window to 2^-log2_inv for every
+   later resample on the context's device, so that the exact recount runs often
+   (0 restores the default).  Results do not change. */
+int gh_debug_count_window(gh_ctx* ctx, int log2_inv);
+
 /* ---- importance sampling ---------------------------------------------------- */
 int gh_is_run(gh_model* m, const gh_obs* obs, int proposal, int64_t n, uint64_t seed,
               double* host_log_norm_weights /* may be NULL */, double* host_states /* may be NULL */,

@@ -162,6 +162,38 @@ def test_batched_run_parity(gh_ctx, model, thr, resampler):
     assert_lml_close(st, orc)
 
 
+@pytest.mark.parametrize("model", ["lg4", "kit"])
+def test_exact_slot_recounts_bitexact(gh_ctx, model):
+    """The systematic slot counts are taken in floating point (incrementally in
+    the fused resample's marks loop) and recounted exactly within a window of
+    the integers, which by default is narrow enough that the recount is rare.
+    With the window widened to 1/8 (gh_debug_count_window) about a quarter of
+    all counts take the exact path, through gh_pf_run and the call-by-call
+    loop: the same filter as the oracle, bit for bit."""
+    m = gen.LinearGaussianSSM.benchmark(4) if model == "lg4" else gen.KitagawaSSM(10.0, 1.0)
+    _, ys = m.simulate(8, np.random.default_rng(4))
+    n = 70001
+    lib = _lib.load()
+    _lib.check(lib.gh_debug_count_window(gh_ctx.h, 3))
+    try:
+        st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=21)
+        orc = O.OraclePF(m, n, 21, O.SYSTEMATIC)
+        orc.init(ys[0])
+        gen.run_particle_filter(st, list(ys[1:5]), n)  # always resample
+        for t in range(2, 6):
+            orc.maybe_resample(n)
+            orc.step(ys[t - 1])
+        for t in range(6, len(ys) + 1):  # the reference caller loop
+            assert gen.maybe_resample(st, n) == orc.maybe_resample(n)[0]
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {m.obs_address(t): ys[t - 1]})
+            orc.step(ys[t - 1])
+        assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+        assert np.array_equal(st.parents, orc.parents())
+        assert_lml_close(st, orc)
+    finally:
+        _lib.check(lib.gh_debug_count_window(gh_ctx.h, 0))
+
+
 @pytest.mark.parametrize("model", ["lg10", "kit"])
 def test_batched_run_chunks_and_thresholds(gh_ctx, model):
     """Several gh_pf_run calls back to back (the grid barrier of the fused

@@ -25,7 +25,7 @@ static __device__ uint64_t g_rs_stamps[1024 * 16];
 #define GH_RS_STAMP(k) \\
   if (threadIdx.x == 0 && blockIdx.x < 1024) g_rs_stamps[blockIdx.x * 16 + (k)] = wall_clock64();
 // per wave of the marks phase: [clock before the first slot count, clock
-// after the loop, wave-wide carry loops, carries those wrote]
+// after the loop, wave-wide carry loops | exact slot counts << 32, carries those wrote]
 static __device__ uint64_t g_rs_wave[1024 * 16 * 4];
 // where the block runs: the HW_ID register (wave, SIMD, CU, SH, SE ids) and the XCC id
 #define GH_RS_PLACE() \\
@@ -80,7 +80,9 @@ def stamped_kernels(s):
                after=False)
     b = insert(b, b.index("GH_RS_STAMP(3)"), "  if (sfail) return;\n", "  GH_RS_EXIT_AT(3);\n  GH_RS_STAMP(4);\n")
     b = insert(b, 0, "const uint32_t N = (uint32_t)r.mk.n_global;  // < 2^31: 32-bit slots and groups\n",
-               "#if defined(GH_RS_STAMPS)\n  const uint64_t wt0 = wall_clock64();\n  uint64_t wmany = 0, wcar = 0;\n#endif\n")
+               "#if defined(GH_RS_STAMPS)\n  const uint64_t wt0 = wall_clock64();\n  uint64_t wmany = 0, wcar = 0, wnear = 0;\n#endif\n")
+    b = insert(b, 0, "if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)\n",
+               "#if defined(GH_RS_STAMPS)\n      wnear += __builtin_popcountll(__builtin_amdgcn_ballot_w64(near));\n#endif\n")
     b = insert(b, 0, "uint64_t bm = __builtin_amdgcn_ballot_w64(many);\n",
                "#if defined(GH_RS_STAMPS)\n    wmany += __builtin_popcountll(bm);\n#endif\n")
     b = insert(b, 0, "a1 = __builtin_amdgcn_readlane((int32_t)g1, L);\n",
@@ -92,7 +94,7 @@ def stamped_kernels(s):
     uint64_t* wp = g_rs_wave + ((uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * 4;
     wp[0] = wt0;
     wp[1] = wall_clock64();
-    wp[2] = wmany;
+    wp[2] = wmany | (wnear << 32);
     wp[3] = wcar;
   }
 #endif

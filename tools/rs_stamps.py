@@ -58,8 +58,14 @@ for a_, b_ in zip(order, order[1:]):
 if waves is not None:  # the marks phase per wave: the latest blocks against the median block
     wd = (waves[:, :, 1] - waves[:, :, 0]) * 0.01
     car = waves[:, :, 3]
+    near = waves[:, :, 2] >> 32
+    waves[:, :, 2] &= 0xFFFFFFFF
+    print("marks per wave index (median over blocks): " + " ".join(f"{x:.2f}" for x in np.median(wd, axis=0)) + " us")
+    print(f"exact slot counts: {int(near.sum())} in {int((near > 0).sum())} waves; marks of those waves median "
+          f"{np.median(wd[near > 0]) if (near > 0).any() else 0:.2f} us, of the others {np.median(wd[near == 0]):.2f} us")
     print(f"marks per wave: median {np.median(wd):.2f} us, carries median {np.median(car):.0f}, "
           f"blocks with a wave-wide carry loop {int((waves[:, :, 2].sum(axis=1) > 0).sum())} of {grid}")
     for b in np.argsort(rel[:, 5])[::-1][:4]:
         print(f"  block {b}: marks waves {' '.join(f'{x:.1f}' for x in wd[b])} us; "
-              f"wave-wide loops {' '.join(str(int(x)) for x in waves[b, :, 2])}; carries {' '.join(str(int(x)) for x in car[b])}")
+              f"wave-wide loops {' '.join(str(int(x)) for x in waves[b, :, 2])}; carries {' '.join(str(int(x)) for x in car[b])}; "
+              f"exact counts {' '.join(str(int(x)) for x in near[b])}")
