@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of bench.py step times on one box (run on the GPU box from
-# the repo root):  bash tools/gpu_ab.sh OUTDIR REPS label=lib.so ...
-# ("head" = the in-tree library).  C2 and C4, the driver's --steps 20
+# the repo root):  bash tools/gpu_ab.sh OUTDIR REPS label=lib.so[@VAR=value] ...
+# ("head" = the in-tree library; @VAR=value: an environment switch).  C2 and C4, the driver's --steps 20
 # --warmup 5; prints per-label runs, median step time and step-kernel time.
 # GH_AB_TESTS="pytest args" runs those GPU tests first; GH_AB_STAMPS=1 adds
 # the resample phase clocks (gen_amd/variants/rs_stamps.so).
@@ -19,7 +19,8 @@ for rep in $(seq 1 $REPS); do
     name=${m%%|*}; args=${m#*|}
     for lv in "$@"; do
       label=${lv%%=*}; lib=${lv#*=}
-      if [ "$lib" = "head" ]; then env=""; else env="GEN_HIP_LIB=$PWD/$lib"; fi
+      xenv=""; case "$lib" in *@*) xenv=${lib#*@}; lib=${lib%%@*};; esac  # label=lib@VAR=value
+      if [ "$lib" = "head" ]; then env="$xenv"; else env="GEN_HIP_LIB=$PWD/$lib $xenv"; fi
       env $env timeout -k 10 120 python bench.py --no-cpu-baseline --no-secondary --steps 20 --warmup 5 $args > $OUT/${name}_${label}_$rep.json 2> $OUT/${name}_${label}_$rep.err
     done
   done

@@ -29,8 +29,11 @@ buf = (ctypes.c_uint64 * (1024 * 16))()
 lib.gh_debug_rs_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 _lib.check(lib.gh_debug_rs_stamps(buf, 1024 * 16))
 grid = -(-n // (1024 * 4))  # IT = 4 (two blocks per CU at 2^21)
+allraw = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16).astype(np.int64)
+if grid < 1024 and allraw[grid, 0] != 0:  # the decider block (no tile) ran too
+    grid += 1
 print(f"{name} n={n} grid={grid}")
-raw = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16)[:grid].astype(np.int64)
+raw = allraw[:grid]
 a = raw[:, :8]
 waves = None
 if hasattr(lib, "gh_debug_rs_waves"):  # (the probe variants have no per-wave clocks)
