@@ -230,6 +230,9 @@ def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn, lo
         record_history=not a.no_history, history_capacity=T + 2, time_kernels=0 if a.no_kernel_timing else a.time_every,
         ctx=ctx,
     )
+    if dist is not None:  # (the ranks' allocations and first launches take different times)
+        ctx.synchronize()
+        dist.barrier()
     gen.run_particle_filter(st, list(ys[1 : 1 + a.warmup]), a.ess_threshold, proposal=prop)
     ctx.synchronize()
     st.kernel_time_ms(reset=True)
@@ -324,13 +327,23 @@ def secondary_c4(gen, ctx, a):
     return out
 
 
-def peer_probe(gen, ctx, world):
+def peer_probe(gen, ctx, world, dist):
     """A few always-resampling steps of a small filter on the peer transport
-    (rows cross ranks every step); returns the log-ML as an exact hex string."""
+    (rows cross ranks every step); returns the log-ML as an exact hex string.
+    The ranks line up after the set-up, so that the device-side waits of the
+    first exchange do not absorb the processes' start-up skew."""
     m = gen.LinearGaussianSSM.benchmark(4)
     _, ys = m.simulate(5, np.random.default_rng(5))
     n = 2048 * world
-    st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=7, ctx=ctx)
+    err = None
+    try:
+        st = gen.initialize_particle_filter(m, (1,), {("chain", 1, "y"): ys[0]}, n, seed=7, ctx=ctx)
+        ctx.synchronize()
+    except Exception as e:  # (still at the barrier: the ranks' collectives stay in step)
+        err = e
+    dist.barrier()
+    if err is not None:
+        raise err
     gen.run_particle_filter(st, list(ys[1:]), float(n))
     lml = float(gen.log_ml_estimate(st)).hex()
     st.close()
@@ -520,7 +533,7 @@ def main(argv=None):
                 # must finish and agree on the log-ML bit for bit
                 probe = None
                 try:
-                    probe = peer_probe(gen, ctx, world)
+                    probe = peer_probe(gen, ctx, world, dist)
                 except Exception as e:
                     print(f"rank {rank}: peer transport probe failed ({e}); RCCL instead", file=sys.stderr, flush=True)
                 probes = [None] * world

@@ -1952,7 +1952,10 @@ struct PeerBox {
 };
 
 
-constexpr unsigned kPeerSpins = 1u << 22;  // ~0.3 s of polling, then GH_E_STATE
+// ~2.5 s of polling, then GH_E_STATE: a backstop against a rank that never
+// comes, long enough for host-side skew between processes (allocation,
+// first launches, descheduling)
+constexpr unsigned kPeerSpins = 1u << 25;
 
 // Wave-level poll: lanes r < R wait until word (base + stride * r) of the own
 // mailbox reaches `want` (monotonic tags).  Returns false on timeout.
