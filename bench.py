@@ -80,8 +80,8 @@ def parse(argv=None):
                         "mapping fails), RCCL collectives, or the host-staged gloo transport (ranks may share a "
                         "GPU; a correctness rehearsal, not a benchmark)")
     p.add_argument("--time-every", type=int, default=None,
-                   help="time every k-th step kernel with launch events (default 1: every launch of the timed "
-                        "region, so kernel_avg_ms averages all of them)")
+                   help="time every k-th step kernel with launch events (default: steps // 5, at most 10, so at "
+                        "least 5 launches of the timed region are averaged in kernel_avg_ms)")
     return p.parse_args(argv)
 
 
@@ -211,6 +211,26 @@ def pmc_profile(name):
         return None
 
 
+def set_traffic(roofline, pmc, tol=0.15):
+    """roofline.traffic = the committed PMC profile's HBM bytes per launch —
+    only when that profile timed the same kernel this run timed: its
+    rocprofv3 average within `tol` of this run's event average (a stale file,
+    made from other code, is not passed off as this run's traffic)."""
+    roofline["traffic"] = None
+    if not pmc or "hbm_bytes_per_launch" not in pmc:
+        roofline["traffic_note"] = "no PMC profile for this configuration"
+        return
+    kms = roofline.get("kernel_avg_ms") or 0.0
+    pms = pmc.get("avg_duration_ns", 0.0) * 1e-6
+    roofline["traffic_source"] = pmc.get("source")
+    if kms <= 0 or pms <= 0 or abs(pms - kms) > tol * kms:
+        roofline["traffic_note"] = (f"null: the PMC profile's kernel average ({pms * 1e3:.2f} us, {pmc.get('source')}) "
+                                    f"differs from this run's ({kms * 1e3:.2f} us) by more than {tol:.0%}")
+        return
+    roofline["traffic"] = pmc["hbm_bytes_per_launch"]
+    roofline["traffic_profile_avg_ms"] = pms
+
+
 # --------------------------------------------------------------- PF runs
 def pf_run(gen, ctx, dist, world, a, model, particles, kernel_name, bytes_fn, loop="run"):
     """One filter: init, warm-up steps, then the timed region over K steps
@@ -309,8 +329,7 @@ def secondary_c4(gen, ctx, a):
     n = 1 << 21
     r = pf_run(gen, ctx, None, 1, a, model, n, "k_step_pairs<KitModel,false>",
                lambda n_res: 16 * 1 + 16)
-    pmc = pmc_profile("pmc_k_step_kitagawa.json")
-    r["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
+    set_traffic(r["roofline"], pmc_profile("pmc_k_step_kitagawa.json"))
     out = {
         "metric": "particle-steps/sec, nonlinear SSM (C4 shard)",
         "value": n * a.steps / r["dt"],
@@ -494,7 +513,10 @@ _KEEP = []
 def main(argv=None):
     a = parse(argv)
     if a.time_every is None:
-        a.time_every = 10  # every 10th step-kernel launch (A/B at 20 steps: events on every launch cost 1.0 us per step)
+        # every k-th step-kernel launch, at least 5 in the timed region (the
+        # driver's 20 steps: every 4th); events on every launch cost 1.0 us
+        # per step against every 10th (A/B at 20 steps, round 5)
+        a.time_every = max(1, min(10, a.steps // 5))
     import gen_amd as gen
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -570,7 +592,7 @@ def main(argv=None):
         pmc = pmc_profile("pmc_k_step.json")
     elif a.model == "kitagawa" and a.particles == 1 << 21:
         pmc = pmc_profile("pmc_k_step_kitagawa.json")
-    r["roofline"]["traffic"] = pmc.get("hbm_bytes_per_launch") if pmc else None
+    set_traffic(r["roofline"], pmc)
 
     ys, n_global, lml = r["ys"], r["n_global"], r["lml"]
     log_ml_error = None

@@ -103,6 +103,8 @@ SIGNATURES = {
     "gh_pf_get_scores": (c_int, [c_void_p, POINTER(c_double), POINTER(c_double)]),
     "gh_debug_mark_bits": (c_int, [c_void_p, c_int]),
     "gh_debug_count_window": (c_int, [c_void_p, c_int]),
+    "gh_debug_set_ancestor": (c_int, [c_void_p, c_int, c_int64, c_int32]),
+    "gh_ctx_set_peer_timeout": (c_int, [c_void_p, c_double]),
     "gh_debug_exchange_lists": (c_int, [c_int64, c_int, c_int, POINTER(c_uint64), c_uint64, c_int, POINTER(c_int),
                                         POINTER(c_int), POINTER(c_uint64), POINTER(c_int), POINTER(c_int),
                                         POINTER(c_uint64)]),

@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libgen_hip.so")
-SOURCES = [os.path.join(CSRC, "gh_api.hip")] + sorted(glob.glob(os.path.join(CSRC, "gh_inst_lg*.hip")))
+SOURCES = [os.path.join(CSRC, "gh_api.hip")] + sorted(glob.glob(os.path.join(CSRC, "gh_inst_*.hip")))
 HEADERS = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "gen_hip.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -46,7 +46,7 @@ def compile_cmd(src: str, obj: str, extra: list[str] | None = None) -> list[str]
 
 
 def _sources(csrc: str) -> list[str]:
-    return [os.path.join(csrc, "gh_api.hip")] + sorted(glob.glob(os.path.join(csrc, "gh_inst_lg*.hip")))
+    return [os.path.join(csrc, "gh_api.hip")] + sorted(glob.glob(os.path.join(csrc, "gh_inst_*.hip")))
 
 
 def link_cmd(objs: list[str], out: str) -> list[str]:

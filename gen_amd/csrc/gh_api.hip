@@ -57,15 +57,24 @@ static int set_err(int code, const char* fmt, ...) {
 }
 
 // message for a status the device raised (DevScalars::error)
+// (the low byte is the gh_status, the byte above it the cause: kErr* in gh_kernels.h)
 static const char* dev_error_msg(int code) {
   switch (code) {
     case GH_E_NUMERIC: return "maybe_resample: all log-weights are -Inf or NaN";
-    case GH_E_STATE:
+    case kErrBarrier:
       return "resample grid barrier timed out: its blocks were not co-resident (the device is running other "
              "kernels); this filter's state is no longer valid";
+    case kErrGenealogy:
+      return "genealogy walk met a broken record (an ancestor that names no particle or no kept row); this "
+             "filter's state is no longer valid";
+    case kErrPeer:
+      return "peer transport: another rank did not publish within the wait bound (gh_ctx_set_peer_timeout); "
+             "this filter's state is no longer valid";
     default: return "error raised on the device";
   }
 }
+// a device-raised error as the call's status
+static int dev_fail(int code) { return set_err(code & 0xff, "%s", dev_error_msg(code)); }
 
 #define HIP_TRY(x)                                                                       \
   do {                                                                                   \
@@ -112,6 +121,8 @@ struct gh_ctx {
   uint64_t* mbox = nullptr;
   uint64_t* mpeer[kPeerMaxRanks] = {};
   uint64_t use_sh = 0, use_rec = 0, use_ag = 0;
+  uint64_t peer_wait_ticks = 0;  // bound of every device wait on a peer (wall-clock ticks)
+  int wall_khz = 100000;         // the device wall clock's rate (hipDeviceAttributeWallClockRate)
 };
 
 static PeerBox peer_box(const gh_ctx* c) {
@@ -119,36 +130,88 @@ static PeerBox peer_box(const gh_ctx* c) {
   for (int r = 0; r < c->world; ++r) pb.peer[r] = c->mpeer[r];
   pb.R = c->world;
   pb.rank = c->rank;
+  pb.wait_ticks = c->peer_wait_ticks;
   return pb;
 }
 
-// Bootstrap exchange of IPC handles over the user's host all-gather: map
-// every other rank's buffer (out[rank] = own).
-static int ipc_exchange(gh_ctx* c, void* own, void** out) {
-  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
-  std::vector<uint8_t> send(64, 0), recv(64 * (size_t)c->world, 0);
-  hipIpcMemHandle_t h;
-  HIP_TRY(hipIpcGetMemHandle(&h, own));
-  memcpy(send.data(), &h, sizeof h);
-  if (c->hc.allgather(c->hc.user, send.data(), recv.data(), 64))
+// The peer transport's bootstrap rounds (the user's host all-gather) are
+// fail-together: every rank takes part in every round of a collective set-up
+// whatever happened locally, each round carries the sender's ok flag, and a
+// round in which any rank failed ends the set-up on every rank at that round
+// (no rank is left waiting in a later collective).  PeerRounds counts the
+// rounds a set-up has completed; peer_abort runs the next one with a failed
+// flag.
+struct PeerRounds {
+  int next = 0;      // rounds completed
+  bool over = false;  // a round reported a failure (or the set-up finished)
+};
+static int peer_round(gh_ctx* c, PeerRounds& pr, bool ok, const void* payload, size_t plen, std::vector<uint8_t>* all) {
+  const size_t rec = plen + 8;
+  std::vector<uint8_t> send(rec, 0), recv(rec * (size_t)c->world, 0);
+  if (payload && plen) memcpy(send.data(), payload, plen);
+  send[plen] = ok ? 1 : 0;
+  const int rc = c->hc.allgather(c->hc.user, send.data(), recv.data(), rec);
+  pr.next++;
+  if (rc) {
+    pr.over = true;
     return set_err(GH_E_RCCL, "peer transport: bootstrap allgather failed");
-  for (int r = 0; r < c->world; ++r) {
-    if (r == c->rank) {
-      out[r] = own;
-      continue;
-    }
-    hipIpcMemHandle_t hr;
-    memcpy(&hr, recv.data() + 64 * (size_t)r, sizeof hr);
-    void* p = nullptr;
-    HIP_TRY(hipIpcOpenMemHandle(&p, hr, hipIpcMemLazyEnablePeerAccess));
-    out[r] = p;
+  }
+  int bad = -1;
+  for (int r = 0; r < c->world; ++r)
+    if (!recv[rec * (size_t)r + plen]) bad = r;
+  if (bad >= 0) {
+    pr.over = true;
+    return ok ? set_err(GH_E_STATE, "peer transport: rank %d failed its part of a collective set-up", bad) : GH_E_STATE;
+  }
+  if (all) {
+    all->resize(plen * (size_t)c->world);
+    for (int r = 0; r < c->world; ++r) memcpy(all->data() + plen * (size_t)r, recv.data() + rec * (size_t)r, plen);
   }
   return GH_OK;
+}
+static void peer_abort(gh_ctx* c, PeerRounds& pr) {
+  if (pr.over) return;
+  peer_round(c, pr, false, nullptr, 0, nullptr);
+  pr.over = true;
 }
 
 static void ipc_close(const gh_ctx* c, void* const* mapped) {
   for (int r = 0; r < c->world; ++r)
-    if (r != c->rank && mapped[r]) hipIpcCloseMemHandle(mapped[r]);
+    if (r != c->rank && mapped[r]) {
+      hipIpcCloseMemHandle(mapped[r]);
+    }
+}
+
+// Bootstrap exchange of IPC handles (two rounds: the handles, then whether
+// every rank mapped every other's): map every other rank's buffer (out[rank]
+// = own).  Fails on every rank or on none; on failure nothing stays mapped.
+static int ipc_exchange(gh_ctx* c, PeerRounds& pr, void* own, void** out) {
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
+  for (int r = 0; r < c->world; ++r) out[r] = nullptr;
+  uint8_t hbuf[64] = {};
+  hipIpcMemHandle_t h;
+  const bool got = hipIpcGetMemHandle(&h, own) == hipSuccess;
+  if (got) memcpy(hbuf, &h, sizeof h);
+  std::vector<uint8_t> all;
+  int rc = peer_round(c, pr, got, hbuf, 64, &all);
+  if (rc) return got ? rc : set_err(GH_E_HIP, "peer transport: hipIpcGetMemHandle failed");
+  bool opened = true;
+  for (int r = 0; r < c->world && opened; ++r) {
+    if (r == c->rank) continue;
+    hipIpcMemHandle_t hr;
+    memcpy(&hr, all.data() + 64 * (size_t)r, sizeof hr);
+    void* p = nullptr;
+    opened = hipIpcOpenMemHandle(&p, hr, hipIpcMemLazyEnablePeerAccess) == hipSuccess;
+    out[r] = opened ? p : nullptr;
+  }
+  rc = peer_round(c, pr, opened, nullptr, 0, nullptr);
+  if (rc) {
+    ipc_close(c, out);
+    for (int r = 0; r < c->world; ++r) out[r] = nullptr;
+    return opened ? rc : set_err(GH_E_HIP, "peer transport: hipIpcOpenMemHandle failed");
+  }
+  out[c->rank] = own;
+  return GH_OK;
 }
 
 // the filter's multi-rank path (collectives, split steps) is in use
@@ -227,33 +290,42 @@ extern "C" int gh_ctx_create_peer(int device, int rank, int world, const gh_host
     return set_err(GH_E_INVAL, "gh_ctx_create_peer: bad argument (rank/world %d/%d, at most %d ranks)", rank, world,
                    kPeerMaxRanks);
   gh_ctx* c = new gh_ctx();
-  int rc = ctx_setup(device, hip_stream, c);
-  if (rc) {
-    delete c;
-    return rc;
-  }
   c->rank = rank;
   c->world = world;
   c->peer = true;
   c->hc = *bootstrap;
-  const size_t bytes = sizeof(uint64_t) * (size_t)mb_words(world);
-  if (hipExtMallocWithFlags((void**)&c->mbox, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
-    delete c;
-    return set_err(GH_E_NOMEM, "peer transport: mailbox");
-  }
-  if (hipMemset(c->mbox, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-    hipFree(c->mbox);
-    delete c;
-    return set_err(GH_E_HIP, "peer transport: mailbox init");
-  }
-  rc = ipc_exchange(c, c->mbox, (void**)c->mpeer);
-  if (rc) {
-    ipc_close(c, (void**)c->mpeer);
-    hipFree(c->mbox);
+  PeerRounds pr;
+  // (a local failure still runs the exchange's first round, flagged, so the
+  // other ranks fail with it instead of waiting)
+  auto fail = [&](int rc) {
+    peer_abort(c, pr);
+    if (c->mbox) hipFree(c->mbox);
+    if (c->own_stream) hipStreamDestroy(c->stream);
     delete c;
     return rc;
+  };
+  int rc = ctx_setup(device, hip_stream, c);
+  if (rc) return fail(rc);
+  if (hipDeviceGetAttribute(&c->wall_khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || c->wall_khz <= 0)
+    c->wall_khz = 100000;
+  c->peer_wait_ticks = (uint64_t)(kPeerWaitDefaultS * 1e3 * c->wall_khz);
+  const size_t bytes = sizeof(uint64_t) * (size_t)mb_words(world);
+  if (hipExtMallocWithFlags((void**)&c->mbox, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+    c->mbox = nullptr;
+    return fail(set_err(GH_E_NOMEM, "peer transport: mailbox"));
   }
+  if (hipMemset(c->mbox, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    return fail(set_err(GH_E_HIP, "peer transport: mailbox init"));
+  rc = ipc_exchange(c, pr, c->mbox, (void**)c->mpeer);
+  if (rc) return fail(rc);
   *out = c;
+  return GH_OK;
+}
+
+extern "C" int gh_ctx_set_peer_timeout(gh_ctx* c, double seconds) {
+  if (!c || !(seconds > 0.0) || seconds > 86400.0) return set_err(GH_E_INVAL, "gh_ctx_set_peer_timeout: bad argument");
+  if (!c->peer) return GH_OK;  // (no device waits on peers on the other transports)
+  c->peer_wait_ticks = (uint64_t)(seconds * 1e3 * c->wall_khz);
   return GH_OK;
 }
 
@@ -361,8 +433,13 @@ static int comm_allgather(gh_ctx* c, const void* dsend, void* drecv, size_t byte
 static int comm_exchange(gh_ctx* c, const std::vector<CommMsg>& sends, const std::vector<CommMsg>& recvs,
                          hipStream_t s) {
   if (sends.empty() && recvs.empty()) return GH_OK;
-  if (c->peer) return set_err(GH_E_STATE, "peer transport: rows move inside the resample kernels only");
-  if (!c->host_comm) {
+  // peer transport: the systematic rows move inside the resample kernels; the
+  // other resamplers' rows (multinomial, conditional SMC, the generic exchange)
+  // go through the bootstrap's host send/recv when it has one
+  if (c->peer && !c->hc.sendrecv)
+    return set_err(GH_E_STATE, "peer transport without a bootstrap sendrecv: rows move inside the systematic "
+                               "resample kernels only");
+  if (!c->host_comm && !c->peer) {
     // an error inside the group still closes it (an open group leaves the
     // communicator unusable); the first error is reported
     NCCL_TRY(ncclGroupStart());
@@ -881,12 +958,15 @@ struct gh_pf {
   // rows_recv, fine-grained, followed by R tag words indexed by sender) and
   // the row exchanges posted so far
   double* prow[kPeerMaxRanks] = {};
+  PeerRounds pr;                  // the set-up's bootstrap rounds (fail-together)
+  bool peer_ready = false;        // set up on every rank: destruction fences the ranks
   uint64_t* ptag[kPeerMaxRanks] = {};
   uint64_t row_use = 0;
   // multi-rank genealogy (record_history): per step, the rows received for
   // it (the parents on other ranks; D + 1 doubles each, row-indexed), kept by
   // the step's part-2 launch; chunked device storage
   std::vector<double*> rh_step;   // index t-1 (nullptr: none received)
+  std::vector<int64_t> rh_cnt;    // index t-1: rows kept for step t
   std::vector<char*> rh_chunks;
   size_t rh_used = 0, rh_cap = 0;
   int64_t* dlo = nullptr;         // [R + 1] floor(N k / R): the ranks' first global slots
@@ -1052,6 +1132,15 @@ static void pf_free(gh_pf* pf) {
   hipSetDevice(pf->ctx->device);
   hipStreamSynchronize(pf->s);
   if (pf->aux) hipStreamSynchronize(pf->aux);
+  if (pf->peer_ready) {
+    // peer transport: other ranks' kernels store rows and tags into this
+    // rank's row buffer; every rank has drained its stream before this fence,
+    // so none is still writing when the buffer is freed (gh_pf_destroy is
+    // collective on this transport)
+    uint8_t one = 1;
+    std::vector<uint8_t> all((size_t)pf->ctx->world);
+    pf->ctx->hc.allgather(pf->ctx->hc.user, &one, all.data(), 1);
+  }
   for (auto c : pf->chunks) hipFree(c);
   for (auto e : pf->ev) hipEventDestroy(e);
   hipFree(pf->logw); hipFree(pf->C); hipFree(pf->mark); hipFree(pf->cmark); hipFree(pf->bsum); hipFree(pf->pm); hipFree(pf->ps);
@@ -1274,7 +1363,9 @@ static int finish_plan(gh_pf* pf);
 static int rhist_reserve(gh_pf* pf, int t, int64_t count, double** out) {
   *out = nullptr;
   if ((int)pf->rh_step.size() < t) pf->rh_step.resize(t, nullptr);
+  if ((int)pf->rh_cnt.size() < t) pf->rh_cnt.resize(t, 0);
   pf->rh_step[t - 1] = nullptr;
+  pf->rh_cnt[t - 1] = 0;
   if (count <= 0) return GH_OK;
   const size_t bytes = (sizeof(double) * (size_t)(pf->D + 1) * (size_t)count + 255) & ~(size_t)255;
   if (pf->rh_used + bytes > pf->rh_cap) {
@@ -1288,6 +1379,7 @@ static int rhist_reserve(gh_pf* pf, int t, int64_t count, double** out) {
   *out = (double*)(pf->rh_chunks.back() + pf->rh_used);
   pf->rh_used += bytes;
   pf->rh_step[t - 1] = *out;
+  pf->rh_cnt[t - 1] = count;
   return GH_OK;
 }
 
@@ -1461,8 +1553,9 @@ extern "C" int gh_pf_init_conditional(gh_model* m, const gh_obs* obs, int64_t n_
   if (!m || !ref_x1 || !out) return set_err(GH_E_INVAL, "gh_pf_init_conditional: null argument");
   if (!opts || opts->resampler != GH_RESAMPLE_MULTINOMIAL)
     return set_err(GH_E_INVAL, "conditional SMC uses multinomial resampling (examples/pmmh/smc.jl:132)");
-  if (mr(m->ctx) && m->ctx->peer)
-    return set_err(GH_E_INVAL, "conditional SMC on R ranks needs the RCCL or host transport (multinomial rows)");
+  if (mr(m->ctx) && m->ctx->peer && !m->ctx->hc.sendrecv)
+    return set_err(GH_E_INVAL, "conditional SMC on R ranks over the peer transport needs a bootstrap with sendrecv "
+                               "(the multinomial rows go through the host)");
   if (m->family == GH_FAMILY_REGRESSION) return set_err(GH_E_INVAL, "conditional SMC needs a state-space model");
   return pf_init_impl(m, obs, GH_PROPOSAL_DEFAULT, n_particles, seed, opts, ref_x1, out);
 }
@@ -1518,7 +1611,14 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
     if (pairs) pf->nb_part = (n + 2 * kBlock - 1) / (2 * kBlock);
   }
   pf->nb_scan = (n + kScanTile - 1) / kScanTile;
-  auto fail = [&](int rc) { pf_free(pf); return rc; };
+  // peer transport: the set-up's bootstrap rounds are fail-together (a rank
+  // that fails runs the next round flagged, so every rank fails with it)
+  const bool peer_setup = mr(ctx) && ctx->peer;
+  auto fail = [&](int rc) {
+    if (peer_setup) peer_abort(ctx, pf->pr);
+    pf_free(pf);
+    return rc;
+  };
 #define ALLOC(ptr, bytes) \
   if (hipMalloc(&(ptr), (bytes)) != hipSuccess) return fail(set_err(GH_E_NOMEM, "hipMalloc %s", #ptr));
   ALLOC(pf->logw, sizeof(double) * n);
@@ -1540,10 +1640,10 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pick_resample_tiles(pf, n);
   ALLOC(pf->amax, sizeof(uint64_t) * 2 * kAmaxShards * kAmaxStride);
   if (mr(ctx)) {
-    if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC && (ctx->peer || ctx->world > kMaxRanks))
-      return fail(set_err(GH_E_INVAL, "multinomial resampling on R ranks needs the RCCL or host transport and "
-                                      "at most %d ranks (the peer transport's rows move inside the systematic "
-                                      "kernels only)", kMaxRanks));
+    if (pf->opts.resampler != GH_RESAMPLE_SYSTEMATIC && ((ctx->peer && !ctx->hc.sendrecv) || ctx->world > kMaxRanks))
+      return fail(set_err(GH_E_INVAL, "multinomial resampling on R ranks needs at most %d ranks and, on the peer "
+                                      "transport, a bootstrap with sendrecv (its rows go through the host)",
+                          kMaxRanks));
     if (!ctx->peer) {
       ALLOC(pf->rows_recv, sizeof(double) * (pf->D + 1) * n);
     } else {
@@ -1554,7 +1654,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
         return fail(set_err(GH_E_NOMEM, "peer transport: row buffer"));
       if (hipMemset(pf->rows_recv, 0, rb) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         return fail(set_err(GH_E_HIP, "peer transport: row buffer init"));
-      const int rc = ipc_exchange(ctx, pf->rows_recv, (void**)pf->prow);
+      const int rc = ipc_exchange(ctx, pf->pr, pf->rows_recv, (void**)pf->prow);
       if (rc) return fail(rc);
       for (int r = 0; r < ctx->world; ++r) {
         const int64_t nr = std::max<int64_t>(1, split_lo(pf->n_global, r + 1, ctx->world) - split_lo(pf->n_global, r, ctx->world));
@@ -1663,6 +1763,12 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   }
   rc = share_stats(pf);
   if (rc) return fail(rc);
+  if (peer_setup) {  // every rank created its shard (the last round), or every rank fails here
+    rc = peer_round(ctx, pf->pr, true, nullptr, 0, nullptr);
+    if (rc) return fail(rc);
+    pf->pr.over = true;
+    pf->peer_ready = true;
+  }
   pf->t = 1;
   pf->last_obs = o_prior;  // rejuvenation scores under the model (prior form)
   pf->obs_hist.assign(1, o_prior);
@@ -1748,10 +1854,9 @@ static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double
   a.stats_out = !mr(pf->ctx) ? pf->stats_all : pf->dev->stats;
   a.buf = slot_doubles(pf->n, pf->D) * 8 < (1LL << 32) ? 1 : 0;
   const bool multi = mr(pf->ctx);
-  // multi-rank, a resample whose ancestors were materialised (a genealogy
-  // query between maybe_resample! and this step): they name received rows
-  // (negative), which only the general load path reads
-  if (multi && flags_live(pf) && !pf->marks_pending) a.buf = 0;
+  // (multi-rank, a resample whose ancestors were materialised by a genealogy
+  // query between maybe_resample! and this step: they may name received rows
+  // (negative); the kernels test each wave's ancestors for that themselves)
   // One rank: every step writes block maxima only — the next maybe_resample!
   // sums the weights in its own pass, any other reader recomputes the sums
   // (ensure_stats) — so a caller's maybe_resample! + particle_filter_step!
@@ -2084,7 +2189,7 @@ static int finish_plan(gh_pf* pf) {
     // them behind this wait (on the filter's stream, after part 1)
     if (R > 1) {
       hipLaunchKernelGGL(k_peer_wait, dim3(1), dim3(64), 0, pf->s, (const uint64_t*)pf->ptag[q], R, q, pf->row_use,
-                         &pf->dev->error);
+                         c->peer_wait_ticks, &pf->dev->error);
       HIP_TRY(hipGetLastError());
     }
     return GH_OK;
@@ -2340,7 +2445,7 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
       if (rc == GH_OK) {
         const uint64_t w = __atomic_load_n(&pf->h_dec[1], __ATOMIC_ACQUIRE);
         const int err = (int)(uint32_t)(w >> 32);
-        if (err) return set_err(err, dev_error_msg(err));
+        if (err) return dev_fail(err);
         if (did) *did = (int)(uint32_t)w;
         if (ess) *ess = as_f64(__atomic_load_n(&pf->h_dec[2], __ATOMIC_ACQUIRE));
         return GH_OK;
@@ -2350,7 +2455,7 @@ extern "C" int gh_pf_maybe_resample(gh_pf* pf, double thr, int* did, double* ess
     DevScalars h;
     HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
     HIP_TRY(hipStreamSynchronize(pf->s));
-    if (h.error) return set_err(h.error, dev_error_msg(h.error));
+    if (h.error) return dev_fail(h.error);
     if (did) *did = h.fire;
     if (ess) *ess = h.ess;
   }
@@ -2393,7 +2498,7 @@ extern "C" int gh_pf_log_ml_estimate(gh_pf* pf, double* out) {
   std::vector<double> st;
   CHECK(ensure_stats(pf));
   CHECK(read_scalars(pf, &h, &st));
-  if (h.error) return set_err(h.error, dev_error_msg(h.error));
+  if (h.error) return dev_fail(h.error);
   if (flags_live(pf) && (h.pending | h.fire)) {  // all weights are 0: logsumexp(w) - log N = 0
     *out = h.log_ml_est;
     return GH_OK;
@@ -2469,6 +2574,16 @@ struct MrWalk {
 static const double* rh_of(const gh_pf* pf, int s) {
   return s >= 1 && s - 1 < (int)pf->rh_step.size() ? pf->rh_step[s - 1] : nullptr;
 }
+static int64_t rh_count(const gh_pf* pf, int s) {
+  return s >= 1 && s - 1 < (int)pf->rh_cnt.size() ? pf->rh_cnt[s - 1] : 0;
+}
+// after a genealogy query's kernels: a broken record they met (kErrGenealogy)
+static int walk_status(gh_pf* pf) {
+  int e = 0;
+  HIP_TRY(hipMemcpyAsync(&e, &pf->dev->error, sizeof(int), hipMemcpyDeviceToHost, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  return e ? dev_fail(e) : GH_OK;
+}
 
 static int mr_walk_begin(gh_pf* pf, MrWalk& w) {
   CHECK(materialize_marks(pf));
@@ -2481,7 +2596,10 @@ static int mr_walk_begin(gh_pf* pf, MrWalk& w) {
   CHECK(d2h(pf, w.res.data(), pf->res_hist, sizeof(int32_t) * (pf->cap + 2)));
   DevScalars h;
   CHECK(d2h(pf, &h, pf->dev, sizeof h));
-  if (h.error) return set_err(h.error, dev_error_msg(h.error));
+  // (a device error raised earlier does not end the walk here: the query is
+  // collective, so every rank runs all of its all-gathers and the error is
+  // reported at the end, walk_status — a rank that returned early would
+  // leave the others waiting in the next all-gather)
   CHECK(dalloc(w.cur, sizeof(int64_t) * (size_t)w.n));
   CHECK(dalloc(w.gp, sizeof(int64_t) * (size_t)w.pad));
   CHECK(dalloc(w.gp_all, sizeof(int64_t) * (size_t)w.pad * w.R));
@@ -2490,7 +2608,8 @@ static int mr_walk_begin(gh_pf* pf, MrWalk& w) {
     // a resample pending after the last step: the particles are its copies,
     // slot j's parent (local, or a row received for the next step)
     hipLaunchKernelGGL(k_mr_gparents, grid, dim3(kBlock), 0, pf->s, (const int32_t*)anc_for_step(pf, pf->t + 1), w.n,
-                       pf->lo, (const double*)pf->rows_recv, pf->D, w.cur.as<int64_t>());
+                       pf->lo, (const double*)pf->rows_recv, w.n, pf->D, w.cur.as<int64_t>(),
+                       &pf->dev->error);
   } else {
     hipLaunchKernelGGL(k_iota64, grid, dim3(kBlock), 0, pf->s, w.cur.as<int64_t>(), w.n, pf->lo);
   }
@@ -2504,11 +2623,12 @@ static int mr_walk_back(MrWalk& w, int s) {
   if (!w.res[s]) return GH_OK;
   const dim3 grid((unsigned)((w.n + kBlock - 1) / kBlock));
   hipLaunchKernelGGL(k_mr_gparents, grid, dim3(kBlock), 0, pf->s, (const int32_t*)anc_for_step(pf, s), w.n, pf->lo,
-                     rh_of(pf, s), pf->D, w.gp.as<int64_t>());
+                     rh_of(pf, s), rh_count(pf, s), pf->D, w.gp.as<int64_t>(), &pf->dev->error);
   HIP_TRY(hipGetLastError());
   CHECK(bulk_allgather(pf->ctx, w.gp.p, w.gp_all.p, sizeof(int64_t) * (size_t)w.pad, pf->s));
   hipLaunchKernelGGL(k_mr_back, grid, dim3(kBlock), 0, pf->s, w.cur.as<int64_t>(), w.n,
-                     (const int64_t*)w.gp_all.as<int64_t>(), (const int64_t*)pf->dlo, w.R, w.N, w.pad);
+                     (const int64_t*)w.gp_all.as<int64_t>(), (const int64_t*)pf->dlo, w.R, w.N, w.pad,
+                     &pf->dev->error);
   HIP_TRY(hipGetLastError());
   return GH_OK;
 }
@@ -2528,10 +2648,9 @@ static int mr_trajectory(gh_pf* pf, int t, double* dout) {
   CHECK(bulk_allgather(pf->ctx, send.p, slab.p, sizeof(double) * (size_t)pad_d, pf->s));
   hipLaunchKernelGGL(k_mr_states, dim3((unsigned)((w.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, pf->s,
                      (const int64_t*)w.cur.as<int64_t>(), w.n, (const double*)slab.as<double>(), pad_d,
-                     (const int64_t*)pf->dlo, w.R, w.N, pf->D, dout);
+                     (const int64_t*)pf->dlo, w.R, w.N, pf->D, dout, &pf->dev->error);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(pf->s));
-  return GH_OK;
+  return walk_status(pf);
 }
 
 // the score columns on R ranks (k_scores' values): per step, every rank
@@ -2552,21 +2671,20 @@ static int mr_scores(gh_pf* pf, const gh_model* m, const std::vector<StepObs>& o
     CHECK(with_model(m, [&](auto model, const auto& p) {
       hipLaunchKernelGGL(k_mr_slot_scores<decltype(model)>, grid, dim3(kBlock), 0, pf->s, (const double*)m->dparams,
                          p, obs[s - 1], s, (const double*)slot_x(pf, s),
-                         (const double*)(s > 1 ? slot_x(pf, s - 1) : nullptr), anc, rh_of(pf, s), n, w.pad,
-                         sc.as<double>());
+                         (const double*)(s > 1 ? slot_x(pf, s - 1) : nullptr), anc, rh_of(pf, s), rh_count(pf, s),
+                         n, w.pad, sc.as<double>(), &pf->dev->error);
     }));
     HIP_TRY(hipGetLastError());
     CHECK(bulk_allgather(pf->ctx, sc.p, sc_all.p, sizeof(double) * 2 * (size_t)w.pad, pf->s));
     hipLaunchKernelGGL(k_mr_take_scores, grid, dim3(kBlock), 0, pf->s, (const int64_t*)w.cur.as<int64_t>(), n,
                        (const double*)sc_all.as<double>(), (const int64_t*)pf->dlo, w.R, w.N, w.pad,
-                       dper + (int64_t)(s - 1) * 2 * n, dper + ((int64_t)(s - 1) * 2 + 1) * n);
+                       dper + (int64_t)(s - 1) * 2 * n, dper + ((int64_t)(s - 1) * 2 + 1) * n, &pf->dev->error);
     HIP_TRY(hipGetLastError());
     if (s > 1) CHECK(mr_walk_back(w, s));
   }
   hipLaunchKernelGGL(k_score_total, grid, dim3(kBlock), 0, pf->s, (const double*)dper, T, n, dtot);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(pf->s));
-  return GH_OK;
+  return walk_status(pf);
 }
 
 extern "C" int gh_pf_get_trajectory(gh_pf* pf, int t, double* out) {
@@ -3316,7 +3434,7 @@ extern "C" int gh_pf_sample_unweighted(gh_pf* pf, int64_t ns, uint64_t seed, int
   HIP_TRY(hipMemcpy(h.data(), all.p, bytes * (size_t)R, hipMemcpyDeviceToHost));
   DevScalars hs;
   CHECK(d2h(pf, &hs, pf->dev, sizeof hs));
-  if (hs.error) return set_err(hs.error, dev_error_msg(hs.error));
+  if (hs.error) return dev_fail(hs.error);
   const size_t stride = bytes / sizeof(int32_t);
   for (int64_t i = 0; i < ns; ++i) {
     idx[i] = -1;
@@ -3416,6 +3534,14 @@ extern "C" int gh_debug_mark_bits(gh_pf* pf, int bits) {
   return GH_OK;
 }
 
+extern "C" int gh_debug_set_ancestor(gh_pf* pf, int t, int64_t j, int32_t value) {
+  if (!pf || t < 2 || t > pf->t || j < 0 || j >= pf->n) return set_err(GH_E_INVAL, "gh_debug_set_ancestor: bad argument");
+  CHECK(materialize_marks(pf));
+  HIP_TRY(hipMemcpyAsync(anc_for_step(pf, t) + j, &value, sizeof(int32_t), hipMemcpyHostToDevice, pf->s));
+  HIP_TRY(hipStreamSynchronize(pf->s));
+  return GH_OK;
+}
+
 extern "C" int gh_debug_count_window(gh_ctx* ctx, int log2_inv) {
   if (!ctx || log2_inv < 0 || log2_inv > 40) return set_err(GH_E_INVAL, "gh_debug_count_window: bad argument");
   HIP_TRY(hipSetDevice(ctx->device));
@@ -3446,9 +3572,9 @@ extern "C" int gh_debug_exchange_lists(int64_t n_global, int world, int rank, co
 }
 
 static int exchange_states(gh_pf* pf, int32_t* anc_out) {
-  if (pf->ctx->peer)
+  if (pf->ctx->peer && !pf->ctx->hc.sendrecv)
     return set_err(GH_E_STATE, "peer transport: this resample needs the fused multi-rank kernels (systematic, "
-                               "at most %d ranks, co-resident tiles)", kMaxRanks);
+                               "at most %d ranks, co-resident tiles) or a bootstrap with sendrecv", kMaxRanks);
   gh_ctx* c = pf->ctx;
   const int R = c->world, q = c->rank;
   const int D = pf->D;
@@ -3459,7 +3585,7 @@ static int exchange_states(gh_pf* pf, int32_t* anc_out) {
   HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
   HIP_TRY(hipMemcpyAsync(tot.data(), pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->s));
   HIP_TRY(hipStreamSynchronize(pf->s));
-  if (h.error) return set_err(h.error, dev_error_msg(h.error));
+  if (h.error) return dev_fail(h.error);
   if (!h.fire) return GH_OK;
   uint64_t S = 0;
   for (int r = 0; r < R; ++r) S += tot[r];
@@ -3558,7 +3684,7 @@ static int exchange_states_mn(gh_pf* pf, int32_t* anc_out) {
   HIP_TRY(hipMemcpyAsync(&h, pf->dev, sizeof h, hipMemcpyDeviceToHost, pf->s));
   HIP_TRY(hipMemcpyAsync(tot.data(), pf->totals_all, sizeof(uint64_t) * R, hipMemcpyDeviceToHost, pf->s));
   HIP_TRY(hipStreamSynchronize(pf->s));
-  if (h.error) return set_err(h.error, dev_error_msg(h.error));
+  if (h.error) return dev_fail(h.error);
   if (!h.fire) return GH_OK;
   // the slot ranges (= the particle ranges) and their blocks
   std::vector<int64_t> lo(R + 1), boff0(R + 1);

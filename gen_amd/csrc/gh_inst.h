@@ -29,7 +29,8 @@
   X __global__ void gh::k_simulate<gh::LGModel<D, S>>(const double*, gh::LGParams, gh::SimArgs);                 \
   X __global__ void gh::k_mr_slot_scores<gh::LGModel<D, S>>(const double*, gh::LGParams, gh::StepObs, int,     \
                                                              const double*, const double*, const int32_t*,       \
-                                                             const double*, int64_t, int64_t, double*);          \
+                                                             const double*, int64_t, int64_t, int64_t, double*,  \
+                                                             int*);                                              \
   X __global__ void gh::k_pin_pre<gh::LGModel<D, S>, true>(const double*, gh::LGParams, gh::StepObs, gh::PinArgs); \
   X __global__ void gh::k_pin_pre<gh::LGModel<D, S>, false>(const double*, gh::LGParams, gh::StepObs, gh::PinArgs);
 

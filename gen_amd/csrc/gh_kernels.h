@@ -70,6 +70,12 @@ struct DevScalars {
   unsigned fire_streak;  // k_resample1: consecutive resamples that fired (its speculation policy)
 };
 
+// DevScalars::error: a gh_status in the low byte, the cause above it (the
+// host reports both: dev_error_msg in gh_api.hip)
+constexpr int kErrBarrier = 7;             // GH_E_STATE: a grid barrier timed out (blocks not co-resident)
+constexpr int kErrGenealogy = 7 | 1 << 8;  // GH_E_STATE: a genealogy walk met a broken record
+constexpr int kErrPeer = 7 | 2 << 8;       // GH_E_STATE: another rank never published (bounded wait)
+
 struct StepArgs {
   const double* xprev;   // wave-tiled states of the previous step (xidx)
   int32_t* anc;          // ancestors for this step (read when a resample is pending;
@@ -439,8 +445,13 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step(const double*
         double xp[D];
         if (pend && !use_marks) src = a.anc[j];
         // one load sequence per uniform case (no per-lane branch: values
-        // defined on divergent paths make the register allocator spill)
-        if (a.buf && a.mark_mode != 2) {  // local rows, slots < 4 GiB: 16-byte buffer loads of component pairs
+        // defined on divergent paths make the register allocator spill).  The
+        // buffer path whenever no lane of the wave takes a received row (a
+        // negative ancestor: multi-rank only, and only in the waves at the
+        // rank's [0, ra) / [rb, n) edges) — the general path's system-scope
+        // loads cannot be if-converted, and taking it for every wave of a
+        // multi-rank step cost k_step 37 -> 44 us at world 1 (round 5)
+        if (a.buf && __builtin_amdgcn_ballot_w64(src < 0) == 0) {  // local rows, slots < 4 GiB: 16-byte buffer loads of component pairs
           const __amdgpu_buffer_rsrc_t rp = gh_rsrc(a.xprev);
           const uint32_t tb = ((uint32_t)src >> 6) * (uint32_t)(kTileP * D * 8), l = (uint32_t)src & 63u;
 #pragma unroll
@@ -581,7 +592,8 @@ __global__ __launch_bounds__(kBlock, Model::kMinWaves) void k_step_pairs(const d
         }
         if (!has1) s1 = s0;
         double xp0, xp1;
-        if (a.remote) {  // uniform (multi-rank): a negative ancestor is row -1 - s of the receive buffer
+        // (wave-uniform: the general path only for a wave with a received row)
+        if (a.remote && __builtin_amdgcn_ballot_w64(s0 < 0 || s1 < 0) != 0) {  // a negative ancestor is row -1 - s of the receive buffer
           skip0 = a.part == 1 && s0 < 0;
           skip1 = a.part == 1 && s1 < 0;
           xp0 = s0 >= 0 ? a.xprev[s0] : (skip0 ? 0.0 : ld_sys(&a.remote[(-1 - s0) * a.ld_remote]));
@@ -1233,10 +1245,16 @@ struct Resample1Args {
 
 // maybe_resample!'s return value for the host (block 0, thread 0): the
 // decision words, a system-scope release, then the tag the host polls
-// (gh_pf_maybe_resample with did / ess: no stream synchronisation)
-__device__ __forceinline__ void post_decision(uint64_t* hdec, uint64_t htag, const Decision& dec) {
+// (gh_pf_maybe_resample with did / ess: no stream synchronisation).  An
+// error an earlier kernel raised (the filter's error word: a grid-barrier or
+// peer-wait timeout) is posted in place of the decision's own, so the call
+// reports it; a barrier timeout later in this same launch surfaces at the
+// filter's next synchronising call.
+__device__ __forceinline__ void post_decision(uint64_t* hdec, uint64_t htag, const Decision& dec, const int* derr) {
   if (!hdec) return;
-  hdec[1] = (uint64_t)(uint32_t)dec.fire | ((uint64_t)(uint32_t)dec.err << 32);
+  const int prior = __hip_atomic_load(const_cast<int*>(derr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int err = prior ? prior : dec.err;
+  hdec[1] = (uint64_t)(uint32_t)dec.fire | ((uint64_t)(uint32_t)err << 32);
   hdec[2] = as_u64(dec.ess);
   __threadfence_system();
   __hip_atomic_store(&hdec[0], htag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1520,7 +1538,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     if (threadIdx.x == 0) {
       sfire = m_ok && ((S1 * S1) / S2 < r.d.thr);
       if (blockIdx.x == 0) {
-        post_decision(r.hdec, r.htag, decision());
+        post_decision(r.hdec, r.htag, decision(), &r.dev->error);
         posted = true;
       }
     }
@@ -1539,7 +1557,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       r.dev->pending = 0;
       commit_decision(r.d, dec, r.dev, 0);
       r.dev->fire_streak = dec.fire ? r.dev->fire_streak + 1u : 0u;
-      if (!posted) post_decision(r.hdec, r.htag, dec);
+      if (!posted) post_decision(r.hdec, r.htag, dec, &r.dev->error);
     }
   };
   if (sums ? !m_ok : !sfire) {  // uniform over the grid: nobody publishes
@@ -1674,7 +1692,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
       if (blockIdx.x == 0 && !sfail && !spec) {
         S1 = g1;
         S2 = g2;
-        post_decision(r.hdec, r.htag, decision());
+        post_decision(r.hdec, r.htag, decision(), &r.dev->error);
         posted = true;
       }
     }
@@ -1927,6 +1945,7 @@ constexpr int kRecWords = 4;  // rank record: integer total, S_r, S2_r (f64 bits
 // (gh_peer.h: the transport's design; gh_ctx_create_peer)
 constexpr int kAgWords = 8;  // largest small all-gather payload (u64 words)
 constexpr int kPeerMaxRanks = 64;
+constexpr double kPeerWaitDefaultS = 30.0;  // default bound of a device wait on a peer (gh_ctx_set_peer_timeout)
 
 // mailbox layout (u64 words), for R ranks
 __host__ __device__ __forceinline__ int64_t mb_sh(int R, int par, int r) { return (int64_t)par * R + r; }
@@ -1949,23 +1968,24 @@ __host__ __device__ __forceinline__ int64_t mb_words(int R) { return 8LL * R + 2
 struct PeerBox {
   uint64_t* peer[kPeerMaxRanks];
   int R, rank;
+  uint64_t wait_ticks;  // the wait bound in wall-clock ticks (gh_ctx_set_peer_timeout)
 };
 
-
-// ~2.5 s of polling, then GH_E_STATE: a backstop against a rank that never
-// comes, long enough for host-side skew between processes (allocation,
-// first launches, descheduling)
-constexpr unsigned kPeerSpins = 1u << 25;
-
 // Wave-level poll: lanes r < R wait until word (base + stride * r) of the own
-// mailbox reaches `want` (monotonic tags).  Returns false on timeout.
-__device__ __forceinline__ bool peer_poll(const uint64_t* own, int64_t base, int R, uint64_t want, int skip = -1) {
+// mailbox reaches `want` (monotonic tags).  Returns false once `ticks` of the
+// constant-rate wall clock (s_memrealtime, 100 MHz) have passed: a backstop
+// against a rank that never comes, measured in time rather than polls (a
+// slow peer — host I/O, a first launch, descheduling — is waited for up to the
+// context's bound, 30 s by default; round 5's bound was ~2.5 s of polls).
+__device__ __forceinline__ bool peer_poll(const uint64_t* own, int64_t base, int R, uint64_t want, uint64_t ticks,
+                                          int skip = -1) {
   const int lane = threadIdx.x & 63;
   bool ok = lane >= R || lane == skip;
+  const uint64_t t0 = wall_clock64();
   for (unsigned spins = 0;; ++spins) {
     if (!ok) ok = ld_sys(own + base + lane) >= want;
     if (__builtin_amdgcn_ballot_w64(!ok) == 0) return true;
-    if (spins == kPeerSpins) return false;
+    if ((spins & 63) == 63 && wall_clock64() - t0 > ticks) return false;
     __builtin_amdgcn_s_sleep(2);
   }
 }
@@ -2044,14 +2064,14 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_a2(RankA2Arg
       const uint64_t* own = r.pb.peer[r.pb.rank];
       if (blockIdx.x == 0)
         peer_publish(r.pb, mb_sh(r.pb.R, par, r.pb.rank), mb_sh_tag(r.pb.R, par, r.pb.rank), amax_key(Ml), 1, r.use_sh);
-      const bool ok = peer_poll(own, mb_sh_tag(r.pb.R, par, 0), r.pb.R, r.use_sh);
+      const bool ok = peer_poll(own, mb_sh_tag(r.pb.R, par, 0), r.pb.R, r.use_sh, r.pb.wait_ticks);
       uint64_t kk = ok && lane < r.pb.R ? ld_sys(own + mb_sh(r.pb.R, par, lane)) : kAmaxEmpty;
       kk = readlane63_u64(wave_incl_max_u64(kk));
       if (lane == 0) {
         sM = ok ? amax_value(kk) : NAN;
         if (!ok) {
           sfail = 1;
-          r.dev->error = 7;  // GH_E_STATE: a rank never published
+          r.dev->error = kErrPeer;  // a rank never published
         }
       }
     }
@@ -2320,11 +2340,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     if (threadIdx.x < 64) {
       const int lane = threadIdx.x & 63, par = (int)(r.use_rec & 1);
       const uint64_t* own = r.pb.peer[r.pb.rank];
-      const bool ok = peer_poll(own, mb_rec_tag(r.pb.R, par, 0), r.pb.R, r.use_rec);
+      const bool ok = peer_poll(own, mb_rec_tag(r.pb.R, par, 0), r.pb.R, r.use_rec, r.pb.wait_ticks);
       if (lane < r.pb.R)
         for (int k = 0; k < kRecWords; ++k)
           srecs[lane * kRecWords + k] = ok ? ld_sys(own + mb_rec(r.pb.R, par, lane) + k) : (k == 3 ? as_u64(NAN) : 0ull);
-      if (!ok && lane == 0) r.dev->error = 7;  // GH_E_STATE: a rank never published its record
+      if (!ok && lane == 0) r.dev->error = kErrPeer;  // a rank never published its record
       if (blockIdx.x == 0 && lane < kAmaxShards) r.amax_reset[lane * kAmaxStride] = kAmaxEmpty;
     }
     lds_barrier();
@@ -2762,21 +2782,33 @@ static __global__ void k_iota64(int64_t* out, int64_t n, int64_t lo) {
 // global parent ids of this rank's slots at one step (rows: the received rows
 // the slots' negative ancestors index; read at system scope: the peer
 // transport's row buffer is written by other processes)
-static __global__ void k_mr_gparents(const int32_t* anc, int64_t n, int64_t lo, const double* rows, int D,
-                                     int64_t* gp) {
+// A record that names no particle (a local index outside [0, n), a received
+// row outside the nrows kept, or any received row when none were kept; nrows
+// < 0: the count is not known here) raises kErrGenealogy through the filter's
+// error word and the query returns GH_E_STATE — a wrong trajectory is never
+// returned.  The cursor becomes -1, which every later walk kernel also reports.
+static __global__ void k_mr_gparents(const int32_t* anc, int64_t n, int64_t lo, const double* rows, int64_t nrows,
+                                     int D, int64_t* gp, int* err) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
   const int32_t a = anc[j];
-  // (a received row without its record cannot happen; -1 makes the query fail, not fault)
-  gp[j] = a >= 0 ? lo + a : (rows ? __double_as_longlong(ld_sys(&rows[(int64_t)(-1 - a) * (D + 1) + D])) : -1);
+  const int64_t row = -1 - (int64_t)a;
+  int64_t g = -1;
+  if (a >= 0 && a < n) g = lo + a;
+  else if (a < 0 && rows && (nrows < 0 || row < nrows)) g = __double_as_longlong(ld_sys(&rows[row * (D + 1) + D]));
+  else *err = kErrGenealogy;
+  gp[j] = g;
 }
 
 // every cursor one step back: cur = parent of the slot it names
 static __global__ void k_mr_back(int64_t* cur, int64_t n, const int64_t* gp_all, const int64_t* dlo, int R, int64_t N,
-                                 int64_t pad) {
+                                 int64_t pad, int* err) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
-  if (cur[j] < 0 || cur[j] >= N) return;  // (a broken walk stays broken: the query's result is wrong, no fault)
+  if (cur[j] < 0 || cur[j] >= N) {  // (a broken walk: reported, not followed)
+    *err = kErrGenealogy;
+    return;
+  }
   int64_t i;
   const int64_t b = mr_pos(cur[j], dlo, R, N, pad, &i);
   cur[j] = gp_all[b + i];
@@ -2785,11 +2817,12 @@ static __global__ void k_mr_back(int64_t* cur, int64_t n, const int64_t* gp_all,
 // the cursors' states from an all-gather of every rank's (wave-tiled) slot,
 // rank r's at r * stride doubles: out[k * n + j]
 static __global__ void k_mr_states(const int64_t* cur, int64_t n, const double* slab, int64_t stride,
-                                   const int64_t* dlo, int R, int64_t N, int D, double* out) {
+                                   const int64_t* dlo, int R, int64_t N, int D, double* out, int* err) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
-  if (cur[j] < 0 || cur[j] >= N) {
+  if (cur[j] < 0 || cur[j] >= N) {  // (the query returns GH_E_STATE, these values are not handed out)
     for (int k = 0; k < D; ++k) out[k * n + j] = NAN;
+    *err = kErrGenealogy;
     return;
   }
   int64_t i;
@@ -2805,8 +2838,8 @@ static __global__ void k_mr_states(const int64_t* cur, int64_t n, const double* 
 template <class Model>
 __global__ __launch_bounds__(kBlock) void k_mr_slot_scores(const double* __restrict__ prm, typename Model::Params p0,
                                                            StepObs o, int s, const double* xs, const double* xprev,
-                                                           const int32_t* anc, const double* rows, int64_t n,
-                                                           int64_t pad, double* out) {
+                                                           const int32_t* anc, const double* rows, int64_t nrows,
+                                                           int64_t n, int64_t pad, double* out, int* err) {
   constexpr int D = Model::kD;
   const typename Model::Params p = p0.rebase(prm);
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -2816,12 +2849,16 @@ __global__ __launch_bounds__(kBlock) void k_mr_slot_scores(const double* __restr
   for (int k = 0; k < D; ++k) x[k] = xs[xidx(j, k, D)];
   if (s > 1) {
     const int64_t a = anc ? anc[j] : j;
-    if (a >= 0) {
+    if (a >= 0 && a < n) {
 #pragma unroll
       for (int k = 0; k < D; ++k) xp[k] = xprev[xidx(a, k, D)];
-    } else {
+    } else if (a < 0 && rows && (nrows < 0 || -1 - a < nrows)) {
 #pragma unroll
-      for (int k = 0; k < D; ++k) xp[k] = rows ? rows[(-1 - a) * (D + 1) + k] : NAN;
+      for (int k = 0; k < D; ++k) xp[k] = rows[(-1 - a) * (D + 1) + k];
+    } else {  // a broken record: reported (the query returns GH_E_STATE)
+#pragma unroll
+      for (int k = 0; k < D; ++k) xp[k] = NAN;
+      *err = kErrGenealogy;
     }
   } else {
 #pragma unroll
@@ -2835,12 +2872,13 @@ __global__ __launch_bounds__(kBlock) void k_mr_slot_scores(const double* __restr
 
 // the cursors' step-s columns from the all-gathered slot scores
 static __global__ void k_mr_take_scores(const int64_t* cur, int64_t n, const double* all, const int64_t* dlo, int R,
-                                        int64_t N, int64_t pad, double* lat, double* ob) {
+                                        int64_t N, int64_t pad, double* lat, double* ob, int* err) {
   const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (j >= n) return;
-  if (cur[j] < 0 || cur[j] >= N) {
+  if (cur[j] < 0 || cur[j] >= N) {  // (reported: the query returns GH_E_STATE)
     lat[j] = NAN;
     ob[j] = NAN;
+    *err = kErrGenealogy;
     return;
   }
   int64_t i;

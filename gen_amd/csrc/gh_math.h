@@ -104,7 +104,7 @@ GH_HD double u53(uint32_t a, uint32_t b) { return (double)u53_bits(a, b) * 0x1p-
 // the theorem's range conditions could fail: never for the model's states)
 // and for 0, inf and NaN the division itself.
 GH_HD double div20(double a) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(GH_DIV20_PLAIN)
   const double m = fabs(a);
   if (!(m >= 0x1p-1000 && m <= 0x1p1000)) return a / 20.0;
   const double y = 0.05;  // RN(1/20)
@@ -124,7 +124,7 @@ GH_HD double div20(double a) {
 // destination VGPRs with two v_mov_b32 per Horner step and uses v_fmac);
 // the same correctly rounded fused operation either way.
 GH_HD double fma_c(double a, double b, double c) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(GH_FMA_C_PLAIN)
   double d;
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
   return d;

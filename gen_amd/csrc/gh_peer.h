@@ -38,8 +38,8 @@ static __global__ __launch_bounds__(64) void k_peer_allgather(const uint64_t* se
   peer_publish(pb, mb_ag(pb.R, par, pb.rank), mb_ag_tag(pb.R, par, pb.rank), lane < words ? send[lane] : 0ull, words,
                use);
   const uint64_t* own = pb.peer[pb.rank];
-  if (!peer_poll(own, mb_ag_tag(pb.R, par, 0), pb.R, use)) {
-    if (lane == 0) *err = 7;  // GH_E_STATE
+  if (!peer_poll(own, mb_ag_tag(pb.R, par, 0), pb.R, use, pb.wait_ticks)) {
+    if (lane == 0) *err = kErrPeer;  // GH_E_STATE
     return;
   }
   for (int r = 0; r < pb.R; ++r)
@@ -60,8 +60,8 @@ static __global__ __launch_bounds__(64) void k_peer_signal(PeerRowTags pt, uint6
 }
 // ... and wait for every other rank's tag in the own row buffer
 static __global__ __launch_bounds__(64) void k_peer_wait(const uint64_t* own_tags, int R, int rank, uint64_t use,
-                                                         int* err) {
-  if (!peer_poll(own_tags, 0, R, use, rank) && (threadIdx.x & 63) == 0) *err = 7;
+                                                         uint64_t ticks, int* err) {
+  if (!peer_poll(own_tags, 0, R, use, ticks, rank) && (threadIdx.x & 63) == 0) *err = kErrPeer;
 }
 
 }  // namespace gh

@@ -48,6 +48,15 @@ struct PmmhArgs {
   int init;             // 1: draw the start from the prior and run the first filter (generate)
 };
 
+// The kernel is compiled in its own unit (gh_inst_pmmh.hip, GH_PMMH_KERNEL)
+// with fma_c as a plain fma (GH_FMA_C_PLAIN): the SGPR-operand form that
+// helps the particle-filter kernels cost this VALU-bound persistent kernel
+// 192.1 -> 177.6 ms per C5 launch pair (three interleaved runs each on one
+// box, round 6).  The values are the same: one correctly rounded fma.
+#if !defined(GH_PMMH_KERNEL)
+__global__ __launch_bounds__(kPmmhMaxInner) void k_pmmh(PmmhArgs a);
+#else
+
 // normal(mu, sd) logpdf in the reference's form (normal.jl:56-60)
 __device__ __forceinline__ double normal_lpdf(double x, double mu, double sd) {
   const double var = sd * sd;
@@ -258,5 +267,7 @@ __global__ __launch_bounds__(kPmmhMaxInner) void k_pmmh(PmmhArgs a) {
     for (int m = 0; m < 4; ++m) a.accepts[cl * 4 + m] = acc[m];
   }
 }
+
+#endif  // GH_PMMH_KERNEL
 
 }  // namespace gh

@@ -143,6 +143,12 @@ class Context:
     def synchronize(self):
         _lib.check(_lib.load().gh_ctx_synchronize(self.h))
 
+    def set_peer_timeout(self, seconds: float):
+        """Bound of every device wait on another rank (peer transport; 30 s
+        by default): a rank that has not posted by then is taken as gone and
+        the waiting filter raises GH_E_STATE."""
+        _lib.check(_lib.load().gh_ctx_set_peer_timeout(self.h, float(seconds)))
+
     def close(self):
         if self.h:
             lib = _lib.load()

@@ -172,14 +172,24 @@ int gh_ctx_create_hostcomm(int device, int rank, int world, const gh_host_comm* 
    received-row buffer), with tagged words and bounded polls — no collective
    call and no host round trip on the step path.  The bootstrap's allgather
    (host buffers) swaps the IPC handles once, at context and filter creation
-   (both collective over the ranks), and at gh_ctx_destroy; sendrecv is not
-   used.  Ranks on one GPU (processes sharing a device) or on GPUs that map
-   each other's memory (xGMI peers of one node).  world <= 64.  Multi-rank
-   filters on it resample systematically through the fused kernels (a
-   configuration that would need another form returns GH_E_STATE); a rank
-   that stops posting makes the others' waits end in GH_E_STATE. */
+   (both collective over the ranks, and fail-together: a rank that fails its
+   part makes every rank's call return an error, none is left waiting), and
+   fences the ranks at gh_ctx_destroy and at gh_pf_destroy of a multi-rank
+   filter — on this transport both destroys are COLLECTIVE: every rank calls
+   them, in the same order.  Ranks on one GPU (processes sharing a device) or
+   on GPUs that map each other's memory (xGMI peers of one node).
+   world <= 64.  Systematic resampling moves its rows inside the fused
+   kernels; the other forms (multinomial, conditional SMC, the generic
+   exchange) move theirs through the bootstrap's sendrecv when it is given
+   (GH_E_STATE without it).  Every device wait on another rank is bounded
+   in time (gh_ctx_set_peer_timeout, 30 s by default): a rank that stops
+   posting makes the others' waits end in GH_E_STATE ("peer transport: ...");
+   a slow one is waited for. */
 int gh_ctx_create_peer(int device, int rank, int world, const gh_host_comm* bootstrap, void* hip_stream,
                        gh_ctx** out);
+/* the bound of every device wait on another rank (peer transport; later
+   launches), seconds in (0, 86400]; no effect on the other transports */
+int gh_ctx_set_peer_timeout(gh_ctx* ctx, double seconds);
 int gh_ctx_destroy(gh_ctx* ctx);
 /* Debug / timing: filters created on this context afterwards take the
    multi-rank code path (collectives, split step after a resample, k_rank_a/b)
@@ -254,7 +264,7 @@ int gh_dist_random_dev(gh_ctx* ctx, const gh_dist_desc* d, int64_t n, uint64_t s
 void gh_pf_opts_default(gh_pf_opts* o);
 int gh_pf_init(gh_model* m, const gh_obs* obs, int proposal, int64_t n_particles, uint64_t seed,
                const gh_pf_opts* opts, gh_pf** out);
-int gh_pf_destroy(gh_pf* pf);
+int gh_pf_destroy(gh_pf* pf);  /* collective for a multi-rank filter on the peer transport */
 int gh_pf_step(gh_pf* pf, const gh_obs* obs, int proposal);
 /* initialize_particle_filter(model, args, obs, proposal, proposal_args, N) and
    particle_filter_step!(state, args, argdiffs, obs, proposal, proposal_args)
@@ -369,6 +379,12 @@ int gh_debug_exchange_lists(int64_t n_global, int world, int rank, const uint64_
    the epoch field, so that a short run crosses several epoch wraps (the marks
    are cleared at each).  Only before the first resample is pending. */
 int gh_debug_mark_bits(gh_pf* pf, int bits);
+
+/* test hook: overwrite the genealogy record of step t (2 <= t <= current):
+   particle j's ancestor index becomes `value` (a corrupted record, so that a
+   test can check that a genealogy query reports GH_E_STATE instead of
+   returning a wrong trajectory).  The filter is unusable afterwards. */
+int gh_debug_set_ancestor(gh_pf* pf, int t, int64_t j, int32_t value);
 
 /* test hook: the systematic slot counts are taken in floating point and
    recounted exactly when within a window of an integer (2^(ceil(log2 N) + 7 - 53)

@@ -62,6 +62,12 @@ def main():
     p.add_argument("--resampler", default="systematic", help="systematic or multinomial")
     p.add_argument("--csmc", action="store_true", help="conditional SMC (multinomial): particle 0 pinned to the "
                    "reference trajectory 0.9 x (the simulated latents)")
+    p.add_argument("--sleep", default=None, help="rank:step:seconds — that rank sleeps before that call-by-call step "
+                   "(a slow peer: the others' device waits must wait for it, not fail)")
+    p.add_argument("--peer-timeout", type=float, default=None, help="gh_ctx_set_peer_timeout (seconds)")
+    p.add_argument("--corrupt", type=int, default=None, help="after the run, rank 0 overwrites particle 0's "
+                   "ancestor record of step T with this value (gh_debug_set_ancestor); every rank then runs the "
+                   "collective get_traces queries and saves the errors they raise")
     p.add_argument("--out", required=True)
     a = p.parse_args()
 
@@ -70,7 +76,10 @@ def main():
     import gen_amd as gen
     from gen_amd.transport import GlooTransport
 
-    dist.init_process_group("gloo")
+    import datetime
+
+    # (bounded: a collective that one rank never joins fails the test instead of hanging it)
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=120))
     rank, world = dist.get_rank(), dist.get_world_size()
     if a.transport in ("gloo", "peer"):
         tr = GlooTransport()
@@ -83,7 +92,11 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         dev = a.device if a.device is not None else int(os.environ.get("LOCAL_RANK", "0"))
         ctx = gen.Context(device=dev, rank=rank, world=world, unique_id=uid[0])
+    if a.peer_timeout is not None:
+        ctx.set_peer_timeout(a.peer_timeout)
     gen.set_default_context(ctx)
+    sleep_rank, sleep_step, sleep_s = (int(v) if i < 2 else float(v) for i, v in
+                                       enumerate(a.sleep.split(":"))) if a.sleep else (-1, -1, 0.0)
     m = build_model(a.model)
     xs, ys = m.simulate(a.T, np.random.default_rng(5))
     addr = m.obs_address
@@ -99,6 +112,10 @@ def main():
         gen.run_particle_filter(st, list(ys[1 : a.T]), a.thr)
     m2 = changed_model(a.model) if a.params_step else None
     for t in range(2, a.T + 1) if not a.batched else ():
+        if rank == sleep_rank and t == sleep_step:
+            import time
+
+            time.sleep(sleep_s)
         did.append(gen.maybe_resample(st, a.thr))
         if a.mid_query and t == 4:
             st.states(2)
@@ -112,6 +129,22 @@ def main():
         if a.rejuv:
             gen.rejuvenate(st, a.rejuv)
     lml = gen.log_ml_estimate(st)
+    if a.corrupt is not None:
+        from gen_amd import _lib
+
+        if rank == 0:
+            _lib.check(_lib.load().gh_debug_set_ancestor(st.h, a.T, 0, a.corrupt))
+        errs = {}
+        for name, q in (("traj", lambda: st.states(1)), ("scores", lambda: gen.get_traces(st).scores())):
+            try:
+                q()
+                errs[name] = ""
+            except Exception as e:  # (the query must fail, not return a wrong trajectory)
+                errs[name] = f"{type(e).__name__}: {e}"
+        np.savez(f"{a.out}.rank{rank}.npz", **{f"err_{k}": np.array(v) for k, v in errs.items()})
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     extra = {}
     if a.genealogy:
         for t in sorted({1, min(5, a.T), a.T}):

@@ -279,7 +279,8 @@ def test_gloo_sharded_oracle_with_product_plan(tmp_path, R):
 @pytest.mark.parametrize("model,R,thr,n", [("lg4", 2, 3001.0, 3001), ("lg4", 3, None, 3001), ("kit", 2, None, 3001),
                                             ("kit", 2, 0.0, 3001), ("lg10", 2, 3001.0, 3001),
                                             ("lg4", 2, 1e9, 20011), ("kit", 4, 1e9, 4003),
-                                            ("kit_sharp", 4, None, 4003)])
+                                            ("kit_sharp", 4, None, 4003), ("kit", 8, 1e9, 8003),
+                                            ("lg4", 8, None, 8192)])
 def test_gpu_multirank_host_transport_equals_single_rank(tmp_path, model, R, thr, n):
     """R ranks share GPU 0 through the gloo host transport; the gathered shards
     equal the single-rank oracle bit for bit (log-ML within 1e-9).  n = 20011
@@ -327,7 +328,8 @@ def _check_against_oracle(out, model, R, n, T, seed, thr, resampler="systematic"
 @pytest.mark.gpu
 @pytest.mark.parametrize("model,R,thr,n", [("lg4", 2, None, 3001), ("lg4", 3, 1e9, 20011), ("kit", 2, None, 4096),
                                             ("kit", 4, 1e9, 8192), ("kit_sharp", 4, None, 4003),
-                                            ("lg10", 2, 3001.0, 3001)])
+                                            ("lg10", 2, 3001.0, 3001), ("kit", 8, 1e9, 16384),
+                                            ("kit_sharp", 8, None, 8003)])
 def test_gpu_multirank_batched_host_transport(tmp_path, model, R, thr, n):
     """The batched loop on R ranks (gh_pf_run: max-only steps whose maxima go to
     the atomic-max shards, the shards' all-gather, k_rank_a2's quantisation +
@@ -364,7 +366,8 @@ def test_gpu_multirank_path_over_rccl_one_rank(tmp_path, model, thr, n, batched)
 @pytest.mark.parametrize("model,R,thr,n,batched", [("lg4", 2, None, 3001, True), ("lg4", 3, 1e9, 20011, True),
                                                     ("kit", 2, None, 4096, True), ("kit", 4, 1e9, 8192, True),
                                                     ("kit_sharp", 4, None, 4003, True), ("lg10", 2, 3001.0, 3001, True),
-                                                    ("lg4", 2, None, 3001, False), ("kit", 3, 1e9, 4003, False)])
+                                                    ("lg4", 2, None, 3001, False), ("kit", 3, 1e9, 4003, False),
+                                                    ("kit", 8, 1e9, 8192, True), ("lg4", 8, None, 4096, False)])
 def test_gpu_multirank_peer_transport(tmp_path, model, R, thr, n, batched):
     """The peer transport (gh_ctx_create_peer): R processes share GPU 0, map
     each other's mailboxes and row buffers by IPC handle (swapped once over
@@ -384,7 +387,9 @@ def test_gpu_multirank_peer_transport(tmp_path, model, R, thr, n, batched):
 @pytest.mark.gpu
 @pytest.mark.parametrize("transport,model,R,thr,n,batched", [
     ("gloo", "lg4", 2, None, 3001, False), ("gloo", "kit", 3, 1e9, 4003, False), ("gloo", "kit_sharp", 4, None, 4003, True),
-    ("gloo", "lg10", 2, 3001.0, 3001, True), ("rccl1", "lg4", 1, 1e9, 3001, False)])
+    ("gloo", "lg10", 2, 3001.0, 3001, True), ("rccl1", "lg4", 1, 1e9, 3001, False),
+    ("peer", "lg4", 2, None, 3001, False), ("peer", "kit", 3, 1e9, 4003, True), ("peer", "kit_sharp", 4, None, 4003, True),
+    ("gloo", "kit", 8, 1e9, 8003, True)])
 def test_gpu_multirank_multinomial(tmp_path, gh_ctx, transport, model, R, thr, n, batched):
     """Multinomial resampling (the reference's own resampler, Categorical draws
     per slot, particle_filter.jl:200) on R ranks: every rank evaluates the
@@ -404,7 +409,8 @@ def test_gpu_multirank_multinomial(tmp_path, gh_ctx, transport, model, R, thr, n
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("transport,model,R,thr,n", [("gloo", "lg4", 2, None, 3001), ("gloo", "kit", 3, 1e9, 4003),
-                                                      ("rccl1", "lg4", 1, 1e9, 3001)])
+                                                      ("rccl1", "lg4", 1, 1e9, 3001), ("peer", "lg4", 2, None, 3001),
+                                                      ("peer", "kit", 3, 1e9, 4003)])
 def test_gpu_multirank_conditional_smc(tmp_path, transport, model, R, thr, n):
     """Conditional SMC (examples/pmmh/smc.jl:100-151) on R ranks: particle 0
     (rank 0's first) is pinned to the reference and is its own parent, the
@@ -490,6 +496,43 @@ def test_gpu_multirank_genealogy(tmp_path, gh_ctx, transport, model, R, thr, n, 
                   *(["--mid-query"] if mid else []), "--genealogy", "--out", out], R, timeout=400)
     _check_against_oracle(out, model, R, n, T, seed, thr)
     _check_genealogy(out, model, R, n, T, seed, thr, batched)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,sleep,timeout", [(2, "1:4:4.0", None), (3, "0:3:3.5", 60.0)])
+def test_gpu_multirank_peer_slow_rank(tmp_path, R, sleep, timeout):
+    """Peer transport, a slow rank: one rank sleeps seconds (longer than the
+    round-5 bound of ~2.5 s of polls) before a call-by-call step while the
+    others' kernels wait on the device for its maxima and rows.  The device
+    waits are bounded in time (30 s by default, gh_ctx_set_peer_timeout), so
+    they wait for it and the filter finishes bit-exact against the oracle."""
+    out = str(tmp_path / "slow")
+    model, n, T, seed, thr = "kit", 4003, 6, 9, 1e9
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", model, "--n", str(n), "--T", str(T),
+                  "--thr", str(thr), "--seed", str(seed), "--transport", "peer", "--sleep", sleep,
+                  *([] if timeout is None else ["--peer-timeout", str(timeout)]), "--out", out], R, timeout=300)
+    _check_against_oracle(out, model, R, n, T, seed, thr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,R,value", [("gloo", 2, 3001 // 2 + 7), ("gloo", 2, -1_000_000), ("rccl1", 1, 5000),
+                                               ("peer", 2, -1_000_000)])
+def test_gpu_multirank_broken_genealogy_raises(tmp_path, gh_ctx, transport, R, value):
+    """A genealogy walk that meets a broken record (an ancestor index outside
+    the rank's particles, or a received row that was never kept) raises
+    GH_E_STATE through the filter's device error word — the collective
+    trajectory and score queries fail on the rank whose walk broke instead of
+    returning NaN or another particle's trajectory."""
+    out = str(tmp_path / "bad")
+    n, T = 3001, 6
+    _run_workers([os.path.join(ROOT, "tests", "mr_worker.py"), "--model", "lg4", "--n", str(n), "--T", str(T),
+                  "--thr", "1e9", "--seed", "9", "--transport", transport,
+                  *(["--device", "0"] if transport == "rccl1" else []), "--corrupt", str(value), "--out", out], R,
+                 timeout=300)
+    r0 = np.load(f"{out}.rank0.npz")
+    for q in ("traj", "scores"):
+        msg = str(r0[f"err_{q}"])
+        assert msg.startswith("GenHipError: GH_E_STATE") and "genealogy" in msg, (q, msg)
 
 
 @pytest.mark.gpu

@@ -91,7 +91,7 @@ def main():
     else:
         jobs.append(("_c4", os.path.join(src, "c4.trace", "run_kernel_stats.csv"),
                      os.path.join(src, "c4.pmc*", "run_counter_collection.csv"),
-                     lambda k: ("k_step_pairs<" in k or "k_step<" in k) and "KitModel, false>" in k,
+                     lambda k: ("k_step_pairs<" in k or "k_step<" in k) and "KitModel, false" in k,
                      "profiles/pmc_k_step_kitagawa.json",
                      "bench.py --model kitagawa --particles 2097152 (C4 per GPU, systematic, resample every step)"))
         jobs.append(("_c3", os.path.join(src, "c3.trace", "run_kernel_stats.csv"),

@@ -29,6 +29,9 @@ VARIANTS = {
     "coal_b512w7": ["GH_COAL_BLOCK=512", "GH_COAL_WIN=7"],
     "coal_b64w10": ["GH_COAL_BLOCK=64", "GH_COAL_WIN=10"],
     "nospec": ["GH_SPEC_STREAK=0xffffffffu"],
+    "fmaplain": ["GH_FMA_C_PLAIN"],
+    "div20plain": ["GH_DIV20_PLAIN"],
+    "mathplain": ["GH_FMA_C_PLAIN", "GH_DIV20_PLAIN"],
     "prev": [],  # A/B: a library built from an earlier commit and copied in by hand
 }
 # instrumented builds (not timed by `run`)
