@@ -6,7 +6,7 @@ inference API (src/inference/particle_filter.jl, importance.jl); see
 DESIGN.md.  Importing it does not touch the GPU; the first call does.
 """
 from .choicemap import ChoiceMap, EmptyChoiceMap, Selection, choicemap, select
-from .models import BayesianLinearRegression, DiscreteHMM, KitagawaSSM, LinearGaussianSSM, Model
+from .models import BayesianLinearRegression, DiscreteHMM, KitagawaSSM, LinearGaussianSSM, Model, SlotSSM
 from .pf import (
     Context,
     NoChange,
@@ -46,7 +46,7 @@ from . import dists
 from ._lib import GenHipError
 
 __all__ = [
-    "ChoiceMap", "EmptyChoiceMap", "choicemap", "BayesianLinearRegression", "DiscreteHMM", "KitagawaSSM", "LinearGaussianSSM", "Model",
+    "ChoiceMap", "EmptyChoiceMap", "choicemap", "BayesianLinearRegression", "DiscreteHMM", "KitagawaSSM", "LinearGaussianSSM", "Model", "SlotSSM",
     "Context", "GaussianProposal", "NoChange", "OptimalProposal", "ParticleFilterState", "UnknownChange", "default_context",
     "get_log_weights", "get_traces", "importance_resampling", "importance_sampling",
     "initialize_particle_filter", "log_ml_estimate", "maybe_resample", "maybe_resample_async",

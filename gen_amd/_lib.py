@@ -23,7 +23,7 @@ STATUS = {
     7: "GH_E_STATE",
 }
 
-FAMILY_LGSSM, FAMILY_HMM, FAMILY_KITAGAWA, FAMILY_REGRESSION = 1, 2, 3, 4
+FAMILY_LGSSM, FAMILY_HMM, FAMILY_KITAGAWA, FAMILY_REGRESSION, FAMILY_SLOTS = 1, 2, 3, 4, 5
 RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = 0, 1
 PROPOSAL_DEFAULT, PROPOSAL_OPTIMAL, PROPOSAL_GAUSSIAN, PROPOSAL_LINEAR = 0, 1, 2, 3
 
@@ -49,7 +49,11 @@ class ModelDesc(ctypes.Structure):
 
 
 class Obs(ctypes.Structure):
-    _fields_ = [("values", POINTER(c_double)), ("n_values", c_int32), ("present", c_int32)]
+    pass
+
+
+Obs._fields_ = [("values", POINTER(c_double)), ("n_values", c_int32), ("present", c_int32), ("slot", c_int32),
+                ("reserved", c_int32), ("next", POINTER(Obs))]
 
 
 class PFOpts(ctypes.Structure):

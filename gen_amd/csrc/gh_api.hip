@@ -42,6 +42,8 @@ GH_LG_UNIT3(GH_EXTERN_TEMPLATE)
 GH_LG_UNIT4(GH_EXTERN_TEMPLATE)
 GH_LG_UNIT5(GH_EXTERN_TEMPLATE)
 GH_LG_UNIT6(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT0(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT1(GH_EXTERN_TEMPLATE)
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_err;
@@ -580,9 +582,140 @@ struct gh_model {
   HMMParams hmm{};
   KitParams kit{};
   RegParams reg{};
+  // slot family (gh_slots.h): the device description and, per mvnormal slot,
+  // the host halves of its observation whitening L_R^-1 (y - c)
+  SlotParams slots{};
+  std::vector<double> slot_c[kMaxSlots], slot_LR[kMaxSlots];
 };
 
 static bool lg_supported(int d) { return d >= 1 && d <= 16; }
+static bool slots_supported(int d) { return d >= 1 && d <= kMaxSlotD; }
+
+// GH_FAMILY_SLOTS: parse the slot description (include/gen_hip.h), derive the
+// device parameters into h (offsets into it in *off) and the model's host
+// halves.  Returns an error message or nullptr.
+static const char* slots_build(gh_model* m, const double* p, int64_t np, std::vector<double>& h,
+                               int64_t off[5 + kMaxSlots]) {
+  const int d = m->d;
+  if (!slots_supported(d)) return "slots: latent dimension d must be in 1..8";
+  if (np < 2) return "slots: need the latent form and the slot count";
+  SlotParams& sp = m->slots;
+  sp.lat = (int)p[0];
+  sp.K = (int)p[1];
+  if (p[0] != sp.lat || (sp.lat != SLOT_LAT_AFFINE && sp.lat != SLOT_LAT_KITAGAWA))
+    return "slots: latent form must be 0 (affine mvnormal) or 1 (Kitagawa)";
+  if (sp.lat == SLOT_LAT_KITAGAWA && d != 1) return "slots: the Kitagawa latent has d = 1";
+  if (p[1] != sp.K || sp.K < 1 || sp.K > kMaxSlots) return "slots: 1..4 observed slots";
+  int64_t i = 2 + 3 * (int64_t)sp.K;
+  if (np < i) return "slots: too few parameters (slot headers)";
+  int voff = 0, yoff = 0;
+  for (int k = 0; k < sp.K; ++k) {
+    const double* hd = p + 2 + 3 * k;
+    sp.dist[k] = (int)hd[0];
+    sp.m[k] = (int)hd[1];
+    sp.link[k] = (int)hd[2];
+    if (hd[0] != sp.dist[k] || hd[1] != sp.m[k] || hd[2] != sp.link[k]) return "slots: slot header not integral";
+    const int dist = sp.dist[k], mm = sp.m[k], link = sp.link[k];
+    int nv = 1;
+    if (dist == SLOT_MVNORMAL) {
+      if (link != LINK_AFFINE || mm < 1 || mm > kMaxObs) return "slots: mvnormal slot needs the affine mean, 1..32 values";
+      nv = mm;
+    } else if (dist == SLOT_NORMAL) {
+      if (mm != 1 || !(link == LINK_AFFINE || (link == LINK_KITAGAWA && d == 1)))
+        return "slots: normal slot: one value, affine mean (or x^2/20 with d = 1)";
+    } else if (dist == SLOT_POISSON) {
+      if (mm != 1 || link != LINK_EXP) return "slots: poisson slot: one count, rate exp(h.x + c)";
+      nv = 2;  // (y, log Gamma(y + 1))
+    } else if (dist == SLOT_BERNOULLI) {
+      if (mm != 1 || link != LINK_LOGISTIC) return "slots: bernoulli slot: one value, prob 1/(1 + exp(-(h.x + c)))";
+    } else if (dist == SLOT_CATEGORICAL) {
+      if (mm < 2 || mm > kMaxSlotClasses || link != LINK_SOFTMAX)
+        return "slots: categorical slot: 2..16 classes, probs softmax(W x + c)";
+    } else {
+      return "slots: unknown slot distribution";
+    }
+    sp.voff[k] = voff;
+    sp.yoff[k] = yoff;
+    voff += nv;
+    yoff += dist == SLOT_MVNORMAL ? mm : 1;
+  }
+  if (voff > kMaxObs || yoff > kMaxObs) return "slots: more than 32 observed values per step";
+  m->dy = yoff;
+  // latent block
+  off[0] = (int64_t)h.size();
+  if (sp.lat == SLOT_LAT_AFFINE) {
+    const int64_t need = 3LL * d * d + 2LL * d;
+    if (np < i + need) return "slots: too few parameters (affine latent: A b Q mu0 P0)";
+    const double *A = p + i, *b = A + d * d, *Q = b + d, *mu0 = Q + d * d, *P0 = mu0 + d;
+    std::vector<double> LQ(d * d), L0(d * d);
+    if (chol(d, Q, LQ.data())) return "slots: Q not positive definite";
+    if (chol(d, P0, L0.data())) return "slots: P0 not positive definite";
+    h.insert(h.end(), A, A + d * d);
+    h.insert(h.end(), b, b + d);
+    h.insert(h.end(), LQ.begin(), LQ.end());
+    h.insert(h.end(), mu0, mu0 + d);
+    h.insert(h.end(), L0.begin(), L0.end());
+    sp.cstQ = gauss_cst(d, LQ.data());
+    sp.cst0 = gauss_cst(d, L0.data());
+    i += need;
+  } else {
+    if (np < i + 3) return "slots: too few parameters (Kitagawa latent: mu1 s1 sd_x)";
+    const double mu1 = p[i], s1 = p[i + 1], sdx = p[i + 2];
+    if (!(s1 > 0.0) || !(sdx > 0.0)) return "slots: Kitagawa latent standard deviations must be > 0";
+    // normal.jl:56-60 with the standard deviations given (var = sd * sd)
+    sp.kit.mu1 = mu1;
+    sp.kit.s1 = s1;
+    sp.kit.sx = sdx;
+    sp.kit.inv2vx = 1.0 / (2.0 * (sdx * sdx));
+    sp.kit.cstx = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (sdx * sdx));
+    sp.kit.inv2v1 = 1.0 / (2.0 * (s1 * s1));
+    sp.kit.cst1 = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (s1 * s1));
+    h.push_back(0.0);
+    i += 3;
+  }
+  // slot blocks
+  for (int k = 0; k < sp.K; ++k) {
+    const int dist = sp.dist[k], mm = sp.m[k];
+    off[5 + k] = (int64_t)h.size();
+    if (dist == SLOT_MVNORMAL) {
+      const int64_t need = (int64_t)mm * d + mm + (int64_t)mm * mm;
+      if (np < i + need) return "slots: too few parameters (mvnormal slot: H c R)";
+      const double *H = p + i, *c = H + mm * d, *R = c + mm;
+      m->slot_LR[k].assign(mm * mm, 0.0);
+      if (chol(mm, R, m->slot_LR[k].data())) return "slots: an mvnormal slot's R is not positive definite";
+      std::vector<double> M(mm * d);
+      fwdsub(mm, d, m->slot_LR[k].data(), H, M.data());
+      m->slot_c[k].assign(c, c + mm);
+      h.insert(h.end(), M.begin(), M.end());
+      h.insert(h.end(), H, H + mm * d);
+      h.insert(h.end(), c, c + mm);
+      h.insert(h.end(), m->slot_LR[k].begin(), m->slot_LR[k].end());
+      sp.cst[k] = gauss_cst(mm, m->slot_LR[k].data());
+      i += need;
+    } else if (dist == SLOT_NORMAL) {
+      const int64_t need = sp.link[k] == LINK_AFFINE ? d + 2 : 1;
+      if (np < i + need) return "slots: too few parameters (normal slot: h c sd, or sd)";
+      if (sp.link[k] == LINK_AFFINE) h.insert(h.end(), p + i, p + i + d + 1);
+      else h.push_back(0.0);
+      const double sd = p[i + need - 1];
+      if (!(sd > 0.0)) return "slots: a normal slot's sd must be > 0";
+      sp.sd[k] = sd;
+      sp.inv2v[k] = 1.0 / (2.0 * (sd * sd));
+      sp.cst[k] = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (sd * sd));
+      i += need;
+    } else if (dist == SLOT_CATEGORICAL) {
+      const int64_t need = (int64_t)mm * d + mm;
+      if (np < i + need) return "slots: too few parameters (categorical slot: W c)";
+      h.insert(h.end(), p + i, p + i + need);
+      i += need;
+    } else {  // poisson, bernoulli: h c
+      if (np < i + d + 1) return "slots: too few parameters (h c)";
+      h.insert(h.end(), p + i, p + i + d + 1);
+      i += d + 1;
+    }
+  }
+  return nullptr;
+}
 
 extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model** out) {
   if (!ctx || !desc || !out) return set_err(GH_E_INVAL, "gh_model_create: null argument");
@@ -595,6 +728,7 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
   m->k = desc->k;
   m->v = desc->v;
   std::vector<double> h;  // packed derived parameters
+  int64_t slot_off[5 + kMaxSlots] = {};  // GH_FAMILY_SLOTS: the latent's and each slot's offset in h
   const double* p = desc->params;
   auto fail = [&](int code, const char* msg) {
     delete m;
@@ -737,6 +871,8 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->reg.n = n;
     for (int i = 0; i < n; ++i) m->reg.xs[i] = p[5 + i];
     h.push_back(0.0);
+  } else if (desc->family == GH_FAMILY_SLOTS) {
+    if (const char* e = slots_build(m, p, desc->n_params, h, slot_off)) return fail(GH_E_INVAL, e);
   } else {
     return fail(GH_E_INVAL, "unknown family");
   }
@@ -767,6 +903,17 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     m->hmm.T = m->dparams + K;
     m->hmm.E = m->dparams + K + K * K;
     m->hmm.logE = m->dparams + K + K * K + V * K;
+  } else if (m->family == GH_FAMILY_SLOTS) {
+    const int d = m->d;
+    SlotParams& sp = m->slots;
+    double* q = m->dparams + slot_off[0];
+    sp.base = m->dparams;
+    sp.A = q;
+    sp.b = sp.lat == SLOT_LAT_AFFINE ? q + d * d : q;
+    sp.LQ = sp.lat == SLOT_LAT_AFFINE ? q + d * d + d : q;
+    sp.mu0 = sp.lat == SLOT_LAT_AFFINE ? q + 2 * d * d + d : q;
+    sp.L0 = sp.lat == SLOT_LAT_AFFINE ? q + 2 * d * d + 2 * d : q;
+    for (int k = 0; k < kMaxSlots; ++k) sp.P[k] = m->dparams + (k < sp.K ? slot_off[5 + k] : 0);
   }
   *out = m;
   return GH_OK;
@@ -787,8 +934,56 @@ extern "C" int gh_model_state_dim(const gh_model* m, int* d) {
 }
 
 // host preprocessing of one step's observation
+// the slot family's observations: a chain of gh_obs, one per constrained slot
+// (any subset, each at most once), into StepObs::v at the slots' offsets and
+// the present bits
+static int make_obs_slots(const gh_model* m, const gh_obs* in, StepObs* o) {
+  const SlotParams& sp = m->slots;
+  int n = 0;
+  for (const gh_obs* e = in; e; e = e->next) {
+    if (++n > kMaxSlots) return set_err(GH_E_INVAL, "slots: more than %d observations in one step", kMaxSlots);
+    if (!e->present || !e->values) continue;
+    const int k = e->slot;
+    if (k < 0 || k >= sp.K) return set_err(GH_E_INVAL, "slots: observation for slot %d (the model has %d)", k, sp.K);
+    if ((o->present >> k) & 1)
+      return set_err(GH_E_DISCARD, "slots: slot %d constrained twice in one step", k);  // (particle_filter.jl:168-170)
+    const int mm = sp.m[k], dist = sp.dist[k];
+    const int nv = dist == SLOT_MVNORMAL ? mm : 1;
+    if (e->n_values != nv) return set_err(GH_E_INVAL, "slots: slot %d takes %d values, got %d", k, nv, e->n_values);
+    double* v = o->v + sp.voff[k];
+    const double y = e->values[0];
+    if (dist == SLOT_MVNORMAL) {
+      double r[kMaxObs];
+      for (int j = 0; j < mm; ++j) r[j] = e->values[j] - m->slot_c[k][j];
+      fwdsub(mm, 1, m->slot_LR[k].data(), r, v);
+    } else if (dist == SLOT_POISSON) {
+      if (!(y >= 0.0) || y != floor(y) || y > 0x1p52)
+        return set_err(GH_E_INVAL, "slots: poisson value %g is not a count (poisson.jl: x::Int)", y);
+      v[0] = y;
+      v[1] = gh_lgamma(y + 1.0);
+    } else if (dist == SLOT_BERNOULLI) {
+      if (!(y == 0.0 || y == 1.0)) return set_err(GH_E_INVAL, "slots: bernoulli value %g is not 0 or 1", y);
+      v[0] = y;
+    } else if (dist == SLOT_CATEGORICAL) {
+      if (!(y >= 0.0) || y >= (double)mm || y != floor(y))
+        return set_err(GH_E_INVAL, "slots: categorical value %g is not a class in 0..%d", y, mm - 1);
+      v[0] = y;
+    } else {
+      v[0] = y;
+    }
+    o->present |= 1 << k;
+  }
+  return GH_OK;
+}
+
 static int make_obs(const gh_model* m, int t, const gh_obs* in, StepObs* o) {
   memset(o, 0, sizeof(*o));
+  if (m->family == GH_FAMILY_SLOTS) {
+    if (m->slots.lat == SLOT_LAT_KITAGAWA) o->ct = 8.0 * gh_cos(1.2 * (double)t);
+    return make_obs_slots(m, in, o);
+  }
+  if (in && (in->next || in->slot != 0))
+    return set_err(GH_E_INVAL, "this family has one observed address (slot 0, no chained observations)");
   o->present = (in && in->present && in->values) ? 1 : 0;
   if (m->family == GH_FAMILY_KITAGAWA) o->ct = 8.0 * gh_cos(1.2 * (double)t);
   if (!o->present) return GH_OK;
@@ -1303,6 +1498,16 @@ static int with_model(const gh_model* m, F&& f) {
     case GH_FAMILY_HMM: f(HMMModel{}, m->hmm); break;
     case GH_FAMILY_KITAGAWA: f(KitModel{}, m->kit); break;
     case GH_FAMILY_REGRESSION: f(RegModel{}, m->reg); break;
+    case GH_FAMILY_SLOTS:
+      switch (m->d) {
+#define GH_SL_CASE(DD) \
+  case DD: f(SlotModel<DD>{}, m->slots); break;
+        GH_SL_CASE(1) GH_SL_CASE(2) GH_SL_CASE(3) GH_SL_CASE(4) GH_SL_CASE(5) GH_SL_CASE(6) GH_SL_CASE(7)
+        GH_SL_CASE(8)
+#undef GH_SL_CASE
+        default: return set_err(GH_E_INVAL, "slots d=%d not instantiated", m->d);
+      }
+      break;
     default: return set_err(GH_E_INVAL, "unknown family");
   }
   return GH_OK;
@@ -2862,6 +3067,8 @@ extern "C" int gh_pf_step_params_conditional(gh_pf* pf, const gh_obs* obs, gh_mo
 static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm, const double* pin_ref) {
   if (!pf->opts.record_history) return set_err(GH_E_STATE, "gh_pf_step_params needs record_history");
   const gh_model* m = pf->m;
+  if (m->family == GH_FAMILY_SLOTS)
+    return set_err(GH_E_INVAL, "gh_pf_step_params: not for the slot family (its parameter changes are not lowered)");
   if (nm->ctx != m->ctx || nm->family != m->family || nm->d != m->d || nm->dy != m->dy || nm->k != m->k ||
       nm->v != m->v)
     return set_err(GH_E_INVAL, "gh_pf_step_params: the new parameters must be of the same family and dimensions");
@@ -2943,7 +3150,9 @@ extern "C" int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double*
   if (n == 0) return GH_OK;
   HIP_TRY(hipSetDevice(m->ctx->device));
   const int d = m->d;
-  const int dy = (m->family == GH_FAMILY_LGSSM || m->family == GH_FAMILY_REGRESSION) ? m->dy : 1;
+  const int dy = (m->family == GH_FAMILY_LGSSM || m->family == GH_FAMILY_REGRESSION || m->family == GH_FAMILY_SLOTS)
+                     ? m->dy
+                     : 1;
   std::vector<StepObs> hobs(T);
   for (int t = 1; t <= T; ++t) CHECK(make_obs(m, t, nullptr, &hobs[t - 1]));
   const size_t nx = (size_t)T * d * n, ny = (size_t)T * dy * n, ns = (size_t)T * 2 * n;

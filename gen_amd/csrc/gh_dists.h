@@ -160,11 +160,11 @@ GH_HD double gamma_std(const DistRng& r, double a, uint32_t d0, const double* ta
 
 // Poisson(lam) by chop-down inversion from the mode m = floor(lam): subtract
 // pmf(m), then alternately pmf(m+1), pmf(m-1), pmf(m+2), ... from one uniform
-GH_HD double poisson_draw(const DistRng& r, double lam, uint32_t draw) {
+// u in [0, 1) (poisson_chop; poisson_draw takes u from the DIST stream)
+GH_HD double poisson_chop(double lam, double u) {
   if (lam == 0.0) return 0.0;
   if (!(lam > 0.0) || lam == INFINITY) return NAN;
   const double m = floor(lam);
-  double u = dist_u(r, draw);
   const double pm = gh_exp(xlogy(m, lam) - lam - gh_lgamma(m + 1.0));
   u -= pm;
   if (u <= 0.0) return m;
@@ -183,6 +183,11 @@ GH_HD double poisson_draw(const DistRng& r, double lam, uint32_t draw) {
     if (ph == 0.0 && (lo <= 0.0 || pl == 0.0)) break;  // rounding residue: all mass visited
   }
   return m;
+}
+GH_HD double poisson_draw(const DistRng& r, double lam, uint32_t draw) {
+  if (lam == 0.0) return 0.0;
+  if (!(lam > 0.0) || lam == INFINITY) return NAN;
+  return poisson_chop(lam, dist_u(r, draw));
 }
 
 // Binomial(n, p), the same chop-down from the mode floor((n + 1) p)

@@ -10,6 +10,7 @@
 #include "gh_scores.h"
 #include "gh_simulate.h"
 #include "gh_csmc.h"
+#include "gh_slots.h"
 
 // X is `extern template` (declaration) or `template` (definition)
 #define GH_LG_KERNELS(X, D, S)                                                                               \
@@ -60,6 +61,31 @@
 #define GH_LG_UNIT4(X) GH_LG_DIM(X, 14)
 #define GH_LG_UNIT5(X) GH_LG_DIM(X, 15)
 #define GH_LG_UNIT6(X) GH_LG_DIM(X, 16)
+
+// the slot family (gh_slots.h): SlotModel<D> for d = 1..8, in gh_inst_slots<k>.hip
+#define GH_SL_KERNELS(X, D)                                                                                     \
+  X __global__ void gh::k_step<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::SlotModel<D>, false, true>(const double*, gh::SlotParams, gh::StepObs,          \
+                                                              gh::StepArgs);                                     \
+  X __global__ void gh::k_rejuv<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::RejuvArgs); \
+  X __global__ void gh::k_rejuv<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs,              \
+                                                         gh::RejuvArgs);                                         \
+  X __global__ void gh::k_mh_drift<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs,            \
+                                                           gh::RejuvArgs, gh::DriftSd);                          \
+  X __global__ void gh::k_mh_drift<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs,           \
+                                                            gh::RejuvArgs, gh::DriftSd);                         \
+  X __global__ void gh::k_scores<gh::SlotModel<D>>(const double*, gh::SlotParams, gh::ScoreArgs,                 \
+                                                   const gh::DevScalars*);                                       \
+  X __global__ void gh::k_simulate<gh::SlotModel<D>>(const double*, gh::SlotParams, gh::SimArgs);                 \
+  X __global__ void gh::k_mr_slot_scores<gh::SlotModel<D>>(const double*, gh::SlotParams, gh::StepObs, int,     \
+                                                            const double*, const double*, const int32_t*,        \
+                                                            const double*, int64_t, int64_t, int64_t, double*,   \
+                                                            int*);                                               \
+  X __global__ void gh::k_pin_pre<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs); \
+  X __global__ void gh::k_pin_pre<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs);
+#define GH_SL_UNIT0(X) GH_SL_KERNELS(X, 1) GH_SL_KERNELS(X, 2) GH_SL_KERNELS(X, 3) GH_SL_KERNELS(X, 4)
+#define GH_SL_UNIT1(X) GH_SL_KERNELS(X, 5) GH_SL_KERNELS(X, 6) GH_SL_KERNELS(X, 7) GH_SL_KERNELS(X, 8)
 
 #define GH_EXTERN_TEMPLATE extern template
 #define GH_TEMPLATE template

@@ -1,0 +1,321 @@
+// gh_slots.h — the slot-described state-space family (GH_FAMILY_SLOTS).
+//
+// A Static-DSL Unfold kernel whose choices are given as address slots rather
+// than as a hand-lowered family: one latent address and up to kMaxSlots
+// observed addresses per step, each {distribution, dimension, mean form}
+// (include/gen_hip.h documents the parameter layout).  The device functor
+// below evaluates what Gen's generated code computes for one particle of
+// such a kernel (static_ir/generate.jl:24-43, 68-109: every constrained
+// choice adds its logpdf to the weight, every unconstrained one is drawn):
+//
+//   latent   x_t ~ mvnormal(A x_{t-1} + b, Q)      (x_1 ~ mvnormal(mu0, P0))
+//         or x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)   (d = 1;
+//            x_1 ~ normal(mu1, s1)) — examples/pmmh/model.jl:9-13
+//   slots    mvnormal(H x + c, R)                         mvnormal.jl:12-16
+//            normal(h.x + c, sd) or normal(x^2/20, sd)    normal.jl:56-60
+//            poisson(exp(h.x + c))                        poisson.jl:10-12
+//            bernoulli(1 / (1 + exp(-(h.x + c))))         bernoulli.jl:10-12
+//            categorical(softmax(W x + c))                categorical.jl:10-12 (0-based values)
+//
+// Each step constrains any subset of the observed slots (a gh_obs chain with
+// slot ids, choice_map.jl:163-225); the weight is the sum of the present
+// slots' logpdfs in slot order.  The arithmetic follows the hand-tuned
+// families where they coincide, so an LGSSM written as slots (affine latent,
+// one mvnormal slot) and the nonlinear SSM written as slots (Kitagawa latent,
+// one normal slot with the x^2/20 mean) give the LGSSM / Kitagawa families'
+// states, weights and ancestors bit for bit; those families stay the fast
+// specialisations.  oracle/gh_oracle.c restates every line (slot_* there).
+#pragma once
+#include "gh_dists.h"
+#include "gh_models.h"
+
+namespace gh {
+
+constexpr int kMaxSlots = 4;        // observed addresses per step
+constexpr int kMaxSlotD = 8;        // latent dimension (SlotModel<1..8> instantiated)
+constexpr int kMaxSlotClasses = 16;  // categorical slot classes
+constexpr uint32_t kSlotSimDraws = 32;  // simulate(): slot k draws from kSimObsDraw + 32 k
+
+enum SlotDist : int { SLOT_MVNORMAL = 1, SLOT_NORMAL = 2, SLOT_POISSON = 3, SLOT_BERNOULLI = 4, SLOT_CATEGORICAL = 5 };
+enum SlotLink : int { LINK_AFFINE = 0, LINK_KITAGAWA = 1, LINK_EXP = 2, LINK_LOGISTIC = 3, LINK_SOFTMAX = 4 };
+enum SlotLatent : int { SLOT_LAT_AFFINE = 0, SLOT_LAT_KITAGAWA = 1 };
+
+struct SlotParams {
+  const double* base;
+  // affine latent: A | b | chol(Q) | mu0 | chol(P0) in the device buffer
+  const double *A, *b, *LQ, *mu0, *L0;
+  double cstQ, cst0;  // their log-normalisers (score columns)
+  KitParams kit;      // Kitagawa latent (mu1, s1, sx, inv2vx, cstx, inv2v1, cst1)
+  int lat, K;
+  int dist[kMaxSlots], m[kMaxSlots], link[kMaxSlots];
+  int voff[kMaxSlots];  // the slot's values in StepObs::v
+  int yoff[kMaxSlots];  // the slot's rows in simulate()'s output
+  // per slot: mvnormal M = L_R^-1 H [m*d] | H [m*d] | c [m] | L_R [m*m];
+  // normal / poisson / bernoulli h [d] | c; categorical W [m*d] | c [m]
+  const double* P[kMaxSlots];
+  double cst[kMaxSlots];    // mvnormal -0.5 (m log 2pi + log det R); normal -0.5 log(2 pi sd^2)
+  double inv2v[kMaxSlots];  // normal 1 / (2 sd^2)
+  double sd[kMaxSlots];     // normal sd (simulate)
+  __device__ SlotParams rebase(const double* __restrict__ prm) const {
+    SlotParams q = *this;
+    q.A = rebased(*this, prm, A);
+    q.b = rebased(*this, prm, b);
+    q.LQ = rebased(*this, prm, LQ);
+    q.mu0 = rebased(*this, prm, mu0);
+    q.L0 = rebased(*this, prm, L0);
+#pragma unroll
+    for (int k = 0; k < kMaxSlots; ++k) q.P[k] = rebased(*this, prm, P[k]);
+    return q;
+  }
+};
+
+template <int D>
+struct SlotModel {
+  static constexpr int kD = D;
+  static constexpr int kMinWaves = D <= 3 ? 8 : (D <= 6 ? 6 : 4);
+  using Params = SlotParams;
+
+  // c + h.x (fma over the components ascending)
+  __device__ static double affine(const double* h, double c, const double* x) {
+    double acc = c;
+#pragma unroll
+    for (int j = 0; j < D; ++j) acc = fma(h[j], x[j], acc);
+    return acc;
+  }
+
+  // the logpdf of slot k's value (o.v + voff) at latent x
+  __device__ static double slot_lpdf(const Params& p, const StepObs& o, int k, const double* x) {
+    const double* P = p.P[k];
+    const double* v = o.v + p.voff[k];
+    const int m = p.m[k];
+    switch (p.dist[k]) {
+      case SLOT_MVNORMAL: {  // LGModel::obs (dense): v = L_R^-1 (y - c)
+        double quad = 0.0;
+        for (int r = 0; r < m; ++r) {
+          double acc = v[r];
+#pragma unroll
+          for (int j = 0; j < D; ++j) acc = fma(-P[r * D + j], x[j], acc);
+          quad = fma(acc, acc, quad);
+        }
+        return p.cst[k] - 0.5 * quad;
+      }
+      case SLOT_NORMAL: {
+        const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : affine(P, P[D], x);
+        const double diff = v[0] - mean;
+        return -(diff * diff) * p.inv2v[k] + p.cst[k];
+      }
+      case SLOT_POISSON: {  // poisson.jl:10-12 with lambda = exp(h.x + c); v[1] = log Gamma(y + 1)
+        const double lam = gh_exp(affine(P, P[D], x));
+        return v[0] < 0.0 ? -INFINITY : (v[0] * gh_log(lam) - lam) - v[1];
+      }
+      case SLOT_BERNOULLI: {  // bernoulli.jl:10-12 with prob = 1 / (1 + exp(-(h.x + c)))
+        const double prob = 1.0 / (1.0 + gh_exp(-affine(P, P[D], x)));
+        return v[0] != 0.0 ? gh_log(prob) : gh_log(1.0 - prob);
+      }
+      default: {  // categorical.jl:10-12 with probs = softmax(W x + c): exp(eta - max) / sum
+        // (eta_j recomputed per pass: no per-lane array indexed at run time)
+        double mx = -INFINITY;
+        for (int j = 0; j < m; ++j) mx = fmax(mx, affine(P + j * D, P[m * D + j], x));
+        double s = 0.0, ey = 0.0;
+        const int y = (int)v[0];
+        for (int j = 0; j < m; ++j) {
+          const double e = gh_exp(affine(P + j * D, P[m * D + j], x) - mx);
+          s += e;
+          if (j == y) ey = e;
+        }
+        return gh_log(ey / s);
+      }
+    }
+  }
+
+  // the weight: the present slots' logpdfs (o.present bit k) in slot order
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) {
+    double w = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxSlots; ++k)
+      if (k < p.K && ((o.present >> k) & 1)) w = w + slot_lpdf(p, o, k, x);
+    return w;
+  }
+
+  // the latent's logpdf (LGModel<D, 0>::score / KitModel::score forms)
+  __device__ static double latent_lpdf(const Params& p, const StepObs& o, uint32_t t, const double* xp,
+                                       const double* x) {
+    if (p.lat == SLOT_LAT_KITAGAWA) {
+      double mean = p.kit.mu1, inv2 = p.kit.inv2v1, cst = p.kit.cst1;
+      if (t > 1) {
+        mean = KitModel::mean(o, xp[0]);
+        inv2 = p.kit.inv2vx;
+        cst = p.kit.cstx;
+      }
+      const double d = x[0] - mean;
+      return -(d * d) * inv2 + cst;
+    }
+    const double* L = t == 1 ? p.L0 : p.LQ;
+    double u[D];
+    double quad = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double mean;
+      if (t == 1) {
+        mean = p.mu0[i];
+      } else {
+        mean = p.b[i];
+#pragma unroll
+        for (int k = 0; k < D; ++k) mean = fma(p.A[i * D + k], xp[k], mean);
+      }
+      double r = x[i] - mean;
+#pragma unroll
+      for (int k = 0; k < i; ++k) r = fma(-L[i * D + k], u[k], r);
+      u[i] = r / L[i * D + i];
+      quad = fma(u[i], u[i], quad);
+    }
+    return (t == 1 ? p.cst0 : p.cstQ) - 0.5 * quad;
+  }
+
+  __device__ static void score(const Params& p, const StepObs& o, uint32_t t, const double* xp, const double* x,
+                               double* lat, double* ob) {
+    *lat = latent_lpdf(p, o, t, xp, x);
+    *ob = loglik(p, o, x);
+  }
+
+  // the latent draw of step t (t = 1: from the initial distribution)
+  __device__ static void draw_latent(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, uint32_t t,
+                                     const double* xp, double* x, const Draw& dr) {
+    if (p.lat == SLOT_LAT_KITAGAWA) {  // the nonlinear SSM's paired normals (KitModel::znorm)
+      const double z = KitModel::znorm(seed, pid, t, dr);
+      x[0] = t == 1 ? p.kit.mu1 + p.kit.s1 * z : KitModel::mean(o, xp[0]) + p.kit.sx * z;
+      return;
+    }
+    double z[D + 1];
+    normals_n<D>(seed, pid, t, dr.stream, dr.base, z, dr.tab);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc;
+      if (t == 1) {
+        acc = p.mu0[i];
+#pragma unroll
+        for (int k = 0; k <= i; ++k) acc = fma(p.L0[i * D + k], z[k], acc);
+      } else {
+        acc = p.b[i];
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc = fma(p.A[i * D + k], xp[k], acc);
+#pragma unroll
+        for (int k = 0; k <= i; ++k) acc = fma(p.LQ[i * D + k], z[k], acc);
+      }
+      x[i] = acc;
+    }
+  }
+
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, int /*proposal*/,
+                                double* x, Draw dr = {STREAM_INIT, 0}) {
+    draw_latent(p, o, seed, pid, 1, nullptr, x, dr);
+    return loglik(p, o, x);
+  }
+
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, uint32_t t,
+                                int /*proposal*/, const double* xp, double* x, Draw dr = {STREAM_STEP, 0}) {
+    draw_latent(p, o, seed, pid, t, xp, x, dr);
+    return loglik(p, o, x);
+  }
+
+  // simulate(): every slot's value drawn from the model (slot k from its own
+  // draws kSimObsDraw + 32 k of the SIM stream), written to rows yoff[k].. with
+  // stride ys, and the sum of their logpdfs
+  __device__ static double sim_obs(const Params& p, uint64_t seed, uint64_t pid, uint32_t t, const double* x,
+                                   double* y, int64_t ys, const double* tab) {
+    double total = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxSlots; ++k) {
+      if (k >= p.K) break;
+      const double* P = p.P[k];
+      const int m = p.m[k];
+      const uint32_t draw = kSimObsDraw + kSlotSimDraws * (uint32_t)k;
+      double* yk = y + (int64_t)p.yoff[k] * ys;
+      double lp;
+      switch (p.dist[k]) {
+        case SLOT_MVNORMAL: {  // y = H x + c + L_R z, scored through L_R^-1 (y - c) (LGModel::sim_obs)
+          const double *H = P + m * D, *c = H + m * D, *LR = c + m;
+          double z[kMaxObs], v[kMaxObs];
+          normals_rt(seed, pid, t, STREAM_SIM, draw, m, z, tab);
+          for (int r = 0; r < m; ++r) {
+            double acc = c[r];
+#pragma unroll
+            for (int j = 0; j < D; ++j) acc = fma(H[r * D + j], x[j], acc);
+            for (int q = 0; q <= r; ++q) acc = fma(LR[r * m + q], z[q], acc);
+            yk[r * ys] = acc;
+            double s = acc - c[r];
+            for (int q = 0; q < r; ++q) s = fma(-LR[r * m + q], v[q], s);
+            v[r] = s / LR[r * m + r];
+          }
+          double quad = 0.0;
+          for (int r = 0; r < m; ++r) {
+            double acc = v[r];
+#pragma unroll
+            for (int j = 0; j < D; ++j) acc = fma(-P[r * D + j], x[j], acc);
+            quad = fma(acc, acc, quad);
+          }
+          lp = p.cst[k] - 0.5 * quad;
+          break;
+        }
+        case SLOT_NORMAL: {
+          double z0, z1;
+          normal_pair(rng_block(seed, pid, t, STREAM_SIM, draw), &z0, &z1, tab);
+          const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : affine(P, P[D], x);
+          yk[0] = mean + p.sd[k] * z0;
+          const double diff = yk[0] - mean;
+          lp = -(diff * diff) * p.inv2v[k] + p.cst[k];
+          break;
+        }
+        case SLOT_POISSON: {
+          const u32x4 w = rng_block(seed, pid, t, STREAM_SIM, draw);
+          const double lam = gh_exp(affine(P, P[D], x));
+          const double v = poisson_chop(lam, u53(w.x, w.y));
+          yk[0] = v;
+          lp = (v * gh_log(lam) - lam) - gh_lgamma(v + 1.0);
+          break;
+        }
+        case SLOT_BERNOULLI: {  // bernoulli.jl:19: rand() < prob
+          const u32x4 w = rng_block(seed, pid, t, STREAM_SIM, draw);
+          const double prob = 1.0 / (1.0 + gh_exp(-affine(P, P[D], x)));
+          const bool b = u53(w.x, w.y) < prob;
+          yk[0] = b ? 1.0 : 0.0;
+          lp = b ? gh_log(prob) : gh_log(1.0 - prob);
+          break;
+        }
+        default: {  // categorical: inverse CDF over the softmax weights e_j (dist_cat's sums)
+          const u32x4 w = rng_block(seed, pid, t, STREAM_SIM, draw);
+          double mx = -INFINITY;
+          for (int j = 0; j < m; ++j) mx = fmax(mx, affine(P + j * D, P[m * D + j], x));
+          double s = 0.0;
+          for (int j = 0; j < m; ++j) s += gh_exp(affine(P + j * D, P[m * D + j], x) - mx);
+          const double target = u53(w.x, w.y) * s;
+          double cum = 0.0, ey = 0.0, elast = 0.0;
+          int yv = -1, last = -1;
+          for (int j = 0; j < m && yv < 0; ++j) {
+            const double e = gh_exp(affine(P + j * D, P[m * D + j], x) - mx);
+            cum += e;
+            if (e > 0.0) {
+              last = j;
+              elast = e;
+            }
+            if (cum > target && e > 0.0) {
+              yv = j;
+              ey = e;
+            }
+          }
+          if (yv < 0) {
+            yv = last;
+            ey = elast;
+          }
+          yk[0] = (double)yv;
+          lp = gh_log(ey / s);
+          break;
+        }
+      }
+      total = total + lp;
+    }
+    return total;
+  }
+};
+
+}  // namespace gh

@@ -15,6 +15,8 @@ Address schemes follow the reference programs they mirror:
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import _lib
@@ -65,6 +67,11 @@ class Model:
 
     def obs_values(self, value) -> np.ndarray:
         return np.ascontiguousarray(np.atleast_1d(np.asarray(value, dtype=np.float64)).ravel())
+
+    def gh_obs(self, value):
+        """(gh_obs of one step's observation, what must stay alive while it is used)."""
+        arr = self.obs_values(value)
+        return _lib.Obs(_lib.dptr(arr), arr.size, 1, 0, 0, None), arr
 
     def desc(self) -> tuple[_lib.ModelDesc, np.ndarray]:
         p = np.ascontiguousarray(self.params(), dtype=np.float64)
@@ -328,3 +335,202 @@ class BayesianLinearRegression(Model):
         xs = np.arange(1.0, 11.0)
         ys = np.array([8.23, 5.87, 3.99, 2.59, 0.23, -0.66, -3.53, -6.91, -7.24, -9.90])
         return BayesianLinearRegression(xs), ys
+
+
+# slot distributions / mean forms of GH_FAMILY_SLOTS (include/gen_hip.h)
+_SLOT_DIST = {"mvnormal": 1, "normal": 2, "poisson": 3, "bernoulli": 4, "categorical": 5}
+_LINK = {"affine": 0, "x^2/20": 1, "exp": 2, "logistic": 3, "softmax": 4}
+
+
+class SlotSSM(Model):
+    """A Static-DSL Unfold kernel given by its address slots (GH_FAMILY_SLOTS,
+    gen_amd/csrc/gh_slots.h): the kernels the four hand-lowered families do not
+    cover drop in without new device code.  One latent address and 1..4 observed
+    addresses per step, any subset of which a step constrains
+    (static_ir/generate.jl:24-43; choice_map.jl:163-225):
+
+        @gen (static) function kernel(t::Int, x_prev, p)
+            x = @trace(mvnormal(p.A * x_prev + p.b, p.Q), :x)       # latent "affine"
+            # or: x = @trace(normal(x_prev/2 + 25x_prev/(1+x_prev^2) + 8cos(1.2t), p.sd_x), :x)
+            @trace(mvnormal(p.H * x + p.c, p.R), :y)                # slot "mvnormal"
+            @trace(normal(p.h' * x + p.c0, p.sd), :z)                # slot "normal" (or mean x^2/20)
+            @trace(poisson(exp(p.h' * x + p.c0)), :count)            # slot "poisson"
+            @trace(bernoulli(1 / (1 + exp(-(p.h' * x + p.c0)))), :on)  # slot "bernoulli"
+            @trace(categorical(softmax(p.W * x + p.c)), :kind)       # slot "categorical" (0-based here)
+            return x
+        end
+
+    latent: {"form": "affine", "A", "b", "Q", "mu0", "P0"} or
+            {"form": "kitagawa", "mu1", "s1", "sd_x"} (d = 1)
+    slots:  [{"name", "dist", ...}] with per distribution
+            mvnormal: H [m, d], c [m], R [m, m]; normal: h [d], c, sd (or mean "x^2/20", sd);
+            poisson / bernoulli: h [d], c; categorical: W [m, d], c [m]
+    Observations of step t: {("chain", t, name): value} (any subset of the slots).
+    """
+
+    family = _lib.FAMILY_SLOTS
+
+    def __init__(self, latent: dict, slots: list, latent_name: str = "x"):
+        self.latent = dict(latent)
+        self.latent_name = latent_name
+        form = self.latent.get("form", "affine")
+        if form == "affine":
+            self.A = np.atleast_2d(np.asarray(latent["A"], dtype=np.float64))
+            self.d = self.A.shape[0]
+            f = lambda k, shape: np.asarray(latent[k], dtype=np.float64).reshape(shape)  # noqa: E731
+            self.b = f("b", (self.d,)) if "b" in latent else np.zeros(self.d)
+            self.Q, self.mu0, self.P0 = f("Q", (self.d, self.d)), f("mu0", (self.d,)), f("P0", (self.d, self.d))
+        elif form == "kitagawa":
+            self.d = 1
+            self.mu1, self.s1, self.sd_x = float(latent["mu1"]), float(latent["s1"]), float(latent["sd_x"])
+        else:
+            raise ValueError(f"latent form {form!r}: 'affine' or 'kitagawa'")
+        self.form = form
+        if not 1 <= len(slots) <= 4:
+            raise ValueError("1..4 observed slots")
+        self.slots = []
+        for s in slots:
+            s = dict(s)
+            dist = s["dist"]
+            if dist not in _SLOT_DIST:
+                raise ValueError(f"slot distribution {dist!r}")
+            if dist == "mvnormal":
+                s["H"] = np.atleast_2d(np.asarray(s["H"], dtype=np.float64))
+                s["m"] = s["H"].shape[0]
+                s["c"] = np.asarray(s.get("c", np.zeros(s["m"])), dtype=np.float64).reshape(s["m"])
+                s["R"] = np.asarray(s["R"], dtype=np.float64).reshape(s["m"], s["m"])
+                s["link"] = "affine"
+            elif dist == "categorical":
+                s["W"] = np.atleast_2d(np.asarray(s["W"], dtype=np.float64))
+                s["m"] = s["W"].shape[0]
+                s["c"] = np.asarray(s.get("c", np.zeros(s["m"])), dtype=np.float64).reshape(s["m"])
+                s["link"] = "softmax"
+            else:
+                s["m"] = 1
+                s["link"] = {"normal": s.get("mean", "affine"), "poisson": "exp", "bernoulli": "logistic"}[dist]
+                if s["link"] == "affine":
+                    s["h"] = np.asarray(s["h"], dtype=np.float64).reshape(self.d)
+                    s["c"] = float(s.get("c", 0.0))
+            self.slots.append(s)
+        self.names = [s["name"] for s in self.slots]
+        self.dy = sum(s["m"] if s["dist"] == "mvnormal" else 1 for s in self.slots)
+
+    def params(self):
+        p = [0.0 if self.form == "affine" else 1.0, float(len(self.slots))]
+        for s in self.slots:
+            p += [float(_SLOT_DIST[s["dist"]]), float(s["m"]), float(_LINK[s["link"]])]
+        if self.form == "affine":
+            p += list(self.A.ravel()) + list(self.b) + list(self.Q.ravel()) + list(self.mu0) + list(self.P0.ravel())
+        else:
+            p += [self.mu1, self.s1, self.sd_x]
+        for s in self.slots:
+            if s["dist"] == "mvnormal":
+                p += list(s["H"].ravel()) + list(s["c"]) + list(s["R"].ravel())
+            elif s["dist"] == "normal":
+                p += ([*s["h"], s["c"]] if s["link"] == "affine" else []) + [float(s["sd"])]
+            elif s["dist"] == "categorical":
+                p += list(s["W"].ravel()) + list(s["c"])
+            else:
+                p += [*s["h"], s["c"]]
+        return np.asarray(p, dtype=np.float64)
+
+    def obs_address(self, t: int, name: str | None = None):
+        return ("chain", t, self.names[0] if name is None else name)
+
+    def obs_from_choicemap(self, cm, t: int):
+        """The constrained slots of step t ({name: value}, None if none); any
+        other address would update or delete an existing choice
+        (particle_filter.jl:168-170)."""
+        out = {}
+        for a, v in cm:
+            if len(a) == 3 and a[0] == "chain" and a[1] == t and a[2] in self.names:
+                out[a[2]] = v
+            else:
+                raise _lib.GenHipError(2, f"constraint at {a}: only the slots {self.names} of step {t} may be "
+                                          "constrained (discard must be empty)")
+        return out or None
+
+    def _slot_dict(self, value) -> dict:
+        if isinstance(value, dict):
+            return value
+        if len(self.slots) == 1:
+            return {self.names[0]: value}
+        raise ValueError("a slot model's observation is a {slot name: value} dict")
+
+    def gh_obs(self, value):
+        """The gh_obs chain of one step's observation (slot ids in model order)."""
+        vals = self._slot_dict(value)
+        present = [(k, np.ascontiguousarray(np.atleast_1d(np.asarray(vals[n], dtype=np.float64)).ravel()))
+                   for k, n in enumerate(self.names) if n in vals and vals[n] is not None]
+        unknown = set(vals) - set(self.names)
+        if unknown:
+            raise _lib.GenHipError(1, f"no slot named {sorted(unknown)}")
+        chain = (_lib.Obs * max(1, len(present)))()
+        for i, (k, arr) in enumerate(present):
+            chain[i] = _lib.Obs(_lib.dptr(arr), arr.size, 1, k, 0, None)
+        for i in range(len(present) - 1):
+            chain[i].next = ctypes.pointer(chain[i + 1])
+        if not present:
+            chain[0] = _lib.Obs(None, 0, 0, 0, 0, None)
+        keep = {self.names[k]: arr for k, arr in present}
+        return chain[0], (chain, keep)
+
+    # ---- host-side reference densities (numpy / closed forms; the tests' pins)
+    def _mean_param(self, s, x):
+        x = np.atleast_1d(x)
+        if s["dist"] == "mvnormal":
+            return s["H"] @ x + s["c"]
+        if s["dist"] == "categorical":
+            eta = s["W"] @ x + s["c"]
+            e = np.exp(eta - eta.max())
+            return e / e.sum()
+        if s["link"] == "x^2/20":
+            return x[0] * x[0] / 20.0
+        eta = float(s["h"] @ x + s["c"])
+        return {"normal": eta, "poisson": np.exp(eta), "bernoulli": 1.0 / (1.0 + np.exp(-eta))}[s["dist"]]
+
+    def slot_logpdf(self, k: int, y, x) -> float:
+        """logpdf of slot k's value y at latent x (scipy-free closed forms of
+        the reference's distributions)."""
+        from math import lgamma
+
+        s = self.slots[k]
+        mp = self._mean_param(s, x)
+        if s["dist"] == "mvnormal":
+            return _mvn_logpdf(np.atleast_1d(y), mp, s["R"])
+        if s["dist"] == "normal":
+            return _normal_logpdf(float(y), mp, s["sd"])
+        if s["dist"] == "poisson":
+            return float(y * np.log(mp) - mp - lgamma(y + 1.0))
+        if s["dist"] == "bernoulli":
+            return float(np.log(mp) if y else np.log(1.0 - mp))
+        return float(np.log(mp[int(y)]))
+
+    def simulate(self, T: int, rng: np.random.Generator):
+        """Draw (xs [T, d], ys [T] of {slot name: value}) from the model (numpy RNG; synthetic data only)."""
+        xs = np.zeros((T, self.d))
+        ys = []
+        for t in range(1, T + 1):
+            if self.form == "affine":
+                x = (rng.multivariate_normal(self.mu0, self.P0) if t == 1 else
+                     rng.multivariate_normal(self.A @ xs[t - 2] + self.b, self.Q))
+            else:
+                v = xs[t - 2, 0]
+                x = np.array([rng.normal(self.mu1, self.s1) if t == 1 else
+                              rng.normal(v / 2 + 25 * v / (1 + v * v) + 8 * np.cos(1.2 * t), self.sd_x)])
+            xs[t - 1] = x
+            y = {}
+            for s in self.slots:
+                mp = self._mean_param(s, x)
+                if s["dist"] == "mvnormal":
+                    y[s["name"]] = rng.multivariate_normal(mp, s["R"])
+                elif s["dist"] == "normal":
+                    y[s["name"]] = float(rng.normal(mp, s["sd"]))
+                elif s["dist"] == "poisson":
+                    y[s["name"]] = float(rng.poisson(mp))
+                elif s["dist"] == "bernoulli":
+                    y[s["name"]] = float(rng.random() < mp)
+                else:
+                    y[s["name"]] = float(rng.choice(s["m"], p=mp))
+            ys.append(y)
+        return xs, ys

@@ -192,9 +192,8 @@ def _step_obs(model: Model, t: int, observations) -> tuple[_lib.Obs, np.ndarray 
     else:
         val = observations
     if val is None:
-        return _lib.Obs(None, 0, 0), None
-    arr = model.obs_values(val)
-    return _lib.Obs(_lib.dptr(arr), arr.size, 1), arr
+        return _lib.Obs(None, 0, 0, 0, 0, None), None
+    return model.gh_obs(val)  # (a slot model: the chain of its constrained addresses)
 
 
 def _proposal_code(proposal) -> int:
@@ -226,7 +225,10 @@ class ParticleFilterState:
         self.observations: dict[int, np.ndarray | None] = {}
 
     def _log_obs(self, t: int, arr) -> None:
-        self.observations[t] = None if arr is None else np.array(arr, copy=True)
+        if isinstance(arr, tuple):  # a slot model's (chain, {name: values})
+            self.observations[t] = {k: np.array(v, copy=True) for k, v in arr[1].items()}
+        else:
+            self.observations[t] = None if arr is None else np.array(arr, copy=True)
 
     @property
     def t(self) -> int:
@@ -305,7 +307,8 @@ class ParticleTraces:
         for t in range(1, self.state.t + 1):
             if m.latent_address(t) == addr:
                 return t, "latent"
-            if m.obs_address(t) == addr:
+            if m.obs_address(t) == addr or (hasattr(m, "names") and len(addr) == 3 and addr[:2] == ("chain", t)
+                                            and addr[2] in m.names):
                 return t, "obs"
         raise KeyError(addr)
 
@@ -394,7 +397,11 @@ class _TraceView:
             x = xs[t - 1]
             cm[m.latent_address(t)] = float(x[0]) if x.size == 1 else x.copy()
             y = st.observations.get(t)
-            if y is not None:
+            if isinstance(y, dict):  # a slot model: every constrained slot
+                for name, v in y.items():
+                    v = np.asarray(v).ravel()
+                    cm[("chain", t, name)] = float(v[0]) if v.size == 1 else v.copy()
+            elif y is not None:
                 y = np.asarray(y).ravel()
                 cm[m.obs_address(t)] = float(y[0]) if y.size == 1 else y.copy()
         return cm
@@ -432,6 +439,13 @@ class _TraceView:
             for t in range(1, st.t + 1):
                 if a == tuple(m.latent_address(t)):
                     total += ps[t - 1, 0, self.i]
+                elif hasattr(m, "names") and len(a) == 3 and a[:2] == ("chain", t) and a[2] in m.names:
+                    # one slot of a slot model (the device column sums the step's slots): its logpdf on the host
+                    y = (st.observations.get(t) or {}).get(a[2])
+                    if y is not None:
+                        total += m.slot_logpdf(m.names.index(a[2]), np.asarray(y).ravel() if
+                                               m.slots[m.names.index(a[2])]["dist"] == "mvnormal" else
+                                               float(np.asarray(y).ravel()[0]), self.trajectory()[t - 1])
                 elif a == tuple(m.obs_address(t)):
                     total += ps[t - 1, 1, self.i]
         return float(total)
@@ -549,10 +563,12 @@ class ObservationBatch:
     marshalling of run_particle_filter, done ahead of a timed loop)."""
 
     def __init__(self, model: Model, observations_per_step):
-        self.values = [None if v is None else model.obs_values(v) for v in observations_per_step]
+        built = [(_lib.Obs(None, 0, 0, 0, 0, None), None) if v is None else model.gh_obs(v)
+                 for v in observations_per_step]
+        self.values = [keep for _, keep in built]  # (kept alive with the array: the gh_obs point into them)
         self.arr = (_lib.Obs * max(1, len(self.values)))()
-        for i, a in enumerate(self.values):
-            self.arr[i] = _lib.Obs(None, 0, 0) if a is None else _lib.Obs(_lib.dptr(a), a.size, 1)
+        for i, (o, _) in enumerate(built):
+            self.arr[i] = o
 
     def __len__(self):
         return len(self.values)

@@ -143,7 +143,7 @@ def simulate(model: Model, model_args: tuple = (), num_traces: int | None = None
     n = 1 if num_traces is None else int(num_traces)
     ctx = ctx or default_context()
     h = ctx.model_handle(model)
-    vec = model.family in (_lib.FAMILY_LGSSM, _lib.FAMILY_REGRESSION)
+    vec = model.family in (_lib.FAMILY_LGSSM, _lib.FAMILY_REGRESSION, _lib.FAMILY_SLOTS)
     d, dy = (model.d, model.dy) if vec else (1, 1)
     xs, ys = np.empty((T, d, n)), np.empty((T, dy, n))
     ps, tot = np.empty((T, 2, n)), np.empty(n)

@@ -91,8 +91,35 @@ typedef enum {
      y_i ~ normal(slope x_i + intercept, sigma), i = 1..dy (dy <= 32 data points)
      params: mu_s sd_s mu_i sd_i sigma x[dy]; the observation is y[dy];
      state (d = 2) = (slope, intercept) */
-  GH_FAMILY_REGRESSION = 4
+  GH_FAMILY_REGRESSION = 4,
+  /* slot-described Unfold kernel (Static-DSL models other than the four
+     above, static_ir/generate.jl:24-43): one latent address and K = 1..4
+     observed addresses ("slots") per step, any subset of which a step
+     constrains (gh_obs.slot / .next).  d (latent dimension) 1..8.
+       params = [lat, K, (dist_k, m_k, link_k) for k < K, latent block, slot blocks]
+     latent block, lat = GH_SLOT_LAT_AFFINE (0):   A[d*d] b[d] Q[d*d] mu0[d] P0[d*d]
+         x_1 ~ mvnormal(mu0, P0); x_t ~ mvnormal(A x_{t-1} + b, Q)
+                   lat = GH_SLOT_LAT_KITAGAWA (1), d = 1: mu1 s1 sd_x
+         x_1 ~ normal(mu1, s1); x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)
+     slot blocks (m_k values of the slot; its value rows in simulate's output
+     follow slot order, one row for a scalar slot):
+       GH_SLOT_MVNORMAL, link GH_LINK_AFFINE, m <= 32: H[m*d] c[m] R[m*m]   y ~ mvnormal(H x + c, R)
+       GH_SLOT_NORMAL, m = 1, GH_LINK_AFFINE: h[d] c sd                     y ~ normal(h.x + c, sd)
+                              GH_LINK_KITAGAWA (d = 1): sd                  y ~ normal(x^2/20, sd)
+       GH_SLOT_POISSON, m = 1, GH_LINK_EXP: h[d] c                         y ~ poisson(exp(h.x + c))
+       GH_SLOT_BERNOULLI, m = 1, GH_LINK_LOGISTIC: h[d] c   y ~ bernoulli(1 / (1 + exp(-(h.x + c)))) (0 / 1)
+       GH_SLOT_CATEGORICAL, m = classes 2..16, GH_LINK_SOFTMAX: W[m*d] c[m]
+                                     y ~ categorical(softmax(W x + c)), 0-based class
+     At most 32 observed values per step (a poisson slot counts 2).  An LGSSM
+     or Kitagawa model written as slots filters bit for bit as its family does
+     (those stay the fast paths); default proposal only; not for
+     gh_pf_step_params. */
+  GH_FAMILY_SLOTS = 5
 } gh_family;
+
+enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1 };
+enum { GH_SLOT_MVNORMAL = 1, GH_SLOT_NORMAL = 2, GH_SLOT_POISSON = 3, GH_SLOT_BERNOULLI = 4, GH_SLOT_CATEGORICAL = 5 };
+enum { GH_LINK_AFFINE = 0, GH_LINK_KITAGAWA = 1, GH_LINK_EXP = 2, GH_LINK_LOGISTIC = 3, GH_LINK_SOFTMAX = 4 };
 
 typedef enum { GH_RESAMPLE_SYSTEMATIC = 0, GH_RESAMPLE_MULTINOMIAL = 1 } gh_resampler;
 
@@ -131,11 +158,18 @@ typedef struct {
 } gh_model_desc;
 
 /* The observations of one step: the value(s) at address :chain => t => :y.
-   values == NULL or present == 0 means "no observation at this step". */
-typedef struct {
+   values == NULL or present == 0 means "no observation at this step".
+   GH_FAMILY_SLOTS: `slot` names the observed address (0..K-1) and `next`
+   chains the step's other constrained addresses (NULL ends the chain; a
+   slot constrained twice is GH_E_DISCARD); the other families take slot 0
+   and no chain. */
+typedef struct gh_obs {
   const double* values;
   int32_t n_values;
   int32_t present;
+  int32_t slot;
+  int32_t reserved;
+  const struct gh_obs* next;
 } gh_obs;
 
 typedef struct {

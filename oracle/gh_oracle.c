@@ -338,6 +338,13 @@ typedef struct {
   /* regression (quickstart.jl:3-9): priors, 1/(2 sigma^2), -0.5 log(2 pi sigma^2), xs */
   double mu_s, sd_s, mu_i, sd_i, sigma, inv2v, cst, inv2s, csts, inv2i, csti;
   double xs[32];
+  /* slot family (gen_amd/csrc/gh_slots.h): latent form, slot count, each slot's
+     distribution, value count, mean form, offsets in obs_t.bt and in the
+     observation vector, parameter block (mvnormal M = L_R^-1 H | H | c | L_R;
+     normal / poisson / bernoulli h | c; categorical W | c) and constants */
+  int lat, K, sdist[4], sm[4], slink[4], svoff[4], syoff[4];
+  double* sP[4];
+  double scst[4], sinv2v[4], ssd[4];
 } model_t;
 
 static void model_free(model_t* m) {
@@ -346,6 +353,7 @@ static void model_free(model_t* m) {
   free(m->L0); free(m->prior); free(m->T); free(m->E); free(m->logE);
   free(m->H); free(m->LS); free(m->Kt); free(m->FA); free(m->Fb); free(m->LSig); free(m->WA); free(m->Wb);
   free(m->LS1); free(m->Kt1); free(m->LSig1);
+  for (int k = 0; k < 4; ++k) free(m->sP[k]);
 }
 
 /* the optimal proposal's factors for state prior covariance P: chol(S), K^T,
@@ -454,6 +462,94 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->cstx = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * p[2]);
     m->inv2v1 = 1.0 / (2.0 * (p[1] * p[1]));
     m->cst1 = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
+  } else if (family == ORC_SLOTS) {
+    /* include/gen_hip.h GH_FAMILY_SLOTS (the engine's slots_build, same checks) */
+    if (d < 1 || d > 8 || np < 2) return -1;
+    m->lat = (int)p[0]; m->K = (int)p[1];
+    if ((double)m->lat != p[0] || (m->lat != 0 && m->lat != 1) || (m->lat == 1 && d != 1)) return -1;
+    if ((double)m->K != p[1] || m->K < 1 || m->K > 4) return -1;
+    int64_t i = 2 + 3 * (int64_t)m->K;
+    if (np < i) return -1;
+    int voff = 0, yoff = 0;
+    for (int k = 0; k < m->K; ++k) {
+      const double* hd = p + 2 + 3 * k;
+      int dist = (int)hd[0], mm = (int)hd[1], link = (int)hd[2], nv = 1;
+      if ((double)dist != hd[0] || (double)mm != hd[1] || (double)link != hd[2]) return -1;
+      if (dist == 1) { if (link != 0 || mm < 1 || mm > 32) return -1; nv = mm; }
+      else if (dist == 2) { if (mm != 1 || !(link == 0 || (link == 1 && d == 1))) return -1; }
+      else if (dist == 3) { if (mm != 1 || link != 2) return -1; nv = 2; }
+      else if (dist == 4) { if (mm != 1 || link != 3) return -1; }
+      else if (dist == 5) { if (mm < 2 || mm > 16 || link != 4) return -1; }
+      else return -1;
+      m->sdist[k] = dist; m->sm[k] = mm; m->slink[k] = link;
+      m->svoff[k] = voff; m->syoff[k] = yoff;
+      voff += nv; yoff += dist == 1 ? mm : 1;
+    }
+    if (voff > 32 || yoff > 32) return -1;
+    m->dy = yoff;
+    if (m->lat == 0) {
+      int64_t need = 3 * (int64_t)d * d + 2 * (int64_t)d;
+      if (np < i + need) return -1;
+      const double *A = p + i, *b = A + d * d, *Q = b + d, *mu0 = Q + d * d, *P0 = mu0 + d;
+      m->A = malloc(sizeof(double) * d * d); memcpy(m->A, A, sizeof(double) * d * d);
+      m->b = malloc(sizeof(double) * d); memcpy(m->b, b, sizeof(double) * d);
+      m->LQ = malloc(sizeof(double) * d * d);
+      if (chol(d, Q, m->LQ)) return -2;
+      m->mu0 = malloc(sizeof(double) * d); memcpy(m->mu0, mu0, sizeof(double) * d);
+      m->L0 = malloc(sizeof(double) * d * d);
+      if (chol(d, P0, m->L0)) return -2;
+      m->cstQ = gauss_cst(d, m->LQ);
+      m->cst0 = gauss_cst(d, m->L0);
+      i += need;
+    } else {
+      if (np < i + 3 || !(p[i + 1] > 0.0) || !(p[i + 2] > 0.0)) return -1;
+      double s1 = p[i + 1], sdx = p[i + 2];
+      m->mu1 = p[i]; m->s1 = s1; m->sx = sdx;  /* normal.jl:56-60: var = sd * sd */
+      m->inv2vx = 1.0 / (2.0 * (sdx * sdx));
+      m->cstx = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (sdx * sdx));
+      m->inv2v1 = 1.0 / (2.0 * (s1 * s1));
+      m->cst1 = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (s1 * s1));
+      i += 3;
+    }
+    for (int k = 0; k < m->K; ++k) {
+      int mm = m->sm[k];
+      if (m->sdist[k] == 1) {
+        int64_t need = (int64_t)mm * d + mm + (int64_t)mm * mm;
+        if (np < i + need) return -1;
+        const double *H = p + i, *c = H + mm * d, *R = c + mm;
+        double* blk = calloc((size_t)(2 * mm * d + mm + mm * mm), sizeof(double));
+        m->sP[k] = blk;
+        double* LR = blk + 2 * mm * d + mm;
+        if (chol(mm, R, LR)) return -2;
+        fwdsub(mm, d, LR, H, blk);
+        memcpy(blk + mm * d, H, sizeof(double) * mm * d);
+        memcpy(blk + 2 * mm * d, c, sizeof(double) * mm);
+        m->scst[k] = gauss_cst(mm, LR);
+        i += need;
+      } else if (m->sdist[k] == 2) {
+        int64_t need = m->slink[k] == 0 ? d + 2 : 1;
+        if (np < i + need) return -1;
+        m->sP[k] = calloc((size_t)d + 1, sizeof(double));
+        if (m->slink[k] == 0) memcpy(m->sP[k], p + i, sizeof(double) * (d + 1));
+        double sd = p[i + need - 1];
+        if (!(sd > 0.0)) return -1;
+        m->ssd[k] = sd;
+        m->sinv2v[k] = 1.0 / (2.0 * (sd * sd));
+        m->scst[k] = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (sd * sd));
+        i += need;
+      } else if (m->sdist[k] == 5) {
+        int64_t need = (int64_t)mm * d + mm;
+        if (np < i + need) return -1;
+        m->sP[k] = malloc(sizeof(double) * need);
+        memcpy(m->sP[k], p + i, sizeof(double) * need);
+        i += need;
+      } else {
+        if (np < i + d + 1) return -1;
+        m->sP[k] = malloc(sizeof(double) * (d + 1));
+        memcpy(m->sP[k], p + i, sizeof(double) * (d + 1));
+        i += d + 1;
+      }
+    }
   } else if (family == ORC_REGRESSION) {
     if (dy < 1 || dy > 32 || np < 5 + (int64_t)dy) return -1;
     m->d = 2;
@@ -489,8 +585,30 @@ static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* 
   o->present = has;
   o->ct = 0.0;
   o->nraw = 0;
-  if (m->family == ORC_KITAGAWA) o->ct = 8.0 * orc_cos(1.2 * (double)t);
+  if (m->family == ORC_KITAGAWA || (m->family == ORC_SLOTS && m->lat == 1)) o->ct = 8.0 * orc_cos(1.2 * (double)t);
   if (!has) return;
+  if (m->family == ORC_SLOTS) {  /* (the engine's make_obs_slots) */
+    o->nraw = m->dy;
+    for (int i = 0; i < m->dy; ++i) o->raw[i] = y[i];
+    for (int k = 0; k < m->K; ++k) {
+      if (!((has >> k) & 1)) continue;
+      const double* yk = y + m->syoff[k];
+      double* v = o->bt + m->svoff[k];
+      if (m->sdist[k] == 1) {
+        int mm = m->sm[k], d = m->d;
+        double r[32];
+        const double* c = m->sP[k] + 2 * mm * d;
+        for (int j = 0; j < mm; ++j) r[j] = yk[j] - c[j];
+        fwdsub(mm, 1, c + mm, r, v);
+      } else if (m->sdist[k] == 3) {
+        v[0] = yk[0];
+        v[1] = orc_lgamma(yk[0] + 1.0);
+      } else {
+        v[0] = yk[0];
+      }
+    }
+    return;
+  }
   o->nraw = (m->family == ORC_LGSSM || m->family == ORC_REGRESSION) ? m->dy : 1;
   for (int i = 0; i < o->nraw; ++i) o->raw[i] = y[i];
   if (m->family == ORC_LGSSM) {
@@ -640,8 +758,152 @@ static double lin_draw(const model_t* m, const double* xp, const double* z, doub
   return m->cstq - 0.5 * quad;
 }
 
+/* ---- the slot family (gen_amd/csrc/gh_slots.h SlotModel, line for line) */
+static double slot_affine(const double* h, double c, const double* x, int d) {
+  double acc = c;
+  for (int j = 0; j < d; ++j) acc = fma(h[j], x[j], acc);
+  return acc;
+}
+static double slot_lpdf(const model_t* m, const obs_t* o, int k, const double* x) {
+  const int d = m->d, mm = m->sm[k];
+  const double* P = m->sP[k];
+  const double* v = o->bt + m->svoff[k];
+  switch (m->sdist[k]) {
+    case 1: {  /* mvnormal(H x + c, R) through L_R^-1 (y - c) (mvnormal.jl:12-16) */
+      double quad = 0.0;
+      for (int r = 0; r < mm; ++r) {
+        double acc = v[r];
+        for (int j = 0; j < d; ++j) acc = fma(-P[r * d + j], x[j], acc);
+        quad = fma(acc, acc, quad);
+      }
+      return m->scst[k] - 0.5 * quad;
+    }
+    case 2: {  /* normal.jl:56-60 */
+      double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_affine(P, P[d], x, d);
+      double diff = v[0] - mean;
+      return -(diff * diff) * m->sinv2v[k] + m->scst[k];
+    }
+    case 3: {  /* poisson.jl:10-12, lambda = exp(h.x + c) */
+      double lam = orc_exp(slot_affine(P, P[d], x, d));
+      return v[0] < 0.0 ? -INFINITY : (v[0] * orc_log(lam) - lam) - v[1];
+    }
+    case 4: {  /* bernoulli.jl:10-12, prob = 1 / (1 + exp(-(h.x + c))) */
+      double prob = 1.0 / (1.0 + orc_exp(-slot_affine(P, P[d], x, d)));
+      return v[0] != 0.0 ? orc_log(prob) : orc_log(1.0 - prob);
+    }
+    default: {  /* categorical.jl:10-12, probs = exp(eta - max eta) / sum (0-based value) */
+      double mx = -INFINITY, s = 0.0, ey = 0.0;
+      for (int j = 0; j < mm; ++j) mx = fmax(mx, slot_affine(P + j * d, P[mm * d + j], x, d));
+      int y = (int)v[0];
+      for (int j = 0; j < mm; ++j) {
+        double e = orc_exp(slot_affine(P + j * d, P[mm * d + j], x, d) - mx);
+        s += e;
+        if (j == y) ey = e;
+      }
+      return orc_log(ey / s);
+    }
+  }
+}
+static double slot_loglik(const model_t* m, const obs_t* o, const double* x) {
+  double w = 0.0;
+  for (int k = 0; k < m->K; ++k)
+    if ((o->present >> k) & 1) w = w + slot_lpdf(m, o, k, x);
+  return w;
+}
+static double kit_z(uint64_t seed, uint64_t pid, uint32_t t, uint32_t stream, uint32_t base);
+/* the latent of step t (t = 1: the initial distribution), dense forms */
+static void slot_latent(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, const obs_t* o,
+                        const double* xp, double* x, uint32_t stream, uint32_t base) {
+  if (m->lat == 1) {
+    double z = kit_z(seed, pid, t, stream, base);
+    if (t == 1) x[0] = m->mu1 + m->s1 * z;
+    else {
+      double v = xp[0];
+      x[0] = (((v / 2.0) + 25.0 * (v / (1.0 + v * v))) + o->ct) + m->sx * z;
+    }
+    return;
+  }
+  int d = m->d;
+  double z[64];
+  normals_at(seed, pid, t, stream, base, d, z);
+  for (int i = 0; i < d; ++i) {
+    double acc;
+    if (t == 1) {
+      acc = m->mu0[i];
+      for (int k = 0; k <= i; ++k) acc = fma(m->L0[i * d + k], z[k], acc);
+    } else {
+      acc = m->b[i];
+      for (int k = 0; k < d; ++k) acc = fma(m->A[i * d + k], xp[k], acc);
+      for (int k = 0; k <= i; ++k) acc = fma(m->LQ[i * d + k], z[k], acc);
+    }
+    x[i] = acc;
+  }
+}
+/* poisson_chop of gh_dists.h: chop-down inversion from the mode with one uniform */
+static double slot_poisson_chop(double lam, double u) {
+  if (lam == 0.0) return 0.0;
+  if (!(lam > 0.0) || lam == INFINITY) return NAN;
+  double m = floor(lam);
+  double pm = orc_exp((m == 0.0 ? 0.0 : m * orc_log(lam)) - lam - orc_lgamma(m + 1.0));
+  u -= pm;
+  if (u <= 0.0) return m;
+  double lo = m, hi = m, pl = pm, ph = pm;
+  for (int it = 0; it < (1 << 24); ++it) {
+    hi += 1.0; ph = ph * lam / hi; u -= ph;
+    if (u <= 0.0) return hi;
+    if (lo > 0.0) { pl = pl * lo / lam; lo -= 1.0; u -= pl; if (u <= 0.0) return lo; }
+    if (ph == 0.0 && (lo <= 0.0 || pl == 0.0)) break;
+  }
+  return m;
+}
+/* simulate(): every slot's value (slot k from draws SIM_OBS_DRAW + 32 k), in
+   the observation vector's layout */
+static void slot_sim(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, const double* x, double* y) {
+  const int d = m->d;
+  for (int k = 0; k < m->K; ++k) {
+    const int mm = m->sm[k];
+    const uint32_t draw = 32u + 32u * (uint32_t)k;
+    const double* P = m->sP[k];
+    double* yk = y + m->syoff[k];
+    uint32_t w[4];
+    if (m->sdist[k] == 1) {
+      const double *H = P + mm * d, *c = H + mm * d, *LR = c + mm;
+      double z[32];
+      normals_at(seed, pid, t, 7, draw, mm, z);
+      for (int r = 0; r < mm; ++r) {
+        double acc = c[r];
+        for (int j = 0; j < d; ++j) acc = fma(H[r * d + j], x[j], acc);
+        for (int q = 0; q <= r; ++q) acc = fma(LR[r * mm + q], z[q], acc);
+        yk[r] = acc;
+      }
+    } else if (m->sdist[k] == 2) {
+      double z[2];
+      normals_at(seed, pid, t, 7, draw, 1, z);
+      double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_affine(P, P[d], x, d);
+      yk[0] = mean + m->ssd[k] * z[0];
+    } else if (m->sdist[k] == 3) {
+      rng(seed, pid, t, 7, draw, w);
+      yk[0] = slot_poisson_chop(orc_exp(slot_affine(P, P[d], x, d)), unif53(w[0], w[1]));
+    } else if (m->sdist[k] == 4) {
+      rng(seed, pid, t, 7, draw, w);
+      double prob = 1.0 / (1.0 + orc_exp(-slot_affine(P, P[d], x, d)));
+      yk[0] = unif53(w[0], w[1]) < prob ? 1.0 : 0.0;
+    } else {
+      rng(seed, pid, t, 7, draw, w);
+      double e[16], mx = -INFINITY;
+      for (int j = 0; j < mm; ++j) mx = fmax(mx, slot_affine(P + j * d, P[mm * d + j], x, d));
+      for (int j = 0; j < mm; ++j) e[j] = orc_exp(slot_affine(P + j * d, P[mm * d + j], x, d) - mx);
+      yk[0] = (double)cat_sample(e, mm, 1, unif53(w[0], w[1]));
+    }
+  }
+}
+
 static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
                             int proposal, double* x, uint32_t stream, uint32_t base) {
+  if (m->family == ORC_SLOTS) {
+    slot_latent(m, seed, pid, 1, o, NULL, x, stream, base);
+    return slot_loglik(m, o, x);
+  }
   if (m->family == ORC_REGRESSION) {
     double z[2];
     normals_at(seed, pid, 1, stream, base, 2, z);
@@ -703,6 +965,10 @@ static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const
 static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t,
                             const obs_t* o, int proposal, const double* xp, double* x, uint32_t stream,
                             uint32_t base) {
+  if (m->family == ORC_SLOTS) {
+    slot_latent(m, seed, pid, t, o, xp, x, stream, base);
+    return slot_loglik(m, o, x);
+  }
   if (m->family == ORC_LGSSM) {
     double z[64];
     normals_at(seed, pid, t, stream, base, m->d, z);
@@ -953,6 +1219,7 @@ int orc_pf_step_conditional(orc_pf* pf, const double* obs, int has_obs, const do
 
 /* log p(y_t | x_t): the step's weight increment under the prior proposal */
 static double model_loglik(const model_t* m, const obs_t* o, const double* x) {
+  if (m->family == ORC_SLOTS) return slot_loglik(m, o, x);
   if (m->family == ORC_LGSSM) return lgssm_obs(m, x, o);
   if (m->family == ORC_REGRESSION) return reg_loglik(m, o, x);
   if (!o->present) return 0.0;
@@ -1254,7 +1521,25 @@ int orc_pf_num_steps(orc_pf* pf) { return pf->t; }
    normal.jl:56-60, categorical.jl:10-12. */
 static void model_score(const model_t* m, const obs_t* o, int t, const double* xp, const double* x, double* lat,
                         double* ob) {
-  if (m->family == ORC_LGSSM) {
+  if (m->family == ORC_SLOTS && m->lat == 0) {  /* dense forward substitution (SlotModel::latent_lpdf) */
+    int d = m->d;
+    const double* L = t == 1 ? m->L0 : m->LQ;
+    double u[64], quad = 0.0;
+    for (int i = 0; i < d; ++i) {
+      double mean;
+      if (t == 1) {
+        mean = m->mu0[i];
+      } else {
+        mean = m->b[i];
+        for (int k = 0; k < d; ++k) mean = fma(m->A[i * d + k], xp[k], mean);
+      }
+      double r = x[i] - mean;
+      for (int k = 0; k < i; ++k) r = fma(-L[i * d + k], u[k], r);
+      u[i] = r / L[i * d + i];
+      quad = fma(u[i], u[i], quad);
+    }
+    *lat = (t == 1 ? m->cst0 : m->cstQ) - 0.5 * quad;
+  } else if (m->family == ORC_LGSSM) {
     int d = m->d;
     const double* L = t == 1 ? m->L0 : m->LQ;
     double u[64], quad = 0.0;
@@ -1273,7 +1558,7 @@ static void model_score(const model_t* m, const obs_t* o, int t, const double* x
       quad = fma(u[i], u[i], quad);
     }
     *lat = (t == 1 ? m->cst0 : m->cstQ) - 0.5 * quad;
-  } else if (m->family == ORC_KITAGAWA) {
+  } else if (m->family == ORC_KITAGAWA || m->family == ORC_SLOTS) {
     double mean = m->mu1, inv2 = m->inv2v1, cst = m->cst1;
     if (t > 1) {
       double v = xp[0];
@@ -1397,7 +1682,7 @@ int orc_simulate(int family, int d, int dy, int k, int v, const double* params, 
     model_free(&m);
     return -1;
   }
-  const int D = m.d, DY = (family == ORC_LGSSM || family == ORC_REGRESSION) ? m.dy : 1;
+  const int D = m.d, DY = (family == ORC_LGSSM || family == ORC_REGRESSION || family == ORC_SLOTS) ? m.dy : 1;
 #pragma omp parallel for schedule(static)
   for (int64_t j = 0; j < n; ++j) {
     double x[64], xp[64] = {0}, y[64], z[64];
@@ -1407,7 +1692,9 @@ int orc_simulate(int family, int d, int dy, int k, int v, const double* params, 
       obs_build(&m, t, NULL, 0, &none);
       if (t == 1) particle_init(&m, seed, (uint64_t)j, &none, 0, x, S_SIM, 0);
       else particle_step(&m, seed, (uint64_t)j, (uint32_t)t, &none, 0, xp, x, S_SIM, 0);
-      if (family == ORC_LGSSM) {
+      if (family == ORC_SLOTS) {
+        slot_sim(&m, seed, (uint64_t)j, (uint32_t)t, x, y);
+      } else if (family == ORC_LGSSM) {
         normals_at(seed, (uint64_t)j, (uint32_t)t, S_SIM, SIM_OBS_DRAW, DY, z);
         for (int r = 0; r < DY; ++r) {
           double acc = m.c[r];
@@ -1426,7 +1713,7 @@ int orc_simulate(int family, int d, int dy, int k, int v, const double* params, 
         normals_at(seed, (uint64_t)j, (uint32_t)t, S_SIM, SIM_OBS_DRAW, DY, z);
         for (int i = 0; i < DY; ++i) y[i] = (x[0] * m.xs[i] + x[1]) + m.sigma * z[i];
       }
-      obs_build(&m, t, y, 1, &oy);
+      obs_build(&m, t, y, family == ORC_SLOTS ? (1 << m.K) - 1 : 1, &oy);
       double lat, ob;
       model_score(&m, &oy, t, xp, x, &lat, &ob);
       if (xs) for (int q = 0; q < D; ++q) xs[((size_t)(t - 1) * D + q) * n + j] = x[q];

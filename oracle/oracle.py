@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 OMP_PATH = os.path.join(HERE, "liboracle_omp.so")  # the same oracle on every host core (CPU baseline only)
 
-LGSSM, HMM, KITAGAWA, REGRESSION = 1, 2, 3, 4
+LGSSM, HMM, KITAGAWA, REGRESSION, SLOTS = 1, 2, 3, 4, 5
 SYSTEMATIC, MULTINOMIAL = 0, 1
 DEFAULT, OPTIMAL, GAUSSIAN, LINEAR = 0, 1, 2, 3
 
@@ -152,6 +152,22 @@ def model_args(model):
     return model.family, model.d, model.dy, model.k, model.v, p
 
 
+def slot_obs(model, value):
+    """A slot model's observation (a {slot name: value} dict) as the oracle
+    takes it (gh_oracle.h ORC_SLOTS): the slots' values in slot order (m for
+    an mvnormal slot, one otherwise) and the bitmask of the present slots."""
+    vals = value if isinstance(value, dict) else {model.names[0]: value}
+    vec = np.zeros(max(1, model.dy))
+    mask, row = 0, 0
+    for k, s in enumerate(model.slots):
+        rows = s["m"] if s["dist"] == "mvnormal" else 1
+        if vals.get(s["name"]) is not None:
+            vec[row:row + rows] = np.atleast_1d(np.asarray(vals[s["name"]], dtype=np.float64)).ravel()
+            mask |= 1 << k
+        row += rows
+    return vec, mask
+
+
 class OraclePF:
     """CPU restatement of ParticleFilterState over particles [lo, lo+n_local)."""
 
@@ -159,7 +175,7 @@ class OraclePF:
         fam, d, dy, k, v, p = model_args(model)
         self.L = lib()
         self._p = p
-        self.d = d if fam in (LGSSM, REGRESSION) else 1
+        self.d = d if fam in (LGSSM, REGRESSION, SLOTS) else 1
         self.n_global = n_global
         self.lo = lo
         self.n = n_global if n_local is None else n_local
@@ -174,10 +190,12 @@ class OraclePF:
             self.L.orc_pf_destroy(self.h)
             self.h = None
 
-    @staticmethod
-    def _obs(y):
+    def _obs(self, y):
         if y is None:
             return None, 0
+        if self.model.family == SLOTS:  # the slots' values in slot order, bitmask of the present ones
+            a, mask = slot_obs(self.model, y)
+            return np.ascontiguousarray(a), mask
         a = np.ascontiguousarray(np.atleast_1d(np.asarray(y, dtype=np.float64)))
         return a, 1
 
@@ -349,8 +367,8 @@ def importance_sampling(model, y, n, seed, proposal=DEFAULT):
 def simulate(model, T, n, seed):
     """simulate(model, (T,)) n times: (xs [T, d, n], ys [T, dy, n], per_step [T, 2, n], total [n])."""
     fam, d, dy, k, v, p = model_args(model)
-    dd = d if fam in (LGSSM, REGRESSION) else 1
-    ddy = dy if fam in (LGSSM, REGRESSION) else 1
+    dd = d if fam in (LGSSM, REGRESSION, SLOTS) else 1
+    ddy = dy if fam in (LGSSM, REGRESSION, SLOTS) else 1
     xs, ys = np.empty((T, dd, n)), np.empty((T, ddy, n))
     ps, tot = np.empty((T, 2, n)), np.empty(n)
     if lib().orc_simulate(fam, d, dy, k, v, _d(p), p.size, T, n, seed, _d(xs), _d(ys), _d(ps), _d(tot)):

@@ -33,7 +33,7 @@
   } while (0)
 
 static gh_obs obs_at(const double* xs, int t) {
-  gh_obs o;
+  gh_obs o = {0};  /* slot 0, no chained observations */
   o.values = &xs[t];
   o.n_values = 1;
   o.present = 1;

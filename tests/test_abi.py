@@ -53,7 +53,8 @@ def test_struct_layouts_match_header():
     from gen_amd import _lib
 
     assert ctypes.sizeof(_lib.ModelDesc) == 5 * 4 + 4 + 8 + 8  # 5 int32, pad, ptr, int64
-    assert ctypes.sizeof(_lib.Obs) == 16
+    assert ctypes.sizeof(_lib.Obs) == 32  # ptr, n_values, present, slot, reserved, next
+    assert _lib.Obs.next.offset == 24 and _lib.Obs.slot.offset == 16
     assert ctypes.sizeof(_lib.PFOpts) == 32
 
 

@@ -1,0 +1,271 @@
+"""The slot-described Unfold family (GH_FAMILY_SLOTS, gen_amd/csrc/gh_slots.h).
+
+A Static-DSL kernel outside the four hand-lowered families is described by
+its address slots — one latent, up to four observed addresses with their
+distributions and mean forms (static_ir/generate.jl:24-43) — and a step may
+constrain any subset of them (choice_map.jl:163-225).  Pins:
+
+* CPU: the oracle's slot restatement reduces to the LGSSM and Kitagawa
+  families' restatements bit for bit when the slots describe those models,
+  and every slot's score equals the reference distribution's closed form
+  (mvnormal.jl:12-16, normal.jl:56-60, poisson.jl:10-12, bernoulli.jl:10-12,
+  categorical.jl:10-12) to 1e-12 — scipy's densities where scipy has them;
+* GPU: the device family equals those families bit for bit (states, weights,
+  ancestors), and equals the oracle bit for bit on a Poisson-count SSM with
+  several observed addresses per step (some steps constraining a subset,
+  one step none), call by call and batched, with simulate, the score columns
+  and rejuvenation.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import gen_amd as gen  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+def lg_as_slots(lg):
+    return gen.SlotSSM({"form": "affine", "A": lg.A, "b": lg.b, "Q": lg.Q, "mu0": lg.mu0, "P0": lg.P0},
+                       [{"name": "y", "dist": "mvnormal", "H": lg.H, "c": lg.c, "R": lg.R}])
+
+
+def kit_as_slots(kit):
+    # (sd_x = sqrt(var_x) exactly: var_x = 4; the family takes variances, the slot a standard deviation)
+    return gen.SlotSSM({"form": "kitagawa", "mu1": kit.mu1, "s1": kit.s1, "sd_x": float(np.sqrt(kit.var_x))},
+                       [{"name": "y", "dist": "normal", "mean": "x^2/20", "sd": float(np.sqrt(kit.var_y))}])
+
+
+def count_model():
+    """A Poisson-count SSM with three more observed addresses per step."""
+    return gen.SlotSSM(
+        {"form": "affine", "A": [[0.9, 0.05], [0.0, 0.8]], "b": [0.0, 0.1], "Q": [[0.05, 0.01], [0.01, 0.04]],
+         "mu0": [0.5, 0.0], "P0": [[0.3, 0.0], [0.0, 0.3]]},
+        [{"name": "count", "dist": "poisson", "h": [1.0, 0.5], "c": 0.2},
+         {"name": "z", "dist": "normal", "h": [0.3, -0.2], "c": 0.1, "sd": 0.7},
+         {"name": "on", "dist": "bernoulli", "h": [1.5, 0.0], "c": -0.3},
+         {"name": "kind", "dist": "categorical", "W": [[1.0, 0.0], [0.0, 1.0], [-1.0, 1.0]], "c": [0.0, 0.2, -0.1]}])
+
+
+def count_obs(T=10, seed=5):
+    """Observations with some slots missing at some steps (and one empty step)."""
+    m = count_model()
+    _, ys = m.simulate(T, np.random.default_rng(seed))
+    obs = [dict(y) for y in ys]
+    del obs[2]["z"]
+    obs[4] = {}
+    del obs[5]["count"]
+    del obs[6]["kind"], obs[6]["on"]
+    return m, obs
+
+
+def _obs_at(model, y, t):
+    if isinstance(y, dict):
+        return {("chain", t, k): v for k, v in y.items()}
+    return {model.obs_address(t): y}
+
+
+# ------------------------------------------------------------------ CPU
+def test_oracle_slots_reduce_to_lgssm_family_bitexact():
+    lg = gen.LinearGaussianSSM.benchmark(4)
+    sl = lg_as_slots(lg)
+    _, ys = lg.simulate(10, np.random.default_rng(2))
+    a = O.run_pf(lg, ys, 3000, 7)
+    b = O.run_pf(sl, [{"y": y} for y in ys], 3000, 7)
+    assert np.array_equal(a.state(), b.state())
+    assert np.array_equal(a.parents(), b.parents())
+    assert np.array_equal(a.log_weights(), b.log_weights())
+    assert a.log_ml_estimate() == b.log_ml_estimate()
+    for x, y in zip(a.scores(per_step=True), b.scores(per_step=True)):
+        assert np.array_equal(x, y)
+
+
+def test_oracle_slots_reduce_to_kitagawa_family_bitexact():
+    kit = gen.KitagawaSSM(4.0, 1.0)
+    _, ys = kit.simulate(12, np.random.default_rng(3))
+    a = O.run_pf(kit, ys, 3000, 7)
+    b = O.run_pf(kit_as_slots(kit), [{"y": y} for y in ys], 3000, 7)
+    assert np.array_equal(a.state(), b.state())
+    assert np.array_equal(a.parents(), b.parents())
+    assert np.array_equal(a.log_weights(), b.log_weights())
+    for x, y in zip(a.scores(per_step=True), b.scores(per_step=True)):
+        assert np.array_equal(x, y)
+
+
+def test_oracle_slot_scores_equal_reference_densities():
+    """simulate's per-step scores: the observation column = the sum of the
+    slots' logpdfs by the reference's formulas (scipy where it has the
+    distribution), the latent column = mvnormal's logpdf."""
+    from scipy import stats
+
+    m = count_model()
+    T, n = 5, 64
+    X, Y, PS, _ = O.simulate(m, T, n, 3)
+    s = m.slots
+    for t in range(T):
+        for j in range(n):
+            x, y = X[t, :, j], Y[t, :, j]
+            eta = [float(np.dot(s[k]["h"], x) + s[k]["c"]) for k in range(3)]
+            logits = s[3]["W"] @ x + s[3]["c"]
+            probs = np.exp(logits - logits.max())
+            probs /= probs.sum()
+            ref = (stats.poisson.logpmf(y[0], np.exp(eta[0])) + stats.norm.logpdf(y[1], eta[1], 0.7)
+                   + stats.bernoulli.logpmf(y[2], 1.0 / (1.0 + np.exp(-eta[2]))) + np.log(probs[int(y[3])]))
+            assert abs(ref - PS[t, 1, j]) < 1e-12 * max(1.0, abs(ref)), (t, j, ref, PS[t, 1, j])
+            xp = X[t - 1, :, j] if t > 0 else None
+            mean, cov = (m.mu0, m.P0) if t == 0 else (m.A @ xp + m.b, m.Q)
+            assert abs(stats.multivariate_normal.logpdf(x, mean, cov) - PS[t, 0, j]) < 1e-12 * 10
+    # the samplers: counts, switches and classes with the model's means
+    T, n = 2, 20000
+    X, Y, _, _ = O.simulate(m, T, n, 4)
+    x = X[1]
+    lam = np.exp(s[0]["h"] @ x + s[0]["c"])
+    assert abs(Y[1, 0].mean() - lam.mean()) < 4 * np.sqrt(lam.mean() / n) + 1e-3
+    p_on = 1.0 / (1.0 + np.exp(-(s[2]["h"] @ x + s[2]["c"])))
+    assert abs(Y[1, 2].mean() - p_on.mean()) < 4 * np.sqrt(0.25 / n)
+
+
+def test_slot_model_rejects_bad_descriptions():
+    with pytest.raises(ValueError):
+        gen.SlotSSM({"form": "affine", "A": np.eye(2), "Q": np.eye(2), "mu0": np.zeros(2), "P0": np.eye(2)},
+                    [{"name": "y", "dist": "gamma"}])
+    m = count_model()
+    with pytest.raises(gen.GenHipError):
+        m.gh_obs({"nope": 1.0})
+    # an address that is not a slot of the step is a discard (particle_filter.jl:168-170)
+    with pytest.raises(gen.GenHipError):
+        m.obs_from_choicemap(gen.ChoiceMap({("chain", 2, "count"): 1.0, ("chain", 3, "count"): 2.0}), 2)
+
+
+# ------------------------------------------------------------------ GPU
+def _gpu_run(model, obs, n, seed, batched, thr=None, rejuv=0):
+    st = gen.initialize_particle_filter(model, (1,), _obs_at(model, obs[0], 1), n, seed=seed)
+    if rejuv:
+        gen.rejuvenate(st, rejuv)
+    if batched:
+        gen.run_particle_filter(st, list(obs[1:]), thr)
+    else:
+        for t in range(2, len(obs) + 1):
+            gen.maybe_resample(st, thr)
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), _obs_at(model, obs[t - 1], t))
+            if rejuv:
+                gen.rejuvenate(st, rejuv)
+    return st
+
+
+def _orc_run(model, obs, n, seed, thr=None, rejuv=0):
+    pf = O.OraclePF(model, n, seed)
+    pf.init(obs[0])
+    if rejuv:
+        pf.rejuvenate(rejuv)
+    for y in obs[1:]:
+        pf.maybe_resample(thr)
+        pf.step(y)
+        if rejuv:
+            pf.rejuvenate(rejuv)
+    return pf
+
+
+def _same(st, ref_st=None, orc=None):
+    if ref_st is not None:
+        assert np.array_equal(st.states(), ref_st.states())
+        assert np.array_equal(st.parents, ref_st.parents)
+        assert np.array_equal(gen.get_log_weights(st), gen.get_log_weights(ref_st))
+        assert gen.log_ml_estimate(st) == gen.log_ml_estimate(ref_st)
+    if orc is not None:
+        assert np.array_equal(st.states().T, orc.state())
+        assert np.array_equal(st.parents, orc.parents())
+        assert np.array_equal(gen.get_log_weights(st), orc.log_weights())
+        a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+        assert abs(a - b) <= 1e-9 * abs(b), (a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched", [False, True])
+@pytest.mark.parametrize("d", [4, 10])
+def test_gpu_lgssm_as_slots_equals_family_bitexact(gh_ctx, d, batched):
+    """The C2 model (and d = 4) written as slots filters as the LGSSM family
+    (LGModel<D, 3>, the benchmark's structured kernel) does: bit for bit."""
+    lg = gen.LinearGaussianSSM.benchmark(d)
+    _, ys = lg.simulate(12, np.random.default_rng(2))
+    n = 20011
+    a = _gpu_run(lg, list(ys), n, 9, batched)
+    b = _gpu_run(lg_as_slots(lg), [{"y": y} for y in ys], n, 9, batched)
+    _same(b, ref_st=a)
+    for x, y in zip(gen.get_traces(a).scores(per_step=True), gen.get_traces(b).scores(per_step=True)):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched", [False, True])
+def test_gpu_kitagawa_as_slots_equals_family_bitexact(gh_ctx, batched):
+    """The nonlinear SSM written as slots (Kitagawa latent, normal slot with
+    the x^2/20 mean) equals the Kitagawa family (whose default step is the pair
+    kernel) bit for bit."""
+    kit = gen.KitagawaSSM(4.0, 1.0)
+    _, ys = kit.simulate(15, np.random.default_rng(3))
+    n = 1 << 15
+    a = _gpu_run(kit, list(ys), n, 9, batched)
+    b = _gpu_run(kit_as_slots(kit), [{"y": y} for y in ys], n, 9, batched)
+    _same(b, ref_st=a)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched,thr,rejuv", [(False, None, 0), (True, None, 0), (False, 1e9, 2), (True, 0.0, 0)])
+def test_gpu_count_ssm_slots_equal_oracle_bitexact(gh_ctx, batched, thr, rejuv):
+    """A Poisson-count SSM with normal, bernoulli and categorical addresses,
+    steps constraining every subset used (one step none): GPU == oracle bit
+    for bit (states, weights, parents; log-ML 1e-9), with rejuvenation moves
+    (mh(trace, select(:x)) per particle) in one case."""
+    m, obs = count_obs()
+    n = 4099
+    st = _gpu_run(m, obs, n, 13, batched, thr, rejuv)
+    orc = _orc_run(m, obs, n, 13, thr, rejuv)
+    _same(st, orc=orc)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    # a trace's choices: every latent and every constrained slot
+    cm = gen.get_traces(st)[0].get_choices()
+    assert cm[("chain", 1, "count")] == obs[0]["count"] and ("chain", 3, "z") not in dict(cm)
+
+
+@pytest.mark.gpu
+def test_gpu_slots_simulate_equals_oracle_bitexact(gh_ctx):
+    for m in (count_model(), lg_as_slots(gen.LinearGaussianSSM.benchmark(3)),
+              kit_as_slots(gen.KitagawaSSM(4.0, 1.0))):
+        tr = gen.simulate(m, (6,), num_traces=777, seed=21)
+        X, Y, PS, TOT = O.simulate(m, 6, 777, 21)
+        assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
+        assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
+
+
+@pytest.mark.gpu
+def test_gpu_slots_constrained_twice_is_discard(gh_ctx):
+    """A step's chain naming one slot twice is rejected (GH_E_DISCARD)."""
+    import ctypes
+
+    from gen_amd import _lib
+
+    m = count_model()
+    ctx = gen.get_default_context() if hasattr(gen, "get_default_context") else None
+    h = ctypes.c_void_p()
+    desc, keep = m.desc()
+    lib = _lib.load()
+    _lib.check(lib.gh_model_create(gh_ctx.h, ctypes.byref(desc), ctypes.byref(h)))
+    v = np.array([1.0])
+    chain = (_lib.Obs * 2)()
+    chain[0] = _lib.Obs(_lib.dptr(v), 1, 1, 0, 0, None)
+    chain[1] = _lib.Obs(_lib.dptr(v), 1, 1, 0, 0, None)
+    chain[0].next = ctypes.pointer(chain[1])
+    opts = _lib.PFOpts()
+    lib.gh_pf_opts_default(ctypes.byref(opts))
+    pf = ctypes.c_void_p()
+    rc = lib.gh_pf_init(h, ctypes.byref(chain[0]), 0, 1024, 1, ctypes.byref(opts), ctypes.byref(pf))
+    assert rc == 2, rc  # GH_E_DISCARD
+    lib.gh_model_destroy(h)
+    del ctx, keep
