@@ -379,7 +379,10 @@ def secondary_multirank_path(gen, a, c2_ms, c4_ms):
 
     out = {}
     for tname, mk in (("rccl", lambda: gen.Context(device=0, force_multirank=True)),
-                      ("peer", lambda: gen.Context(device=0, transport=LocalTransport(), peer=True))):
+                      # (force_multirank: a world-1 peer context otherwise takes the one-rank path —
+                      # rounds 4-5 timed that by mistake as the peer path)
+                      ("peer", lambda: gen.Context(device=0, transport=LocalTransport(), peer=True,
+                                                   force_multirank=True))):
         ctx = mk()
         try:
             for name, model, n, d, base in (("C2", gen.LinearGaussianSSM.benchmark(a.d), a.particles, a.d, c2_ms),
@@ -571,6 +574,11 @@ def main(argv=None):
             uid = [gen.Context.unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
             ctx = gen.Context(device=local, rank=rank, world=world, unique_id=uid[0])
+    elif a.force_multirank and a.transport == "peer":
+        # the peer transport's multi-rank kernels at world 1 (the rank's own mailbox)
+        from gen_amd.transport import LocalTransport
+
+        ctx = gen.Context(device=0, transport=LocalTransport(), peer=True, force_multirank=True)
     else:
         ctx = gen.Context(device=0, force_multirank=a.force_multirank)
     gen.set_default_context(ctx)
@@ -623,7 +631,7 @@ def main(argv=None):
             "d": d,
             "resampler": a.resampler,
             "parallelism": f"particle-dp{world}",
-            "transport": a.transport if world > 1 else "none",
+            "transport": a.transport if world > 1 else (f"{a.transport} (forced multi-rank)" if a.force_multirank else "none"),
             "resample_steps_timed": r["n_res"],
             "log_ml": lml,
         },

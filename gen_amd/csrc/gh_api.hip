@@ -31,6 +31,7 @@
 #include "gh_csmc.h"
 #include "gh_inst.h"
 #include "gh_peer.h"
+#include "gh_rank_ab.h"
 
 using namespace gh;
 
@@ -44,6 +45,8 @@ GH_LG_UNIT5(GH_EXTERN_TEMPLATE)
 GH_LG_UNIT6(GH_EXTERN_TEMPLATE)
 GH_SL_UNIT0(GH_EXTERN_TEMPLATE)
 GH_SL_UNIT1(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT2(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT3(GH_EXTERN_TEMPLATE)
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_err;
@@ -338,7 +341,7 @@ extern "C" int gh_ctx_force_multirank(gh_ctx* c) {
   // would run the multi-rank kernels and collectives on missing buffers
   if (c->n_filters > 0)
     return set_err(GH_E_STATE, "gh_ctx_force_multirank: %d filter(s) exist on this context", c->n_filters);
-  if (c->world == 1 && !c->host_comm && !c->comm) {  // a one-rank RCCL communicator
+  if (c->world == 1 && !c->host_comm && !c->peer && !c->comm) {  // a one-rank RCCL communicator
     ncclUniqueId u;
     NCCL_TRY(ncclGetUniqueId(&u));
     HIP_TRY(hipSetDevice(c->device));
@@ -597,7 +600,7 @@ static bool slots_supported(int d) { return d >= 1 && d <= kMaxSlotD; }
 static const char* slots_build(gh_model* m, const double* p, int64_t np, std::vector<double>& h,
                                int64_t off[5 + kMaxSlots]) {
   const int d = m->d;
-  if (!slots_supported(d)) return "slots: latent dimension d must be in 1..8";
+  if (!slots_supported(d)) return "slots: latent dimension d must be in 1..16";
   if (np < 2) return "slots: need the latent form and the slot count";
   SlotParams& sp = m->slots;
   sp.lat = (int)p[0];
@@ -1155,6 +1158,8 @@ struct gh_pf {
   double* prow[kPeerMaxRanks] = {};
   PeerRounds pr;                  // the set-up's bootstrap rounds (fail-together)
   bool peer_ready = false;        // set up on every rank: destruction fences the ranks
+  bool ab_fits = false;           // the grid is co-resident for k_rank_ab (it polls every tile)
+  bool no_fused_rank = false;     // (GH_NO_FUSED_RANK in the environment: the two-kernel peer resample, for A/B)
   uint64_t* ptag[kPeerMaxRanks] = {};
   uint64_t row_use = 0;
   // multi-rank genealogy (record_history): per step, the rows received for
@@ -1224,7 +1229,26 @@ template <int IT>
 static int rank_cap(int cus) {  // multi-rank: k_rank_a's (k_rank_b has no grid barrier)
   return occ_blocks(k_rank_a<IT>) * cus;
 }
+template <int IT>
+static int rank_ab_cap(int cus) {  // the fused peer resample's co-resident blocks
+  return occ_blocks(k_rank_ab<IT>) * cus;
+}
+static void pick_ab(gh_pf* pf) {  // the fused kernel only where its grid fits
+  const int cus = pf->ctx->cus;
+  const int cap = pf->rs_it == 4 ? rank_ab_cap<4>(cus) : pf->rs_it == 8 ? rank_ab_cap<8>(cus)
+                : pf->rs_it == 16 ? rank_ab_cap<16>(cus) : 0;
+  // judged on the largest shard's grid, as the tiles are, so that every rank
+  // takes the same path
+  const int64_t n = (pf->n_global + pf->ctx->world - 1) / pf->ctx->world;
+  const int64_t g = pf->rs_it ? (n + (int64_t)pf->rs_it * kRsBlock - 1) / ((int64_t)pf->rs_it * kRsBlock) : 0;
+  pf->ab_fits = pf->rs_grid > 0 && g <= cap;
+}
+static void pick_resample_tiles_(gh_pf* pf, int64_t n);
 static void pick_resample_tiles(gh_pf* pf, int64_t n) {
+  pick_resample_tiles_(pf, n);
+  if (mr(pf->ctx) && pf->ctx->peer) pick_ab(pf);
+}
+static void pick_resample_tiles_(gh_pf* pf, int64_t n) {
   const int cus = pf->ctx->cus;
   pf->rs_grid = 0;
   pf->rs_it = 0;
@@ -1503,7 +1527,8 @@ static int with_model(const gh_model* m, F&& f) {
 #define GH_SL_CASE(DD) \
   case DD: f(SlotModel<DD>{}, m->slots); break;
         GH_SL_CASE(1) GH_SL_CASE(2) GH_SL_CASE(3) GH_SL_CASE(4) GH_SL_CASE(5) GH_SL_CASE(6) GH_SL_CASE(7)
-        GH_SL_CASE(8)
+        GH_SL_CASE(8) GH_SL_CASE(9) GH_SL_CASE(10) GH_SL_CASE(11) GH_SL_CASE(12) GH_SL_CASE(13) GH_SL_CASE(14)
+        GH_SL_CASE(15) GH_SL_CASE(16)
 #undef GH_SL_CASE
         default: return set_err(GH_E_INVAL, "slots d=%d not instantiated", m->d);
       }
@@ -1792,6 +1817,7 @@ static int pf_init_impl(gh_model* m, const gh_obs* obs, int proposal, int64_t n_
   pf->s = ctx->stream;
   pf->D = m->d;
   pf->cond = pin_ref != nullptr;  // before the first step kernel (use_pairs)
+  pf->no_fused_rank = getenv("GH_NO_FUSED_RANK") != nullptr;
   for (int i = 0; i < 4; ++i) pf->qargs[i] = q0[i];
   pf->has_q = has_q;
   if (opts) pf->opts = *opts;
@@ -2201,13 +2227,16 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
   // otherwise k_rank_a on the all-gathered triples and the totals' all-gather
   const bool sums = pf->max_only && pf->amax_valid;
   uint64_t* shards = pf->amax + (t & 1) * kAmaxShards * kAmaxStride;
+  // peer transport, batched loop: ONE launch (k_rank_ab, gh_rank_ab.h) for
+  // k_rank_a2 + k_rank_b — nothing between them needs the host
+  const bool fused = sums && c->peer && pf->ab_fits && pf->n_global < (1LL << 31) && !pf->no_fused_rank;
+  RankA2Args a2{};
   if (sums) {
     // peer transport: the shards' and the records' all-gathers happen inside
     // k_rank_a2 / k_rank_b through the mailboxes
     if (!c->peer)
       CHECK(comm_allgather(c, shards, pf->amax_all, sizeof(uint64_t) * kAmaxShards * kAmaxStride, pf->s,
                            &pf->dev->error));
-    RankA2Args a2{};
     a2.logw = pf->logw;
     a2.n = pf->n;
     a2.shift = shift;
@@ -2226,12 +2255,14 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
       a2.use_sh = ++c->use_sh;
       a2.use_rec = ++c->use_rec;
     }
-    switch (pf->rs_it) {
-      case 4: hipLaunchKernelGGL(k_rank_a2<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
-      case 8: hipLaunchKernelGGL(k_rank_a2<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
-      default: hipLaunchKernelGGL(k_rank_a2<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
+    if (!fused) {
+      switch (pf->rs_it) {
+        case 4: hipLaunchKernelGGL(k_rank_a2<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
+        case 8: hipLaunchKernelGGL(k_rank_a2<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
+        default: hipLaunchKernelGGL(k_rank_a2<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, a2); break;
+      }
+      HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipGetLastError());
     if (!c->peer) CHECK(comm_allgather(c, pf->rec, pf->recs_all, sizeof(uint64_t) * kRecWords, pf->s, &pf->dev->error));
   } else {
     RankAArgs ra{};
@@ -2293,7 +2324,16 @@ static int rank_resample(gh_pf* pf, const DecideArgs& d, int shift, int t) {
     for (int r = 0; r < R; ++r) rb.prow[r] = pf->prow[r];
     rb.rows_cap = INT64_MAX;
   }
-  launch_rank_b(pf, rb);
+  if (fused) {
+    const RankABArgs ab{a2, rb};
+    switch (pf->rs_it) {
+      case 4: hipLaunchKernelGGL(k_rank_ab<4>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ab); break;
+      case 8: hipLaunchKernelGGL(k_rank_ab<8>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ab); break;
+      default: hipLaunchKernelGGL(k_rank_ab<16>, dim3((unsigned)pf->rs_grid), dim3(kRsBlock), 0, pf->s, ab); break;
+    }
+  } else {
+    launch_rank_b(pf, rb);
+  }
   HIP_TRY(hipGetLastError());
   if (c->peer) {
     // every rank tags every other rank's row buffer once its rows are in

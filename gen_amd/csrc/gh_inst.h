@@ -62,7 +62,7 @@
 #define GH_LG_UNIT5(X) GH_LG_DIM(X, 15)
 #define GH_LG_UNIT6(X) GH_LG_DIM(X, 16)
 
-// the slot family (gh_slots.h): SlotModel<D> for d = 1..8, in gh_inst_slots<k>.hip
+// the slot family (gh_slots.h): SlotModel<D> for d = 1..16, in gh_inst_slots<k>.hip
 #define GH_SL_KERNELS(X, D)                                                                                     \
   X __global__ void gh::k_step<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
   X __global__ void gh::k_step<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
@@ -84,8 +84,11 @@
                                                             int*);                                               \
   X __global__ void gh::k_pin_pre<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs); \
   X __global__ void gh::k_pin_pre<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs);
-#define GH_SL_UNIT0(X) GH_SL_KERNELS(X, 1) GH_SL_KERNELS(X, 2) GH_SL_KERNELS(X, 3) GH_SL_KERNELS(X, 4)
-#define GH_SL_UNIT1(X) GH_SL_KERNELS(X, 5) GH_SL_KERNELS(X, 6) GH_SL_KERNELS(X, 7) GH_SL_KERNELS(X, 8)
+#define GH_SL_UNIT0(X) \
+  GH_SL_KERNELS(X, 1) GH_SL_KERNELS(X, 2) GH_SL_KERNELS(X, 3) GH_SL_KERNELS(X, 4) GH_SL_KERNELS(X, 5) GH_SL_KERNELS(X, 6)
+#define GH_SL_UNIT1(X) GH_SL_KERNELS(X, 7) GH_SL_KERNELS(X, 8) GH_SL_KERNELS(X, 9) GH_SL_KERNELS(X, 10)
+#define GH_SL_UNIT2(X) GH_SL_KERNELS(X, 11) GH_SL_KERNELS(X, 12) GH_SL_KERNELS(X, 13)
+#define GH_SL_UNIT3(X) GH_SL_KERNELS(X, 14) GH_SL_KERNELS(X, 15) GH_SL_KERNELS(X, 16)
 
 #define GH_EXTERN_TEMPLATE extern template
 #define GH_TEMPLATE template

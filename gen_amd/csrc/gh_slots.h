@@ -32,7 +32,7 @@
 namespace gh {
 
 constexpr int kMaxSlots = 4;        // observed addresses per step
-constexpr int kMaxSlotD = 8;        // latent dimension (SlotModel<1..8> instantiated)
+constexpr int kMaxSlotD = 16;       // latent dimension (SlotModel<1..16> instantiated)
 constexpr int kMaxSlotClasses = 16;  // categorical slot classes
 constexpr uint32_t kSlotSimDraws = 32;  // simulate(): slot k draws from kSimObsDraw + 32 k
 
@@ -72,7 +72,7 @@ struct SlotParams {
 template <int D>
 struct SlotModel {
   static constexpr int kD = D;
-  static constexpr int kMinWaves = D <= 3 ? 8 : (D <= 6 ? 6 : 4);
+  static constexpr int kMinWaves = D <= 3 ? 8 : (D <= 6 ? 6 : (D <= 10 ? 4 : 3));
   using Params = SlotParams;
 
   // c + h.x (fma over the components ascending)

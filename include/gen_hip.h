@@ -95,7 +95,7 @@ typedef enum {
   /* slot-described Unfold kernel (Static-DSL models other than the four
      above, static_ir/generate.jl:24-43): one latent address and K = 1..4
      observed addresses ("slots") per step, any subset of which a step
-     constrains (gh_obs.slot / .next).  d (latent dimension) 1..8.
+     constrains (gh_obs.slot / .next).  d (latent dimension) 1..16.
        params = [lat, K, (dist_k, m_k, link_k) for k < K, latent block, slot blocks]
      latent block, lat = GH_SLOT_LAT_AFFINE (0):   A[d*d] b[d] Q[d*d] mu0[d] P0[d*d]
          x_1 ~ mvnormal(mu0, P0); x_t ~ mvnormal(A x_{t-1} + b, Q)

@@ -464,7 +464,7 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     m->cst1 = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (p[1] * p[1]));
   } else if (family == ORC_SLOTS) {
     /* include/gen_hip.h GH_FAMILY_SLOTS (the engine's slots_build, same checks) */
-    if (d < 1 || d > 8 || np < 2) return -1;
+    if (d < 1 || d > 16 || np < 2) return -1;
     m->lat = (int)p[0]; m->K = (int)p[1];
     if ((double)m->lat != p[0] || (m->lat != 0 && m->lat != 1) || (m->lat == 1 && d != 1)) return -1;
     if ((double)m->K != p[1] || m->K < 1 || m->K > 4) return -1;

@@ -14,7 +14,8 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke
 timeout -k 10 400 python bench.py > "$O/bench.json" 2> "$O/bench.err"
 bash tools/gpu_profile.sh "$O/prof"
 bash tools/gpu_profile_c345.sh "$O/prof345"
-for v in "c2mr|--force-multirank" "c4mr|--model kitagawa --particles 2097152 --force-multirank"; do
+for v in "c2mr|--force-multirank --transport rccl" "c4mr|--model kitagawa --particles 2097152 --force-multirank --transport rccl" \
+         "c2mr_peer|--force-multirank --transport peer" "c4mr_peer|--model kitagawa --particles 2097152 --force-multirank --transport peer"; do
   name=${v%%|*}; args=${v#*|}
   GH_PROF_STEPS=20 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$O/$name" -o run --output-format csv -- python3 tools/profile_run.py $args > "$O/$name.log" 2>&1
 done
