@@ -644,6 +644,7 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
   }
   if (voff > kMaxObs || yoff > kMaxObs) return "slots: more than 32 observed values per step";
   m->dy = yoff;
+  sp.nv = voff;
   // latent block
   off[0] = (int64_t)h.size();
   if (sp.lat == SLOT_LAT_AFFINE) {
@@ -1029,7 +1030,8 @@ static int make_obs_gauss(const gh_model* m, int t, const gh_obs* in, const doub
 // the observation with u_t of the linear proposal behind it (o.v[dy + i])
 static int make_obs_lin(const gh_model* m, int t, const gh_obs* in, const double* u, StepObs* o) {
   CHECK(make_obs(m, t, in, o));
-  for (int i = 0; i < m->d; ++i) o->v[m->dy + i] = u[i];
+  const int at = m->family == GH_FAMILY_SLOTS ? m->slots.nv : m->dy;
+  for (int i = 0; i < m->d; ++i) o->v[at + i] = u[i];
   return GH_OK;
 }
 
@@ -1071,7 +1073,9 @@ static int make_obs_opt(const gh_model* m, int t, const gh_obs* in, StepObs* o) 
 static bool proposal_ok(const gh_model* m, int proposal) {
   if (proposal == GH_PROPOSAL_DEFAULT) return true;
   if (proposal == GH_PROPOSAL_GAUSSIAN) return m->family == GH_FAMILY_KITAGAWA;
-  if (proposal == GH_PROPOSAL_LINEAR) return m->family == GH_FAMILY_LGSSM && m->d + m->dy <= kMaxObs;
+  if (proposal == GH_PROPOSAL_LINEAR)  // (u_t follows the step's observed values)
+    return (m->family == GH_FAMILY_LGSSM && m->d + m->dy <= kMaxObs) ||
+           (m->family == GH_FAMILY_SLOTS && m->d + m->slots.nv <= kMaxObs);
   if (proposal != GH_PROPOSAL_OPTIMAL) return false;
   return m->family == GH_FAMILY_HMM || (m->family == GH_FAMILY_LGSSM && m->lg_opt);
 }
@@ -1547,7 +1551,24 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
     HIP_TRY(hipGetLastError());
     return GH_OK;
   }
-  if (a.proposal == GH_PROPOSAL_LINEAR) {  // LGSSM only (proposal_ok); P and chol(Sigma_q) in the filter's buffer
+  if (a.proposal == GH_PROPOSAL_LINEAR && pf->m->family == GH_FAMILY_SLOTS) {  // (proposal_ok)
+    SlotParams p = pf->m->slots;
+    p.QP = pf->qlin;
+    p.QL = pf->qlin + pf->D * pf->D;
+    p.cstq = pf->cstq;
+    switch (pf->m->d) {
+#define GH_SLL_CASE(DD) \
+  case DD: launch_step_t<SlotLinModel<DD>>(pf, p, o, a, init, e0, e1); break;
+      GH_SLL_CASE(1) GH_SLL_CASE(2) GH_SLL_CASE(3) GH_SLL_CASE(4) GH_SLL_CASE(5) GH_SLL_CASE(6)
+      GH_SLL_CASE(7) GH_SLL_CASE(8) GH_SLL_CASE(9) GH_SLL_CASE(10) GH_SLL_CASE(11) GH_SLL_CASE(12)
+      GH_SLL_CASE(13) GH_SLL_CASE(14) GH_SLL_CASE(15) GH_SLL_CASE(16)
+#undef GH_SLL_CASE
+      default: return set_err(GH_E_INVAL, "slot model d=%d not instantiated", pf->m->d);
+    }
+    HIP_TRY(hipGetLastError());
+    return GH_OK;
+  }
+  if (a.proposal == GH_PROPOSAL_LINEAR) {  // LGSSM (proposal_ok); P and chol(Sigma_q) in the filter's buffer
     LGParams p = pf->m->lg;
     p.QP = pf->qlin;
     p.QL = pf->qlin + pf->D * pf->D;

@@ -65,6 +65,12 @@
 // the slot family (gh_slots.h): SlotModel<D> for d = 1..16, in gh_inst_slots<k>.hip
 #define GH_SL_KERNELS(X, D)                                                                                     \
   X __global__ void gh::k_step<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::SlotLinModel<D>, true>(const double*, gh::SlotParams, gh::StepObs,             \
+                                                          gh::StepArgs);                                          \
+  X __global__ void gh::k_step<gh::SlotLinModel<D>, false>(const double*, gh::SlotParams, gh::StepObs,            \
+                                                           gh::StepArgs);                                         \
+  X __global__ void gh::k_step<gh::SlotLinModel<D>, false, true>(const double*, gh::SlotParams, gh::StepObs,      \
+                                                                 gh::StepArgs);                                   \
   X __global__ void gh::k_step<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
   X __global__ void gh::k_step<gh::SlotModel<D>, false, true>(const double*, gh::SlotParams, gh::StepObs,          \
                                                               gh::StepArgs);                                     \

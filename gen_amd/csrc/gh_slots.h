@@ -56,6 +56,12 @@ struct SlotParams {
   double cst[kMaxSlots];    // mvnormal -0.5 (m log 2pi + log det R); normal -0.5 log(2 pi sd^2)
   double inv2v[kMaxSlots];  // normal 1 / (2 sd^2)
   double sd[kMaxSlots];     // normal sd (simulate)
+  int nv;                   // observed values per step in StepObs::v (a poisson slot takes 2)
+  // the linear custom proposal (SlotLinModel): the filter's own buffer,
+  // absolute pointers (not rebased): P d*d | chol(Sigma_q) d*d; u_t in v[nv..]
+  const double* QP;
+  const double* QL;
+  double cstq;              // -0.5 (d log 2pi + log det Sigma_q)
   __device__ SlotParams rebase(const double* __restrict__ prm) const {
     SlotParams q = *this;
     q.A = rebased(*this, prm, A);
@@ -315,6 +321,76 @@ struct SlotModel {
       total = total + lp;
     }
     return total;
+  }
+};
+
+// A user-parameterised linear-Gaussian custom proposal for the slot family
+// (GH_PROPOSAL_LINEAR; the LG-SSM's LGLinModel over any slot model):
+// q(x_t | x_{t-1}) = mvnormal(P x_{t-1} + u_t, Sigma_q) (t = 1: mvnormal(u_1,
+// Sigma_q)), u_t per step after the slot values.  The weight is Gen's
+// custom-proposal weight (particle_filter.jl:79-91,139-154 via
+// trace_translators.jl:775-802): the model's score of the new choices — the
+// latent's logpdf (affine or Kitagawa) and the present slots' — minus q's
+// logpdf of the drawn value.
+template <int D>
+struct SlotLinModel {
+  static constexpr int kD = D;
+  static constexpr int kMinWaves = SlotModel<D>::kMinWaves;
+  using Params = SlotParams;
+  using Prior = SlotModel<D>;
+
+  __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return Prior::loglik(p, o, x); }
+
+  // x = mean + L_q z with mean = u (+ P xp); returns log q(x), the mean
+  // recomputed in the same order (LGLinModel::draw)
+  __device__ static double draw(const Params& p, const StepObs& o, const double* xp, const double* z, double* x) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = o.v[p.nv + i];
+      if (xp) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc = fma(p.QP[i * D + k], xp[k], acc);
+      }
+#pragma unroll
+      for (int k = 0; k <= i; ++k) acc = fma(p.QL[i * D + k], z[k], acc);
+      x[i] = acc;
+    }
+    double w[D];
+    double quad = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double mean = o.v[p.nv + i];
+      if (xp) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) mean = fma(p.QP[i * D + k], xp[k], mean);
+      }
+      double r = x[i] - mean;
+#pragma unroll
+      for (int k = 0; k < i; ++k) r = fma(-p.QL[i * D + k], w[k], r);
+      w[i] = r / p.QL[i * D + i];
+      quad = fma(w[i], w[i], quad);
+    }
+    return p.cstq - 0.5 * quad;
+  }
+
+  __device__ static double init(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, int /*proposal*/,
+                                double* x, Draw dr = {STREAM_INIT, 0}) {
+    double z[D + 1];
+    normals_n<D>(seed, pid, 1, dr.stream, dr.base, z, dr.tab);
+    const double lq = draw(p, o, nullptr, z, x);
+    double lat, ob;
+    Prior::score(p, o, 1, x, x, &lat, &ob);
+    return (lat + ob) - lq;
+  }
+
+  __device__ static double step(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, uint32_t t,
+                                int /*proposal*/, const double* xp, double* x, Draw dr = {STREAM_STEP, 0}) {
+    double z[D + 1];
+    normals_n<D>(seed, pid, t, dr.stream, dr.base, z, dr.tab);
+    const double lq = draw(p, o, xp, z, x);
+    double lat, ob;
+    Prior::score(p, o, t, xp, x, &lat, &ob);
+    return (lat + ob) - lq;
   }
 };
 

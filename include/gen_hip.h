@@ -112,8 +112,8 @@ typedef enum {
                                      y ~ categorical(softmax(W x + c)), 0-based class
      At most 32 observed values per step (a poisson slot counts 2).  An LGSSM
      or Kitagawa model written as slots filters bit for bit as its family does
-     (those stay the fast paths); default proposal only; not for
-     gh_pf_step_params. */
+     (those stay the fast paths); the default proposal or GH_PROPOSAL_LINEAR
+     (d + observed values <= 32); not for gh_pf_step_params. */
   GH_FAMILY_SLOTS = 5
 } gh_family;
 
@@ -135,7 +135,7 @@ typedef enum {
                               m the prior mean; proposal_args = (alpha, beta, gamma, sigma_q)
                               through gh_pf_init_q / gh_pf_step_q; weight log p(x_t|x_{t-1})
                               + log p(y_t|x_t) - log q(x_t) */,
-  GH_PROPOSAL_LINEAR = 3  /* user-parameterised custom proposal of the LGSSM (the same
+  GH_PROPOSAL_LINEAR = 3  /* user-parameterised custom proposal of the LGSSM and of slot models (the same
                               translator): x_t ~ mvnormal(P x_{t-1} + u_t, Sigma_q) (t = 1:
                               mvnormal(u_1, Sigma_q)); proposal_args = P[d*d] Sigma_q[d*d] u[d]
                               (required at gh_pf_init_q), or u[d] alone to keep P and Sigma_q

@@ -342,7 +342,7 @@ typedef struct {
      distribution, value count, mean form, offsets in obs_t.bt and in the
      observation vector, parameter block (mvnormal M = L_R^-1 H | H | c | L_R;
      normal / poisson / bernoulli h | c; categorical W | c) and constants */
-  int lat, K, sdist[4], sm[4], slink[4], svoff[4], syoff[4];
+  int lat, K, sdist[4], sm[4], slink[4], svoff[4], syoff[4], snv;
   double* sP[4];
   double scst[4], sinv2v[4], ssd[4];
 } model_t;
@@ -487,6 +487,7 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     }
     if (voff > 32 || yoff > 32) return -1;
     m->dy = yoff;
+    m->snv = voff;  /* (the linear proposal's u_t follows these values on the device) */
     if (m->lat == 0) {
       int64_t need = 3 * (int64_t)d * d + 2 * (int64_t)d;
       if (np < i + need) return -1;
@@ -901,6 +902,14 @@ static void slot_sim(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, 
 static double particle_init(const model_t* m, uint64_t seed, uint64_t pid, const obs_t* o,
                             int proposal, double* x, uint32_t stream, uint32_t base) {
   if (m->family == ORC_SLOTS) {
+    if (proposal == ORC_PROPOSAL_LINEAR) {  /* custom proposal: model weight - proposal score */
+      double z[64];
+      normals_at(seed, pid, 1, stream, base, m->d, z);
+      const double lq = lin_draw(m, NULL, z, x);
+      double lat, ob;
+      model_score(m, o, 1, x, x, &lat, &ob);
+      return (lat + ob) - lq;
+    }
     slot_latent(m, seed, pid, 1, o, NULL, x, stream, base);
     return slot_loglik(m, o, x);
   }
@@ -966,6 +975,14 @@ static double particle_step(const model_t* m, uint64_t seed, uint64_t pid, uint3
                             const obs_t* o, int proposal, const double* xp, double* x, uint32_t stream,
                             uint32_t base) {
   if (m->family == ORC_SLOTS) {
+    if (proposal == ORC_PROPOSAL_LINEAR) {
+      double z[64];
+      normals_at(seed, pid, t, stream, base, m->d, z);
+      const double lq = lin_draw(m, xp, z, x);
+      double lat, ob;
+      model_score(m, o, (int)t, xp, x, &lat, &ob);
+      return (lat + ob) - lq;
+    }
     slot_latent(m, seed, pid, t, o, xp, x, stream, base);
     return slot_loglik(m, o, x);
   }
@@ -1131,12 +1148,13 @@ static int init_impl(orc_pf* pf, const double* obs, int has_obs, int proposal, c
 static int proposal_ok(const model_t* m, int proposal) {
   if (proposal == 0) return 1;
   if (proposal == ORC_PROPOSAL_GAUSSIAN) return m->family == ORC_KITAGAWA && m->qa[3] > 0.0;
-  if (proposal == ORC_PROPOSAL_LINEAR) return m->family == ORC_LGSSM && m->qlin && m->d + m->dy <= 32;
+  if (proposal == ORC_PROPOSAL_LINEAR)
+    return m->qlin && ((m->family == ORC_LGSSM && m->d + m->dy <= 32) || (m->family == ORC_SLOTS && m->d + m->snv <= 32));
   return proposal == ORC_PROPOSAL_OPTIMAL && (m->family == ORC_HMM || (m->family == ORC_LGSSM && m->opt));
 }
 int orc_pf_set_proposal_args(orc_pf* pf, const double* args, int n) {
   model_t* m = &pf->m;
-  if (m->family == ORC_LGSSM) {  /* the linear proposal: P Sigma_q u, or u alone */
+  if (m->family == ORC_LGSSM || m->family == ORC_SLOTS) {  /* the linear proposal: P Sigma_q u, or u alone */
     const int d = m->d;
     if (n == d && m->qlin) {
       for (int i = 0; i < d; ++i) m->qu[i] = args[i];

@@ -26,7 +26,19 @@ def build_model(name):
         return gen.KitagawaSSM(10.0, 1.0)
     if name == "kit_sharp":  # peaked weights: one particle (one rank) holds nearly all of them
         return gen.KitagawaSSM(10.0, 0.01)
+    if name == "count":  # the slot-described family: Poisson, normal, Bernoulli, categorical addresses
+        from tests.test_slots import count_model
+
+        return count_model()
     raise ValueError(name)
+
+
+def obs_at(m, y, t):
+    """The step-t constraints: a slot model's dict of observed slots, or the
+    family's one observed address."""
+    if isinstance(y, dict):
+        return {("chain", t, k): v for k, v in y.items()}
+    return {m.obs_address(t): y}
 
 
 def changed_model(name):
@@ -99,12 +111,11 @@ def main():
                                        enumerate(a.sleep.split(":"))) if a.sleep else (-1, -1, 0.0)
     m = build_model(a.model)
     xs, ys = m.simulate(a.T, np.random.default_rng(5))
-    addr = m.obs_address
     ref = np.asarray(xs, dtype=np.float64).reshape(len(ys), -1) * 0.9
     if a.csmc:
-        st = gen.initialize_conditional_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, ref[0], seed=a.seed)
+        st = gen.initialize_conditional_particle_filter(m, (1,), obs_at(m, ys[0], 1), a.n, ref[0], seed=a.seed)
     else:
-        st = gen.initialize_particle_filter(m, (1,), {addr(1): ys[0]}, a.n, seed=a.seed, resampler=a.resampler)
+        st = gen.initialize_particle_filter(m, (1,), obs_at(m, ys[0], 1), a.n, seed=a.seed, resampler=a.resampler)
     if a.rejuv:
         gen.rejuvenate(st, a.rejuv)
     did = []
@@ -121,11 +132,11 @@ def main():
             st.states(2)
             gen.get_traces(st).scores()
         if a.csmc:
-            gen.conditional_particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]}, ref[t - 1])
+            gen.conditional_particle_filter_step(st, (t,), (gen.UnknownChange(),), obs_at(m, ys[t - 1], t), ref[t - 1])
         elif t == a.params_step:
-            gen.particle_filter_step(st, (t, m2), (gen.UnknownChange(), gen.UnknownChange()), {addr(t): ys[t - 1]})
+            gen.particle_filter_step(st, (t, m2), (gen.UnknownChange(), gen.UnknownChange()), obs_at(m, ys[t - 1], t))
         else:
-            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {addr(t): ys[t - 1]})
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), obs_at(m, ys[t - 1], t))
         if a.rejuv:
             gen.rejuvenate(st, a.rejuv)
     lml = gen.log_ml_estimate(st)

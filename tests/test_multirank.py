@@ -389,7 +389,7 @@ def test_gpu_multirank_peer_transport(tmp_path, model, R, thr, n, batched):
     ("gloo", "lg4", 2, None, 3001, False), ("gloo", "kit", 3, 1e9, 4003, False), ("gloo", "kit_sharp", 4, None, 4003, True),
     ("gloo", "lg10", 2, 3001.0, 3001, True), ("rccl1", "lg4", 1, 1e9, 3001, False),
     ("peer", "lg4", 2, None, 3001, False), ("peer", "kit", 3, 1e9, 4003, True), ("peer", "kit_sharp", 4, None, 4003, True),
-    ("gloo", "kit", 8, 1e9, 8003, True)])
+    ("gloo", "kit", 8, 1e9, 8003, True), ("peer", "count", 3, 1e9, 4003, False)])
 def test_gpu_multirank_multinomial(tmp_path, gh_ctx, transport, model, R, thr, n, batched):
     """Multinomial resampling (the reference's own resampler, Categorical draws
     per slot, particle_filter.jl:200) on R ranks: every rank evaluates the
@@ -448,7 +448,7 @@ def _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="systema
     indices equal a one-rank GPU filter's (the same global integer CDF)."""
     import gen_amd as gen
     from oracle import oracle as O
-    from tests.mr_worker import build_model
+    from tests.mr_worker import build_model, obs_at
 
     m = build_model(model)
     _, ys = m.simulate(T, np.random.default_rng(5))
@@ -461,13 +461,13 @@ def _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="systema
     assert np.array_equal(np.concatenate([p["score_tot"] for p in parts]).view(np.uint64), rtot.view(np.uint64))
     assert np.array_equal(np.concatenate([p["score_ps"] for p in parts], axis=2).view(np.uint64), rps.view(np.uint64))
     # the same filter on one rank of this process's GPU
-    st = gen.initialize_particle_filter(m, (1,), {m.obs_address(1): ys[0]}, n, seed=seed, resampler=resampler)
+    st = gen.initialize_particle_filter(m, (1,), obs_at(m, ys[0], 1), n, seed=seed, resampler=resampler)
     if batched:
         gen.run_particle_filter(st, list(ys[1:T]), thr)
     else:
         for t in range(2, T + 1):
             gen.maybe_resample(st, thr)
-            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), {m.obs_address(t): ys[t - 1]})
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), obs_at(m, ys[t - 1], t))
     _, idx = gen.sample_unweighted_traces(st, 500, seed=3)
     st.close()
     for p in parts:
@@ -478,7 +478,8 @@ def _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="systema
 @pytest.mark.parametrize("transport,model,R,thr,n,batched", [
     ("gloo", "lg4", 2, None, 3001, False), ("gloo", "kit", 3, 1e9, 4003, True), ("gloo", "kit_sharp", 3, None, 4003, True),
     ("peer", "lg4", 2, 1e9, 3001, True), ("peer", "kit", 3, None, 4096, True), ("peer", "lg10", 2, 3001.0, 3001, False),
-    ("rccl1", "lg4", 1, None, 3001, True), ("gloo", "kit", 2, 1e9, 3001, "mid"), ("peer", "lg4", 3, 1e9, 3001, "mid")])
+    ("rccl1", "lg4", 1, None, 3001, True), ("gloo", "kit", 2, 1e9, 3001, "mid"), ("peer", "lg4", 3, 1e9, 3001, "mid"),
+    ("peer", "count", 3, None, 4003, True), ("gloo", "count", 2, 1e9, 3001, False), ("rccl1", "count", 1, 1e9, 3001, True)])
 def test_gpu_multirank_genealogy(tmp_path, gh_ctx, transport, model, R, thr, n, batched):
     """The genealogy across ranks (get_traces at earlier steps, the trace score
     columns, sample_unweighted_traces; particle_filter.jl:31-34, 62-70): each

@@ -141,6 +141,79 @@ def test_slot_model_rejects_bad_descriptions():
         m.obs_from_choicemap(gen.ChoiceMap({("chain", 2, "count"): 1.0, ("chain", 3, "count"): 2.0}), 2)
 
 
+# ------------------------------------------- the linear custom proposal (CPU)
+def _flat(*a):
+    return np.concatenate([np.asarray(x, dtype=np.float64).ravel() for x in a])
+
+
+def _count_obs_lpdf(m, x, y):
+    """The count model's observed-slot logpdfs at latent x for the present
+    slots of y (the reference's closed forms; scipy where it has them)."""
+    from scipy import stats
+
+    s, tot = m.slots, 0.0
+    for k, sl in enumerate(s):
+        if sl["name"] not in y:
+            continue
+        v = y[sl["name"]]
+        if sl["dist"] == "categorical":
+            logits = np.asarray(sl["W"]) @ x + np.asarray(sl["c"])
+            tot += logits[int(v)] - logits.max() - np.log(np.exp(logits - logits.max()).sum())
+            continue
+        eta = float(np.dot(sl["h"], x) + sl["c"])
+        if sl["dist"] == "poisson":
+            tot += stats.poisson.logpmf(v, np.exp(eta))
+        elif sl["dist"] == "normal":
+            tot += stats.norm.logpdf(v, eta, sl["sd"])
+        else:
+            tot += stats.bernoulli.logpmf(v, 1.0 / (1.0 + np.exp(-eta)))
+    return tot
+
+
+def test_oracle_slot_linear_proposal_weights():
+    """GH_PROPOSAL_LINEAR on a slot model: q = mvnormal(P x_{t-1} + u_t,
+    Sigma_q); weight = log p(x_t | x_{t-1}) + sum of the present slots'
+    logpdfs - log q(x_t) (particle_filter.jl:79-91,139-154 via
+    trace_translators.jl:775-802) against scipy."""
+    from scipy import stats
+
+    m, obs = count_obs()
+    n = 200
+    P, S, u1, u2 = 0.6 * m.A, np.array([[0.08, 0.01], [0.01, 0.06]]), np.array([0.4, 0.1]), np.array([-0.2, 0.3])
+    pf = O.OraclePF(m, n, 3)
+    pf.set_proposal_args(_flat(P, S, u1))
+    pf.init(obs[0], O.LINEAR)
+    x1 = pf.state().copy()
+    w1 = np.array([stats.multivariate_normal.logpdf(x1[:, i], m.mu0, m.P0) + _count_obs_lpdf(m, x1[:, i], obs[0])
+                   - stats.multivariate_normal.logpdf(x1[:, i], u1, S) for i in range(n)])
+    np.testing.assert_allclose(pf.log_weights(), w1, rtol=1e-11, atol=1e-10)
+    pf.set_proposal_args(u2)  # u alone: P and Sigma_q kept
+    pf.maybe_resample(0.0)
+    pf.step(obs[1], O.LINEAR)
+    x2 = pf.state()
+    w2 = w1 + np.array([stats.multivariate_normal.logpdf(x2[:, i], m.A @ x1[:, i] + m.b, m.Q)
+                        + _count_obs_lpdf(m, x2[:, i], obs[1])
+                        - stats.multivariate_normal.logpdf(x2[:, i], P @ x1[:, i] + u2, S) for i in range(n)])
+    np.testing.assert_allclose(pf.log_weights(), w2, rtol=1e-11, atol=1e-9)
+
+
+def test_oracle_slot_prior_as_linear_proposal_is_the_bootstrap_filter():
+    """q = the prior (P = A, u = b, Sigma_q = Q; t = 1: mu0, P0) draws the
+    bootstrap filter's latents and weighs them to rounding."""
+    m, obs = count_obs()
+    n = 400
+    boot = O.run_pf(m, obs, n, 9, thr=0.0)
+    pf = O.OraclePF(m, n, 9)
+    pf.set_proposal_args(_flat(m.A, m.P0, m.mu0))
+    pf.init(obs[0], O.LINEAR)
+    pf.set_proposal_args(_flat(m.A, m.Q, m.b))
+    for y in obs[1:]:
+        pf.maybe_resample(0.0)
+        pf.step(y, O.LINEAR)
+    np.testing.assert_allclose(pf.state(), boot.state(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(pf.log_weights(), boot.log_weights(), rtol=1e-10, atol=1e-9)
+
+
 # ------------------------------------------------------------------ GPU
 def _gpu_run(model, obs, n, seed, batched, thr=None, rejuv=0):
     st = gen.initialize_particle_filter(model, (1,), _obs_at(model, obs[0], 1), n, seed=seed)
@@ -269,3 +342,53 @@ def test_gpu_slots_constrained_twice_is_discard(gh_ctx):
     assert rc == 2, rc  # GH_E_DISCARD
     lib.gh_model_destroy(h)
     del ctx, keep
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["count", "kit"])
+def test_gpu_slot_linear_proposal_bitexact(gh_ctx, name):
+    """The linear custom proposal on slot models (an affine latent with four
+    observed addresses; the Kitagawa latent with its x^2/20 slot), arguments
+    changing between steps (full and u-only), resampling on some steps:
+    states, weights, parents and score columns bit-exact against the oracle."""
+    if name == "count":
+        m, obs = count_obs()
+        d = 2
+    else:
+        kit = gen.KitagawaSSM(4.0, 1.0)
+        m = kit_as_slots(kit)
+        _, ys = kit.simulate(9, np.random.default_rng(3))
+        obs = [{"y": y} for y in ys]
+        obs[3] = {}
+        d = 1
+    rng = np.random.default_rng(8)
+
+    def full(t):
+        G = rng.standard_normal((d, d))
+        return _flat(0.5 * np.eye(d) + 0.05 * rng.standard_normal((d, d)), 0.1 * np.eye(d) + 0.02 * G @ G.T,
+                     0.3 * rng.standard_normal(d))
+
+    n, seed = 6007, 19
+    a0 = full(1)
+    st = gen.initialize_particle_filter(m, (1,), _obs_at(m, obs[0], 1), gen.LinearGaussianProposal, (a0,), n,
+                                        seed=seed)
+    orc = O.OraclePF(m, n, seed)
+    orc.set_proposal_args(a0)
+    orc.init(obs[0], O.LINEAR)
+    for t in range(2, len(obs) + 1):
+        thr = n if t % 3 else None
+        assert gen.maybe_resample(st, thr) == orc.maybe_resample(thr)[0]
+        args = full(t) if t % 2 == 0 else full(t)[-d:]
+        gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), _obs_at(m, obs[t - 1], t),
+                                 gen.LinearGaussianProposal, (args,))
+        orc.set_proposal_args(args)
+        orc.step(obs[t - 1], O.LINEAR)
+        assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64)), t
+        assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64)), t
+        assert np.array_equal(st.parents, orc.parents()), t
+    a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+    assert abs(a - b) <= 1e-9 * abs(b)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    st.close()
