@@ -2036,7 +2036,42 @@ static void log_raw_obs(gh_pf* pf, int t, const gh_obs* obs) {
   if ((int)pf->raw_obs.size() < t) pf->raw_obs.resize(t);
   auto& r = pf->raw_obs[t - 1];
   r.clear();
+  if (pf->m->family == GH_FAMILY_SLOTS) {  // the chain as (slot, count, values...) records (make_obs validated it)
+    for (const gh_obs* e = obs; e; e = e->next) {
+      if (!e->present || !e->values) continue;
+      r.push_back((double)e->slot);
+      r.push_back((double)e->n_values);
+      r.insert(r.end(), e->values, e->values + e->n_values);
+    }
+    return;
+  }
   if (obs && obs->present && obs->values && obs->n_values > 0) r.assign(obs->values, obs->values + obs->n_values);
+}
+
+// a slot model's logged step (log_raw_obs) as a gh_obs chain again, in
+// chain[0..kMaxSlots) (nullptr: nothing observed)
+static const gh_obs* slot_chain(const std::vector<double>& r, gh_obs* chain) {
+  int k = 0;
+  for (size_t i = 0; i + 1 < r.size() && k < kMaxSlots; ++k) {
+    const int nv = (int)r[i + 1];
+    chain[k] = gh_obs{};
+    chain[k].values = r.data() + i + 2;
+    chain[k].n_values = nv;
+    chain[k].present = 1;
+    chain[k].slot = (int32_t)r[i];
+    if (k > 0) chain[k - 1].next = &chain[k];
+    i += 2 + (size_t)nv;
+  }
+  return k ? chain : nullptr;
+}
+
+// the same slot layout (a parameter change keeps every address and its form)
+static bool same_slots(const gh_model* a, const gh_model* b) {
+  const SlotParams &p = a->slots, &q = b->slots;
+  if (p.lat != q.lat || p.K != q.K) return false;
+  for (int k = 0; k < p.K; ++k)
+    if (p.dist[k] != q.dist[k] || p.m[k] != q.m[k] || p.link[k] != q.link[k]) return false;
+  return true;
 }
 
 static int pf_step_impl(gh_pf* pf, const gh_obs* obs, int proposal, const double* pin_ref);
@@ -3128,8 +3163,9 @@ extern "C" int gh_pf_step_params_conditional(gh_pf* pf, const gh_obs* obs, gh_mo
 static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model* nm, const double* pin_ref) {
   if (!pf->opts.record_history) return set_err(GH_E_STATE, "gh_pf_step_params needs record_history");
   const gh_model* m = pf->m;
-  if (m->family == GH_FAMILY_SLOTS)
-    return set_err(GH_E_INVAL, "gh_pf_step_params: not for the slot family (its parameter changes are not lowered)");
+  if (m->family == GH_FAMILY_SLOTS && (nm->family != m->family || !same_slots(m, nm)))
+    return set_err(GH_E_INVAL, "gh_pf_step_params: the new slot model must keep the latent form and every slot's "
+                               "distribution, size and mean form");
   if (nm->ctx != m->ctx || nm->family != m->family || nm->d != m->d || nm->dy != m->dy || nm->k != m->k ||
       nm->v != m->v)
     return set_err(GH_E_INVAL, "gh_pf_step_params: the new parameters must be of the same family and dimensions");
@@ -3141,6 +3177,11 @@ static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model
   std::vector<StepObs> rebuilt(T);
   for (int s = 1; s <= T; ++s) {
     const auto& r = pf->raw_obs[s - 1];
+    if (m->family == GH_FAMILY_SLOTS) {
+      gh_obs chain[kMaxSlots];
+      CHECK(make_obs(nm, s, slot_chain(r, chain), &rebuilt[s - 1]));
+      continue;
+    }
     const gh_obs in{r.empty() ? nullptr : r.data(), (int32_t)r.size(), r.empty() ? 0 : 1};
     CHECK(make_obs(nm, s, &in, &rebuilt[s - 1]));
   }

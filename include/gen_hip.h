@@ -113,7 +113,8 @@ typedef enum {
      At most 32 observed values per step (a poisson slot counts 2).  An LGSSM
      or Kitagawa model written as slots filters bit for bit as its family does
      (those stay the fast paths); the default proposal or GH_PROPOSAL_LINEAR
-     (d + observed values <= 32); not for gh_pf_step_params. */
+     (d + observed values <= 32); gh_pf_step_params takes a new slot model
+     with the same latent form and slot layout (only the numbers change). */
   GH_FAMILY_SLOTS = 5
 } gh_family;
 

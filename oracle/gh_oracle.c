@@ -1655,6 +1655,15 @@ int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const doubl
     model_free(&m2);
     return -1;
   }
+  if (m->family == ORC_SLOTS) {  /* the same latent form and slot layout (the engine's same_slots) */
+    int same = m2.lat == m->lat && m2.K == m->K;
+    for (int k = 0; same && k < m->K; ++k)
+      same = m2.sdist[k] == m->sdist[k] && m2.sm[k] == m->sm[k] && m2.slink[k] == m->slink[k];
+    if (!same) {
+      model_free(&m2);
+      return -1;
+    }
+  }
   if (proposal != ORC_PROPOSAL_LINEAR && !proposal_ok(&m2, proposal)) {  /* (the linear one: the filter's args) */
     model_free(&m2);
     return -1;

@@ -45,6 +45,10 @@ def changed_model(name):
     """The Unfold of `name` with other parameters (a parameter change, --params-step)."""
     import gen_amd as gen
 
+    if name == "count":
+        from tests.test_slots import changed_count_model
+
+        return changed_count_model()
     if name.startswith("lg"):
         m = build_model(name)
         return gen.LinearGaussianSSM(0.8 * m.A, 1.5 * m.Q, m.H, 0.7 * m.R, m.mu0 + 0.1, m.P0, b=m.b + 0.05, c=m.c - 0.1)

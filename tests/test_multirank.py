@@ -537,7 +537,7 @@ def test_gpu_multirank_broken_genealogy_raises(tmp_path, gh_ctx, transport, R, v
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport,model,R", [("gloo", "lg4", 2), ("peer", "kit", 3)])
+@pytest.mark.parametrize("transport,model,R", [("gloo", "lg4", 2), ("peer", "kit", 3), ("peer", "count", 2)])
 def test_gpu_multirank_step_params(tmp_path, transport, model, R):
     """particle_filter_step with changed Unfold parameters on R ranks
     (gh_pf_step_params: every particle re-scored along its genealogy, which

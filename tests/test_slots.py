@@ -51,6 +51,18 @@ def count_model():
          {"name": "kind", "dist": "categorical", "W": [[1.0, 0.0], [0.0, 1.0], [-1.0, 1.0]], "c": [0.0, 0.2, -0.1]}])
 
 
+def changed_count_model():
+    """count_model() with other numbers in every block (the same slot layout):
+    a parameter change, new_args = (t, model')."""
+    return gen.SlotSSM(
+        {"form": "affine", "A": [[0.8, 0.1], [-0.05, 0.85]], "b": [0.05, 0.0], "Q": [[0.07, 0.0], [0.0, 0.05]],
+         "mu0": [0.5, 0.0], "P0": [[0.3, 0.0], [0.0, 0.3]]},
+        [{"name": "count", "dist": "poisson", "h": [0.9, 0.6], "c": 0.1},
+         {"name": "z", "dist": "normal", "h": [0.25, -0.1], "c": 0.0, "sd": 0.9},
+         {"name": "on", "dist": "bernoulli", "h": [1.2, 0.3], "c": -0.1},
+         {"name": "kind", "dist": "categorical", "W": [[0.8, 0.0], [0.1, 1.1], [-1.0, 0.7]], "c": [0.1, 0.0, -0.2]}])
+
+
 def count_obs(T=10, seed=5):
     """Observations with some slots missing at some steps (and one empty step)."""
     m = count_model()
@@ -212,6 +224,30 @@ def test_oracle_slot_prior_as_linear_proposal_is_the_bootstrap_filter():
         pf.step(y, O.LINEAR)
     np.testing.assert_allclose(pf.state(), boot.state(), rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(pf.log_weights(), boot.log_weights(), rtol=1e-10, atol=1e-9)
+
+
+def test_oracle_slot_step_params():
+    """A parameter change on a slot model (orc_pf_step_params): to the same
+    numbers it is the plain step bit for bit; a model with another slot
+    layout is refused."""
+    m, obs = count_obs()
+    runs = []
+    for change in (False, True):
+        pf = O.OraclePF(m, 500, 4)
+        pf.init(obs[0])
+        for t in range(2, 7):
+            pf.maybe_resample(None)
+            if change and t == 5:
+                pf.step_params(count_model(), obs[t - 1])
+            else:
+                pf.step(obs[t - 1])
+        runs.append(pf)
+    assert np.array_equal(runs[0].log_weights(), runs[1].log_weights())
+    assert np.array_equal(runs[0].state(), runs[1].state())
+    other = gen.SlotSSM({"form": "affine", "A": m.A, "b": m.b, "Q": m.Q, "mu0": m.mu0, "P0": m.P0},
+                        [{"name": "count", "dist": "poisson", "h": [1.0, 0.5], "c": 0.2}])
+    with pytest.raises(ValueError):
+        runs[0].step_params(other, {"count": 1.0})
 
 
 # ------------------------------------------------------------------ GPU
@@ -391,4 +427,43 @@ def test_gpu_slot_linear_proposal_bitexact(gh_ctx, name):
     tot, ps = gen.get_traces(st).scores(per_step=True)
     otot, ops = orc.scores(per_step=True)
     assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    st.close()
+
+
+@pytest.mark.gpu
+def test_gpu_slot_step_params_bitexact(gh_ctx):
+    """particle_filter_step with new_args = (t, model') on a slot model
+    (gh_pf_step_params: every particle re-scored along its genealogy under the
+    new numbers, then the step under them) and later steps: states, weights,
+    parents, log-ML and score columns bit-exact against the oracle; a model
+    with another slot layout is refused."""
+    m, obs = count_obs()
+    m2 = changed_count_model()
+    n, seed, K = 5003, 21, 5
+    st = gen.initialize_particle_filter(m, (1,), _obs_at(m, obs[0], 1), n, seed=seed)
+    orc = O.OraclePF(m, n, seed)
+    orc.init(obs[0])
+    for t in range(2, len(obs) + 1):
+        assert gen.maybe_resample(st, None) == orc.maybe_resample(None)[0]
+        if t == K:
+            gen.particle_filter_step(st, (t, m2), (gen.UnknownChange(), gen.UnknownChange()), _obs_at(m2, obs[t - 1], t))
+            orc.step_params(m2, obs[t - 1])
+        else:
+            mt = m2 if t > K else m
+            gen.particle_filter_step(st, (t,), (gen.UnknownChange(),), _obs_at(mt, obs[t - 1], t))
+            orc.step(obs[t - 1])
+        assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64)), t
+        assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64)), t
+        assert np.array_equal(st.parents, orc.parents()), t
+    a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+    assert abs(a - b) <= 1e-9 * abs(b)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    other = gen.SlotSSM({"form": "affine", "A": m.A, "b": m.b, "Q": m.Q, "mu0": m.mu0, "P0": m.P0},
+                        [{"name": "count", "dist": "poisson", "h": [1.0, 0.5], "c": 0.2}])
+    t = len(obs) + 1
+    with pytest.raises(gen.GenHipError):
+        gen.particle_filter_step(st, (t, other), (gen.UnknownChange(), gen.UnknownChange()),
+                                 {("chain", t, "count"): 1.0})
     st.close()
