@@ -397,8 +397,8 @@ def secondary_multirank_path(gen, a, c2_ms, c4_ms):
             ctx.close()
     out["note"] = ("world = 1 on the multi-rank path: C2 / C4 over RCCL (the collectives are one-rank copies), "
                    "C2_peer / C4_peer over the peer transport (the maxima and records through the rank's own "
-                   "mailbox inside k_rank_a2 / k_rank_b, no collective launch); no rows move, so the extra time "
-                   "is the path's launches, host plan and exchanges, not xGMI")
+                   "mailbox inside the fused k_rank_ab, no collective launch); no rows move, so the extra time "
+                   "is the path's launches, mailbox round trips and host plan, not xGMI")
     return out
 
 
