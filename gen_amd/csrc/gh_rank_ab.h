@@ -263,7 +263,8 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_ab(RankABArg
   // ---- the marks (k_resample1's loop on the global CDF: incremental slot
   // counts, the exact recount near integers) clamped to this rank's slots,
   // and the rows of slots other ranks own, stored into their buffers
-  const int64_t own_lo = rb.lo, own_hi = rb.lo + rb.n;
+  // (32-bit: N < 2^31, so the clamp below is one v_med3_i32, not 64-bit compares and selects)
+  const int32_t own_lo = (int32_t)rb.lo, own_hi = (int32_t)(rb.lo + rb.n);
   uint64_t run = sd.base + sbefore + incl - tsum;
   const double ns = as_f64(readfirstlane_u64(as_u64((double)N * sd.invS)));
   const double hw = as_f64(readfirstlane_u64(as_u64(0.5 - count_window(N))));
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_ab(RankABArg
     return j;
   };
   auto local = [&](int32_t s) {  // clamp to [own_lo, own_hi), local index
-    return (uint32_t)((s < own_lo ? own_lo : (s > own_hi ? own_hi : s)) - own_lo);
+    return (uint32_t)(min(max(s, own_lo), own_hi) - own_lo);
   };
   int32_t s_i = count(run);
 #pragma unroll
