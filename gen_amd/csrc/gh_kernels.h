@@ -2441,32 +2441,50 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   }
   const uint64_t incl = blk16_incl_u64(tsum, smu);
   uint64_t run = sbase + incl - tsum;
-  const int64_t own_lo = sown_lo, own_hi = sown_hi;
-  auto clamp_own = [&](int64_t s) { return s < own_lo ? own_lo : (s > own_hi ? own_hi : s); };
-  int64_t s0 = sys_count(&sd, N, run);
+  // (32-bit slots: N < 2^31, gh_pf_init; the clamp is one v_med3_i32)
+  const int32_t own_lo = (int32_t)sown_lo, own_hi = (int32_t)sown_hi;
+  const uint32_t N32 = (uint32_t)N;
   // more rows than the bounded send buffer holds (this rank carries most of
   // the weight): keep the CDF, the host regrows the buffer and k_rows_fill
   // writes every row from it (rare; the hot path only tests the flag)
   const bool spill = ssend > r.rows_cap;
-  // particle i's slots [s0, s1) (global); the part this rank owns, [l0, l1)
-  // in local slots, gets a tagged mark at l0 and the carry of every 64-slot
-  // group starting inside it — a lane writes up to two carries, a longer
-  // range gets them from its whole wave (as k_resample1's marks phase: no
-  // LDS copy of the range ends, no block barrier)
+  // particle i's slots [s_i, e_i) (global) by k_resample1's incremental
+  // counts (its error bound: exact outside count_window, the exact count
+  // inside); the part this rank owns, [l0, l1) in local slots, gets a tagged
+  // mark at l0 and the carry of every 64-slot group starting inside it — a
+  // lane writes up to two carries, a longer range gets them from its whole
+  // wave (no LDS copy of the range ends, no block barrier)
+  static_assert(IT <= 16, "the error bound of the incremental slot counts");
+  const double ns = as_f64(readfirstlane_u64(as_u64((double)N32 * sd.invS)));
+  const double hw = as_f64(readfirstlane_u64(as_u64(0.5 - count_window(N32))));
+  double v = fma((double)run, (double)N32, -(double)sd.o) * sd.invS;
+  auto count = [&](uint64_t X) {
+    const double fl = floor(v);
+    const double fr = v - fl;
+    int32_t j = (int32_t)fl + 1;
+    const bool near = fabs(fr - 0.5) >= hw;
+    if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)
+      if (near) j = sys_count_exact_call(&sd, N32, X);
+    }
+    return j;
+  };
+  auto local = [&](int32_t sl) { return (uint32_t)(min(max(sl, own_lo), own_hi) - own_lo); };
+  int32_t s_i = count(run);
 #pragma unroll
   for (int k = 0; k < IT; ++k) {
     run += qv[k];
+    v = fma(u52_to_f64(qv[k]), ns, v);
     const int64_t i = i0 + k;
-    // (a particle past n or of zero weight leaves run, hence the count, unchanged)
-    const int64_t s1 = sys_count_w(&sd, N, run);
-    const int64_t l0 = clamp_own(s0) - own_lo, l1 = clamp_own(s1) - own_lo;
+    // (a particle past n or of zero weight leaves run, v, hence the count, unchanged)
+    const int32_t e_i = count(run);
+    const uint32_t l0 = local(s_i), l1 = local(e_i);
     const uint32_t tagged = r.mk.tag | (uint32_t)i;
     if (l1 > l0) r.mk.mark[l0] = tagged;
-    const int64_t g0 = (l0 + 63) >> 6, g1 = (l1 + 63) >> 6;  // local groups g with 64 g in [l0, l1)
-    const bool many = g1 - g0 > 2;
+    const uint32_t g0 = (l0 + 63u) >> 6, g1 = (l1 + 63u) >> 6;  // local groups g with 64 g in [l0, l1)
+    const bool many = g1 - g0 > 2u;
     if (!many) {
       if (g1 > g0) r.mk.cmark[g0] = tagged;
-      if (g1 > g0 + 1) r.mk.cmark[g0 + 1] = tagged;
+      if (g1 > g0 + 1u) r.mk.cmark[g0 + 1u] = tagged;
     }
     uint64_t bm = __builtin_amdgcn_ballot_w64(many);
     while (bm) {
@@ -2477,12 +2495,16 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
       for (int32_t g = a0 + (threadIdx.x & 63); g < a1; g += 64) r.mk.cmark[g] = tg;
     }
     if (spill && i < r.n) r.C[i] = run;
-    // slots of other ranks: state rows, by destination then slot
-    if (r.peer_rows)
-      send_rows_peer(s0, s1, i, own_lo, own_hi, R, N, sdst_lo, sra_all, srb_all, r.prow, r.xprev, r.D, r.lo);
-    else if (!spill)
-      send_rows(s0, s1, i, own_lo, own_hi, R, N, sdst_lo, sseg_lo, ssoff, r.rows_cap, r.rows, r.xprev, r.D, r.lo);
-    s0 = s1;
+    // slots of other ranks (only a range that crosses this rank's block edge):
+    // state rows, by destination then slot
+    if (e_i > s_i && (s_i < own_lo || e_i > own_hi)) {
+      if (r.peer_rows)
+        send_rows_peer(s_i, e_i, i, own_lo, own_hi, R, N, sdst_lo, sra_all, srb_all, r.prow, r.xprev, r.D, r.lo);
+      else if (!spill)
+        send_rows(s_i, e_i, i, own_lo, own_hi, R, N, sdst_lo, sseg_lo, ssoff, r.rows_cap, r.rows, r.xprev, r.D,
+                  r.lo);
+    }
+    s_i = e_i;
   }
 }
 
