@@ -346,6 +346,58 @@ def secondary_c4(gen, ctx, a):
     return out
 
 
+def secondary_slots(gen, ctx, a):
+    """Slot-described Unfold kernels (GH_FAMILY_SLOTS) at the C2
+    size: a count SSM (2-d affine latent; Poisson, normal, Bernoulli and
+    categorical addresses, every one observed each step) and the C2 model
+    written as slots, beside the hand-lowered family on the same data — the
+    generic functor's price."""
+    n = a.particles
+    T = a.warmup + a.steps + 1
+
+    def timed(model, obs, init_cm):
+        st = gen.initialize_particle_filter(model, (1,), init_cm, n, seed=42,
+                                            record_history=not a.no_history, history_capacity=T + 2, ctx=ctx)
+        gen.run_particle_filter(st, list(obs[1 : 1 + a.warmup]), a.ess_threshold)
+        batch = gen.prepare_observations(model, list(obs[1 + a.warmup : 1 + a.warmup + a.steps]))
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        gen.run_particle_filter(st, batch, a.ess_threshold)
+        ctx.synchronize()
+        dt = time.perf_counter() - t0
+        _, did = st.ess_history()
+        n_res = int(did[a.warmup : a.warmup + a.steps].sum())
+        st.close()
+        return {"ms_per_step": dt * 1e3 / a.steps, "particle_steps_per_s": n * a.steps / dt, "resample_steps_timed": n_res}
+
+    count = gen.SlotSSM(
+        {"form": "affine", "A": [[0.9, 0.05], [0.0, 0.8]], "b": [0.0, 0.1], "Q": [[0.05, 0.01], [0.01, 0.04]],
+         "mu0": [0.5, 0.0], "P0": [[0.3, 0.0], [0.0, 0.3]]},
+        [{"name": "count", "dist": "poisson", "h": [1.0, 0.5], "c": 0.2},
+         {"name": "z", "dist": "normal", "h": [0.3, -0.2], "c": 0.1, "sd": 0.7},
+         {"name": "on", "dist": "bernoulli", "h": [1.5, 0.0], "c": -0.3},
+         {"name": "kind", "dist": "categorical", "W": [[1.0, 0.0], [0.0, 1.0], [-1.0, 1.0]], "c": [0.0, 0.2, -0.1]}])
+    _, cys = count.simulate(T, np.random.default_rng(5))
+    lg = gen.LinearGaussianSSM.benchmark(a.d)
+    lgs = gen.SlotSSM({"form": "affine", "A": lg.A, "b": lg.b, "Q": lg.Q, "mu0": lg.mu0, "P0": lg.P0},
+                      [{"name": "y", "dist": "mvnormal", "H": lg.H, "c": lg.c, "R": lg.R}])
+    _, ys = lg.simulate(T, np.random.default_rng(2))
+    fam = timed(lg, list(ys), {("chain", 1, "y"): ys[0]})
+    sl = timed(lgs, [{"y": y} for y in ys], {("chain", 1, "y"): ys[0]})
+    return {
+        "metric": "particle-steps/sec, slot-described SSMs",
+        "unit": "particle-steps/s",
+        "particles": n,
+        "steps": a.steps,
+        "count_ssm": timed(count, [dict(y) for y in cys], {("chain", 1, k): v for k, v in cys[0].items()}),
+        "lgssm_d%d_as_slots" % a.d: sl,
+        "lgssm_d%d_family" % a.d: fam,
+        "slots_vs_family": fam["ms_per_step"] / sl["ms_per_step"],
+        "note": "the generic slot functor (parameters through pointers, a loop over slots) against the hand-lowered "
+                "LG-SSM family on the same observations (bit-identical results, tests/test_slots.py)",
+    }
+
+
 def peer_probe(gen, ctx, world, dist):
     """A few always-resampling steps of a small filter on the peer transport
     (rows cross ranks every step); returns the log-ML as an exact hex string.
@@ -654,7 +706,8 @@ def main(argv=None):
             out["log_ml_error"]["vs_cpu_reference_same_seed"] = {"particles": par["particles"], "rel": par["rel"]}
     if rank == 0 and world == 1 and not a.no_secondary and a.model == "lgssm":
         c4 = secondary_c4(gen, ctx, a)
-        out["secondary"] = {"C4": c4, "C3": secondary_c3(gen, ctx, a), "C5": secondary_c5(gen, ctx, a)}
+        out["secondary"] = {"C4": c4, "C3": secondary_c3(gen, ctx, a), "C5": secondary_c5(gen, ctx, a),
+                            "slots": secondary_slots(gen, ctx, a)}
         if a.proposal == "default":
             out["secondary"]["call_by_call"] = secondary_call_by_call(gen, ctx, a, out["ms_per_step"])
         if a.proposal == "default":  # (world 1: both transports, whatever --transport says)
