@@ -410,7 +410,7 @@ def test_gpu_multirank_multinomial(tmp_path, gh_ctx, transport, model, R, thr, n
 @pytest.mark.gpu
 @pytest.mark.parametrize("transport,model,R,thr,n", [("gloo", "lg4", 2, None, 3001), ("gloo", "kit", 3, 1e9, 4003),
                                                       ("rccl1", "lg4", 1, 1e9, 3001), ("peer", "lg4", 2, None, 3001),
-                                                      ("peer", "kit", 3, 1e9, 4003)])
+                                                      ("peer", "kit", 3, 1e9, 4003), ("peer", "count", 2, None, 3001)])
 def test_gpu_multirank_conditional_smc(tmp_path, transport, model, R, thr, n):
     """Conditional SMC (examples/pmmh/smc.jl:100-151) on R ranks: particle 0
     (rank 0's first) is pinned to the reference and is its own parent, the

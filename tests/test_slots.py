@@ -467,3 +467,33 @@ def test_gpu_slot_step_params_bitexact(gh_ctx):
         gen.particle_filter_step(st, (t, other), (gen.UnknownChange(), gen.UnknownChange()),
                                  {("chain", t, "count"): 1.0})
     st.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thr", [None, 1e9])
+def test_gpu_slot_conditional_smc_bitexact(gh_ctx, thr):
+    """Conditional SMC (examples/pmmh/smc.jl:100-151) on the count SSM:
+    particle 0 pinned to a reference trajectory, the others resampled
+    multinomially — states, weights, parents and trajectories bit-exact
+    against the oracle's conditional run."""
+    m, obs = count_obs()
+    xs, _ = m.simulate(len(obs), np.random.default_rng(5))
+    ref = np.asarray(xs, dtype=np.float64).reshape(len(obs), -1) * 0.9
+    n, seed = 3001, 17
+    st = gen.initialize_conditional_particle_filter(m, (1,), _obs_at(m, obs[0], 1), n, ref[0], seed=seed)
+    orc = O.OraclePF(m, n, seed, O.MULTINOMIAL)
+    orc.init_conditional(obs[0], ref[0])
+    for t in range(2, len(obs) + 1):
+        assert gen.maybe_resample(st, thr) == orc.maybe_resample(thr)[0]
+        gen.conditional_particle_filter_step(st, (t,), (gen.UnknownChange(),), _obs_at(m, obs[t - 1], t), ref[t - 1])
+        orc.step_conditional(obs[t - 1], ref[t - 1])
+        assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64)), t
+        assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64)), t
+        assert np.array_equal(st.parents, orc.parents()), t
+    a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+    assert abs(a - b) <= 1e-9 * abs(b)
+    T = len(obs)
+    for t in (1, T // 2, T):
+        assert np.array_equal(st.states(t).T, orc.trajectory(t)), t
+    assert np.array_equal(np.stack([st.states(t)[0] for t in range(1, T + 1)]), ref)
+    st.close()
