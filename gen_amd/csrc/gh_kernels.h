@@ -1893,8 +1893,12 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_a(RankAArgs r) {
   const double M = sM;
   const int64_t i0 = (int64_t)blockIdx.x * (kRsBlock * IT) + (int64_t)threadIdx.x * IT;
   uint64_t tsum = 0;
+  const double qscale = as_f64((uint64_t)(r.shift + 1023) << 52);
 #pragma unroll
-  for (int k = 0; k < IT; ++k) tsum += (i0 + k < r.n) ? quantize_weight(r.logw[i0 + k], M, r.shift) : 0;
+  for (int k = 0; k < IT; ++k) {  // (= quantize_weight: the branch-free exp, 3-instruction conversion)
+    const double e = (i0 + k < r.n) ? gh_exp_nonpos(r.logw[i0 + k] - M) : 0.0;
+    tsum += e == e ? f64_to_u52(e * qscale) : 0;
+  }
   const uint64_t tot = blk16_sum_u64(tsum, smu);
   const uint64_t kTag = 1ull << 63;
   const uint64_t par = (sgen & 1u) ? kTag : 0ull;
@@ -2434,9 +2438,11 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
   const double M = sMq;
   uint64_t qv[IT];
   uint64_t tsum = 0;
+  const double qscale = as_f64((uint64_t)(r.shift + 1023) << 52);
 #pragma unroll
-  for (int k = 0; k < IT; ++k) {
-    qv[k] = (i0 + k < r.n) ? quantize_weight(lw[k], M, r.shift) : 0;
+  for (int k = 0; k < IT; ++k) {  // (k_rank_a2's form: the branch-free exp, 3-instruction conversion)
+    const double e = (i0 + k < r.n) ? gh_exp_nonpos(lw[k] - M) : 0.0;
+    qv[k] = e == e ? f64_to_u52(e * qscale) : 0;
     tsum += qv[k];
   }
   const uint64_t incl = blk16_incl_u64(tsum, smu);
