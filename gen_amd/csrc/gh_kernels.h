@@ -1816,9 +1816,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_resample1(Resampl
     const double fr = v - fl;
     int32_t j = (int32_t)fl + 1;
     const bool near = fabs(fr - 0.5) >= hw;
-    if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)
-      if (near) j = sys_count_exact_call(&sd, N, X);
-    }
+    if (near) j = sys_count_exact_call(&sd, N, X);  // (exec-masked call, skipped when no lane is near)
     return j;
   };
   int32_t s_i = count(run);
@@ -2469,9 +2467,7 @@ __global__ __launch_bounds__(kRsBlock) void k_rank_b(RankBArgs r) {
     const double fr = v - fl;
     int32_t j = (int32_t)fl + 1;
     const bool near = fabs(fr - 0.5) >= hw;
-    if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)
-      if (near) j = sys_count_exact_call(&sd, N32, X);
-    }
+    if (near) j = sys_count_exact_call(&sd, N32, X);  // (exec-masked call, skipped when no lane is near)
     return j;
   };
   auto local = [&](int32_t sl) { return (uint32_t)(min(max(sl, own_lo), own_hi) - own_lo); };

@@ -274,9 +274,7 @@ __global__ __launch_bounds__(kRsBlock, IT <= 4 ? 8 : 1) void k_rank_ab(RankABArg
     const double fr = v - fl;
     int32_t j = (int32_t)fl + 1;
     const bool near = fabs(fr - 0.5) >= hw;
-    if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)
-      if (near) j = sys_count_exact_call(&sd, N, X);
-    }
+    if (near) j = sys_count_exact_call(&sd, N, X);  // (exec-masked call, skipped when no lane is near)
     return j;
   };
   auto local = [&](int32_t s) {  // clamp to [own_lo, own_hi), local index
