@@ -24,6 +24,7 @@ STATUS = {
 }
 
 FAMILY_LGSSM, FAMILY_HMM, FAMILY_KITAGAWA, FAMILY_REGRESSION, FAMILY_SLOTS = 1, 2, 3, 4, 5
+SLOT_INPUT = -1  # gh_obs.slot of a step's latent input (GH_SLOT_INPUT)
 RESAMPLE_SYSTEMATIC, RESAMPLE_MULTINOMIAL = 0, 1
 PROPOSAL_DEFAULT, PROPOSAL_OPTIMAL, PROPOSAL_GAUSSIAN, PROPOSAL_LINEAR = 0, 1, 2, 3
 

@@ -603,10 +603,12 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
   if (!slots_supported(d)) return "slots: latent dimension d must be in 1..16";
   if (np < 2) return "slots: need the latent form and the slot count";
   SlotParams& sp = m->slots;
-  sp.lat = (int)p[0];
+  const int form = (int)p[0];
+  sp.lat = form == GH_SLOT_LAT_AFFINE_INPUT ? SLOT_LAT_AFFINE : form;
+  const bool inputs = form == GH_SLOT_LAT_AFFINE_INPUT;
   sp.K = (int)p[1];
-  if (p[0] != sp.lat || (sp.lat != SLOT_LAT_AFFINE && sp.lat != SLOT_LAT_KITAGAWA))
-    return "slots: latent form must be 0 (affine mvnormal) or 1 (Kitagawa)";
+  if (p[0] != form || (form != SLOT_LAT_AFFINE && form != SLOT_LAT_KITAGAWA && !inputs))
+    return "slots: latent form must be 0 (affine mvnormal), 1 (Kitagawa) or 2 (affine with per-step inputs)";
   if (sp.lat == SLOT_LAT_KITAGAWA && d != 1) return "slots: the Kitagawa latent has d = 1";
   if (p[1] != sp.K || sp.K < 1 || sp.K > kMaxSlots) return "slots: 1..4 observed slots";
   int64_t i = 2 + 3 * (int64_t)sp.K;
@@ -642,9 +644,12 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
     voff += nv;
     yoff += dist == SLOT_MVNORMAL ? mm : 1;
   }
-  if (voff > kMaxObs || yoff > kMaxObs) return "slots: more than 32 observed values per step";
+  if (voff + (inputs ? d : 0) > kMaxObs || yoff > kMaxObs)
+    return "slots: more than 32 observed values (and inputs) per step";
   m->dy = yoff;
   sp.nv = voff;
+  sp.uoff = inputs ? voff : -1;
+  sp.qoff = voff + (inputs ? d : 0);
   // latent block
   off[0] = (int64_t)h.size();
   if (sp.lat == SLOT_LAT_AFFINE) {
@@ -944,10 +949,23 @@ extern "C" int gh_model_state_dim(const gh_model* m, int* d) {
 static int make_obs_slots(const gh_model* m, const gh_obs* in, StepObs* o) {
   const SlotParams& sp = m->slots;
   int n = 0;
+  bool has_input = false;
   for (const gh_obs* e = in; e; e = e->next) {
-    if (++n > kMaxSlots) return set_err(GH_E_INVAL, "slots: more than %d observations in one step", kMaxSlots);
+    if (++n > kMaxSlots + 1)
+      return set_err(GH_E_INVAL, "slots: more than %d observations (and an input) in one step", kMaxSlots);
     if (!e->present || !e->values) continue;
     const int k = e->slot;
+    if (k == GH_SLOT_INPUT) {  // the step's latent input u_t (an Unfold argument, not a choice)
+      if (sp.uoff < 0) return set_err(GH_E_INVAL, "slots: a step input for a model without inputs (latent form 2)");
+      if (has_input) return set_err(GH_E_INVAL, "slots: two inputs in one step");
+      if (e->n_values != m->d) return set_err(GH_E_INVAL, "slots: the input has d = %d values, got %d", m->d, e->n_values);
+      for (int j = 0; j < m->d; ++j) {
+        if (!std::isfinite(e->values[j])) return set_err(GH_E_INVAL, "slots: non-finite input");
+        o->v[sp.uoff + j] = e->values[j];
+      }
+      has_input = true;
+      continue;
+    }
     if (k < 0 || k >= sp.K) return set_err(GH_E_INVAL, "slots: observation for slot %d (the model has %d)", k, sp.K);
     if ((o->present >> k) & 1)
       return set_err(GH_E_DISCARD, "slots: slot %d constrained twice in one step", k);  // (particle_filter.jl:168-170)
@@ -1030,7 +1048,7 @@ static int make_obs_gauss(const gh_model* m, int t, const gh_obs* in, const doub
 // the observation with u_t of the linear proposal behind it (o.v[dy + i])
 static int make_obs_lin(const gh_model* m, int t, const gh_obs* in, const double* u, StepObs* o) {
   CHECK(make_obs(m, t, in, o));
-  const int at = m->family == GH_FAMILY_SLOTS ? m->slots.nv : m->dy;
+  const int at = m->family == GH_FAMILY_SLOTS ? m->slots.qoff : m->dy;
   for (int i = 0; i < m->d; ++i) o->v[at + i] = u[i];
   return GH_OK;
 }
@@ -1075,7 +1093,7 @@ static bool proposal_ok(const gh_model* m, int proposal) {
   if (proposal == GH_PROPOSAL_GAUSSIAN) return m->family == GH_FAMILY_KITAGAWA;
   if (proposal == GH_PROPOSAL_LINEAR)  // (u_t follows the step's observed values)
     return (m->family == GH_FAMILY_LGSSM && m->d + m->dy <= kMaxObs) ||
-           (m->family == GH_FAMILY_SLOTS && m->d + m->slots.nv <= kMaxObs);
+           (m->family == GH_FAMILY_SLOTS && m->d + m->slots.qoff <= kMaxObs);
   if (proposal != GH_PROPOSAL_OPTIMAL) return false;
   return m->family == GH_FAMILY_HMM || (m->family == GH_FAMILY_LGSSM && m->lg_opt);
 }
@@ -2068,7 +2086,7 @@ static const gh_obs* slot_chain(const std::vector<double>& r, gh_obs* chain) {
 // the same slot layout (a parameter change keeps every address and its form)
 static bool same_slots(const gh_model* a, const gh_model* b) {
   const SlotParams &p = a->slots, &q = b->slots;
-  if (p.lat != q.lat || p.K != q.K) return false;
+  if (p.lat != q.lat || p.K != q.K || (p.uoff >= 0) != (q.uoff >= 0)) return false;
   for (int k = 0; k < p.K; ++k)
     if (p.dist[k] != q.dist[k] || p.m[k] != q.m[k] || p.link[k] != q.link[k]) return false;
   return true;
@@ -3249,6 +3267,8 @@ extern "C" int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double*
   if (m->family == GH_FAMILY_REGRESSION && T != 1)
     return set_err(GH_E_INVAL, "gh_simulate: the regression model has no time steps (T = 1)");
   if (n < 0 || n > INT32_MAX) return set_err(GH_E_INVAL, "gh_simulate: n = %lld", (long long)n);
+  if (m->family == GH_FAMILY_SLOTS && m->slots.uoff >= 0)
+    return set_err(GH_E_INVAL, "gh_simulate: a slot model with per-step inputs (its inputs are not arguments here)");
   if (n == 0) return GH_OK;
   HIP_TRY(hipSetDevice(m->ctx->device));
   const int d = m->d;

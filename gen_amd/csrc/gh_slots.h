@@ -57,8 +57,10 @@ struct SlotParams {
   double inv2v[kMaxSlots];  // normal 1 / (2 sd^2)
   double sd[kMaxSlots];     // normal sd (simulate)
   int nv;                   // observed values per step in StepObs::v (a poisson slot takes 2)
+  int uoff;                 // the step's latent input u_t (affine latent with inputs) in v[uoff..], or -1
+  int qoff;                 // the linear proposal's mean offset in v[qoff..] (after the input, if any)
   // the linear custom proposal (SlotLinModel): the filter's own buffer,
-  // absolute pointers (not rebased): P d*d | chol(Sigma_q) d*d; u_t in v[nv..]
+  // absolute pointers (not rebased): P d*d | chol(Sigma_q) d*d
   const double* QP;
   const double* QL;
   double cstq;              // -0.5 (d log 2pi + log det Sigma_q)
@@ -165,7 +167,7 @@ struct SlotModel {
       if (t == 1) {
         mean = p.mu0[i];
       } else {
-        mean = p.b[i];
+        mean = p.uoff >= 0 ? p.b[i] + o.v[p.uoff + i] : p.b[i];  // (the step's input u_t: an Unfold argument)
 #pragma unroll
         for (int k = 0; k < D; ++k) mean = fma(p.A[i * D + k], xp[k], mean);
       }
@@ -202,7 +204,7 @@ struct SlotModel {
 #pragma unroll
         for (int k = 0; k <= i; ++k) acc = fma(p.L0[i * D + k], z[k], acc);
       } else {
-        acc = p.b[i];
+        acc = p.uoff >= 0 ? p.b[i] + o.v[p.uoff + i] : p.b[i];
 #pragma unroll
         for (int k = 0; k < D; ++k) acc = fma(p.A[i * D + k], xp[k], acc);
 #pragma unroll
@@ -327,7 +329,7 @@ struct SlotModel {
 // A user-parameterised linear-Gaussian custom proposal for the slot family
 // (GH_PROPOSAL_LINEAR; the LG-SSM's LGLinModel over any slot model):
 // q(x_t | x_{t-1}) = mvnormal(P x_{t-1} + u_t, Sigma_q) (t = 1: mvnormal(u_1,
-// Sigma_q)), u_t per step after the slot values.  The weight is Gen's
+// Sigma_q)), u_t per step after the slot values (and the latent input).  The weight is Gen's
 // custom-proposal weight (particle_filter.jl:79-91,139-154 via
 // trace_translators.jl:775-802): the model's score of the new choices — the
 // latent's logpdf (affine or Kitagawa) and the present slots' — minus q's
@@ -346,7 +348,7 @@ struct SlotLinModel {
   __device__ static double draw(const Params& p, const StepObs& o, const double* xp, const double* z, double* x) {
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      double acc = o.v[p.nv + i];
+      double acc = o.v[p.qoff + i];
       if (xp) {
 #pragma unroll
         for (int k = 0; k < D; ++k) acc = fma(p.QP[i * D + k], xp[k], acc);
@@ -359,7 +361,7 @@ struct SlotLinModel {
     double quad = 0.0;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      double mean = o.v[p.nv + i];
+      double mean = o.v[p.qoff + i];
       if (xp) {
 #pragma unroll
         for (int k = 0; k < D; ++k) mean = fma(p.QP[i * D + k], xp[k], mean);

@@ -360,8 +360,11 @@ class SlotSSM(Model):
             return x
         end
 
-    latent: {"form": "affine", "A", "b", "Q", "mu0", "P0"} or
+    latent: {"form": "affine", "A", "b", "Q", "mu0", "P0"[, "inputs": True]} or
             {"form": "kitagawa", "mu1", "s1", "sd_x"} (d = 1)
+            "inputs": the kernel takes a per-step argument u_t (d values, zero when a
+            step gives none): x_t ~ mvnormal(A x_{t-1} + (b + u_t), Q) — the Unfold's
+            arguments extended by one value per step, new_args = (t, u_t)
     slots:  [{"name", "dist", ...}] with per distribution
             mvnormal: H [m, d], c [m], R [m, m]; normal: h [d], c, sd (or mean "x^2/20", sd);
             poisson / bernoulli: h [d], c; categorical: W [m, d], c [m]
@@ -380,7 +383,9 @@ class SlotSSM(Model):
             f = lambda k, shape: np.asarray(latent[k], dtype=np.float64).reshape(shape)  # noqa: E731
             self.b = f("b", (self.d,)) if "b" in latent else np.zeros(self.d)
             self.Q, self.mu0, self.P0 = f("Q", (self.d, self.d)), f("mu0", (self.d,)), f("P0", (self.d, self.d))
+            self.inputs = bool(latent.get("inputs", False))
         elif form == "kitagawa":
+            self.inputs = False
             self.d = 1
             self.mu1, self.s1, self.sd_x = float(latent["mu1"]), float(latent["s1"]), float(latent["sd_x"])
         else:
@@ -416,7 +421,7 @@ class SlotSSM(Model):
         self.dy = sum(s["m"] if s["dist"] == "mvnormal" else 1 for s in self.slots)
 
     def params(self):
-        p = [0.0 if self.form == "affine" else 1.0, float(len(self.slots))]
+        p = [(2.0 if self.inputs else 0.0) if self.form == "affine" else 1.0, float(len(self.slots))]
         for s in self.slots:
             p += [float(_SLOT_DIST[s["dist"]]), float(s["m"]), float(_LINK[s["link"]])]
         if self.form == "affine":
@@ -457,14 +462,19 @@ class SlotSSM(Model):
             return {self.names[0]: value}
         raise ValueError("a slot model's observation is a {slot name: value} dict")
 
-    def gh_obs(self, value):
-        """The gh_obs chain of one step's observation (slot ids in model order)."""
-        vals = self._slot_dict(value)
+    def gh_obs(self, value, u=None):
+        """The gh_obs chain of one step's observation (slot ids in model order),
+        and the step's input u_t (an entry with slot GH_SLOT_INPUT) if given."""
+        vals = {} if value is None else self._slot_dict(value)
         present = [(k, np.ascontiguousarray(np.atleast_1d(np.asarray(vals[n], dtype=np.float64)).ravel()))
                    for k, n in enumerate(self.names) if n in vals and vals[n] is not None]
         unknown = set(vals) - set(self.names)
         if unknown:
             raise _lib.GenHipError(1, f"no slot named {sorted(unknown)}")
+        if u is not None:
+            if not self.inputs:
+                raise _lib.GenHipError(1, "this slot model takes no per-step input (latent 'inputs': True)")
+            present.append((_lib.SLOT_INPUT, np.ascontiguousarray(np.asarray(u, dtype=np.float64).reshape(self.d))))
         chain = (_lib.Obs * max(1, len(present)))()
         for i, (k, arr) in enumerate(present):
             chain[i] = _lib.Obs(_lib.dptr(arr), arr.size, 1, k, 0, None)
@@ -472,8 +482,8 @@ class SlotSSM(Model):
             chain[i].next = ctypes.pointer(chain[i + 1])
         if not present:
             chain[0] = _lib.Obs(None, 0, 0, 0, 0, None)
-        keep = {self.names[k]: arr for k, arr in present}
-        return chain[0], (chain, keep)
+        keep = {self.names[k]: arr for k, arr in present if k >= 0}
+        return chain[0], (chain, keep, [arr for k, arr in present if k < 0])
 
     # ---- host-side reference densities (numpy / closed forms; the tests' pins)
     def _mean_param(self, s, x):
@@ -506,14 +516,17 @@ class SlotSSM(Model):
             return float(np.log(mp) if y else np.log(1.0 - mp))
         return float(np.log(mp[int(y)]))
 
-    def simulate(self, T: int, rng: np.random.Generator):
-        """Draw (xs [T, d], ys [T] of {slot name: value}) from the model (numpy RNG; synthetic data only)."""
+    def simulate(self, T: int, rng: np.random.Generator, inputs=None):
+        """Draw (xs [T, d], ys [T] of {slot name: value}) from the model (numpy
+        RNG; synthetic data only); inputs [T, d]: the per-step inputs u_t of a
+        model with inputs (row t - 1 for step t; row 0 unused)."""
         xs = np.zeros((T, self.d))
         ys = []
         for t in range(1, T + 1):
             if self.form == "affine":
+                u = np.zeros(self.d) if inputs is None or t == 1 else np.asarray(inputs[t - 1], dtype=np.float64)
                 x = (rng.multivariate_normal(self.mu0, self.P0) if t == 1 else
-                     rng.multivariate_normal(self.A @ xs[t - 2] + self.b, self.Q))
+                     rng.multivariate_normal(self.A @ xs[t - 2] + (self.b + u), self.Q))
             else:
                 v = xs[t - 2, 0]
                 x = np.array([rng.normal(self.mu1, self.s1) if t == 1 else

@@ -181,8 +181,9 @@ def set_default_context(ctx: Context) -> None:
 
 
 # ------------------------------------------------------------- observations
-def _step_obs(model: Model, t: int, observations) -> tuple[_lib.Obs, np.ndarray | None]:
-    """The gh_obs of step t from a ChoiceMap / dict / array / None."""
+def _step_obs(model: Model, t: int, observations, u=None) -> tuple[_lib.Obs, np.ndarray | None]:
+    """The gh_obs of step t from a ChoiceMap / dict / array / None (and a slot
+    model's per-step input u_t)."""
     val = None
     if observations is None:
         val = None
@@ -191,6 +192,8 @@ def _step_obs(model: Model, t: int, observations) -> tuple[_lib.Obs, np.ndarray 
         val = model.obs_from_choicemap(cm, t)
     else:
         val = observations
+    if u is not None:
+        return model.gh_obs(val, u)  # (a slot model with inputs: the chain with an input entry)
     if val is None:
         return _lib.Obs(None, 0, 0, 0, 0, None), None
     return model.gh_obs(val)  # (a slot model: the chain of its constrained addresses)
@@ -511,7 +514,10 @@ def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: 
     Unfold by one step; new_args = (t, model') also changes the Unfold's
     parameters to those of model' (the same family and dimensions) with an
     UnknownChange() argdiff for them: every retained kernel application is
-    re-scored (gh_pf_step_params), as the Unfold's update does."""
+    re-scored (gh_pf_step_params), as the Unfold's update does.  A slot model
+    with per-step inputs takes new_args = (t, u_t) or (t, model', u_t): the
+    Unfold's argument vector extended by one value (earlier steps keep theirs,
+    so nothing is re-scored for it)."""
     t = state.t + 1
     new_args = tuple(new_args)
     argdiffs = tuple(argdiffs)
@@ -519,6 +525,11 @@ def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: 
         raise _lib.GenHipError(1, f"new_args must extend the Unfold by one step: expected ({t}, ...), got {new_args}")
     if argdiffs and not isinstance(argdiffs[0], UnknownChange):
         raise _lib.GenHipError(1, "the length argument changes: its argdiff must be UnknownChange()")
+    u = None
+    if getattr(state.model, "inputs", False) and len(new_args) >= 2 and not isinstance(new_args[-1], Model):
+        u = new_args[-1]  # (t, u_t) / (t, model', u_t)
+        new_args = new_args[:-1]
+        argdiffs = argdiffs[:len(new_args)]
     if len(new_args) > 2:
         raise _lib.GenHipError(1, "new_args = (t,) or (t, model with the new parameters)")
     new_model = new_args[1] if len(new_args) == 2 else None
@@ -528,7 +539,7 @@ def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: 
             raise _lib.GenHipError(1, "the parameters differ from the filter's but their argdiff is NoChange()")
         if type(new_model) is not type(state.model):
             raise _lib.GenHipError(1, "new parameters of another model family")
-        obs, keep = _step_obs(new_model, t, observations)
+        obs, keep = _step_obs(new_model, t, observations, u)
         if proposal_args:
             raise _lib.GenHipError(1, "a parameter change takes the proposal's stored arguments")
         mh = state.ctx.model_handle(new_model)
@@ -536,7 +547,7 @@ def particle_filter_step(state: ParticleFilterState, new_args: tuple, argdiffs: 
         state.model = new_model
         state._log_obs(t, keep)
         return
-    obs, keep = _step_obs(state.model, t, observations)
+    obs, keep = _step_obs(state.model, t, observations, u)
     qa, nq = _qargs(proposal, proposal_args)
     _lib.check(_lib.load().gh_pf_step_q(state.h, byref(obs), _proposal_code(proposal),
                                         _lib.dptr(qa) if qa is not None else None, nq))
@@ -562,9 +573,13 @@ class ObservationBatch:
     """The gh_obs array of several consecutive steps, built once (the host-side
     marshalling of run_particle_filter, done ahead of a timed loop)."""
 
-    def __init__(self, model: Model, observations_per_step):
-        built = [(_lib.Obs(None, 0, 0, 0, 0, None), None) if v is None else model.gh_obs(v)
-                 for v in observations_per_step]
+    def __init__(self, model: Model, observations_per_step, inputs_per_step=None):
+        ins = [None] * len(observations_per_step) if inputs_per_step is None else list(inputs_per_step)
+        if len(ins) != len(observations_per_step):
+            raise ValueError("one input per step")
+        built = [(_lib.Obs(None, 0, 0, 0, 0, None), None) if v is None and u is None
+                 else (model.gh_obs(v, u) if u is not None else model.gh_obs(v))
+                 for v, u in zip(observations_per_step, ins)]
         self.values = [keep for _, keep in built]  # (kept alive with the array: the gh_obs point into them)
         self.arr = (_lib.Obs * max(1, len(self.values)))()
         for i, (o, _) in enumerate(built):
@@ -574,18 +589,21 @@ class ObservationBatch:
         return len(self.values)
 
 
-def prepare_observations(model: Model, observations_per_step) -> ObservationBatch:
-    return ObservationBatch(model, observations_per_step)
+def prepare_observations(model: Model, observations_per_step, inputs_per_step=None) -> ObservationBatch:
+    return ObservationBatch(model, observations_per_step, inputs_per_step)
 
 
 def run_particle_filter(state: ParticleFilterState, observations_per_step, ess_threshold: float | None = None,
-                        proposal=None, proposal_args: tuple | None = None) -> None:
+                        proposal=None, proposal_args: tuple | None = None, inputs_per_step=None) -> None:
     """The reference caller loop {maybe_resample!; particle_filter_step!} over
     the given per-step observations (arrays or None, or an ObservationBatch of
     them), enqueued without host sync.  A proposal with arguments uses
-    proposal_args, or the last ones given."""
+    proposal_args, or the last ones given.  inputs_per_step: a slot model's
+    per-step inputs u_t (None entries: no input)."""
     model = state.model
     if isinstance(observations_per_step, ObservationBatch):
+        if inputs_per_step is not None:
+            raise ValueError("run_particle_filter: inputs with a prepared ObservationBatch (prepare them with it)")
         if proposal_args is not None:
             raise ValueError("run_particle_filter: proposal_args with a prepared ObservationBatch; pass the "
                              "observations as a list (its first step takes the arguments) or set them with a "
@@ -596,10 +614,14 @@ def run_particle_filter(state: ParticleFilterState, observations_per_step, ess_t
             qa, nq = _qargs(proposal, proposal_args)
             if qa is not None:  # store them (the library keeps the last arguments)
                 maybe_resample_async(state, ess_threshold)
-                particle_filter_step(state, (state.t + 1,), (UnknownChange(),), observations_per_step[0], proposal,
-                                     proposal_args)
+                u0 = None if inputs_per_step is None else inputs_per_step[0]
+                particle_filter_step(state, (state.t + 1,) + (() if u0 is None else (u0,)),
+                                     (UnknownChange(),) * (1 if u0 is None else 2), observations_per_step[0],
+                                     proposal, proposal_args)
                 observations_per_step = list(observations_per_step)[1:]
-        batch = ObservationBatch(model, observations_per_step)
+                if inputs_per_step is not None:
+                    inputs_per_step = list(inputs_per_step)[1:]
+        batch = ObservationBatch(model, observations_per_step, inputs_per_step)
     t0 = state.t
     thr = state.num_particles / 2 if ess_threshold is None else float(ess_threshold)
     _lib.check(_lib.load().gh_pf_run(state.h, len(batch), batch.arr, _proposal_code(proposal), thr))

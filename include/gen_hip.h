@@ -99,6 +99,12 @@ typedef enum {
        params = [lat, K, (dist_k, m_k, link_k) for k < K, latent block, slot blocks]
      latent block, lat = GH_SLOT_LAT_AFFINE (0):   A[d*d] b[d] Q[d*d] mu0[d] P0[d*d]
          x_1 ~ mvnormal(mu0, P0); x_t ~ mvnormal(A x_{t-1} + b, Q)
+                   lat = GH_SLOT_LAT_AFFINE_INPUT (2): the same block, and
+         x_t ~ mvnormal(A x_{t-1} + (b + u_t), Q) with u_t the step's input (a
+         gh_obs entry with slot GH_SLOT_INPUT and d values; zero when a step
+         gives none): the Unfold's kernel arguments extended by one value per
+         step, new_args = (t, u_t) (no re-scoring: earlier steps keep theirs);
+         gh_simulate refuses such a model
                    lat = GH_SLOT_LAT_KITAGAWA (1), d = 1: mu1 s1 sd_x
          x_1 ~ normal(mu1, s1); x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)
      slot blocks (m_k values of the slot; its value rows in simulate's output
@@ -118,7 +124,10 @@ typedef enum {
   GH_FAMILY_SLOTS = 5
 } gh_family;
 
-enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1 };
+enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1, GH_SLOT_LAT_AFFINE_INPUT = 2 };
+/* gh_obs.slot of a step's latent input u_t (latent form 2): d values, an
+   argument of the step's kernel application, not a choice */
+enum { GH_SLOT_INPUT = -1 };
 enum { GH_SLOT_MVNORMAL = 1, GH_SLOT_NORMAL = 2, GH_SLOT_POISSON = 3, GH_SLOT_BERNOULLI = 4, GH_SLOT_CATEGORICAL = 5 };
 enum { GH_LINK_AFFINE = 0, GH_LINK_KITAGAWA = 1, GH_LINK_EXP = 2, GH_LINK_LOGISTIC = 3, GH_LINK_SOFTMAX = 4 };
 

@@ -342,7 +342,7 @@ typedef struct {
      distribution, value count, mean form, offsets in obs_t.bt and in the
      observation vector, parameter block (mvnormal M = L_R^-1 H | H | c | L_R;
      normal / poisson / bernoulli h | c; categorical W | c) and constants */
-  int lat, K, sdist[4], sm[4], slink[4], svoff[4], syoff[4], snv;
+  int lat, K, sdist[4], sm[4], slink[4], svoff[4], syoff[4], snv, uin;  /* uin: per-step latent inputs (form 2) */
   double* sP[4];
   double scst[4], sinv2v[4], ssd[4];
 } model_t;
@@ -466,7 +466,9 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     /* include/gen_hip.h GH_FAMILY_SLOTS (the engine's slots_build, same checks) */
     if (d < 1 || d > 16 || np < 2) return -1;
     m->lat = (int)p[0]; m->K = (int)p[1];
-    if ((double)m->lat != p[0] || (m->lat != 0 && m->lat != 1) || (m->lat == 1 && d != 1)) return -1;
+    if ((double)m->lat != p[0] || m->lat < 0 || m->lat > 2 || (m->lat == 1 && d != 1)) return -1;
+    m->uin = m->lat == 2;  /* affine with per-step inputs: x_t ~ mvnormal(A x + (b + u_t), Q) */
+    if (m->uin) m->lat = 0;
     if ((double)m->K != p[1] || m->K < 1 || m->K > 4) return -1;
     int64_t i = 2 + 3 * (int64_t)m->K;
     if (np < i) return -1;
@@ -485,9 +487,9 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
       m->svoff[k] = voff; m->syoff[k] = yoff;
       voff += nv; yoff += dist == 1 ? mm : 1;
     }
-    if (voff > 32 || yoff > 32) return -1;
+    if (voff + (m->uin ? d : 0) > 32 || yoff > 32) return -1;
     m->dy = yoff;
-    m->snv = voff;  /* (the linear proposal's u_t follows these values on the device) */
+    m->snv = voff;  /* (the input, then the linear proposal's u_t, follow these values on the device) */
     if (m->lat == 0) {
       int64_t need = 3 * (int64_t)d * d + 2 * (int64_t)d;
       if (np < i + need) return -1;
@@ -587,10 +589,15 @@ static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* 
   o->ct = 0.0;
   o->nraw = 0;
   if (m->family == ORC_KITAGAWA || (m->family == ORC_SLOTS && m->lat == 1)) o->ct = 8.0 * orc_cos(1.2 * (double)t);
+  if (m->family == ORC_SLOTS && m->uin)
+    for (int i = 0; i < m->d; ++i) o->bt[m->snv + i] = 0.0;  /* no input given: u_t = 0 */
   if (!has) return;
   if (m->family == ORC_SLOTS) {  /* (the engine's make_obs_slots) */
-    o->nraw = m->dy;
-    for (int i = 0; i < m->dy; ++i) o->raw[i] = y[i];
+    const int inp = m->uin && ((has >> 4) & 1);  /* bit 4: the step's input follows the dy values */
+    o->nraw = m->dy + (inp ? m->d : 0);
+    for (int i = 0; i < o->nraw; ++i) o->raw[i] = y[i];
+    if (inp)
+      for (int i = 0; i < m->d; ++i) o->bt[m->snv + i] = y[m->dy + i];
     for (int k = 0; k < m->K; ++k) {
       if (!((has >> k) & 1)) continue;
       const double* yk = y + m->syoff[k];
@@ -833,7 +840,7 @@ static void slot_latent(const model_t* m, uint64_t seed, uint64_t pid, uint32_t 
       acc = m->mu0[i];
       for (int k = 0; k <= i; ++k) acc = fma(m->L0[i * d + k], z[k], acc);
     } else {
-      acc = m->b[i];
+      acc = m->uin ? m->b[i] + o->bt[m->snv + i] : m->b[i];
       for (int k = 0; k < d; ++k) acc = fma(m->A[i * d + k], xp[k], acc);
       for (int k = 0; k <= i; ++k) acc = fma(m->LQ[i * d + k], z[k], acc);
     }
@@ -1149,7 +1156,8 @@ static int proposal_ok(const model_t* m, int proposal) {
   if (proposal == 0) return 1;
   if (proposal == ORC_PROPOSAL_GAUSSIAN) return m->family == ORC_KITAGAWA && m->qa[3] > 0.0;
   if (proposal == ORC_PROPOSAL_LINEAR)
-    return m->qlin && ((m->family == ORC_LGSSM && m->d + m->dy <= 32) || (m->family == ORC_SLOTS && m->d + m->snv <= 32));
+    return m->qlin && ((m->family == ORC_LGSSM && m->d + m->dy <= 32) ||
+                       (m->family == ORC_SLOTS && m->d + m->snv + (m->uin ? m->d : 0) <= 32));
   return proposal == ORC_PROPOSAL_OPTIMAL && (m->family == ORC_HMM || (m->family == ORC_LGSSM && m->opt));
 }
 int orc_pf_set_proposal_args(orc_pf* pf, const double* args, int n) {
@@ -1548,7 +1556,7 @@ static void model_score(const model_t* m, const obs_t* o, int t, const double* x
       if (t == 1) {
         mean = m->mu0[i];
       } else {
-        mean = m->b[i];
+        mean = m->uin ? m->b[i] + o->bt[m->snv + i] : m->b[i];
         for (int k = 0; k < d; ++k) mean = fma(m->A[i * d + k], xp[k], mean);
       }
       double r = x[i] - mean;
@@ -1656,7 +1664,7 @@ int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const doubl
     return -1;
   }
   if (m->family == ORC_SLOTS) {  /* the same latent form and slot layout (the engine's same_slots) */
-    int same = m2.lat == m->lat && m2.K == m->K;
+    int same = m2.lat == m->lat && m2.K == m->K && m2.uin == m->uin;
     for (int k = 0; same && k < m->K; ++k)
       same = m2.sdist[k] == m->sdist[k] && m2.sm[k] == m->sm[k] && m2.slink[k] == m->slink[k];
     if (!same) {
@@ -1705,7 +1713,8 @@ int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const doubl
 int orc_simulate(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T, int64_t n,
                  uint64_t seed, double* xs, double* ys, double* per_step, double* total) {
   model_t m;
-  if (model_build(&m, family, d, dy, k, v, params, np) || T < 1 || (family == ORC_REGRESSION && T != 1)) {
+  if (model_build(&m, family, d, dy, k, v, params, np) || T < 1 || (family == ORC_REGRESSION && T != 1) ||
+      (family == ORC_SLOTS && m.uin)) {  /* (per-step inputs: not simulate's arguments, as gh_simulate) */
     model_free(&m);
     return -1;
   }

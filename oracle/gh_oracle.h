@@ -41,7 +41,9 @@ enum { ORC_LGSSM = 1, ORC_HMM = 2, ORC_KITAGAWA = 3, ORC_REGRESSION = 4,
        /* slot-described Unfold kernel (gen_amd/csrc/gh_slots.h, include/gen_hip.h
           GH_FAMILY_SLOTS): an observation is the slots' values concatenated in
           slot order (m values for an mvnormal slot, one for the others) and
-          has_obs the bitmask of the slots present */
+          has_obs the bitmask of the slots present; with per-step inputs
+          (latent form 2) bit 4 marks the step's input u_t, d values after
+          the dy slot values */
        ORC_SLOTS = 5 };
 enum { ORC_SYSTEMATIC = 0, ORC_MULTINOMIAL = 1 };
 enum { ORC_PROPOSAL_DEFAULT = 0, ORC_PROPOSAL_OPTIMAL = 1, ORC_PROPOSAL_GAUSSIAN = 2, ORC_PROPOSAL_LINEAR = 3 };

@@ -155,9 +155,10 @@ def model_args(model):
 def slot_obs(model, value):
     """A slot model's observation (a {slot name: value} dict) as the oracle
     takes it (gh_oracle.h ORC_SLOTS): the slots' values in slot order (m for
-    an mvnormal slot, one otherwise) and the bitmask of the present slots."""
+    an mvnormal slot, one otherwise) and the bitmask of the present slots; a
+    "__input__" entry is the step's latent input (bit 4, d values after them)."""
     vals = value if isinstance(value, dict) else {model.names[0]: value}
-    vec = np.zeros(max(1, model.dy))
+    vec = np.zeros(max(1, model.dy) + model.d)
     mask, row = 0, 0
     for k, s in enumerate(model.slots):
         rows = s["m"] if s["dist"] == "mvnormal" else 1
@@ -165,6 +166,9 @@ def slot_obs(model, value):
             vec[row:row + rows] = np.atleast_1d(np.asarray(vals[s["name"]], dtype=np.float64)).ravel()
             mask |= 1 << k
         row += rows
+    if vals.get("__input__") is not None:  # a model with per-step inputs: u_t after the dy values, bit 4
+        vec[model.dy:model.dy + model.d] = np.asarray(vals["__input__"], dtype=np.float64).reshape(model.d)
+        mask |= 1 << 4
     return vec, mask
 
 

@@ -63,6 +63,24 @@ def changed_count_model():
          {"name": "kind", "dist": "categorical", "W": [[0.8, 0.0], [0.1, 1.1], [-1.0, 0.7]], "c": [0.1, 0.0, -0.2]}])
 
 
+def count_model_inputs():
+    """count_model() whose kernel takes a per-step input u_t:
+    x_t ~ mvnormal(A x_{t-1} + (b + u_t), Q)."""
+    m = count_model()
+    lat = dict(m.latent)
+    lat["inputs"] = True
+    return gen.SlotSSM(lat, [dict(sl) for sl in count_model().slots])
+
+
+def count_inputs(T=10, seed=11):
+    """Per-step inputs (row t - 1 for step t), some steps without one (None)."""
+    rng = np.random.default_rng(seed)
+    u = [0.4 * rng.standard_normal(2) for _ in range(T)]
+    u[0] = None  # (step 1 has no transition)
+    u[3] = None
+    return u
+
+
 def count_obs(T=10, seed=5):
     """Observations with some slots missing at some steps (and one empty step)."""
     m = count_model()
@@ -248,6 +266,45 @@ def test_oracle_slot_step_params():
                         [{"name": "count", "dist": "poisson", "h": [1.0, 0.5], "c": 0.2}])
     with pytest.raises(ValueError):
         runs[0].step_params(other, {"count": 1.0})
+
+
+def _with_input(y, u):
+    y = dict(y)
+    if u is not None:
+        y["__input__"] = u
+    return y
+
+
+def test_oracle_slot_zero_inputs_are_the_plain_model():
+    """A model with per-step inputs given none (or zeros) filters as the model
+    without inputs, bit for bit; with inputs, each state moves by its step's
+    input (the same normals) and the latent score is mvnormal(A x + b + u, Q)."""
+    from scipy import stats
+
+    m, obs = count_obs()
+    mi = count_model_inputs()
+    a = O.run_pf(m, obs, 400, 7, thr=0.0)
+    b = O.run_pf(mi, obs, 400, 7, thr=0.0)
+    c = O.run_pf(mi, [_with_input(y, np.zeros(2)) for y in obs], 400, 7, thr=0.0)
+    for r in (b, c):
+        assert np.array_equal(a.state(), r.state()) and np.array_equal(a.log_weights(), r.log_weights())
+        for x, y in zip(a.scores(per_step=True), r.scores(per_step=True)):
+            assert np.array_equal(x, y)
+    u = count_inputs()
+    # step 2: x2 = A x1 + (b + u2) + L z with the plain model's normals z
+    pc, pd = O.OraclePF(m, 300, 4), O.OraclePF(mi, 300, 4)
+    pc.init(obs[0])
+    pd.init(obs[0])
+    x1 = pd.state().copy()
+    pc.maybe_resample(0.0)
+    pd.maybe_resample(0.0)
+    pc.step(obs[1])
+    pd.step(_with_input(obs[1], u[1]))
+    np.testing.assert_allclose(pd.state() - pc.state(), np.repeat(u[1][:, None], 300, axis=1), atol=1e-12)
+    _, ps = pd.scores(per_step=True)
+    x2 = pd.state()
+    ref = [stats.multivariate_normal.logpdf(x2[:, i], m.A @ x1[:, i] + m.b + u[1], m.Q) for i in range(300)]
+    np.testing.assert_allclose(ps[1, 0], ref, rtol=1e-12, atol=1e-10)
 
 
 # ------------------------------------------------------------------ GPU
@@ -497,3 +554,54 @@ def test_gpu_slot_conditional_smc_bitexact(gh_ctx, thr):
         assert np.array_equal(st.states(t).T, orc.trajectory(t)), t
     assert np.array_equal(np.stack([st.states(t)[0] for t in range(1, T + 1)]), ref)
     st.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched,linear", [(False, False), (True, False), (False, True)])
+def test_gpu_slot_inputs_bitexact(gh_ctx, batched, linear):
+    """Per-step inputs of a slot model (new_args = (t, u_t); run_particle_filter's
+    inputs_per_step), some steps without one, with the default and the linear
+    custom proposal (whose mean offset follows the input): states, weights,
+    parents and score columns bit-exact against the oracle; an input to a
+    model without inputs and simulate of an input model are refused."""
+    mi = count_model_inputs()
+    _, obs = count_obs()
+    u = count_inputs()
+    n, seed = 4099, 23
+    q = (np.concatenate([(0.6 * mi.A).ravel(), (0.5 * mi.Q).ravel(), [0.1, -0.2]]),) if linear else ()
+    prop = gen.LinearGaussianProposal if linear else None
+    st = gen.initialize_particle_filter(mi, (1,), _obs_at(mi, obs[0], 1), *((prop, q) if linear else ()), n,
+                                        seed=seed)
+    orc = O.OraclePF(mi, n, seed)
+    if linear:
+        orc.set_proposal_args(q[0])
+    orc.init(obs[0], O.LINEAR if linear else O.DEFAULT)
+    if batched:
+        gen.run_particle_filter(st, list(obs[1:]), None, inputs_per_step=u[1:])
+        for t in range(2, len(obs) + 1):
+            orc.maybe_resample(None)
+            orc.step(_with_input(obs[t - 1], u[t - 1]))
+    else:
+        for t in range(2, len(obs) + 1):
+            assert gen.maybe_resample(st, None) == orc.maybe_resample(None)[0]
+            na = (t,) if u[t - 1] is None else (t, u[t - 1])
+            gen.particle_filter_step(st, na, (gen.UnknownChange(),) * len(na), _obs_at(mi, obs[t - 1], t),
+                                     *((prop, ()) if linear else ()))
+            orc.step(_with_input(obs[t - 1], u[t - 1]), O.LINEAR if linear else O.DEFAULT)
+            assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64)), t
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(st.parents, orc.parents())
+    a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+    assert abs(a - b) <= 1e-9 * abs(b)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    st.close()
+    m = count_model()
+    st2 = gen.initialize_particle_filter(m, (1,), _obs_at(m, obs[0], 1), 1000, seed=1)
+    with pytest.raises(gen.GenHipError):  # (the plain model takes no input: new_args[1] must be a model)
+        gen.particle_filter_step(st2, (2, np.zeros(2)), (gen.UnknownChange(),) * 2, _obs_at(m, obs[1], 2))
+    st2.close()
+    with pytest.raises(gen.GenHipError):
+        gen.simulate(mi, (4,), num_traces=10, seed=1)
