@@ -647,7 +647,6 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
   if (voff + (inputs ? d : 0) > kMaxObs || yoff > kMaxObs)
     return "slots: more than 32 observed values (and inputs) per step";
   m->dy = yoff;
-  sp.nv = voff;
   sp.uoff = inputs ? voff : -1;
   sp.qoff = voff + (inputs ? d : 0);
   // latent block

@@ -56,7 +56,7 @@ struct SlotParams {
   double cst[kMaxSlots];    // mvnormal -0.5 (m log 2pi + log det R); normal -0.5 log(2 pi sd^2)
   double inv2v[kMaxSlots];  // normal 1 / (2 sd^2)
   double sd[kMaxSlots];     // normal sd (simulate)
-  int nv;                   // observed values per step in StepObs::v (a poisson slot takes 2)
+  // (the observed values fill StepObs::v[0..voff of the last slot + its count); a poisson slot takes 2)
   int uoff;                 // the step's latent input u_t (affine latent with inputs) in v[uoff..], or -1
   int qoff;                 // the linear proposal's mean offset in v[qoff..] (after the input, if any)
   // the linear custom proposal (SlotLinModel): the filter's own buffer,
