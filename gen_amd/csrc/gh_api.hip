@@ -607,8 +607,11 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
   sp.lat = form == GH_SLOT_LAT_AFFINE_INPUT ? SLOT_LAT_AFFINE : form;
   const bool inputs = form == GH_SLOT_LAT_AFFINE_INPUT;
   sp.K = (int)p[1];
-  if (p[0] != form || (form != SLOT_LAT_AFFINE && form != SLOT_LAT_KITAGAWA && !inputs))
-    return "slots: latent form must be 0 (affine mvnormal), 1 (Kitagawa) or 2 (affine with per-step inputs)";
+  if (p[0] != form || (form != SLOT_LAT_AFFINE && form != SLOT_LAT_KITAGAWA && !inputs &&
+                       form != SLOT_LAT_CATEGORICAL))
+    return "slots: latent form must be 0 (affine mvnormal), 1 (Kitagawa), 2 (affine with per-step inputs) or 3 "
+           "(categorical)";
+  if (form == SLOT_LAT_CATEGORICAL && d < 2) return "slots: a categorical latent has d = K >= 2 classes";
   if (sp.lat == SLOT_LAT_KITAGAWA && d != 1) return "slots: the Kitagawa latent has d = 1";
   if (p[1] != sp.K || sp.K < 1 || sp.K > kMaxSlots) return "slots: 1..4 observed slots";
   int64_t i = 2 + 3 * (int64_t)sp.K;
@@ -665,6 +668,13 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
     h.insert(h.end(), L0.begin(), L0.end());
     sp.cstQ = gauss_cst(d, LQ.data());
     sp.cst0 = gauss_cst(d, L0.data());
+    i += need;
+  } else if (sp.lat == SLOT_LAT_CATEGORICAL) {
+    const int64_t need = (int64_t)d + (int64_t)d * d;
+    if (np < i + need) return "slots: too few parameters (categorical latent: prior[K] T[K*K])";
+    for (int64_t j = 0; j < need; ++j)
+      if (!(p[i + j] >= 0.0) || !std::isfinite(p[i + j])) return "slots: categorical latent probabilities must be >= 0";
+    h.insert(h.end(), p + i, p + i + need);  // prior | T (T[new*K + prev], as the HMM family)
     i += need;
   } else {
     if (np < i + 3) return "slots: too few parameters (Kitagawa latent: mu1 s1 sd_x)";
@@ -921,6 +931,8 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     sp.LQ = sp.lat == SLOT_LAT_AFFINE ? q + d * d + d : q;
     sp.mu0 = sp.lat == SLOT_LAT_AFFINE ? q + 2 * d * d + d : q;
     sp.L0 = sp.lat == SLOT_LAT_AFFINE ? q + 2 * d * d + 2 * d : q;
+    sp.cprior = q;
+    sp.cT = sp.lat == SLOT_LAT_CATEGORICAL ? q + d : q;
     for (int k = 0; k < kMaxSlots; ++k) sp.P[k] = m->dparams + (k < sp.K ? slot_off[5 + k] : 0);
   }
   *out = m;
@@ -1092,7 +1104,7 @@ static bool proposal_ok(const gh_model* m, int proposal) {
   if (proposal == GH_PROPOSAL_GAUSSIAN) return m->family == GH_FAMILY_KITAGAWA;
   if (proposal == GH_PROPOSAL_LINEAR)  // (u_t follows the step's observed values)
     return (m->family == GH_FAMILY_LGSSM && m->d + m->dy <= kMaxObs) ||
-           (m->family == GH_FAMILY_SLOTS && m->d + m->slots.qoff <= kMaxObs);
+           (m->family == GH_FAMILY_SLOTS && m->slots.lat != SLOT_LAT_CATEGORICAL && m->d + m->slots.qoff <= kMaxObs);
   if (proposal != GH_PROPOSAL_OPTIMAL) return false;
   return m->family == GH_FAMILY_HMM || (m->family == GH_FAMILY_LGSSM && m->lg_opt);
 }
@@ -3613,8 +3625,9 @@ extern "C" int gh_pf_mh_select(gh_pf* pf, uint32_t selection, int n_moves, int64
 extern "C" int gh_pf_mh_drift(gh_pf* pf, uint32_t selection, const double* sd, int n_moves, int64_t* accepted) {
   if (!pf || !sd) return set_err(GH_E_INVAL, "gh_pf_mh_drift: null argument");
   if (n_moves < 0) return set_err(GH_E_INVAL, "gh_pf_mh_drift: n_moves < 0");
-  if (pf->m->family == GH_FAMILY_HMM)
-    return set_err(GH_E_INVAL, "gh_pf_mh_drift: a Gaussian drift needs a continuous latent (not the HMM)");
+  if (pf->m->family == GH_FAMILY_HMM ||
+      (pf->m->family == GH_FAMILY_SLOTS && pf->m->slots.lat == SLOT_LAT_CATEGORICAL))
+    return set_err(GH_E_INVAL, "gh_pf_mh_drift: a Gaussian drift needs a continuous latent (not a categorical one)");
   if (selection == 0 || (selection & ~latent_addresses(pf->m)) != 0)
     return set_err(GH_E_INVAL, "gh_pf_mh_drift: selection 0x%x names no latent address of this step (valid: 0x%x)",
                    selection, latent_addresses(pf->m));

@@ -9,6 +9,7 @@
 // choice adds its logpdf to the weight, every unconstrained one is drawn):
 //
 //   latent   x_t ~ mvnormal(A x_{t-1} + b, Q)      (x_1 ~ mvnormal(mu0, P0))
+//         or z_t ~ categorical(T[:, z_{t-1}])       (z_1 ~ categorical(prior); stored one-hot, d = K)
 //         or x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)   (d = 1;
 //            x_1 ~ normal(mu1, s1)) — examples/pmmh/model.jl:9-13
 //   slots    mvnormal(H x + c, R)                         mvnormal.jl:12-16
@@ -38,12 +39,15 @@ constexpr uint32_t kSlotSimDraws = 32;  // simulate(): slot k draws from kSimObs
 
 enum SlotDist : int { SLOT_MVNORMAL = 1, SLOT_NORMAL = 2, SLOT_POISSON = 3, SLOT_BERNOULLI = 4, SLOT_CATEGORICAL = 5 };
 enum SlotLink : int { LINK_AFFINE = 0, LINK_KITAGAWA = 1, LINK_EXP = 2, LINK_LOGISTIC = 3, LINK_SOFTMAX = 4 };
-enum SlotLatent : int { SLOT_LAT_AFFINE = 0, SLOT_LAT_KITAGAWA = 1 };
+// (latent form 2 — affine with per-step inputs — is SLOT_LAT_AFFINE with uoff >= 0)
+enum SlotLatent : int { SLOT_LAT_AFFINE = 0, SLOT_LAT_KITAGAWA = 1, SLOT_LAT_CATEGORICAL = 3 };
 
 struct SlotParams {
   const double* base;
   // affine latent: A | b | chol(Q) | mu0 | chol(P0) in the device buffer
   const double *A, *b, *LQ, *mu0, *L0;
+  // categorical latent (K = d classes, one-hot state): prior[K] | T[K*K], T[new*K + prev]
+  const double *cprior, *cT;
   double cstQ, cst0;  // their log-normalisers (score columns)
   KitParams kit;      // Kitagawa latent (mu1, s1, sx, inv2vx, cstx, inv2v1, cst1)
   int lat, K;
@@ -71,6 +75,8 @@ struct SlotParams {
     q.LQ = rebased(*this, prm, LQ);
     q.mu0 = rebased(*this, prm, mu0);
     q.L0 = rebased(*this, prm, L0);
+    q.cprior = rebased(*this, prm, cprior);
+    q.cT = rebased(*this, prm, cT);
 #pragma unroll
     for (int k = 0; k < kMaxSlots; ++k) q.P[k] = rebased(*this, prm, P[k]);
     return q;
@@ -89,6 +95,14 @@ struct SlotModel {
 #pragma unroll
     for (int j = 0; j < D; ++j) acc = fma(h[j], x[j], acc);
     return acc;
+  }
+
+  // the class of a one-hot categorical latent
+  __device__ static int onehot(const double* x) {
+    int z = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) z = x[j] != 0.0 ? j : z;
+    return z;
   }
 
   // the logpdf of slot k's value (o.v + voff) at latent x
@@ -148,6 +162,8 @@ struct SlotModel {
   // the latent's logpdf (LGModel<D, 0>::score / KitModel::score forms)
   __device__ static double latent_lpdf(const Params& p, const StepObs& o, uint32_t t, const double* xp,
                                        const double* x) {
+    if (p.lat == SLOT_LAT_CATEGORICAL)  // categorical.jl:10-12: log prior[z] or log T[z | z_prev]
+      return gh_log(t == 1 ? p.cprior[onehot(x)] : p.cT[onehot(x) * D + onehot(xp)]);
     if (p.lat == SLOT_LAT_KITAGAWA) {
       double mean = p.kit.mu1, inv2 = p.kit.inv2v1, cst = p.kit.cst1;
       if (t > 1) {
@@ -189,6 +205,14 @@ struct SlotModel {
   // the latent draw of step t (t = 1: from the initial distribution)
   __device__ static void draw_latent(const Params& p, const StepObs& o, uint64_t seed, uint64_t pid, uint32_t t,
                                      const double* xp, double* x, const Draw& dr) {
+    if (p.lat == SLOT_LAT_CATEGORICAL) {  // inverse-CDF draw (categorical.jl:20-22), as HMMModel's
+      const u32x4 w = rng_block(seed, pid, t, dr.stream, dr.base);
+      const double u = u53(w.x, w.y);
+      const int z = t == 1 ? cat_sample(p.cprior, D, 1, u) : cat_sample(p.cT + onehot(xp), D, D, u);
+#pragma unroll
+      for (int j = 0; j < D; ++j) x[j] = j == z ? 1.0 : 0.0;
+      return;
+    }
     if (p.lat == SLOT_LAT_KITAGAWA) {  // the nonlinear SSM's paired normals (KitModel::znorm)
       const double z = KitModel::znorm(seed, pid, t, dr);
       x[0] = t == 1 ? p.kit.mu1 + p.kit.s1 * z : KitModel::mean(o, xp[0]) + p.kit.sx * z;

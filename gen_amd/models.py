@@ -65,6 +65,14 @@ class Model:
                 )
         return cm.get(addr)
 
+    def latent_value(self, x):
+        """A latent state row as its choice value (get_choices)."""
+        return float(x[0]) if x.size == 1 else x.copy()
+
+    def latent_column(self, col):
+        """Latent rows [n, d] as the choice values of n traces (trace[addr])."""
+        return col[:, 0] if col.shape[1] == 1 else col
+
     def obs_values(self, value) -> np.ndarray:
         return np.ascontiguousarray(np.atleast_1d(np.asarray(value, dtype=np.float64)).ravel())
 
@@ -361,7 +369,10 @@ class SlotSSM(Model):
         end
 
     latent: {"form": "affine", "A", "b", "Q", "mu0", "P0"[, "inputs": True]} or
-            {"form": "kitagawa", "mu1", "s1", "sd_x"} (d = 1)
+            {"form": "kitagawa", "mu1", "s1", "sd_x"} (d = 1) or
+            {"form": "categorical", "prior" [K], "T" [K, K] (T[new, prev])}: z_t ~
+            categorical(T[:, z_{t-1}]); the engine keeps z one-hot (d = K), so a
+            slot's affine mean h.x + c is h[z] + c — per-class parameters
             "inputs": the kernel takes a per-step argument u_t (d values, zero when a
             step gives none): x_t ~ mvnormal(A x_{t-1} + (b + u_t), Q) — the Unfold's
             arguments extended by one value per step, new_args = (t, u_t)
@@ -384,12 +395,17 @@ class SlotSSM(Model):
             self.b = f("b", (self.d,)) if "b" in latent else np.zeros(self.d)
             self.Q, self.mu0, self.P0 = f("Q", (self.d, self.d)), f("mu0", (self.d,)), f("P0", (self.d, self.d))
             self.inputs = bool(latent.get("inputs", False))
+        elif form == "categorical":
+            self.inputs = False
+            self.prior = np.asarray(latent["prior"], dtype=np.float64).ravel()
+            self.d = self.prior.size
+            self.T = np.asarray(latent["T"], dtype=np.float64).reshape(self.d, self.d)
         elif form == "kitagawa":
             self.inputs = False
             self.d = 1
             self.mu1, self.s1, self.sd_x = float(latent["mu1"]), float(latent["s1"]), float(latent["sd_x"])
         else:
-            raise ValueError(f"latent form {form!r}: 'affine' or 'kitagawa'")
+            raise ValueError(f"latent form {form!r}: 'affine', 'kitagawa' or 'categorical'")
         self.form = form
         if not 1 <= len(slots) <= 4:
             raise ValueError("1..4 observed slots")
@@ -421,11 +437,14 @@ class SlotSSM(Model):
         self.dy = sum(s["m"] if s["dist"] == "mvnormal" else 1 for s in self.slots)
 
     def params(self):
-        p = [(2.0 if self.inputs else 0.0) if self.form == "affine" else 1.0, float(len(self.slots))]
+        code = {"affine": 2.0 if self.inputs else 0.0, "kitagawa": 1.0, "categorical": 3.0}[self.form]
+        p = [code, float(len(self.slots))]
         for s in self.slots:
             p += [float(_SLOT_DIST[s["dist"]]), float(s["m"]), float(_LINK[s["link"]])]
         if self.form == "affine":
             p += list(self.A.ravel()) + list(self.b) + list(self.Q.ravel()) + list(self.mu0) + list(self.P0.ravel())
+        elif self.form == "categorical":
+            p += list(self.prior) + list(self.T.ravel())
         else:
             p += [self.mu1, self.s1, self.sd_x]
         for s in self.slots:
@@ -485,6 +504,16 @@ class SlotSSM(Model):
         keep = {self.names[k]: arr for k, arr in present if k >= 0}
         return chain[0], (chain, keep, [arr for k, arr in present if k < 0])
 
+    def latent_value(self, x):
+        if self.form == "categorical":  # (the class: Gen's categorical returns an Int; 0-based here)
+            return int(np.argmax(x))
+        return super().latent_value(x)
+
+    def latent_column(self, col):
+        if self.form == "categorical":
+            return np.argmax(col, axis=1)
+        return super().latent_column(col)
+
     # ---- host-side reference densities (numpy / closed forms; the tests' pins)
     def _mean_param(self, s, x):
         x = np.atleast_1d(x)
@@ -527,6 +556,9 @@ class SlotSSM(Model):
                 u = np.zeros(self.d) if inputs is None or t == 1 else np.asarray(inputs[t - 1], dtype=np.float64)
                 x = (rng.multivariate_normal(self.mu0, self.P0) if t == 1 else
                      rng.multivariate_normal(self.A @ xs[t - 2] + (self.b + u), self.Q))
+            elif self.form == "categorical":  # (one-hot, as the engine stores it)
+                pz = self.prior if t == 1 else self.T[:, int(np.argmax(xs[t - 2]))]
+                x = np.eye(self.d)[rng.choice(self.d, p=pz / pz.sum())]
             else:
                 v = xs[t - 2, 0]
                 x = np.array([rng.normal(self.mu1, self.s1) if t == 1 else

@@ -327,8 +327,7 @@ class ParticleTraces:
         self._fresh()
         if t not in self._cache:
             self._cache[t] = self.state.states(t)
-        col = self._cache[t]
-        return col[:, 0] if col.shape[1] == 1 else col
+        return self.state.model.latent_column(self._cache[t])
 
     def __getitem__(self, i):
         return _TraceView(self, int(i))
@@ -398,7 +397,7 @@ class _TraceView:
             return cm
         for t in range(1, st.t + 1):
             x = xs[t - 1]
-            cm[m.latent_address(t)] = float(x[0]) if x.size == 1 else x.copy()
+            cm[m.latent_address(t)] = m.latent_value(x)
             y = st.observations.get(t)
             if isinstance(y, dict):  # a slot model: every constrained slot
                 for name, v in y.items():

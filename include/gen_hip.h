@@ -107,6 +107,10 @@ typedef enum {
          gh_simulate refuses such a model
                    lat = GH_SLOT_LAT_KITAGAWA (1), d = 1: mu1 s1 sd_x
          x_1 ~ normal(mu1, s1); x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)
+                   lat = GH_SLOT_LAT_CATEGORICAL (3), d = K classes (2..16): prior[K] T[K*K]
+         z_1 ~ categorical(prior); z_t ~ categorical(T[:, z_{t-1}]) (T[new*K + prev]);
+         the state is stored one-hot (K values), so a slot's affine mean h.x + c
+         is h[z] + c (per-class parameters); no drift MH, no linear proposal
      slot blocks (m_k values of the slot; its value rows in simulate's output
      follow slot order, one row for a scalar slot):
        GH_SLOT_MVNORMAL, link GH_LINK_AFFINE, m <= 32: H[m*d] c[m] R[m*m]   y ~ mvnormal(H x + c, R)
@@ -124,7 +128,7 @@ typedef enum {
   GH_FAMILY_SLOTS = 5
 } gh_family;
 
-enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1, GH_SLOT_LAT_AFFINE_INPUT = 2 };
+enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1, GH_SLOT_LAT_AFFINE_INPUT = 2, GH_SLOT_LAT_CATEGORICAL = 3 };
 /* gh_obs.slot of a step's latent input u_t (latent form 2): d values, an
    argument of the step's kernel application, not a choice */
 enum { GH_SLOT_INPUT = -1 };

@@ -466,7 +466,8 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     /* include/gen_hip.h GH_FAMILY_SLOTS (the engine's slots_build, same checks) */
     if (d < 1 || d > 16 || np < 2) return -1;
     m->lat = (int)p[0]; m->K = (int)p[1];
-    if ((double)m->lat != p[0] || m->lat < 0 || m->lat > 2 || (m->lat == 1 && d != 1)) return -1;
+    if ((double)m->lat != p[0] || m->lat < 0 || m->lat > 3 || (m->lat == 1 && d != 1) || (m->lat == 3 && d < 2))
+      return -1;
     m->uin = m->lat == 2;  /* affine with per-step inputs: x_t ~ mvnormal(A x + (b + u_t), Q) */
     if (m->uin) m->lat = 0;
     if ((double)m->K != p[1] || m->K < 1 || m->K > 4) return -1;
@@ -503,6 +504,14 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
       if (chol(d, P0, m->L0)) return -2;
       m->cstQ = gauss_cst(d, m->LQ);
       m->cst0 = gauss_cst(d, m->L0);
+      i += need;
+    } else if (m->lat == 3) {  /* categorical latent: prior[K] T[K*K] (T[new*K + prev]), one-hot state */
+      int64_t need = (int64_t)d + (int64_t)d * d;
+      if (np < i + need) return -1;
+      for (int64_t j = 0; j < need; ++j)
+        if (!(p[i + j] >= 0.0) || p[i + j] == INFINITY) return -1;
+      m->prior = malloc(sizeof(double) * d); memcpy(m->prior, p + i, sizeof(double) * d);
+      m->T = malloc(sizeof(double) * d * d); memcpy(m->T, p + i + d, sizeof(double) * d * d);
       i += need;
     } else {
       if (np < i + 3 || !(p[i + 1] > 0.0) || !(p[i + 2] > 0.0)) return -1;
@@ -820,8 +829,23 @@ static double slot_loglik(const model_t* m, const obs_t* o, const double* x) {
 }
 static double kit_z(uint64_t seed, uint64_t pid, uint32_t t, uint32_t stream, uint32_t base);
 /* the latent of step t (t = 1: the initial distribution), dense forms */
+/* the class of a one-hot categorical latent (SlotModel::onehot) */
+static int slot_onehot(const double* x, int d) {
+  int z = 0;
+  for (int j = 0; j < d; ++j) z = x[j] != 0.0 ? j : z;
+  return z;
+}
 static void slot_latent(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, const obs_t* o,
                         const double* xp, double* x, uint32_t stream, uint32_t base) {
+  if (m->lat == 3) {  /* inverse-CDF draw (categorical.jl:20-22), as the HMM family's */
+    uint32_t w[4];
+    rng(seed, pid, t, stream, base, w);
+    const double u = unif53(w[0], w[1]);
+    const int d = m->d;
+    const int z = t == 1 ? cat_sample(m->prior, d, 1, u) : cat_sample(m->T + slot_onehot(xp, d), d, d, u);
+    for (int j = 0; j < d; ++j) x[j] = j == z ? 1.0 : 0.0;
+    return;
+  }
   if (m->lat == 1) {
     double z = kit_z(seed, pid, t, stream, base);
     if (t == 1) x[0] = m->mu1 + m->s1 * z;
@@ -1157,7 +1181,7 @@ static int proposal_ok(const model_t* m, int proposal) {
   if (proposal == ORC_PROPOSAL_GAUSSIAN) return m->family == ORC_KITAGAWA && m->qa[3] > 0.0;
   if (proposal == ORC_PROPOSAL_LINEAR)
     return m->qlin && ((m->family == ORC_LGSSM && m->d + m->dy <= 32) ||
-                       (m->family == ORC_SLOTS && m->d + m->snv + (m->uin ? m->d : 0) <= 32));
+                       (m->family == ORC_SLOTS && m->lat != 3 && m->d + m->snv + (m->uin ? m->d : 0) <= 32));
   return proposal == ORC_PROPOSAL_OPTIMAL && (m->family == ORC_HMM || (m->family == ORC_LGSSM && m->opt));
 }
 int orc_pf_set_proposal_args(orc_pf* pf, const double* args, int n) {
@@ -1565,6 +1589,9 @@ static void model_score(const model_t* m, const obs_t* o, int t, const double* x
       quad = fma(u[i], u[i], quad);
     }
     *lat = (t == 1 ? m->cst0 : m->cstQ) - 0.5 * quad;
+  } else if (m->family == ORC_SLOTS && m->lat == 3) {  /* categorical.jl:10-12 */
+    const int z = slot_onehot(x, m->d);
+    *lat = orc_log(t == 1 ? m->prior[z] : m->T[z * m->d + slot_onehot(xp, m->d)]);
   } else if (m->family == ORC_LGSSM) {
     int d = m->d;
     const double* L = t == 1 ? m->L0 : m->LQ;

@@ -81,6 +81,20 @@ def count_inputs(T=10, seed=11):
     return u
 
 
+def switching_model():
+    """A 3-state switching model: a categorical latent z_t (one-hot) with
+    per-class normal, Poisson, Bernoulli and categorical emissions (a slot's
+    affine mean h.x + c is h[z] + c)."""
+    return gen.SlotSSM(
+        {"form": "categorical", "prior": [0.5, 0.3, 0.2],
+         "T": [[0.8, 0.1, 0.2], [0.15, 0.85, 0.1], [0.05, 0.05, 0.7]]},
+        [{"name": "level", "dist": "normal", "h": [-1.0, 0.5, 2.0], "c": 0.1, "sd": 0.6},
+         {"name": "count", "dist": "poisson", "h": [0.0, 1.0, 2.0], "c": -0.2},
+         {"name": "alarm", "dist": "bernoulli", "h": [-2.0, 0.0, 1.5], "c": 0.0},
+         {"name": "kind", "dist": "categorical", "W": [[1.0, 0.0, -1.0], [0.0, 1.0, 0.0], [-1.0, 0.0, 1.0]],
+          "c": [0.0, 0.0, 0.1]}])
+
+
 def count_obs(T=10, seed=5):
     """Observations with some slots missing at some steps (and one empty step)."""
     m = count_model()
@@ -305,6 +319,32 @@ def test_oracle_slot_zero_inputs_are_the_plain_model():
     x2 = pd.state()
     ref = [stats.multivariate_normal.logpdf(x2[:, i], m.A @ x1[:, i] + m.b + u[1], m.Q) for i in range(300)]
     np.testing.assert_allclose(ps[1, 0], ref, rtol=1e-12, atol=1e-10)
+
+
+def test_oracle_hmm_as_slots_matches_reference_forward_algorithm():
+    """The categorical latent pinned to the reference's HMM test
+    (test/inference/particle_filter.jl:96-168): the HMM written as a slot model
+    (categorical latent, one categorical emission slot with W = log E, so
+    softmax(W[:, z]) = E[:, z]) draws the HMM family's latents (no
+    resampling: the same states) and its log-ML at the reference's N is within
+    the reference's atol of the exact forward algorithm."""
+    import json
+
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "hmm.json")))["pf_test"]
+    E = np.array(g["emission"])
+    hmm = gen.DiscreteHMM(g["prior"], np.array(g["transition"]), E)
+    sl = gen.SlotSSM({"form": "categorical", "prior": g["prior"], "T": g["transition"]},
+                     [{"name": "x", "dist": "categorical", "W": np.log(E), "c": np.zeros(E.shape[0])}])
+    obs = g["obs"]
+    a = O.run_pf(hmm, [[o] for o in obs], 2000, 3, thr=0.0)
+    b = O.run_pf(sl, [{"x": float(o)} for o in obs], 2000, 3, thr=0.0)
+    assert np.array_equal(np.argmax(b.state(), axis=0), a.state()[0].astype(int))
+    np.testing.assert_allclose(b.log_weights(), a.log_weights(), rtol=1e-12, atol=1e-12)
+    pf = O.run_pf(sl, [{"x": float(o)} for o in obs], g["num_particles"], 0, thr=g["ess_threshold"])
+    assert abs(pf.log_ml_estimate() - g["log_ml"]) < g["atol"]
+    _, ps = b.scores(per_step=True)
+    _, ps_h = a.scores(per_step=True)
+    np.testing.assert_allclose(ps[:, 0], ps_h[:, 0], rtol=0, atol=0)  # log prior / log T: identical
 
 
 # ------------------------------------------------------------------ GPU
@@ -605,3 +645,38 @@ def test_gpu_slot_inputs_bitexact(gh_ctx, batched, linear):
     st2.close()
     with pytest.raises(gen.GenHipError):
         gen.simulate(mi, (4,), num_traces=10, seed=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched,rejuv", [(False, 0), (True, 0), (False, 2)])
+def test_gpu_categorical_latent_bitexact(gh_ctx, batched, rejuv):
+    """A switching model (categorical latent, four per-class emission slots,
+    some steps constraining a subset): states (one-hot), weights, parents,
+    score columns and simulate bit-exact against the oracle; the trace's latent
+    choice is the class index; a Gaussian drift and the linear proposal are
+    refused for it."""
+    m = switching_model()
+    xs, ys = m.simulate(9, np.random.default_rng(4))
+    obs = [dict(y) for y in ys]
+    del obs[2]["count"]
+    obs[5] = {}
+    n, seed = 5003, 29
+    st = _gpu_run(m, obs, n, seed, batched, None, rejuv)
+    orc = _orc_run(m, obs, n, seed, None, rejuv)
+    _same(st, orc=orc)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    z = gen.get_traces(st)[0].get_choices()[("chain", 3, "x")]
+    assert isinstance(z, int) and 0 <= z < 3
+    assert np.array_equal(gen.get_traces(st).column(("chain", 3, "x")), np.argmax(st.states(3), axis=1))
+    with pytest.raises(gen.GenHipError):
+        gen.mh(st, gen.gaussian_drift, (gen.select(m.latent_address(len(obs))), [0.1, 0.1, 0.1]))
+    st.close()
+    with pytest.raises(gen.GenHipError):
+        gen.initialize_particle_filter(m, (1,), _obs_at(m, obs[0], 1), gen.LinearGaussianProposal,
+                                       (np.zeros(3 * 3 * 2 + 3),), 100, seed=1)
+    tr = gen.simulate(m, (6,), num_traces=555, seed=8)
+    X, Y, PS, TOT = O.simulate(m, 6, 555, 8)
+    assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
+    assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
