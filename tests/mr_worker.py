@@ -30,6 +30,10 @@ def build_model(name):
         from tests.test_slots import count_model
 
         return count_model()
+    if name == "switch":  # a slot model with a categorical (one-hot) latent
+        from tests.test_slots import switching_model
+
+        return switching_model()
     raise ValueError(name)
 
 
