@@ -8,7 +8,8 @@
 // such a kernel (static_ir/generate.jl:24-43, 68-109: every constrained
 // choice adds its logpdf to the weight, every unconstrained one is drawn):
 //
-//   latent   x_t ~ mvnormal(A x_{t-1} + b, Q)      (x_1 ~ mvnormal(mu0, P0))
+//   latent   x_t ~ mvnormal(A x_{t-1} + b, Q)      (x_1 ~ mvnormal(mu0, P0); with per-step
+//            inputs b + u_t, u_t the step's kernel argument)
 //         or z_t ~ categorical(T[:, z_{t-1}])       (z_1 ~ categorical(prior); stored one-hot, d = K)
 //         or x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)   (d = 1;
 //            x_1 ~ normal(mu1, s1)) — examples/pmmh/model.jl:9-13
