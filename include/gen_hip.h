@@ -175,8 +175,10 @@ typedef struct {
    values == NULL or present == 0 means "no observation at this step".
    GH_FAMILY_SLOTS: `slot` names the observed address (0..K-1) and `next`
    chains the step's other constrained addresses (NULL ends the chain; a
-   slot constrained twice is GH_E_DISCARD); the other families take slot 0
-   and no chain. */
+   slot constrained twice is GH_E_DISCARD); an entry with slot
+   GH_SLOT_INPUT (-1) carries the step's latent input u_t (latent form 2, d
+   values, at most one per step); the other families take slot 0 and no
+   chain. */
 typedef struct gh_obs {
   const double* values;
   int32_t n_values;
