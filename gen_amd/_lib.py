@@ -119,6 +119,8 @@ SIGNATURES = {
     "gh_dist_random_dev": (c_int, [c_void_p, c_void_p, c_int64, c_uint64, c_void_p]),
     "gh_simulate": (c_int, [c_void_p, c_int, c_int64, c_uint64, POINTER(c_double), POINTER(c_double),
                             POINTER(c_double), POINTER(c_double)]),
+    "gh_simulate_inputs": (c_int, [c_void_p, c_int, c_int64, c_uint64, POINTER(c_double), POINTER(c_double),
+                                   POINTER(c_double), POINTER(c_double), POINTER(c_double)]),
     "gh_pf_init_conditional": (c_int, [c_void_p, POINTER(Obs), c_int64, c_uint64, POINTER(PFOpts), POINTER(c_double),
                                        POINTER(c_void_p)]),
     "gh_pf_step_conditional": (c_int, [c_void_p, POINTER(Obs), POINTER(c_double)]),

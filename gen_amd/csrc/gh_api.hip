@@ -3271,15 +3271,33 @@ static int step_params_impl(gh_pf* pf, const gh_obs* obs, int proposal, gh_model
 }
 
 // simulate(model, (T,)) for n independent traces (gh_simulate.h).
+static int simulate_impl(gh_model* m, int T, int64_t n, uint64_t seed, const double* inputs, double* xs, double* ys,
+                         double* per_step, double* total);
+
 extern "C" int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double* xs, double* ys, double* per_step,
                            double* total) {
+  return simulate_impl(m, T, n, seed, nullptr, xs, ys, per_step, total);
+}
+
+// simulate(model, (T, U)) for a slot model with per-step inputs: U[T*d], row t-1
+// the input of step t (row 0 unused: the transition starts at t = 2)
+extern "C" int gh_simulate_inputs(gh_model* m, int T, int64_t n, uint64_t seed, const double* inputs, double* xs,
+                                  double* ys, double* per_step, double* total) {
+  if (!m || !inputs) return set_err(GH_E_INVAL, "gh_simulate_inputs: null argument");
+  if (m->family != GH_FAMILY_SLOTS || m->slots.uoff < 0)
+    return set_err(GH_E_INVAL, "gh_simulate_inputs: the model takes no per-step inputs (slot latent form 2)");
+  return simulate_impl(m, T, n, seed, inputs, xs, ys, per_step, total);
+}
+
+static int simulate_impl(gh_model* m, int T, int64_t n, uint64_t seed, const double* inputs, double* xs, double* ys,
+                         double* per_step, double* total) {
   if (!m) return set_err(GH_E_INVAL, "gh_simulate: null model");
   if (T < 1) return set_err(GH_E_INVAL, "gh_simulate: T = %d (need >= 1)", T);
   if (m->family == GH_FAMILY_REGRESSION && T != 1)
     return set_err(GH_E_INVAL, "gh_simulate: the regression model has no time steps (T = 1)");
   if (n < 0 || n > INT32_MAX) return set_err(GH_E_INVAL, "gh_simulate: n = %lld", (long long)n);
-  if (m->family == GH_FAMILY_SLOTS && m->slots.uoff >= 0)
-    return set_err(GH_E_INVAL, "gh_simulate: a slot model with per-step inputs (its inputs are not arguments here)");
+  if (m->family == GH_FAMILY_SLOTS && m->slots.uoff >= 0 && !inputs)
+    return set_err(GH_E_INVAL, "gh_simulate: a slot model with per-step inputs takes them (gh_simulate_inputs)");
   if (n == 0) return GH_OK;
   HIP_TRY(hipSetDevice(m->ctx->device));
   const int d = m->d;
@@ -3287,7 +3305,15 @@ extern "C" int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double*
                      ? m->dy
                      : 1;
   std::vector<StepObs> hobs(T);
-  for (int t = 1; t <= T; ++t) CHECK(make_obs(m, t, nullptr, &hobs[t - 1]));
+  for (int t = 1; t <= T; ++t) {
+    CHECK(make_obs(m, t, nullptr, &hobs[t - 1]));
+    if (inputs && t > 1)
+      for (int j = 0; j < d; ++j) {
+        const double u = inputs[(size_t)(t - 1) * d + j];
+        if (!std::isfinite(u)) return set_err(GH_E_INVAL, "gh_simulate_inputs: non-finite input");
+        hobs[t - 1].v[m->slots.uoff + j] = u;
+      }
+  }
   const size_t nx = (size_t)T * d * n, ny = (size_t)T * dy * n, ns = (size_t)T * 2 * n;
   double* buf = nullptr;
   StepObs* dobs = nullptr;

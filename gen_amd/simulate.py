@@ -134,11 +134,15 @@ def simulate(model: Model, model_args: tuple = (), num_traces: int | None = None
     SimulatedTraces batch of n traces simulated in one launch."""
     from .pf import default_context
 
+    U = None
     if model.static:  # its argument (the xs) is part of the model object
         T = 1
     else:
+        if getattr(model, "inputs", False) and len(model_args) == 2:  # (T, U): a slot model's per-step inputs
+            U = np.ascontiguousarray(np.asarray(model_args[1], dtype=np.float64).reshape(int(model_args[0]), model.d))
+            model_args = model_args[:1]
         if len(model_args) != 1:
-            raise _lib.GenHipError(1, "simulate: model_args = (T,) for an Unfold model")
+            raise _lib.GenHipError(1, "simulate: model_args = (T,) for an Unfold model, (T, U) with per-step inputs")
         T = int(model_args[0])
     n = 1 if num_traces is None else int(num_traces)
     ctx = ctx or default_context()
@@ -147,7 +151,11 @@ def simulate(model: Model, model_args: tuple = (), num_traces: int | None = None
     d, dy = (model.d, model.dy) if vec else (1, 1)
     xs, ys = np.empty((T, d, n)), np.empty((T, dy, n))
     ps, tot = np.empty((T, 2, n)), np.empty(n)
-    _lib.check(_lib.load().gh_simulate(h, T, n, int(seed), _lib.dptr(xs), _lib.dptr(ys), _lib.dptr(ps),
-                                       _lib.dptr(tot)))
+    if U is not None:
+        _lib.check(_lib.load().gh_simulate_inputs(h, T, n, int(seed), _lib.dptr(U), _lib.dptr(xs), _lib.dptr(ys),
+                                                  _lib.dptr(ps), _lib.dptr(tot)))
+    else:
+        _lib.check(_lib.load().gh_simulate(h, T, n, int(seed), _lib.dptr(xs), _lib.dptr(ys), _lib.dptr(ps),
+                                           _lib.dptr(tot)))
     out = SimulatedTraces(model, T, xs, ys, ps, tot)
     return out[0] if num_traces is None else out

@@ -104,7 +104,7 @@ typedef enum {
          gh_obs entry with slot GH_SLOT_INPUT and d values; zero when a step
          gives none): the Unfold's kernel arguments extended by one value per
          step, new_args = (t, u_t) (no re-scoring: earlier steps keep theirs);
-         gh_simulate refuses such a model
+         simulate(model, (T, U)) is gh_simulate_inputs (gh_simulate refuses)
                    lat = GH_SLOT_LAT_KITAGAWA (1), d = 1: mu1 s1 sd_x
          x_1 ~ normal(mu1, s1); x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)
                    lat = GH_SLOT_LAT_CATEGORICAL (3), d = K classes (2..16): prior[K] T[K*K]
@@ -269,6 +269,11 @@ int gh_model_state_dim(const gh_model* m, int* d);
    The regression model takes T = 1. */
 int gh_simulate(gh_model* m, int T, int64_t n, uint64_t seed, double* xs, double* ys, double* per_step,
                 double* total);
+/* simulate(model, (T, U)) for a slot model with per-step inputs (latent form
+   2; gh_simulate refuses one): inputs[T*d], row t-1 the input u_t of step t
+   (row 0 unused); outputs as gh_simulate. */
+int gh_simulate_inputs(gh_model* m, int T, int64_t n, uint64_t seed, const double* inputs, double* xs, double* ys,
+                       double* per_step, double* total);
 
 /* ---- distributions ----------------------------------------------------------- */
 /* Gen's distribution library (src/modeling_library/distributions/), batched:

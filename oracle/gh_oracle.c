@@ -1737,12 +1737,28 @@ int orc_pf_step_params(orc_pf* pf, const double* params, int64_t np, const doubl
    observation from draw SIM_OBS_DRAW on, scored as a given observation is
    (obs_build + model_loglik); the latent's score is model_score's.  Outputs
    time-major: xs[t][k][n], ys[t][r][n], per_step[t][2][n], total[n]. */
+static int simulate_impl(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T,
+                         int64_t n, uint64_t seed, const double* inputs, double* xs, double* ys, double* per_step,
+                         double* total);
 int orc_simulate(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T, int64_t n,
                  uint64_t seed, double* xs, double* ys, double* per_step, double* total) {
+  return simulate_impl(family, d, dy, k, v, params, np, T, n, seed, NULL, xs, ys, per_step, total);
+}
+/* simulate(model, (T, U)) of a slot model with per-step inputs: inputs[T*d],
+   row t-1 the input of step t (row 0 unused), as gh_simulate_inputs */
+int orc_simulate_inputs(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T, int64_t n,
+                        uint64_t seed, const double* inputs, double* xs, double* ys, double* per_step,
+                        double* total) {
+  if (!inputs) return -1;
+  return simulate_impl(family, d, dy, k, v, params, np, T, n, seed, inputs, xs, ys, per_step, total);
+}
+static int simulate_impl(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T,
+                         int64_t n, uint64_t seed, const double* inputs, double* xs, double* ys, double* per_step,
+                         double* total) {
   model_t m;
   if (model_build(&m, family, d, dy, k, v, params, np) || T < 1 || (family == ORC_REGRESSION && T != 1) ||
-      (family == ORC_SLOTS && m.uin)) {  /* (per-step inputs: not simulate's arguments, as gh_simulate) */
-    model_free(&m);
+      (family == ORC_SLOTS && (m.uin != (inputs != NULL))) || (family != ORC_SLOTS && inputs)) {
+    model_free(&m);  /* (a model with per-step inputs takes them; no other model does) */
     return -1;
   }
   const int D = m.d, DY = (family == ORC_LGSSM || family == ORC_REGRESSION || family == ORC_SLOTS) ? m.dy : 1;
@@ -1752,7 +1768,15 @@ int orc_simulate(int family, int d, int dy, int k, int v, const double* params, 
     double tot = 0.0;
     for (int t = 1; t <= T; ++t) {
       obs_t none, oy;
-      obs_build(&m, t, NULL, 0, &none);
+      double yin[96];
+      const int inb = inputs && t > 1;  /* the step's input rides after the dy slot values (bit 4) */
+      if (inb) {
+        for (int r = 0; r < m.dy; ++r) yin[r] = 0.0;
+        for (int i = 0; i < D; ++i) yin[m.dy + i] = inputs[(size_t)(t - 1) * D + i];
+        obs_build(&m, t, yin, 16, &none);
+      } else {
+        obs_build(&m, t, NULL, 0, &none);
+      }
       if (t == 1) particle_init(&m, seed, (uint64_t)j, &none, 0, x, S_SIM, 0);
       else particle_step(&m, seed, (uint64_t)j, (uint32_t)t, &none, 0, xp, x, S_SIM, 0);
       if (family == ORC_SLOTS) {
@@ -1776,7 +1800,12 @@ int orc_simulate(int family, int d, int dy, int k, int v, const double* params, 
         normals_at(seed, (uint64_t)j, (uint32_t)t, S_SIM, SIM_OBS_DRAW, DY, z);
         for (int i = 0; i < DY; ++i) y[i] = (x[0] * m.xs[i] + x[1]) + m.sigma * z[i];
       }
-      obs_build(&m, t, y, family == ORC_SLOTS ? (1 << m.K) - 1 : 1, &oy);
+      if (inb) {
+        for (int r = 0; r < m.dy; ++r) yin[r] = y[r];
+        obs_build(&m, t, yin, ((1 << m.K) - 1) | 16, &oy);
+      } else {
+        obs_build(&m, t, y, family == ORC_SLOTS ? (1 << m.K) - 1 : 1, &oy);
+      }
       double lat, ob;
       model_score(&m, &oy, t, xp, x, &lat, &ob);
       if (xs) for (int q = 0; q < D; ++q) xs[((size_t)(t - 1) * D + q) * n + j] = x[q];

@@ -105,6 +105,9 @@ int orc_dist_random(int dist, int dim, int np, int stride, const double* params,
                     double* out);
 int orc_simulate(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T, int64_t n,
                  uint64_t seed, double* xs, double* ys, double* per_step, double* total);
+int orc_simulate_inputs(int family, int d, int dy, int k, int v, const double* params, int64_t np, int T, int64_t n,
+                        uint64_t seed, const double* inputs, double* xs, double* ys, double* per_step,
+                        double* total);
 
 /* distributed building blocks (sharded oracle, exercised with gloo) */
 void orc_pf_local_stats(orc_pf* pf, double out[3]);      /* (max, sum e, sum e^2) local */

@@ -95,6 +95,7 @@ def _load(path):
             "orc_dist_logpdf": (I, [I, I, I, I, D, I64, D, D]),
             "orc_dist_random": (I, [I, I, I, I, D, I64, U64, D]),
             "orc_simulate": (I, [I, I, I, I, I, D, I64, I, I64, U64, D, D, D, D]),
+            "orc_simulate_inputs": (I, [I, I, I, I, I, D, I64, I, I64, U64, D, D, D, D, D]),
             "orc_pf_local_stats": (None, [V, D]),
             "orc_combine_stats": (I, [D, I, I64, c_double, D, D, D]),
             "orc_pf_local_qtotal": (U64, [V, c_double]),
@@ -368,14 +369,21 @@ def importance_sampling(model, y, n, seed, proposal=DEFAULT):
     return st, lnw, lml.value
 
 
-def simulate(model, T, n, seed):
-    """simulate(model, (T,)) n times: (xs [T, d, n], ys [T, dy, n], per_step [T, 2, n], total [n])."""
+def simulate(model, T, n, seed, inputs=None):
+    """simulate(model, (T,)) n times — (T, U) with a slot model's per-step
+    inputs U [T, d] — : (xs [T, d, n], ys [T, dy, n], per_step [T, 2, n], total [n])."""
     fam, d, dy, k, v, p = model_args(model)
     dd = d if fam in (LGSSM, REGRESSION, SLOTS) else 1
     ddy = dy if fam in (LGSSM, REGRESSION, SLOTS) else 1
     xs, ys = np.empty((T, dd, n)), np.empty((T, ddy, n))
     ps, tot = np.empty((T, 2, n)), np.empty(n)
-    if lib().orc_simulate(fam, d, dy, k, v, _d(p), p.size, T, n, seed, _d(xs), _d(ys), _d(ps), _d(tot)):
+    if inputs is not None:
+        U = np.ascontiguousarray(np.asarray(inputs, dtype=np.float64).reshape(T, dd))
+        rc = lib().orc_simulate_inputs(fam, d, dy, k, v, _d(p), p.size, T, n, seed, _d(U), _d(xs), _d(ys), _d(ps),
+                                       _d(tot))
+    else:
+        rc = lib().orc_simulate(fam, d, dy, k, v, _d(p), p.size, T, n, seed, _d(xs), _d(ys), _d(ps), _d(tot))
+    if rc:
         raise ValueError("oracle simulate failed")
     return xs, ys, ps, tot
 

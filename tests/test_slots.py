@@ -347,6 +347,27 @@ def test_oracle_hmm_as_slots_matches_reference_forward_algorithm():
     np.testing.assert_allclose(ps[:, 0], ps_h[:, 0], rtol=0, atol=0)  # log prior / log T: identical
 
 
+def test_oracle_simulate_with_inputs_moves_the_latents():
+    """simulate(model, (T, U)) of a model with per-step inputs: zero inputs
+    reproduce the plain model's traces bit for bit; each step's latent moves
+    by its input (the same normals) and scores as mvnormal(A x + b + u, Q)."""
+    from scipy import stats
+
+    m, mi = count_model(), count_model_inputs()
+    T, n = 5, 200
+    X0, Y0, P0, _ = O.simulate(m, T, n, 9)
+    Xz, Yz, Pz, _ = O.simulate(mi, T, n, 9, inputs=np.zeros((T, 2)))
+    assert np.array_equal(X0, Xz) and np.array_equal(Y0, Yz) and np.array_equal(P0, Pz)
+    U = np.zeros((T, 2))
+    U[1] = [0.5, -0.3]
+    X1, _, P1, _ = O.simulate(mi, T, n, 9, inputs=U)
+    np.testing.assert_allclose(X1[1] - X0[1], np.repeat(U[1][:, None], n, axis=1), atol=1e-12)
+    ref = [stats.multivariate_normal.logpdf(X1[1, :, j], m.A @ X1[0, :, j] + m.b + U[1], m.Q) for j in range(n)]
+    np.testing.assert_allclose(P1[1, 0], ref, rtol=1e-12, atol=1e-10)
+    with pytest.raises(ValueError):  # (the inputs are required arguments)
+        O.simulate(mi, T, n, 9)
+
+
 # ------------------------------------------------------------------ GPU
 def _gpu_run(model, obs, n, seed, batched, thr=None, rejuv=0):
     st = gen.initialize_particle_filter(model, (1,), _obs_at(model, obs[0], 1), n, seed=seed)
@@ -643,8 +664,13 @@ def test_gpu_slot_inputs_bitexact(gh_ctx, batched, linear):
     with pytest.raises(gen.GenHipError):  # (the plain model takes no input: new_args[1] must be a model)
         gen.particle_filter_step(st2, (2, np.zeros(2)), (gen.UnknownChange(),) * 2, _obs_at(m, obs[1], 2))
     st2.close()
-    with pytest.raises(gen.GenHipError):
+    with pytest.raises(gen.GenHipError):  # (its inputs are arguments: simulate(model, (T, U)))
         gen.simulate(mi, (4,), num_traces=10, seed=1)
+    U = np.stack([np.zeros(2) if v is None else v for v in u])
+    tr = gen.simulate(mi, (len(u), U), num_traces=777, seed=5)
+    X, Y, PS, TOT = O.simulate(mi, len(u), 777, 5, inputs=U)
+    assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
+    assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
 
 
 @pytest.mark.gpu
