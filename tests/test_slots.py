@@ -706,3 +706,33 @@ def test_gpu_categorical_latent_bitexact(gh_ctx, batched, rejuv):
     X, Y, PS, TOT = O.simulate(m, 6, 555, 8)
     assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
     assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["count", "switch"])
+def test_gpu_slot_models_full_size_bitexact(gh_ctx, name):
+    """Slot models at the C2 size (2^20 particles, the batched loop with the
+    one-launch resample at ESS < N/2): final states, weights and parents
+    bit-exact against the oracle's OpenMP build."""
+    if name == "count":
+        m, obs = count_obs(T=8)
+    else:
+        m = switching_model()
+        _, ys = m.simulate(8, np.random.default_rng(6))
+        obs = [dict(y) for y in ys]
+    n = 1 << 20
+    st = gen.initialize_particle_filter(m, (1,), _obs_at(m, obs[0], 1), n, seed=42)
+    gen.run_particle_filter(st, list(obs[1:]))
+    O.set_openmp(True)
+    try:
+        orc = O.run_pf(m, obs, n, 42, record_history=False)
+    finally:
+        O.set_openmp(False)
+    _, did = st.ess_history()
+    assert did.sum() >= 1
+    assert np.array_equal(st.states().T.view(np.uint64), orc.state().view(np.uint64))
+    assert np.array_equal(gen.get_log_weights(st).view(np.uint64), orc.log_weights().view(np.uint64))
+    assert np.array_equal(st.parents, orc.parents())
+    a, b = gen.log_ml_estimate(st), orc.log_ml_estimate()
+    assert abs(a - b) <= 1e-9 * abs(b)
+    st.close()
