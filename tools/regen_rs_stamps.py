@@ -81,8 +81,9 @@ def stamped_kernels(s):
     b = insert(b, b.index("GH_RS_STAMP(3)"), "  if (sfail) return;\n", "  GH_RS_EXIT_AT(3);\n  GH_RS_STAMP(4);\n")
     b = insert(b, 0, "const uint32_t N = (uint32_t)r.mk.n_global;  // < 2^31: 32-bit slots and groups\n",
                "#if defined(GH_RS_STAMPS)\n  const uint64_t wt0 = wall_clock64();\n  uint64_t wmany = 0, wcar = 0, wnear = 0;\n#endif\n")
-    b = insert(b, 0, "if (__builtin_amdgcn_ballot_w64(near) != 0) {  // (wave-uniform: straight-line code otherwise)\n",
-               "#if defined(GH_RS_STAMPS)\n      wnear += __builtin_popcountll(__builtin_amdgcn_ballot_w64(near));\n#endif\n")
+    b = insert(b, 0, "    if (near) j = sys_count_exact_call(&sd, N, X);",
+               "#if defined(GH_RS_STAMPS)\n    wnear += __builtin_popcountll(__builtin_amdgcn_ballot_w64(near));\n#endif\n",
+               after=False)
     b = insert(b, 0, "uint64_t bm = __builtin_amdgcn_ballot_w64(many);\n",
                "#if defined(GH_RS_STAMPS)\n    wmany += __builtin_popcountll(bm);\n#endif\n")
     b = insert(b, 0, "a1 = __builtin_amdgcn_readlane((int32_t)g1, L);\n",
