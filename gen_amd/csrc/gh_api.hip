@@ -629,8 +629,8 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
       if (link != LINK_AFFINE || mm < 1 || mm > kMaxObs) return "slots: mvnormal slot needs the affine mean, 1..32 values";
       nv = mm;
     } else if (dist == SLOT_NORMAL) {
-      if (mm != 1 || !(link == LINK_AFFINE || (link == LINK_KITAGAWA && d == 1)))
-        return "slots: normal slot: one value, affine mean (or x^2/20 with d = 1)";
+      if (mm != 1 || !(link == LINK_AFFINE || link == LINK_LOGSCALE || (link == LINK_KITAGAWA && d == 1)))
+        return "slots: normal slot: one value, affine mean (or x^2/20 with d = 1), fixed or log-linear sd";
     } else if (dist == SLOT_POISSON) {
       if (mm != 1 || link != LINK_EXP) return "slots: poisson slot: one count, rate exp(h.x + c)";
       nv = 2;  // (y, log Gamma(y + 1))
@@ -709,6 +709,11 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
       h.insert(h.end(), c, c + mm);
       h.insert(h.end(), m->slot_LR[k].begin(), m->slot_LR[k].end());
       sp.cst[k] = gauss_cst(mm, m->slot_LR[k].data());
+      i += need;
+    } else if (dist == SLOT_NORMAL && sp.link[k] == LINK_LOGSCALE) {  // h c g s: sd = exp(g.x + s)
+      const int64_t need = 2LL * d + 2;
+      if (np < i + need) return "slots: too few parameters (log-linear normal slot: h c g s)";
+      h.insert(h.end(), p + i, p + i + need);
       i += need;
     } else if (dist == SLOT_NORMAL) {
       const int64_t need = sp.link[k] == LINK_AFFINE ? d + 2 : 1;

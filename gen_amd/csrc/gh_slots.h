@@ -15,6 +15,7 @@
 //            x_1 ~ normal(mu1, s1)) — examples/pmmh/model.jl:9-13
 //   slots    mvnormal(H x + c, R)                         mvnormal.jl:12-16
 //            normal(h.x + c, sd) or normal(x^2/20, sd)    normal.jl:56-60
+//            normal(h.x + c, exp(g.x + s))                normal.jl:56-60 (stochastic volatility)
 //            poisson(exp(h.x + c))                        poisson.jl:10-12
 //            bernoulli(1 / (1 + exp(-(h.x + c))))         bernoulli.jl:10-12
 //            categorical(softmax(W x + c))                categorical.jl:10-12 (0-based values)
@@ -39,7 +40,10 @@ constexpr int kMaxSlotClasses = 16;  // categorical slot classes
 constexpr uint32_t kSlotSimDraws = 32;  // simulate(): slot k draws from kSimObsDraw + 32 k
 
 enum SlotDist : int { SLOT_MVNORMAL = 1, SLOT_NORMAL = 2, SLOT_POISSON = 3, SLOT_BERNOULLI = 4, SLOT_CATEGORICAL = 5 };
-enum SlotLink : int { LINK_AFFINE = 0, LINK_KITAGAWA = 1, LINK_EXP = 2, LINK_LOGISTIC = 3, LINK_SOFTMAX = 4 };
+enum SlotLink : int {
+  LINK_AFFINE = 0, LINK_KITAGAWA = 1, LINK_EXP = 2, LINK_LOGISTIC = 3, LINK_SOFTMAX = 4,
+  LINK_LOGSCALE = 5  // normal slot with a log-linear standard deviation
+};
 // (latent form 2 — affine with per-step inputs — is SLOT_LAT_AFFINE with uoff >= 0)
 enum SlotLatent : int { SLOT_LAT_AFFINE = 0, SLOT_LAT_KITAGAWA = 1, SLOT_LAT_CATEGORICAL = 3 };
 
@@ -56,7 +60,8 @@ struct SlotParams {
   int voff[kMaxSlots];  // the slot's values in StepObs::v
   int yoff[kMaxSlots];  // the slot's rows in simulate()'s output
   // per slot: mvnormal M = L_R^-1 H [m*d] | H [m*d] | c [m] | L_R [m*m];
-  // normal / poisson / bernoulli h [d] | c; categorical W [m*d] | c [m]
+  // normal / poisson / bernoulli h [d] | c (log-linear normal: h [d] | c | g [d] | s);
+  // categorical W [m*d] | c [m]
   const double* P[kMaxSlots];
   double cst[kMaxSlots];    // mvnormal -0.5 (m log 2pi + log det R); normal -0.5 log(2 pi sd^2)
   double inv2v[kMaxSlots];  // normal 1 / (2 sd^2)
@@ -98,6 +103,14 @@ struct SlotModel {
     return acc;
   }
 
+  // normal.jl:56-60 literally, with std = exp(eta): var = std * std,
+  // -(diff * diff) / (2 var) - 0.5 log(2 pi var)
+  __device__ static double normal_logscale_lpdf(double diff, double eta) {
+    const double sd = gh_exp(eta);
+    const double var = sd * sd;
+    return -(diff * diff) / (2.0 * var) - 0.5 * gh_log(0x1.921fb54442d18p+2 * var);
+  }
+
   // the class of a one-hot categorical latent
   __device__ static int onehot(const double* x) {
     int z = 0;
@@ -125,6 +138,7 @@ struct SlotModel {
       case SLOT_NORMAL: {
         const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : affine(P, P[D], x);
         const double diff = v[0] - mean;
+        if (p.link[k] == LINK_LOGSCALE) return normal_logscale_lpdf(diff, affine(P + D + 1, P[2 * D + 1], x));
         return -(diff * diff) * p.inv2v[k] + p.cst[k];
       }
       case SLOT_POISSON: {  // poisson.jl:10-12 with lambda = exp(h.x + c); v[1] = log Gamma(y + 1)
@@ -294,6 +308,12 @@ struct SlotModel {
           double z0, z1;
           normal_pair(rng_block(seed, pid, t, STREAM_SIM, draw), &z0, &z1, tab);
           const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : affine(P, P[D], x);
+          if (p.link[k] == LINK_LOGSCALE) {
+            const double eta = affine(P + D + 1, P[2 * D + 1], x);
+            yk[0] = mean + gh_exp(eta) * z0;
+            lp = normal_logscale_lpdf(yk[0] - mean, eta);
+            break;
+          }
           yk[0] = mean + p.sd[k] * z0;
           const double diff = yk[0] - mean;
           lp = -(diff * diff) * p.inv2v[k] + p.cst[k];

@@ -347,7 +347,7 @@ class BayesianLinearRegression(Model):
 
 # slot distributions / mean forms of GH_FAMILY_SLOTS (include/gen_hip.h)
 _SLOT_DIST = {"mvnormal": 1, "normal": 2, "poisson": 3, "bernoulli": 4, "categorical": 5}
-_LINK = {"affine": 0, "x^2/20": 1, "exp": 2, "logistic": 3, "softmax": 4}
+_LINK = {"affine": 0, "x^2/20": 1, "exp": 2, "logistic": 3, "softmax": 4, "logscale": 5}
 
 
 class SlotSSM(Model):
@@ -362,6 +362,7 @@ class SlotSSM(Model):
             # or: x = @trace(normal(x_prev/2 + 25x_prev/(1+x_prev^2) + 8cos(1.2t), p.sd_x), :x)
             @trace(mvnormal(p.H * x + p.c, p.R), :y)                # slot "mvnormal"
             @trace(normal(p.h' * x + p.c0, p.sd), :z)                # slot "normal" (or mean x^2/20)
+            @trace(normal(p.h' * x + p.c0, exp(p.g' * x + p.s)), :r)  # slot "normal", log-linear sd
             @trace(poisson(exp(p.h' * x + p.c0)), :count)            # slot "poisson"
             @trace(bernoulli(1 / (1 + exp(-(p.h' * x + p.c0)))), :on)  # slot "bernoulli"
             @trace(categorical(softmax(p.W * x + p.c)), :kind)       # slot "categorical" (0-based here)
@@ -377,7 +378,8 @@ class SlotSSM(Model):
             step gives none): x_t ~ mvnormal(A x_{t-1} + (b + u_t), Q) — the Unfold's
             arguments extended by one value per step, new_args = (t, u_t)
     slots:  [{"name", "dist", ...}] with per distribution
-            mvnormal: H [m, d], c [m], R [m, m]; normal: h [d], c, sd (or mean "x^2/20", sd);
+            mvnormal: H [m, d], c [m], R [m, m]; normal: h [d], c, sd (or mean "x^2/20", sd;
+            or h [d], c, "log_sd": {"g": [d], "s"} for sd = exp(g.x + s) — stochastic volatility);
             poisson / bernoulli: h [d], c; categorical: W [m, d], c [m]
     Observations of step t: {("chain", t, name): value} (any subset of the slots).
     """
@@ -429,8 +431,14 @@ class SlotSSM(Model):
             else:
                 s["m"] = 1
                 s["link"] = {"normal": s.get("mean", "affine"), "poisson": "exp", "bernoulli": "logistic"}[dist]
-                if s["link"] == "affine":
-                    s["h"] = np.asarray(s["h"], dtype=np.float64).reshape(self.d)
+                if dist == "normal" and "log_sd" in s:
+                    if s["link"] != "affine":
+                        raise ValueError("a log-linear sd takes the affine mean")
+                    s["link"] = "logscale"
+                    s["g"] = np.asarray(s["log_sd"]["g"], dtype=np.float64).reshape(self.d)
+                    s["s"] = float(s["log_sd"].get("s", 0.0))
+                if s["link"] in ("affine", "logscale"):
+                    s["h"] = np.asarray(s.get("h", np.zeros(self.d)), dtype=np.float64).reshape(self.d)
                     s["c"] = float(s.get("c", 0.0))
             self.slots.append(s)
         self.names = [s["name"] for s in self.slots]
@@ -450,6 +458,8 @@ class SlotSSM(Model):
         for s in self.slots:
             if s["dist"] == "mvnormal":
                 p += list(s["H"].ravel()) + list(s["c"]) + list(s["R"].ravel())
+            elif s["dist"] == "normal" and s["link"] == "logscale":
+                p += [*s["h"], s["c"], *s["g"], s["s"]]
             elif s["dist"] == "normal":
                 p += ([*s["h"], s["c"]] if s["link"] == "affine" else []) + [float(s["sd"])]
             elif s["dist"] == "categorical":
@@ -528,6 +538,12 @@ class SlotSSM(Model):
         eta = float(s["h"] @ x + s["c"])
         return {"normal": eta, "poisson": np.exp(eta), "bernoulli": 1.0 / (1.0 + np.exp(-eta))}[s["dist"]]
 
+    def slot_sd(self, s, x) -> float:
+        """A normal slot's standard deviation at latent x."""
+        if s["link"] == "logscale":
+            return float(np.exp(s["g"] @ np.atleast_1d(x) + s["s"]))
+        return s["sd"]
+
     def slot_logpdf(self, k: int, y, x) -> float:
         """logpdf of slot k's value y at latent x (scipy-free closed forms of
         the reference's distributions)."""
@@ -538,7 +554,7 @@ class SlotSSM(Model):
         if s["dist"] == "mvnormal":
             return _mvn_logpdf(np.atleast_1d(y), mp, s["R"])
         if s["dist"] == "normal":
-            return _normal_logpdf(float(y), mp, s["sd"])
+            return _normal_logpdf(float(y), mp, self.slot_sd(s, x))
         if s["dist"] == "poisson":
             return float(y * np.log(mp) - mp - lgamma(y + 1.0))
         if s["dist"] == "bernoulli":
@@ -570,7 +586,7 @@ class SlotSSM(Model):
                 if s["dist"] == "mvnormal":
                     y[s["name"]] = rng.multivariate_normal(mp, s["R"])
                 elif s["dist"] == "normal":
-                    y[s["name"]] = float(rng.normal(mp, s["sd"]))
+                    y[s["name"]] = float(rng.normal(mp, self.slot_sd(s, x)))
                 elif s["dist"] == "poisson":
                     y[s["name"]] = float(rng.poisson(mp))
                 elif s["dist"] == "bernoulli":

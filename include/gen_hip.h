@@ -116,6 +116,9 @@ typedef enum {
        GH_SLOT_MVNORMAL, link GH_LINK_AFFINE, m <= 32: H[m*d] c[m] R[m*m]   y ~ mvnormal(H x + c, R)
        GH_SLOT_NORMAL, m = 1, GH_LINK_AFFINE: h[d] c sd                     y ~ normal(h.x + c, sd)
                               GH_LINK_KITAGAWA (d = 1): sd                  y ~ normal(x^2/20, sd)
+                              GH_LINK_LOGSCALE: h[d] c g[d] s   y ~ normal(h.x + c, exp(g.x + s))
+         (a log-linear standard deviation: the stochastic-volatility emission
+         y_t ~ normal(0, exp(x_t / 2)) is h = 0, c = 0, g = 1/2, s = 0)
        GH_SLOT_POISSON, m = 1, GH_LINK_EXP: h[d] c                         y ~ poisson(exp(h.x + c))
        GH_SLOT_BERNOULLI, m = 1, GH_LINK_LOGISTIC: h[d] c   y ~ bernoulli(1 / (1 + exp(-(h.x + c)))) (0 / 1)
        GH_SLOT_CATEGORICAL, m = classes 2..16, GH_LINK_SOFTMAX: W[m*d] c[m]
@@ -133,7 +136,8 @@ enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1, GH_SLOT_LAT_AFFINE_INPU
    argument of the step's kernel application, not a choice */
 enum { GH_SLOT_INPUT = -1 };
 enum { GH_SLOT_MVNORMAL = 1, GH_SLOT_NORMAL = 2, GH_SLOT_POISSON = 3, GH_SLOT_BERNOULLI = 4, GH_SLOT_CATEGORICAL = 5 };
-enum { GH_LINK_AFFINE = 0, GH_LINK_KITAGAWA = 1, GH_LINK_EXP = 2, GH_LINK_LOGISTIC = 3, GH_LINK_SOFTMAX = 4 };
+enum { GH_LINK_AFFINE = 0, GH_LINK_KITAGAWA = 1, GH_LINK_EXP = 2, GH_LINK_LOGISTIC = 3, GH_LINK_SOFTMAX = 4,
+       GH_LINK_LOGSCALE = 5 };
 
 typedef enum { GH_RESAMPLE_SYSTEMATIC = 0, GH_RESAMPLE_MULTINOMIAL = 1 } gh_resampler;
 

@@ -479,7 +479,7 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
       int dist = (int)hd[0], mm = (int)hd[1], link = (int)hd[2], nv = 1;
       if ((double)dist != hd[0] || (double)mm != hd[1] || (double)link != hd[2]) return -1;
       if (dist == 1) { if (link != 0 || mm < 1 || mm > 32) return -1; nv = mm; }
-      else if (dist == 2) { if (mm != 1 || !(link == 0 || (link == 1 && d == 1))) return -1; }
+      else if (dist == 2) { if (mm != 1 || !(link == 0 || link == 5 || (link == 1 && d == 1))) return -1; }
       else if (dist == 3) { if (mm != 1 || link != 2) return -1; nv = 2; }
       else if (dist == 4) { if (mm != 1 || link != 3) return -1; }
       else if (dist == 5) { if (mm < 2 || mm > 16 || link != 4) return -1; }
@@ -537,6 +537,12 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
         memcpy(blk + mm * d, H, sizeof(double) * mm * d);
         memcpy(blk + 2 * mm * d, c, sizeof(double) * mm);
         m->scst[k] = gauss_cst(mm, LR);
+        i += need;
+      } else if (m->sdist[k] == 2 && m->slink[k] == 5) {  /* h c g s: sd = exp(g.x + s) */
+        int64_t need = 2 * (int64_t)d + 2;
+        if (np < i + need) return -1;
+        m->sP[k] = malloc(sizeof(double) * need);
+        memcpy(m->sP[k], p + i, sizeof(double) * need);
         i += need;
       } else if (m->sdist[k] == 2) {
         int64_t need = m->slink[k] == 0 ? d + 2 : 1;
@@ -781,6 +787,12 @@ static double slot_affine(const double* h, double c, const double* x, int d) {
   for (int j = 0; j < d; ++j) acc = fma(h[j], x[j], acc);
   return acc;
 }
+/* normal.jl:56-60 with std = exp(eta): var = std * std, -(diff^2) / (2 var) - 0.5 log(2 pi var) */
+static double slot_logscale_lpdf(double diff, double eta) {
+  double sd = orc_exp(eta);
+  double var = sd * sd;
+  return -(diff * diff) / (2.0 * var) - 0.5 * orc_log(0x1.921fb54442d18p+2 * var);
+}
 static double slot_lpdf(const model_t* m, const obs_t* o, int k, const double* x) {
   const int d = m->d, mm = m->sm[k];
   const double* P = m->sP[k];
@@ -798,6 +810,7 @@ static double slot_lpdf(const model_t* m, const obs_t* o, int k, const double* x
     case 2: {  /* normal.jl:56-60 */
       double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_affine(P, P[d], x, d);
       double diff = v[0] - mean;
+      if (m->slink[k] == 5) return slot_logscale_lpdf(diff, slot_affine(P + d + 1, P[2 * d + 1], x, d));
       return -(diff * diff) * m->sinv2v[k] + m->scst[k];
     }
     case 3: {  /* poisson.jl:10-12, lambda = exp(h.x + c) */
@@ -912,7 +925,8 @@ static void slot_sim(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, 
       double z[2];
       normals_at(seed, pid, t, 7, draw, 1, z);
       double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_affine(P, P[d], x, d);
-      yk[0] = mean + m->ssd[k] * z[0];
+      double sd = m->slink[k] == 5 ? orc_exp(slot_affine(P + d + 1, P[2 * d + 1], x, d)) : m->ssd[k];
+      yk[0] = mean + sd * z[0];
     } else if (m->sdist[k] == 3) {
       rng(seed, pid, t, 7, draw, w);
       yk[0] = slot_poisson_chop(orc_exp(slot_affine(P, P[d], x, d)), unif53(w[0], w[1]));

@@ -95,6 +95,28 @@ def switching_model():
           "c": [0.0, 0.0, 0.1]}])
 
 
+def sv_model():
+    """A stochastic-volatility model: an AR(1) log-volatility
+    h_t ~ normal(mu + phi (h_{t-1} - mu), sigma) and returns
+    r_t ~ normal(0, exp(h_t / 2)), plus a second return with a mean and its own
+    log-linear scale (normal slots with a log-linear standard deviation)."""
+    mu, phi, sig = -0.5, 0.95, 0.25
+    return gen.SlotSSM(
+        {"form": "affine", "A": [[phi]], "b": [mu * (1 - phi)], "Q": [[sig * sig]], "mu0": [mu],
+         "P0": [[sig * sig / (1 - phi * phi)]]},
+        [{"name": "r", "dist": "normal", "log_sd": {"g": [0.5], "s": 0.0}},
+         {"name": "r2", "dist": "normal", "h": [0.3], "c": 0.1, "log_sd": {"g": [0.25], "s": -0.5}}])
+
+
+def sv_obs(T=12, seed=8):
+    m = sv_model()
+    _, ys = m.simulate(T, np.random.default_rng(seed))
+    obs = [dict(y) for y in ys]
+    del obs[3]["r2"]
+    obs[5] = {}
+    return m, obs
+
+
 def count_obs(T=10, seed=5):
     """Observations with some slots missing at some steps (and one empty step)."""
     m = count_model()
@@ -171,6 +193,41 @@ def test_oracle_slot_scores_equal_reference_densities():
     assert abs(Y[1, 0].mean() - lam.mean()) < 4 * np.sqrt(lam.mean() / n) + 1e-3
     p_on = 1.0 / (1.0 + np.exp(-(s[2]["h"] @ x + s[2]["c"])))
     assert abs(Y[1, 2].mean() - p_on.mean()) < 4 * np.sqrt(0.25 / n)
+
+
+def test_oracle_sv_slot_scores_equal_reference_density():
+    """The log-linear-scale normal slot: simulate's observation column is
+    normal.jl:56-60's logpdf with std = exp(g.x + s) (scipy), the returns
+    divided by their standard deviation are standard normal, and with g = 0
+    the slot scores as the fixed-sd normal slot (to rounding: the fixed slot
+    folds 1/(2 var) and the log-normaliser into constants)."""
+    from scipy import stats
+
+    m = sv_model()
+    T, n = 6, 128
+    X, Y, PS, _ = O.simulate(m, T, n, 3)
+    for t in range(T):
+        h = X[t, 0]
+        ref = (stats.norm.logpdf(Y[t, 0], 0.0, np.exp(0.5 * h))
+               + stats.norm.logpdf(Y[t, 1], 0.3 * h + 0.1, np.exp(0.25 * h - 0.5)))
+        np.testing.assert_allclose(PS[t, 1], ref, rtol=1e-12, atol=1e-12)
+    X, Y, _, _ = O.simulate(m, 2, 40000, 4)
+    z = Y[1, 0] / np.exp(0.5 * X[1, 0])
+    assert abs(z.mean()) < 4 / np.sqrt(40000) and abs(z.var() - 1.0) < 6 * np.sqrt(2 / 40000)
+    lat = {"form": "affine", "A": [[0.9]], "b": [0.0], "Q": [[0.1]], "mu0": [0.0], "P0": [[1.0]]}
+    fixed = gen.SlotSSM(lat, [{"name": "y", "dist": "normal", "h": [1.0], "c": 0.2, "sd": 0.7}])
+    logs = gen.SlotSSM(lat, [{"name": "y", "dist": "normal", "h": [1.0], "c": 0.2,
+                              "log_sd": {"g": [0.0], "s": float(np.log(0.7))}}])
+    _, ys = fixed.simulate(8, np.random.default_rng(1))
+    a = O.run_pf(fixed, ys, 500, 5, thr=0.0)
+    b = O.run_pf(logs, ys, 500, 5, thr=0.0)
+    assert np.array_equal(a.state(), b.state())
+    np.testing.assert_allclose(b.log_weights(), a.log_weights(), rtol=1e-13, atol=1e-12)
+    # the particle filter on it: the log-ML of two seeds agree at this size
+    m, obs = sv_obs()
+    l1 = O.run_pf(m, obs, 20000, 1).log_ml_estimate()
+    l2 = O.run_pf(m, obs, 20000, 2).log_ml_estimate()
+    assert np.isfinite(l1) and abs(l1 - l2) < 0.2
 
 
 def test_slot_model_rejects_bad_descriptions():
@@ -469,6 +526,27 @@ def test_gpu_slots_simulate_equals_oracle_bitexact(gh_ctx):
         X, Y, PS, TOT = O.simulate(m, 6, 777, 21)
         assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
         assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched", [False, True])
+def test_gpu_stochastic_volatility_slots_equal_oracle_bitexact(gh_ctx, batched):
+    """Normal slots with a log-linear standard deviation (the stochastic-
+    volatility emission): GPU == oracle bit for bit (states, weights, parents,
+    score columns; log-ML 1e-9), some steps constraining one slot or none;
+    simulate bit-exact too."""
+    m, obs = sv_obs()
+    n = 6151
+    st = _gpu_run(m, obs, n, 17, batched)
+    orc = _orc_run(m, obs, n, 17)
+    _same(st, orc=orc)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    tr = gen.simulate(m, (7,), num_traces=999, seed=23)
+    X, Y, PS, TOT = O.simulate(m, 7, 999, 23)
+    assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
+    assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
 
 
 @pytest.mark.gpu
