@@ -47,6 +47,10 @@ GH_SL_UNIT0(GH_EXTERN_TEMPLATE)
 GH_SL_UNIT1(GH_EXTERN_TEMPLATE)
 GH_SL_UNIT2(GH_EXTERN_TEMPLATE)
 GH_SL_UNIT3(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT4(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT5(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT6(GH_EXTERN_TEMPLATE)
+GH_SL_UNIT7(GH_EXTERN_TEMPLATE)
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_err;
@@ -588,6 +592,7 @@ struct gh_model {
   // slot family (gh_slots.h): the device description and, per mvnormal slot,
   // the host halves of its observation whitening L_R^-1 (y - c)
   SlotParams slots{};
+  bool slot_lib = false;  // a library slot: the SlotModel<D, true> instantiations
   std::vector<double> slot_c[kMaxSlots], slot_LR[kMaxSlots];
 };
 
@@ -639,6 +644,9 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
     } else if (dist == SLOT_CATEGORICAL) {
       if (mm < 2 || mm > kMaxSlotClasses || link != LINK_SOFTMAX)
         return "slots: categorical slot: 2..16 classes, probs softmax(W x + c)";
+    } else if (dist == SLOT_LIBRARY) {
+      if (lib_nargs(mm) == 0 || link != 0) return "slots: library slot: m names a scalar distribution (gen_hip.h)";
+      m->slot_lib = true;
     } else {
       return "slots: unknown slot distribution";
     }
@@ -725,6 +733,17 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
       sp.sd[k] = sd;
       sp.inv2v[k] = 1.0 / (2.0 * (sd * sd));
       sp.cst[k] = -0.5 * gh_log(2.0 * 0x1.921fb54442d18p+1 * (sd * sd));
+      i += need;
+    } else if (dist == SLOT_LIBRARY) {  // (link h[d] c) per argument
+      const int na = lib_nargs(mm);
+      const int64_t need = (int64_t)na * (d + 2);
+      if (np < i + need) return "slots: too few parameters (library slot: link h c per argument)";
+      for (int j = 0; j < na; ++j) {
+        const double l = p[i + j * (d + 2)];
+        if (!(l == LIB_IDENTITY || l == LIB_EXP || l == LIB_LOGISTIC))
+          return "slots: a library slot's argument link is 0 (identity), 2 (exp) or 3 (logistic)";
+      }
+      h.insert(h.end(), p + i, p + i + need);
       i += need;
     } else if (dist == SLOT_CATEGORICAL) {
       const int64_t need = (int64_t)mm * d + mm;
@@ -1563,7 +1582,10 @@ static int with_model(const gh_model* m, F&& f) {
     case GH_FAMILY_SLOTS:
       switch (m->d) {
 #define GH_SL_CASE(DD) \
-  case DD: f(SlotModel<DD>{}, m->slots); break;
+  case DD:                                                    \
+    if (m->slot_lib) f(SlotModel<DD, true>{}, m->slots);      \
+    else f(SlotModel<DD>{}, m->slots);                        \
+    break;
         GH_SL_CASE(1) GH_SL_CASE(2) GH_SL_CASE(3) GH_SL_CASE(4) GH_SL_CASE(5) GH_SL_CASE(6) GH_SL_CASE(7)
         GH_SL_CASE(8) GH_SL_CASE(9) GH_SL_CASE(10) GH_SL_CASE(11) GH_SL_CASE(12) GH_SL_CASE(13) GH_SL_CASE(14)
         GH_SL_CASE(15) GH_SL_CASE(16)
@@ -1592,7 +1614,10 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
     p.cstq = pf->cstq;
     switch (pf->m->d) {
 #define GH_SLL_CASE(DD) \
-  case DD: launch_step_t<SlotLinModel<DD>>(pf, p, o, a, init, e0, e1); break;
+  case DD:                                                                     \
+    if (pf->m->slot_lib) launch_step_t<SlotLinModel<DD, true>>(pf, p, o, a, init, e0, e1); \
+    else launch_step_t<SlotLinModel<DD>>(pf, p, o, a, init, e0, e1);                     \
+    break;
       GH_SLL_CASE(1) GH_SLL_CASE(2) GH_SLL_CASE(3) GH_SLL_CASE(4) GH_SLL_CASE(5) GH_SLL_CASE(6)
       GH_SLL_CASE(7) GH_SLL_CASE(8) GH_SLL_CASE(9) GH_SLL_CASE(10) GH_SLL_CASE(11) GH_SLL_CASE(12)
       GH_SLL_CASE(13) GH_SLL_CASE(14) GH_SLL_CASE(15) GH_SLL_CASE(16)

@@ -101,10 +101,15 @@ GH_HD double normal_logpdf(double x, double mu, double std) {  // normal.jl:56-6
 }
 
 // ----------------------------------------------------------------- draws
+// (the distribution kernels draw from (seed, id, 0, STREAM_DIST, draw); a slot
+// model's simulate from (seed, particle, t, STREAM_SIM, base + draw))
 struct DistRng {
   uint64_t seed, id;
+  uint32_t t = 0, stream = STREAM_DIST, base = 0;
 };
-GH_HD u32x4 dist_block(const DistRng& r, uint32_t draw) { return rng_block(r.seed, r.id, 0, STREAM_DIST, draw); }
+GH_HD u32x4 dist_block(const DistRng& r, uint32_t draw) {
+  return rng_block(r.seed, r.id, r.t, r.stream, r.base + draw);
+}
 GH_HD double dist_u(const DistRng& r, uint32_t draw) {  // [0, 1)
   const u32x4 w = dist_block(r, draw);
   return u53(w.x, w.y);

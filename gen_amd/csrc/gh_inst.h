@@ -63,38 +63,46 @@
 #define GH_LG_UNIT6(X) GH_LG_DIM(X, 16)
 
 // the slot family (gh_slots.h): SlotModel<D> for d = 1..16, in gh_inst_slots<k>.hip
-#define GH_SL_KERNELS(X, D)                                                                                     \
-  X __global__ void gh::k_step<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
-  X __global__ void gh::k_step<gh::SlotLinModel<D>, true>(const double*, gh::SlotParams, gh::StepObs,             \
+#define GH_SL_KERNELS_L(X, D, L)                                                                                     \
+  X __global__ void gh::k_step<gh::SlotModel<D, L>, true>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::SlotLinModel<D, L>, true>(const double*, gh::SlotParams, gh::StepObs,             \
                                                           gh::StepArgs);                                          \
-  X __global__ void gh::k_step<gh::SlotLinModel<D>, false>(const double*, gh::SlotParams, gh::StepObs,            \
+  X __global__ void gh::k_step<gh::SlotLinModel<D, L>, false>(const double*, gh::SlotParams, gh::StepObs,            \
                                                            gh::StepArgs);                                         \
-  X __global__ void gh::k_step<gh::SlotLinModel<D>, false, true>(const double*, gh::SlotParams, gh::StepObs,      \
+  X __global__ void gh::k_step<gh::SlotLinModel<D, L>, false, true>(const double*, gh::SlotParams, gh::StepObs,      \
                                                                  gh::StepArgs);                                   \
-  X __global__ void gh::k_step<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
-  X __global__ void gh::k_step<gh::SlotModel<D>, false, true>(const double*, gh::SlotParams, gh::StepObs,          \
+  X __global__ void gh::k_step<gh::SlotModel<D, L>, false>(const double*, gh::SlotParams, gh::StepObs, gh::StepArgs); \
+  X __global__ void gh::k_step<gh::SlotModel<D, L>, false, true>(const double*, gh::SlotParams, gh::StepObs,          \
                                                               gh::StepArgs);                                     \
-  X __global__ void gh::k_rejuv<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::RejuvArgs); \
-  X __global__ void gh::k_rejuv<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs,              \
+  X __global__ void gh::k_rejuv<gh::SlotModel<D, L>, true>(const double*, gh::SlotParams, gh::StepObs, gh::RejuvArgs); \
+  X __global__ void gh::k_rejuv<gh::SlotModel<D, L>, false>(const double*, gh::SlotParams, gh::StepObs,              \
                                                          gh::RejuvArgs);                                         \
-  X __global__ void gh::k_mh_drift<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs,            \
+  X __global__ void gh::k_mh_drift<gh::SlotModel<D, L>, true>(const double*, gh::SlotParams, gh::StepObs,            \
                                                            gh::RejuvArgs, gh::DriftSd);                          \
-  X __global__ void gh::k_mh_drift<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs,           \
+  X __global__ void gh::k_mh_drift<gh::SlotModel<D, L>, false>(const double*, gh::SlotParams, gh::StepObs,           \
                                                             gh::RejuvArgs, gh::DriftSd);                         \
-  X __global__ void gh::k_scores<gh::SlotModel<D>>(const double*, gh::SlotParams, gh::ScoreArgs,                 \
+  X __global__ void gh::k_scores<gh::SlotModel<D, L>>(const double*, gh::SlotParams, gh::ScoreArgs,                 \
                                                    const gh::DevScalars*);                                       \
-  X __global__ void gh::k_simulate<gh::SlotModel<D>>(const double*, gh::SlotParams, gh::SimArgs);                 \
-  X __global__ void gh::k_mr_slot_scores<gh::SlotModel<D>>(const double*, gh::SlotParams, gh::StepObs, int,     \
+  X __global__ void gh::k_simulate<gh::SlotModel<D, L>>(const double*, gh::SlotParams, gh::SimArgs);                 \
+  X __global__ void gh::k_mr_slot_scores<gh::SlotModel<D, L>>(const double*, gh::SlotParams, gh::StepObs, int,     \
                                                             const double*, const double*, const int32_t*,        \
                                                             const double*, int64_t, int64_t, int64_t, double*,   \
                                                             int*);                                               \
-  X __global__ void gh::k_pin_pre<gh::SlotModel<D>, true>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs); \
-  X __global__ void gh::k_pin_pre<gh::SlotModel<D>, false>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs);
+  X __global__ void gh::k_pin_pre<gh::SlotModel<D, L>, true>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs); \
+  X __global__ void gh::k_pin_pre<gh::SlotModel<D, L>, false>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs);
+// (L: the instantiations for models with a library slot, gh_inst_slots4..7.hip)
+#define GH_SL_KERNELS(X, D) GH_SL_KERNELS_L(X, D, false)
+#define GH_SLL_KERNELS(X, D) GH_SL_KERNELS_L(X, D, true)
 #define GH_SL_UNIT0(X) \
   GH_SL_KERNELS(X, 1) GH_SL_KERNELS(X, 2) GH_SL_KERNELS(X, 3) GH_SL_KERNELS(X, 4) GH_SL_KERNELS(X, 5) GH_SL_KERNELS(X, 6)
 #define GH_SL_UNIT1(X) GH_SL_KERNELS(X, 7) GH_SL_KERNELS(X, 8) GH_SL_KERNELS(X, 9) GH_SL_KERNELS(X, 10)
 #define GH_SL_UNIT2(X) GH_SL_KERNELS(X, 11) GH_SL_KERNELS(X, 12) GH_SL_KERNELS(X, 13)
 #define GH_SL_UNIT3(X) GH_SL_KERNELS(X, 14) GH_SL_KERNELS(X, 15) GH_SL_KERNELS(X, 16)
+#define GH_SL_UNIT4(X) \
+  GH_SLL_KERNELS(X, 1) GH_SLL_KERNELS(X, 2) GH_SLL_KERNELS(X, 3) GH_SLL_KERNELS(X, 4) GH_SLL_KERNELS(X, 5) GH_SLL_KERNELS(X, 6)
+#define GH_SL_UNIT5(X) GH_SLL_KERNELS(X, 7) GH_SLL_KERNELS(X, 8) GH_SLL_KERNELS(X, 9) GH_SLL_KERNELS(X, 10)
+#define GH_SL_UNIT6(X) GH_SLL_KERNELS(X, 11) GH_SLL_KERNELS(X, 12) GH_SLL_KERNELS(X, 13)
+#define GH_SL_UNIT7(X) GH_SLL_KERNELS(X, 14) GH_SLL_KERNELS(X, 15) GH_SLL_KERNELS(X, 16)
 
 #define GH_EXTERN_TEMPLATE extern template
 #define GH_TEMPLATE template

@@ -19,6 +19,10 @@
 //            poisson(exp(h.x + c))                        poisson.jl:10-12
 //            bernoulli(1 / (1 + exp(-(h.x + c))))         bernoulli.jl:10-12
 //            categorical(softmax(W x + c))                categorical.jl:10-12 (0-based values)
+//            any scalar distribution of Gen's library (gh_dists.h: normal, uniform,
+//            uniform_discrete, bernoulli, gamma, inv_gamma, beta, exponential, poisson,
+//            binom, neg_binom, geometric, laplace, cauchy, beta_uniform) whose
+//            arguments are each link_j(h_j.x + c_j), link identity / exp / logistic
 //
 // Each step constrains any subset of the observed slots (a gh_obs chain with
 // slot ids, choice_map.jl:163-225); the weight is the sum of the present
@@ -39,7 +43,80 @@ constexpr int kMaxSlotD = 16;       // latent dimension (SlotModel<1..16> instan
 constexpr int kMaxSlotClasses = 16;  // categorical slot classes
 constexpr uint32_t kSlotSimDraws = 32;  // simulate(): slot k draws from kSimObsDraw + 32 k
 
-enum SlotDist : int { SLOT_MVNORMAL = 1, SLOT_NORMAL = 2, SLOT_POISSON = 3, SLOT_BERNOULLI = 4, SLOT_CATEGORICAL = 5 };
+enum SlotDist : int {
+  SLOT_MVNORMAL = 1, SLOT_NORMAL = 2, SLOT_POISSON = 3, SLOT_BERNOULLI = 4, SLOT_CATEGORICAL = 5,
+  SLOT_LIBRARY = 6  // m = the gh_dists.h distribution id
+};
+constexpr uint32_t kSlotLibDraw = 1024;  // simulate(): library slot k draws from kSlotLibDraw + 256 k
+
+// A library slot's distribution: its argument count (0: not a scalar
+// distribution a slot may name)
+GH_HD int lib_nargs(int dist) {
+  switch (dist) {
+    case DIST_BERNOULLI: case DIST_EXPONENTIAL: case DIST_POISSON: case DIST_GEOMETRIC:
+      return 1;
+    case DIST_NORMAL: case DIST_UNIFORM_CONTINUOUS: case DIST_UNIFORM_DISCRETE: case DIST_GAMMA:
+    case DIST_INV_GAMMA: case DIST_BETA: case DIST_BINOMIAL: case DIST_NEG_BINOMIAL: case DIST_LAPLACE:
+    case DIST_CAUCHY:
+      return 2;
+    case DIST_BETA_UNIFORM:
+      return 3;
+    default:
+      return 0;
+  }
+}
+// argument j of a library slot: link (0 identity, 2 exp, 3 logistic) applied to c + h.x
+// (the block holds link h[d] c per argument)
+enum : int { LIB_IDENTITY = 0, LIB_EXP = 2, LIB_LOGISTIC = 3 };
+GH_HD double lib_link(int link, double eta) {
+  return link == LIB_EXP ? gh_exp(eta) : (link == LIB_LOGISTIC ? 1.0 / (1.0 + gh_exp(-eta)) : eta);
+}
+// the library's logpdf and sampler by run-time id (out of line: one call per
+// library slot, no registers taken from the other slots' code)
+static __device__ __noinline__ double lib_logpdf(int dist, double v, double a0, double a1, double a2) {
+  const double P[3] = {a0, a1, a2};
+  switch (dist) {
+    case DIST_NORMAL: return dist_logpdf<DIST_NORMAL>(&v, 1, P, 1, 0);
+    case DIST_UNIFORM_CONTINUOUS: return dist_logpdf<DIST_UNIFORM_CONTINUOUS>(&v, 1, P, 1, 0);
+    case DIST_UNIFORM_DISCRETE: return dist_logpdf<DIST_UNIFORM_DISCRETE>(&v, 1, P, 1, 0);
+    case DIST_BERNOULLI: return dist_logpdf<DIST_BERNOULLI>(&v, 1, P, 1, 0);
+    case DIST_GAMMA: return dist_logpdf<DIST_GAMMA>(&v, 1, P, 1, 0);
+    case DIST_INV_GAMMA: return dist_logpdf<DIST_INV_GAMMA>(&v, 1, P, 1, 0);
+    case DIST_BETA: return dist_logpdf<DIST_BETA>(&v, 1, P, 1, 0);
+    case DIST_EXPONENTIAL: return dist_logpdf<DIST_EXPONENTIAL>(&v, 1, P, 1, 0);
+    case DIST_POISSON: return dist_logpdf<DIST_POISSON>(&v, 1, P, 1, 0);
+    case DIST_BINOMIAL: return dist_logpdf<DIST_BINOMIAL>(&v, 1, P, 1, 0);
+    case DIST_NEG_BINOMIAL: return dist_logpdf<DIST_NEG_BINOMIAL>(&v, 1, P, 1, 0);
+    case DIST_GEOMETRIC: return dist_logpdf<DIST_GEOMETRIC>(&v, 1, P, 1, 0);
+    case DIST_LAPLACE: return dist_logpdf<DIST_LAPLACE>(&v, 1, P, 1, 0);
+    case DIST_CAUCHY: return dist_logpdf<DIST_CAUCHY>(&v, 1, P, 1, 0);
+    default: return dist_logpdf<DIST_BETA_UNIFORM>(&v, 1, P, 1, 0);
+  }
+}
+static __device__ __noinline__ double lib_random(int dist, uint64_t seed, uint64_t pid, uint32_t t, uint32_t base, double a0,
+                                          double a1, double a2, const double* tab) {
+  const double P[3] = {a0, a1, a2};
+  const DistRng r{seed, pid, t, STREAM_SIM, base};
+  double x = 0.0;
+  switch (dist) {
+    case DIST_NORMAL: dist_random<DIST_NORMAL>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_UNIFORM_CONTINUOUS: dist_random<DIST_UNIFORM_CONTINUOUS>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_UNIFORM_DISCRETE: dist_random<DIST_UNIFORM_DISCRETE>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_BERNOULLI: dist_random<DIST_BERNOULLI>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_GAMMA: dist_random<DIST_GAMMA>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_INV_GAMMA: dist_random<DIST_INV_GAMMA>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_BETA: dist_random<DIST_BETA>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_EXPONENTIAL: dist_random<DIST_EXPONENTIAL>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_POISSON: dist_random<DIST_POISSON>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_BINOMIAL: dist_random<DIST_BINOMIAL>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_NEG_BINOMIAL: dist_random<DIST_NEG_BINOMIAL>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_GEOMETRIC: dist_random<DIST_GEOMETRIC>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_LAPLACE: dist_random<DIST_LAPLACE>(r, &x, 1, P, 1, 0, tab); break;
+    case DIST_CAUCHY: dist_random<DIST_CAUCHY>(r, &x, 1, P, 1, 0, tab); break;
+    default: dist_random<DIST_BETA_UNIFORM>(r, &x, 1, P, 1, 0, tab); break;
+  }
+  return x;
+}
 enum SlotLink : int {
   LINK_AFFINE = 0, LINK_KITAGAWA = 1, LINK_EXP = 2, LINK_LOGISTIC = 3, LINK_SOFTMAX = 4,
   LINK_LOGSCALE = 5  // normal slot with a log-linear standard deviation
@@ -61,7 +138,7 @@ struct SlotParams {
   int yoff[kMaxSlots];  // the slot's rows in simulate()'s output
   // per slot: mvnormal M = L_R^-1 H [m*d] | H [m*d] | c [m] | L_R [m*m];
   // normal / poisson / bernoulli h [d] | c (log-linear normal: h [d] | c | g [d] | s);
-  // categorical W [m*d] | c [m]
+  // categorical W [m*d] | c [m]; library (link | h [d] | c) per argument
   const double* P[kMaxSlots];
   double cst[kMaxSlots];    // mvnormal -0.5 (m log 2pi + log det R); normal -0.5 log(2 pi sd^2)
   double inv2v[kMaxSlots];  // normal 1 / (2 sd^2)
@@ -89,7 +166,9 @@ struct SlotParams {
   }
 };
 
-template <int D>
+// LIB: the model has a library slot (its logpdf and sampler are out-of-line
+// calls; the instantiations without them keep call-free kernels)
+template <int D, bool LIB = false>
 struct SlotModel {
   static constexpr int kD = D;
   static constexpr int kMinWaves = D <= 3 ? 8 : (D <= 6 ? 6 : (D <= 10 ? 4 : 3));
@@ -111,6 +190,15 @@ struct SlotModel {
     return -(diff * diff) / (2.0 * var) - 0.5 * gh_log(0x1.921fb54442d18p+2 * var);
   }
 
+  // a library slot's arguments at latent x
+  __device__ static void lib_args(const double* P, int na, const double* x, double a[3]) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double* B = P + j * (D + 2);
+      a[j] = j < na ? lib_link((int)B[0], affine(B + 1, B[D + 1], x)) : 0.0;
+    }
+  }
+
   // the class of a one-hot categorical latent
   __device__ static int onehot(const double* x) {
     int z = 0;
@@ -125,6 +213,15 @@ struct SlotModel {
     const double* v = o.v + p.voff[k];
     const int m = p.m[k];
     switch (p.dist[k]) {
+      case SLOT_LIBRARY: {  // the library's logpdf (gh_dists.h, the reference's formulas)
+        if constexpr (LIB) {
+          double a[3];
+          lib_args(P, lib_nargs(m), x, a);
+          return lib_logpdf(m, v[0], a[0], a[1], a[2]);
+        } else {
+          return NAN;  // (never: the host picks the LIB instantiation for such a model)
+        }
+      }
       case SLOT_MVNORMAL: {  // LGModel::obs (dense): v = L_R^-1 (y - c)
         double quad = 0.0;
         for (int r = 0; r < m; ++r) {
@@ -280,6 +377,18 @@ struct SlotModel {
       double* yk = y + (int64_t)p.yoff[k] * ys;
       double lp;
       switch (p.dist[k]) {
+        case SLOT_LIBRARY: {  // the library's sampler (gh_dists.h) on draws kSlotLibDraw + 256 k
+          if constexpr (LIB) {
+            double a[3];
+            lib_args(P, lib_nargs(m), x, a);
+            yk[0] = lib_random(m, seed, pid, t, kSlotLibDraw + 256u * (uint32_t)k, a[0], a[1], a[2], tab);
+            lp = lib_logpdf(m, yk[0], a[0], a[1], a[2]);
+          } else {
+            yk[0] = NAN;
+            lp = NAN;
+          }
+          break;
+        }
         case SLOT_MVNORMAL: {  // y = H x + c + L_R z, scored through L_R^-1 (y - c) (LGModel::sim_obs)
           const double *H = P + m * D, *c = H + m * D, *LR = c + m;
           double z[kMaxObs], v[kMaxObs];
@@ -379,12 +488,12 @@ struct SlotModel {
 // trace_translators.jl:775-802): the model's score of the new choices — the
 // latent's logpdf (affine or Kitagawa) and the present slots' — minus q's
 // logpdf of the drawn value.
-template <int D>
+template <int D, bool LIB = false>
 struct SlotLinModel {
   static constexpr int kD = D;
-  static constexpr int kMinWaves = SlotModel<D>::kMinWaves;
+  static constexpr int kMinWaves = SlotModel<D, LIB>::kMinWaves;
   using Params = SlotParams;
-  using Prior = SlotModel<D>;
+  using Prior = SlotModel<D, LIB>;
 
   __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return Prior::loglik(p, o, x); }
 

@@ -348,6 +348,12 @@ class BayesianLinearRegression(Model):
 # slot distributions / mean forms of GH_FAMILY_SLOTS (include/gen_hip.h)
 _SLOT_DIST = {"mvnormal": 1, "normal": 2, "poisson": 3, "bernoulli": 4, "categorical": 5}
 _LINK = {"affine": 0, "x^2/20": 1, "exp": 2, "logistic": 3, "softmax": 4, "logscale": 5}
+# library slots (slot distribution 6): any scalar distribution of Gen's library by
+# its gh_dists.h id, each argument link(h.x + c)
+_LIB = {"normal": (1, 2), "uniform": (4, 2), "uniform_discrete": (5, 2), "bernoulli": (6, 1), "gamma": (8, 2),
+        "inv_gamma": (9, 2), "beta": (10, 2), "exponential": (11, 1), "poisson": (12, 1), "binom": (13, 2),
+        "neg_binom": (14, 2), "geometric": (15, 1), "laplace": (16, 2), "cauchy": (17, 2), "beta_uniform": (19, 3)}
+_ARG_LINK = {"identity": 0, "exp": 2, "logistic": 3}
 
 
 class SlotSSM(Model):
@@ -366,6 +372,8 @@ class SlotSSM(Model):
             @trace(poisson(exp(p.h' * x + p.c0)), :count)            # slot "poisson"
             @trace(bernoulli(1 / (1 + exp(-(p.h' * x + p.c0)))), :on)  # slot "bernoulli"
             @trace(categorical(softmax(p.W * x + p.c)), :kind)       # slot "categorical" (0-based here)
+            @trace(gamma(exp(p.h' * x + p.c0), 2.0), :g)               # a library slot (any scalar
+                                                                     # distribution, arguments link(h.x + c))
             return x
         end
 
@@ -380,7 +388,12 @@ class SlotSSM(Model):
     slots:  [{"name", "dist", ...}] with per distribution
             mvnormal: H [m, d], c [m], R [m, m]; normal: h [d], c, sd (or mean "x^2/20", sd;
             or h [d], c, "log_sd": {"g": [d], "s"} for sd = exp(g.x + s) — stochastic volatility);
-            poisson / bernoulli: h [d], c; categorical: W [m, d], c [m]
+            poisson / bernoulli: h [d], c; categorical: W [m, d], c [m];
+            library: "args": [a_1, ...], one per argument of the named distribution
+            (normal, uniform, uniform_discrete, bernoulli, gamma, inv_gamma, beta,
+            exponential, poisson, binom, neg_binom, geometric, laplace, cauchy,
+            beta_uniform — Gen's argument order), each a constant or
+            {"link": "identity" | "exp" | "logistic", "h": [d], "c"}
     Observations of step t: {("chain", t, name): value} (any subset of the slots).
     """
 
@@ -415,6 +428,25 @@ class SlotSSM(Model):
         for s in slots:
             s = dict(s)
             dist = s["dist"]
+            if "args" in s:  # a library slot
+                if dist not in _LIB:
+                    raise ValueError(f"library slot distribution {dist!r}: one of {sorted(_LIB)}")
+                lid, na = _LIB[dist]
+                if len(s["args"]) != na:
+                    raise ValueError(f"{dist} takes {na} arguments")
+                args = []
+                for a in s["args"]:
+                    if isinstance(a, dict):
+                        link = a.get("link", "identity")
+                        if link not in _ARG_LINK:
+                            raise ValueError(f"argument link {link!r}")
+                        h = np.asarray(a.get("h", np.zeros(self.d)), dtype=np.float64).reshape(self.d)
+                        args.append((link, h, float(a.get("c", 0.0))))
+                    else:
+                        args.append(("identity", np.zeros(self.d), float(a)))
+                s.update(args=args, lib=lid, m=lid, link="library")
+                self.slots.append(s)
+                continue
             if dist not in _SLOT_DIST:
                 raise ValueError(f"slot distribution {dist!r}")
             if dist == "mvnormal":
@@ -442,12 +474,15 @@ class SlotSSM(Model):
                     s["c"] = float(s.get("c", 0.0))
             self.slots.append(s)
         self.names = [s["name"] for s in self.slots]
-        self.dy = sum(s["m"] if s["dist"] == "mvnormal" else 1 for s in self.slots)
+        self.dy = sum(s["m"] if s["dist"] == "mvnormal" and "lib" not in s else 1 for s in self.slots)
 
     def params(self):
         code = {"affine": 2.0 if self.inputs else 0.0, "kitagawa": 1.0, "categorical": 3.0}[self.form]
         p = [code, float(len(self.slots))]
         for s in self.slots:
+            if "lib" in s:
+                p += [6.0, float(s["lib"]), 0.0]
+                continue
             p += [float(_SLOT_DIST[s["dist"]]), float(s["m"]), float(_LINK[s["link"]])]
         if self.form == "affine":
             p += list(self.A.ravel()) + list(self.b) + list(self.Q.ravel()) + list(self.mu0) + list(self.P0.ravel())
@@ -456,7 +491,10 @@ class SlotSSM(Model):
         else:
             p += [self.mu1, self.s1, self.sd_x]
         for s in self.slots:
-            if s["dist"] == "mvnormal":
+            if "lib" in s:
+                for link, h, c in s["args"]:
+                    p += [float(_ARG_LINK[link]), *h, c]
+            elif s["dist"] == "mvnormal":
                 p += list(s["H"].ravel()) + list(s["c"]) + list(s["R"].ravel())
             elif s["dist"] == "normal" and s["link"] == "logscale":
                 p += [*s["h"], s["c"], *s["g"], s["s"]]
@@ -538,6 +576,87 @@ class SlotSSM(Model):
         eta = float(s["h"] @ x + s["c"])
         return {"normal": eta, "poisson": np.exp(eta), "bernoulli": 1.0 / (1.0 + np.exp(-eta))}[s["dist"]]
 
+    @staticmethod
+    def lib_args(s, x) -> list:
+        """A library slot's arguments at latent x."""
+        x = np.atleast_1d(x)
+        out = []
+        for link, h, c in s["args"]:
+            eta = float(h @ x + c)
+            out.append({"identity": eta, "exp": float(np.exp(eta)), "logistic": 1.0 / (1.0 + np.exp(-eta))}[link])
+        return out
+
+    @staticmethod
+    def lib_logpdf(dist: str, y: float, a: list) -> float:
+        """The reference's logpdf of a library distribution (scipy's densities;
+        Gen's argument conventions: exponential(rate), gamma / inv_gamma(shape,
+        scale), neg_binom / geometric count failures, uniform_discrete(lo, hi)
+        inclusive, beta_uniform(theta, a, b))."""
+        from scipy import stats
+
+        if dist == "normal":
+            return float(stats.norm.logpdf(y, a[0], a[1]))
+        if dist == "uniform":
+            return float(stats.uniform.logpdf(y, a[0], a[1] - a[0]))
+        if dist == "uniform_discrete":
+            return float(stats.randint.logpmf(y, a[0], a[1] + 1))
+        if dist == "bernoulli":
+            return float(np.log(a[0]) if y else np.log(1.0 - a[0]))
+        if dist == "gamma":
+            return float(stats.gamma.logpdf(y, a[0], scale=a[1]))
+        if dist == "inv_gamma":
+            return float(stats.invgamma.logpdf(y, a[0], scale=a[1]))
+        if dist == "beta":
+            return float(stats.beta.logpdf(y, a[0], a[1]))
+        if dist == "exponential":
+            return float(stats.expon.logpdf(y, scale=1.0 / a[0]))
+        if dist == "poisson":
+            return float(stats.poisson.logpmf(y, a[0]))
+        if dist == "binom":
+            return float(stats.binom.logpmf(y, a[0], a[1]))
+        if dist == "neg_binom":
+            return float(stats.nbinom.logpmf(y, a[0], a[1]))
+        if dist == "geometric":
+            return float(stats.geom.logpmf(y + 1, a[0]))
+        if dist == "laplace":
+            return float(stats.laplace.logpdf(y, a[0], a[1]))
+        if dist == "cauchy":
+            return float(stats.cauchy.logpdf(y, a[0], a[1]))
+        th = a[0]  # beta_uniform
+        return float(np.logaddexp(np.log(th) + stats.beta.logpdf(y, a[1], a[2]), np.log(1.0 - th)))
+
+    @staticmethod
+    def lib_sample(dist: str, a: list, rng: np.random.Generator) -> float:
+        if dist == "normal":
+            return float(rng.normal(a[0], a[1]))
+        if dist == "uniform":
+            return float(rng.uniform(a[0], a[1]))
+        if dist == "uniform_discrete":
+            return float(rng.integers(int(a[0]), int(a[1]) + 1))
+        if dist == "bernoulli":
+            return float(rng.random() < a[0])
+        if dist == "gamma":
+            return float(rng.gamma(a[0], a[1]))
+        if dist == "inv_gamma":
+            return float(a[1] / rng.gamma(a[0], 1.0))
+        if dist == "beta":
+            return float(rng.beta(a[0], a[1]))
+        if dist == "exponential":
+            return float(rng.exponential(1.0 / a[0]))
+        if dist == "poisson":
+            return float(rng.poisson(a[0]))
+        if dist == "binom":
+            return float(rng.binomial(int(a[0]), a[1]))
+        if dist == "neg_binom":
+            return float(rng.negative_binomial(a[0], a[1]))
+        if dist == "geometric":
+            return float(rng.geometric(a[0]) - 1)
+        if dist == "laplace":
+            return float(rng.laplace(a[0], a[1]))
+        if dist == "cauchy":
+            return float(a[0] + a[1] * rng.standard_cauchy())
+        return float(rng.beta(a[1], a[2]) if rng.random() < a[0] else rng.random())
+
     def slot_sd(self, s, x) -> float:
         """A normal slot's standard deviation at latent x."""
         if s["link"] == "logscale":
@@ -550,6 +669,8 @@ class SlotSSM(Model):
         from math import lgamma
 
         s = self.slots[k]
+        if "lib" in s:
+            return self.lib_logpdf(s["dist"], float(y), self.lib_args(s, x))
         mp = self._mean_param(s, x)
         if s["dist"] == "mvnormal":
             return _mvn_logpdf(np.atleast_1d(y), mp, s["R"])
@@ -582,6 +703,9 @@ class SlotSSM(Model):
             xs[t - 1] = x
             y = {}
             for s in self.slots:
+                if "lib" in s:
+                    y[s["name"]] = self.lib_sample(s["dist"], self.lib_args(s, x), rng)
+                    continue
                 mp = self._mean_param(s, x)
                 if s["dist"] == "mvnormal":
                     y[s["name"]] = rng.multivariate_normal(mp, s["R"])

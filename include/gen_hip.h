@@ -123,6 +123,14 @@ typedef enum {
        GH_SLOT_BERNOULLI, m = 1, GH_LINK_LOGISTIC: h[d] c   y ~ bernoulli(1 / (1 + exp(-(h.x + c)))) (0 / 1)
        GH_SLOT_CATEGORICAL, m = classes 2..16, GH_LINK_SOFTMAX: W[m*d] c[m]
                                      y ~ categorical(softmax(W x + c)), 0-based class
+       GH_SLOT_LIBRARY, m = a scalar distribution of Gen's library by its
+         gh_dist_desc id (GH_DIST_NORMAL, _UNIFORM_CONTINUOUS, _UNIFORM_DISCRETE,
+         _BERNOULLI, _GAMMA, _INV_GAMMA, _BETA, _EXPONENTIAL, _POISSON, _BINOMIAL,
+         _NEG_BINOMIAL, _GEOMETRIC, _LAPLACE, _CAUCHY, _BETA_UNIFORM), link 0:
+         per argument (Gen's order) link_j h_j[d] c_j, the argument being
+         link_j(h_j.x + c_j) with link_j GH_ARG_IDENTITY, GH_ARG_EXP or
+         GH_ARG_LOGISTIC; y ~ dist(args...) scored by the library's logpdf
+         (gh_dist_logpdf's formulas) and drawn by its sampler in simulate
      At most 32 observed values per step (a poisson slot counts 2).  An LGSSM
      or Kitagawa model written as slots filters bit for bit as its family does
      (those stay the fast paths); the default proposal or GH_PROPOSAL_LINEAR
@@ -135,7 +143,9 @@ enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1, GH_SLOT_LAT_AFFINE_INPU
 /* gh_obs.slot of a step's latent input u_t (latent form 2): d values, an
    argument of the step's kernel application, not a choice */
 enum { GH_SLOT_INPUT = -1 };
-enum { GH_SLOT_MVNORMAL = 1, GH_SLOT_NORMAL = 2, GH_SLOT_POISSON = 3, GH_SLOT_BERNOULLI = 4, GH_SLOT_CATEGORICAL = 5 };
+enum { GH_SLOT_MVNORMAL = 1, GH_SLOT_NORMAL = 2, GH_SLOT_POISSON = 3, GH_SLOT_BERNOULLI = 4, GH_SLOT_CATEGORICAL = 5,
+       GH_SLOT_LIBRARY = 6 };
+enum { GH_ARG_IDENTITY = 0, GH_ARG_EXP = 2, GH_ARG_LOGISTIC = 3 };  /* a library slot's argument links */
 enum { GH_LINK_AFFINE = 0, GH_LINK_KITAGAWA = 1, GH_LINK_EXP = 2, GH_LINK_LOGISTIC = 3, GH_LINK_SOFTMAX = 4,
        GH_LINK_LOGSCALE = 5 };
 

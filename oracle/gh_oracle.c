@@ -390,6 +390,17 @@ out:
   return rc;
 }
 
+/* a library slot (dist 6, m = the distribution id of gh_dists.h): the scalar
+   distributions and their argument counts (lib_nargs); argument j is
+   link_j(c_j + h_j.x), link 0 identity, 2 exp, 3 logistic */
+static int slot_lib_nargs(int dist) {
+  switch (dist) {
+    case 6: case 11: case 12: case 15: return 1;
+    case 1: case 4: case 5: case 8: case 9: case 10: case 13: case 14: case 16: case 17: return 2;
+    case 19: return 3;
+    default: return 0;
+  }
+}
 static int model_build(model_t* m, int family, int d, int dy, int k, int v, const double* p,
                        int64_t np) {
   memset(m, 0, sizeof(*m));
@@ -483,6 +494,7 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
       else if (dist == 3) { if (mm != 1 || link != 2) return -1; nv = 2; }
       else if (dist == 4) { if (mm != 1 || link != 3) return -1; }
       else if (dist == 5) { if (mm < 2 || mm > 16 || link != 4) return -1; }
+      else if (dist == 6) { if (slot_lib_nargs(mm) == 0 || link != 0) return -1; }
       else return -1;
       m->sdist[k] = dist; m->sm[k] = mm; m->slink[k] = link;
       m->svoff[k] = voff; m->syoff[k] = yoff;
@@ -554,6 +566,18 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
         m->ssd[k] = sd;
         m->sinv2v[k] = 1.0 / (2.0 * (sd * sd));
         m->scst[k] = -0.5 * orc_log(2.0 * 0x1.921fb54442d18p+1 * (sd * sd));
+        i += need;
+      } else if (m->sdist[k] == 6) {  /* (link h[d] c) per argument */
+        int na = slot_lib_nargs(mm);
+        int64_t need = (int64_t)na * (d + 2);
+        if (np < i + need) return -1;
+        for (int j = 0; j < na; ++j) {
+          double l = p[i + j * (d + 2)];
+          if (!(l == 0.0 || l == 2.0 || l == 3.0)) return -1;
+        }
+        m->sP[k] = malloc(sizeof(double) * (size_t)(3 * (d + 2)));
+        memset(m->sP[k], 0, sizeof(double) * (size_t)(3 * (d + 2)));
+        memcpy(m->sP[k], p + i, sizeof(double) * need);
         i += need;
       } else if (m->sdist[k] == 5) {
         int64_t need = (int64_t)mm * d + mm;
@@ -782,6 +806,12 @@ static double lin_draw(const model_t* m, const double* xp, const double* z, doub
 }
 
 /* ---- the slot family (gen_amd/csrc/gh_slots.h SlotModel, line for line) */
+/* a draw's counter: (seed, id, 0, S_DIST, draw) for the distribution entry
+   points, (seed, particle, t, S_SIM, base + draw) for a slot model's simulate */
+typedef struct { uint64_t seed, id; uint32_t t, stream, base; } od_rng;
+static double od_logpdf(int dist, const double* x, int64_t xs, const double* P, int D, int K);
+static void od_random(int dist, const od_rng* r, double* x, int64_t xs, const double* P, int D, int K);
+#define SLOT_LIB_DRAW 1024u /* simulate(): library slot k draws from SLOT_LIB_DRAW + 256 k */
 static double slot_affine(const double* h, double c, const double* x, int d) {
   double acc = c;
   for (int j = 0; j < d; ++j) acc = fma(h[j], x[j], acc);
@@ -793,11 +823,25 @@ static double slot_logscale_lpdf(double diff, double eta) {
   double var = sd * sd;
   return -(diff * diff) / (2.0 * var) - 0.5 * orc_log(0x1.921fb54442d18p+2 * var);
 }
+static double slot_link(int link, double eta) {
+  return link == 2 ? orc_exp(eta) : (link == 3 ? 1.0 / (1.0 + orc_exp(-eta)) : eta);
+}
+static void slot_lib_args(const double* P, int na, const double* x, int d, double a[3]) {
+  for (int j = 0; j < 3; ++j) {
+    const double* B = P + j * (d + 2);
+    a[j] = j < na ? slot_link((int)B[0], slot_affine(B + 1, B[d + 1], x, d)) : 0.0;
+  }
+}
 static double slot_lpdf(const model_t* m, const obs_t* o, int k, const double* x) {
   const int d = m->d, mm = m->sm[k];
   const double* P = m->sP[k];
   const double* v = o->bt + m->svoff[k];
   switch (m->sdist[k]) {
+    case 6: {  /* the library's logpdf (od_logpdf: the reference's formulas) */
+      double a[3];
+      slot_lib_args(P, slot_lib_nargs(mm), x, d, a);
+      return od_logpdf(mm, v, 1, a, 1, 0);
+    }
     case 1: {  /* mvnormal(H x + c, R) through L_R^-1 (y - c) (mvnormal.jl:12-16) */
       double quad = 0.0;
       for (int r = 0; r < mm; ++r) {
@@ -911,7 +955,12 @@ static void slot_sim(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, 
     const double* P = m->sP[k];
     double* yk = y + m->syoff[k];
     uint32_t w[4];
-    if (m->sdist[k] == 1) {
+    if (m->sdist[k] == 6) {
+      double a[3];
+      slot_lib_args(P, slot_lib_nargs(mm), x, d, a);
+      const od_rng r = {seed, pid, t, 7, SLOT_LIB_DRAW + 256u * (uint32_t)k};
+      od_random(mm, &r, yk, 1, a, 1, 0);
+    } else if (m->sdist[k] == 1) {
       const double *H = P + mm * d, *c = H + mm * d, *LR = c + mm;
       double z[32];
       normals_at(seed, pid, t, 7, draw, mm, z);
@@ -2455,23 +2504,24 @@ double orc_lgamma(double x) {
 static double od_xlogy(double x, double y) { return x == 0.0 ? 0.0 : x * orc_log(y); }
 static double od_xlog1py(double x, double y) { return x == 0.0 ? 0.0 : x * orc_log1p(y); }
 
-static double od_u(uint64_t seed, uint64_t id, uint32_t draw) {
+static void od_block(const od_rng* r, uint32_t draw, uint32_t w[4]) { rng(r->seed, r->id, r->t, r->stream, r->base + draw, w); }
+static double od_u(const od_rng* r, uint32_t draw) {
   uint32_t w[4];
-  rng(seed, id, 0, S_DIST, draw, w);
+  od_block(r, draw, w);
   return unif53(w[0], w[1]);
 }
 static double od_one_minus_u(uint32_t a, uint32_t b) {
   uint32_t hi = a >> 11, lo = ((a << 21) & 0xFC000000u) | (b >> 6);
   return fma(-(double)lo, 0x1p-53, fma(-(double)hi, 0x1p-21, 1.0));
 }
-static double od_upos(uint64_t seed, uint64_t id, uint32_t draw) {
+static double od_upos(const od_rng* r, uint32_t draw) {
   uint32_t w[4];
-  rng(seed, id, 0, S_DIST, draw, w);
+  od_block(r, draw, w);
   return od_one_minus_u(w[0], w[1]);
 }
-static double od_normal(uint64_t seed, uint64_t id, uint32_t draw) {
+static double od_normal(const od_rng* r, uint32_t draw) {
   uint32_t w[4];
-  rng(seed, id, 0, S_DIST, draw, w);
+  od_block(r, draw, w);
   double z0, z1;
   box_muller(w[0], w[1], w[2], &z0, &z1);
   return z0;
@@ -2491,20 +2541,20 @@ static int od_cat(const double* p, int K, double u) {
 
 /* Gamma(a, 1): Marsaglia & Tsang, "A simple method for generating gamma
    variables" (2000); round i: normal from draw d0 + 2i, uniform from d0 + 2i + 1 */
-static double od_gamma(uint64_t seed, uint64_t id, double a, uint32_t d0) {
+static double od_gamma(const od_rng* r, double a, uint32_t d0) {
   if (!(a > 0.0)) return NAN;
   double boost = 1.0;
   if (a < 1.0) {
-    boost = orc_exp(orc_log(od_upos(seed, id, d0 + OD_GAMMA_BOOST)) / a);
+    boost = orc_exp(orc_log(od_upos(r, d0 + OD_GAMMA_BOOST)) / a);
     a = a + 1.0;
   }
   double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d);
   for (int i = 0; i < OD_GAMMA_ITERS; ++i) {
-    double x = od_normal(seed, id, d0 + 2u * (uint32_t)i);
+    double x = od_normal(r, d0 + 2u * (uint32_t)i);
     double v = 1.0 + c * x;
     if (v <= 0.0) continue;
     v = v * v * v;
-    double u = od_upos(seed, id, d0 + 2u * (uint32_t)i + 1u);
+    double u = od_upos(r, d0 + 2u * (uint32_t)i + 1u);
     double x2 = x * x;
     if (u < 1.0 - 0.0331 * (x2 * x2)) return (d * v) * boost;
     if (orc_log(u) < 0.5 * x2 + d * ((1.0 - v) + orc_log(v))) return (d * v) * boost;
@@ -2513,10 +2563,10 @@ static double od_gamma(uint64_t seed, uint64_t id, double a, uint32_t d0) {
 }
 
 /* chop-down inversion from the mode: U - pmf(m) - pmf(m+1) - pmf(m-1) - ... */
-static double od_poisson(uint64_t seed, uint64_t id, double lam, uint32_t draw) {
+static double od_poisson(const od_rng* r, double lam, uint32_t draw) {
   if (lam == 0.0) return 0.0;
   if (!(lam > 0.0) || lam == INFINITY) return NAN;
-  double m = floor(lam), u = od_u(seed, id, draw);
+  double m = floor(lam), u = od_u(r, draw);
   double pm = orc_exp(od_xlogy(m, lam) - lam - orc_lgamma(m + 1.0));
   u -= pm;
   if (u <= 0.0) return m;
@@ -2530,13 +2580,13 @@ static double od_poisson(uint64_t seed, uint64_t id, double lam, uint32_t draw) 
   return m;
 }
 
-static double od_binomial(uint64_t seed, uint64_t id, double n, double p, uint32_t draw) {
+static double od_binomial(const od_rng* r, double n, double p, uint32_t draw) {
   if (!(p >= 0.0 && p <= 1.0) || !(n >= 0.0)) return NAN;
   if (p == 0.0 || n == 0.0) return 0.0;
   if (p == 1.0) return n;
   double q = 1.0 - p, m = floor((n + 1.0) * p);
   if (m > n) m = n;
-  double u = od_u(seed, id, draw);
+  double u = od_u(r, draw);
   double pm = orc_exp(((orc_lgamma(n + 1.0) - orc_lgamma(m + 1.0)) - orc_lgamma(n - m + 1.0)) + od_xlogy(m, p) +
                       od_xlog1py(n - m, -p));
   u -= pm;
@@ -2623,9 +2673,10 @@ static double od_logpdf(int dist, const double* x, int64_t xs, const double* P, 
   }
 }
 
-static void od_random(int dist, uint64_t seed, uint64_t id, double* x, int64_t xs, const double* P, int D, int K) {
+static void od_random(int dist, const od_rng* r, double* x, int64_t xs, const double* P, int D, int K) {
+  const uint64_t seed = r->seed, id = r->id;  /* (the vector draws: distribution entry points only) */
   switch (dist) {
-    case OD_NORMAL: x[0] = P[0] + P[1] * od_normal(seed, id, 0); return; /* normal.jl:96 */
+    case OD_NORMAL: x[0] = P[0] + P[1] * od_normal(r, 0); return; /* normal.jl:96 */
     case OD_BNORMAL:
     case OD_MVNORMAL: {
       double z[32];
@@ -2642,52 +2693,52 @@ static void od_random(int dist, uint64_t seed, uint64_t id, double* x, int64_t x
       }
       return;
     }
-    case OD_UNIF: x[0] = od_u(seed, id, 0) * (P[1] - P[0]) + P[0]; return; /* uniform_continuous.jl:21-23 */
-    case OD_UDISC: x[0] = P[0] + floor(od_u(seed, id, 0) * ((P[1] - P[0]) + 1.0)); return;
-    case OD_BERN: x[0] = od_u(seed, id, 0) < P[0] ? 1.0 : 0.0; return; /* bernoulli.jl:19 */
-    case OD_CAT: x[0] = (double)(od_cat(P, K, od_u(seed, id, 0)) + 1); return;
-    case OD_GAMMA: x[0] = P[1] * od_gamma(seed, id, P[0], 0); return;
-    case OD_INVGAMMA: x[0] = P[1] / od_gamma(seed, id, P[0], 0); return;
+    case OD_UNIF: x[0] = od_u(r, 0) * (P[1] - P[0]) + P[0]; return; /* uniform_continuous.jl:21-23 */
+    case OD_UDISC: x[0] = P[0] + floor(od_u(r, 0) * ((P[1] - P[0]) + 1.0)); return;
+    case OD_BERN: x[0] = od_u(r, 0) < P[0] ? 1.0 : 0.0; return; /* bernoulli.jl:19 */
+    case OD_CAT: x[0] = (double)(od_cat(P, K, od_u(r, 0)) + 1); return;
+    case OD_GAMMA: x[0] = P[1] * od_gamma(r, P[0], 0); return;
+    case OD_INVGAMMA: x[0] = P[1] / od_gamma(r, P[0], 0); return;
     case OD_BETA: {
-      double g1 = od_gamma(seed, id, P[0], 0), g2 = od_gamma(seed, id, P[1], OD_SECOND);
+      double g1 = od_gamma(r, P[0], 0), g2 = od_gamma(r, P[1], OD_SECOND);
       x[0] = g1 / (g1 + g2);
       return;
     }
-    case OD_EXP: x[0] = (1.0 / P[0]) * -orc_log(od_upos(seed, id, 0)); return;
-    case OD_POIS: x[0] = od_poisson(seed, id, P[0], 0); return;
-    case OD_BINOM: x[0] = od_binomial(seed, id, P[0], P[1], 0); return;
+    case OD_EXP: x[0] = (1.0 / P[0]) * -orc_log(od_upos(r, 0)); return;
+    case OD_POIS: x[0] = od_poisson(r, P[0], 0); return;
+    case OD_BINOM: x[0] = od_binomial(r, P[0], P[1], 0); return;
     case OD_NEGBINOM: {
-      double lam = ((1.0 - P[1]) / P[1]) * od_gamma(seed, id, P[0], 0);
-      x[0] = od_poisson(seed, id, lam, OD_SECOND);
+      double lam = ((1.0 - P[1]) / P[1]) * od_gamma(r, P[0], 0);
+      x[0] = od_poisson(r, lam, OD_SECOND);
       return;
     }
-    case OD_GEOM: x[0] = floor(orc_log(od_upos(seed, id, 0)) / orc_log1p(-P[0])) + 0.0; return;
+    case OD_GEOM: x[0] = floor(orc_log(od_upos(r, 0)) / orc_log1p(-P[0])) + 0.0; return;
     case OD_LAPLACE: {
       uint32_t w[4];
-      rng(seed, id, 0, S_DIST, 0, w);
+      od_block(r, 0, w);
       double e = -orc_log(od_one_minus_u(w[0], w[1]));
       x[0] = P[0] + P[1] * ((w[2] & 1u) ? -e : e);
       return;
     }
     case OD_CAUCHY: {
       uint32_t w[4];
-      rng(seed, id, 0, S_DIST, 0, w);
+      od_block(r, 0, w);
       double u = ((double)bits53(w[0], w[1]) + 0.5) * 0x1p-53, s, c;
       orc_sincos_2pi(u * 0.5, &s, &c);
       x[0] = P[0] - P[1] * (c / s);
       return;
     }
     case OD_PWUNIF: {
-      int bin = od_cat(P + K + 1, K, od_u(seed, id, 0));
-      x[0] = od_u(seed, id, 1) * (P[bin + 1] - P[bin]) + P[bin];
+      int bin = od_cat(P + K + 1, K, od_u(r, 0));
+      x[0] = od_u(r, 1) * (P[bin + 1] - P[bin]) + P[bin];
       return;
     }
     default: /* beta_uniform.jl:36-42 */
-      if (od_u(seed, id, 255) < P[0]) {
-        double g1 = od_gamma(seed, id, P[1], 0), g2 = od_gamma(seed, id, P[2], OD_SECOND);
+      if (od_u(r, 255) < P[0]) {
+        double g1 = od_gamma(r, P[1], 0), g2 = od_gamma(r, P[2], OD_SECOND);
         x[0] = g1 / (g1 + g2);
       } else {
-        x[0] = od_u(seed, id, 254);
+        x[0] = od_u(r, 254);
       }
   }
 }
@@ -2730,7 +2781,8 @@ int orc_dist_random(int dist, int dim, int np, int stride, const double* params,
   if (np > 1024 + 33) return -1;
   for (int64_t i = 0; i < n; ++i) {
     if (i == 0 || stride) if (od_row(dist, dim, np, params + i * stride, row, &D, &K) < 0) return -1;
-    od_random(dist, seed, (uint64_t)i, out + i, n, row, D, K);
+    const od_rng r = {seed, (uint64_t)i, 0, S_DIST, 0};
+    od_random(dist, &r, out + i, n, row, D, K);
   }
   return 0;
 }

@@ -117,6 +117,51 @@ def sv_obs(T=12, seed=8):
     return m, obs
 
 
+_LAT2 = {"form": "affine", "A": [[0.9, 0.05], [0.0, 0.8]], "b": [0.0, 0.1], "Q": [[0.05, 0.01], [0.01, 0.04]],
+         "mu0": [0.5, 0.0], "P0": [[0.3, 0.0], [0.0, 0.3]]}
+
+
+def _arg(link, h, c):
+    return {"link": link, "h": h, "c": c}
+
+
+def library_models():
+    """Slot models whose observed addresses are library distributions with
+    latent-dependent arguments: between them every scalar distribution a
+    library slot may name."""
+    return {
+        "m1": gen.SlotSSM(_LAT2, [
+            {"name": "g", "dist": "gamma", "args": [_arg("exp", [0.5, 0.2], 0.3), 2.0]},
+            {"name": "nb", "dist": "neg_binom", "args": [3.0, _arg("logistic", [1.0, -0.5], 0.2)]},
+            {"name": "lp", "dist": "laplace", "args": [_arg("identity", [1.0, 0.5], 0.1), 0.5]},
+            {"name": "b", "dist": "beta", "args": [_arg("exp", [0.4, 0.0], 0.5), _arg("exp", [0.0, -0.4], 0.7)]}]),
+        "m2": gen.SlotSSM(_LAT2, [
+            {"name": "e", "dist": "exponential", "args": [_arg("exp", [0.3, 0.3], 0.0)]},
+            {"name": "bn", "dist": "binom", "args": [10.0, _arg("logistic", [1.2, 0.0], -0.3)]},
+            {"name": "ge", "dist": "geometric", "args": [_arg("logistic", [0.0, 1.0], -0.5)]},
+            {"name": "ca", "dist": "cauchy", "args": [_arg("identity", [0.8, 0.0], 0.0), 0.7]}]),
+        "m3": gen.SlotSSM(_LAT2, [
+            {"name": "n", "dist": "normal", "args": [_arg("identity", [1.0, 0.0], 0.0), _arg("exp", [0.0, 0.5], -0.7)]},
+            {"name": "u", "dist": "uniform", "args": [-4.0, 4.0]},
+            {"name": "ig", "dist": "inv_gamma", "args": [_arg("exp", [0.2, 0.2], 1.0), 1.5]},
+            {"name": "ud", "dist": "uniform_discrete", "args": [0.0, 5.0]}]),
+        "m4": gen.SlotSSM(_LAT2, [
+            {"name": "p", "dist": "poisson", "args": [_arg("exp", [1.0, 0.5], 0.2)]},
+            {"name": "be", "dist": "bernoulli", "args": [_arg("logistic", [1.5, 0.0], -0.3)]},
+            {"name": "bu", "dist": "beta_uniform", "args": [_arg("logistic", [0.5, 0.5], 0.0), 2.0,
+                                                            _arg("exp", [0.3, 0.0], 0.4)]}]),
+    }
+
+
+def library_obs(name, T=10, seed=6):
+    m = library_models()[name]
+    _, ys = m.simulate(T, np.random.default_rng(seed))
+    obs = [dict(y) for y in ys]
+    del obs[2][m.names[0]]
+    obs[4] = {}
+    return m, obs
+
+
 def count_obs(T=10, seed=5):
     """Observations with some slots missing at some steps (and one empty step)."""
     m = count_model()
@@ -230,10 +275,60 @@ def test_oracle_sv_slot_scores_equal_reference_density():
     assert np.isfinite(l1) and abs(l1 - l2) < 0.2
 
 
+def test_oracle_library_slot_scores_equal_reference_densities():
+    """Library slots (any scalar distribution of Gen's library, arguments
+    link(h.x + c)): simulate's observation column is the sum of the slots'
+    reference logpdfs (scipy's densities under Gen's argument conventions) for
+    all fifteen distributions, and the samplers' means match the model's."""
+    for name, m in library_models().items():
+        T, n = 4, 48
+        X, Y, PS, _ = O.simulate(m, T, n, 5)
+        for t in range(T):
+            for j in range(n):
+                x = X[t, :, j]
+                ref = sum(m.slot_logpdf(k, Y[t, k, j], x) for k in range(len(m.slots)))
+                assert np.isfinite(ref), (name, t, j)
+                assert abs(ref - PS[t, 1, j]) < 1e-10 * max(1.0, abs(ref)), (name, t, j, ref, PS[t, 1, j])
+    m = library_models()["m1"]
+    X, Y, _, _ = O.simulate(m, 2, 40000, 6)
+    x = X[1]
+    shape = np.exp(0.5 * x[0] + 0.2 * x[1] + 0.3)
+    assert abs(Y[1, 0].mean() - (2.0 * shape).mean()) < 6 * np.sqrt((4.0 * shape).mean() / 40000)
+    p = 1.0 / (1.0 + np.exp(-(x[0] - 0.5 * x[1] + 0.2)))
+    nb_mean = 3.0 * (1 - p) / p
+    assert abs(Y[1, 1].mean() - nb_mean.mean()) < 6 * np.sqrt((nb_mean / p).mean() / 40000)
+
+
+def test_oracle_library_slots_reduce_to_the_fixed_slots():
+    """A library poisson(exp(h.x + c)) or bernoulli(logistic(h.x + c)) slot is
+    the fixed Poisson / Bernoulli slot bit for bit; a library normal with
+    constant sd is the fixed normal slot to rounding (which folds its
+    constants)."""
+    fixed = gen.SlotSSM(_LAT2, [{"name": "count", "dist": "poisson", "h": [1.0, 0.5], "c": 0.2},
+                                {"name": "on", "dist": "bernoulli", "h": [1.5, 0.0], "c": -0.3},
+                                {"name": "z", "dist": "normal", "h": [0.3, -0.2], "c": 0.1, "sd": 0.7}])
+    lib = gen.SlotSSM(_LAT2, [{"name": "count", "dist": "poisson", "args": [_arg("exp", [1.0, 0.5], 0.2)]},
+                              {"name": "on", "dist": "bernoulli", "args": [_arg("logistic", [1.5, 0.0], -0.3)]},
+                              {"name": "z", "dist": "normal", "args": [_arg("identity", [0.3, -0.2], 0.1), 0.7]}])
+    _, ys = fixed.simulate(8, np.random.default_rng(2))
+    two = [{k: y[k] for k in ("count", "on")} for y in ys]
+    a = O.run_pf(fixed, two, 600, 5)
+    b = O.run_pf(lib, two, 600, 5)
+    assert np.array_equal(a.state(), b.state()) and np.array_equal(a.log_weights(), b.log_weights())
+    a = O.run_pf(fixed, ys, 600, 5, thr=0.0)
+    b = O.run_pf(lib, ys, 600, 5, thr=0.0)
+    assert np.array_equal(a.state(), b.state())
+    np.testing.assert_allclose(b.log_weights(), a.log_weights(), rtol=1e-13, atol=1e-12)
+
+
 def test_slot_model_rejects_bad_descriptions():
     with pytest.raises(ValueError):
         gen.SlotSSM({"form": "affine", "A": np.eye(2), "Q": np.eye(2), "mu0": np.zeros(2), "P0": np.eye(2)},
                     [{"name": "y", "dist": "gamma"}])
+    with pytest.raises(ValueError):  # (gamma takes two arguments)
+        gen.SlotSSM(_LAT2, [{"name": "y", "dist": "gamma", "args": [1.0]}])
+    with pytest.raises(ValueError):
+        gen.SlotSSM(_LAT2, [{"name": "y", "dist": "dirichlet", "args": [1.0]}])
     m = count_model()
     with pytest.raises(gen.GenHipError):
         m.gh_obs({"nope": 1.0})
@@ -545,6 +640,28 @@ def test_gpu_stochastic_volatility_slots_equal_oracle_bitexact(gh_ctx, batched):
     assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
     tr = gen.simulate(m, (7,), num_traces=999, seed=23)
     X, Y, PS, TOT = O.simulate(m, 7, 999, 23)
+    assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
+    assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,batched", [("m1", False), ("m1", True), ("m2", True), ("m3", True), ("m4", False)])
+def test_gpu_library_slots_equal_oracle_bitexact(gh_ctx, name, batched):
+    """Library slots (gamma, neg_binom, laplace, beta / exponential, binom,
+    geometric, cauchy / normal, uniform, inv_gamma, uniform_discrete / poisson,
+    bernoulli, beta_uniform, arguments linked to the latent): GPU == oracle bit
+    for bit (states, weights, parents, score columns; log-ML 1e-9), and
+    simulate (the device samplers) bit-exact."""
+    m, obs = library_obs(name)
+    n = 3001
+    st = _gpu_run(m, obs, n, 19, batched)
+    orc = _orc_run(m, obs, n, 19)
+    _same(st, orc=orc)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    tr = gen.simulate(m, (5,), num_traces=513, seed=29)
+    X, Y, PS, TOT = O.simulate(m, 5, 513, 29)
     assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
     assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
 
