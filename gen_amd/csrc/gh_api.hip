@@ -592,7 +592,7 @@ struct gh_model {
   // slot family (gh_slots.h): the device description and, per mvnormal slot,
   // the host halves of its observation whitening L_R^-1 (y - c)
   SlotParams slots{};
-  bool slot_lib = false;  // a library slot: the SlotModel<D, true> instantiations
+  bool slot_ext = false;  // a library slot or the switching latent: the SlotModel<D, true> instantiations
   std::vector<double> slot_c[kMaxSlots], slot_LR[kMaxSlots];
 };
 
@@ -613,9 +613,9 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
   const bool inputs = form == GH_SLOT_LAT_AFFINE_INPUT;
   sp.K = (int)p[1];
   if (p[0] != form || (form != SLOT_LAT_AFFINE && form != SLOT_LAT_KITAGAWA && !inputs &&
-                       form != SLOT_LAT_CATEGORICAL))
-    return "slots: latent form must be 0 (affine mvnormal), 1 (Kitagawa), 2 (affine with per-step inputs) or 3 "
-           "(categorical)";
+                       form != SLOT_LAT_CATEGORICAL && form != SLOT_LAT_SWITCHING))
+    return "slots: latent form must be 0 (affine mvnormal), 1 (Kitagawa), 2 (affine with per-step inputs), 3 "
+           "(categorical) or 4 (switching linear-Gaussian)";
   if (form == SLOT_LAT_CATEGORICAL && d < 2) return "slots: a categorical latent has d = K >= 2 classes";
   if (sp.lat == SLOT_LAT_KITAGAWA && d != 1) return "slots: the Kitagawa latent has d = 1";
   if (p[1] != sp.K || sp.K < 1 || sp.K > kMaxSlots) return "slots: 1..4 observed slots";
@@ -646,7 +646,7 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
         return "slots: categorical slot: 2..16 classes, probs softmax(W x + c)";
     } else if (dist == SLOT_LIBRARY) {
       if (lib_nargs(mm) == 0 || link != 0) return "slots: library slot: m names a scalar distribution (gen_hip.h)";
-      m->slot_lib = true;
+      m->slot_ext = true;
     } else {
       return "slots: unknown slot distribution";
     }
@@ -676,6 +676,37 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
     h.insert(h.end(), L0.begin(), L0.end());
     sp.cstQ = gauss_cst(d, LQ.data());
     sp.cst0 = gauss_cst(d, L0.data());
+    i += need;
+  } else if (sp.lat == SLOT_LAT_SWITCHING) {  // nz prior[nz] T[nz*nz] (A_z b_z Q_z per regime) mu0 P0
+    if (np < i + 1) return "slots: too few parameters (switching latent)";
+    const int nz = (int)p[i];
+    const int dx = d - nz;
+    if (p[i] != nz || nz < 2 || nz > kMaxRegimes || dx < 1)
+      return "slots: a switching latent has 2..8 regimes and d = dx + regimes with dx >= 1";
+    sp.nz = nz;
+    m->slot_ext = true;
+    const int64_t per = 2LL * dx * dx + dx;
+    const int64_t need = 1 + nz + (int64_t)nz * nz + nz * per + dx + (int64_t)dx * dx;
+    if (np < i + need) return "slots: too few parameters (switching latent: nz prior T (A b Q per regime) mu0 P0)";
+    const double* pr = p + i + 1;
+    for (int64_t j = 0; j < nz + (int64_t)nz * nz; ++j)
+      if (!(pr[j] >= 0.0) || !std::isfinite(pr[j])) return "slots: regime probabilities must be >= 0";
+    h.insert(h.end(), pr, pr + nz + nz * nz);
+    const double* rb = pr + nz + nz * nz;
+    std::vector<double> L(dx * dx);
+    for (int z = 0; z < nz; ++z, rb += per) {
+      const double *A = rb, *b = rb + dx * dx, *Q = b + dx;
+      if (chol(dx, Q, L.data())) return "slots: a regime's Q is not positive definite";
+      h.insert(h.end(), A, A + dx * dx);
+      h.insert(h.end(), b, b + dx);
+      h.insert(h.end(), L.begin(), L.end());
+      sp.cstQz[z] = gauss_cst(dx, L.data());
+    }
+    const double *mu0 = rb, *P0 = rb + dx;
+    if (chol(dx, P0, L.data())) return "slots: P0 not positive definite";
+    h.insert(h.end(), mu0, mu0 + dx);
+    h.insert(h.end(), L.begin(), L.end());
+    sp.cst0 = gauss_cst(dx, L.data());
     i += need;
   } else if (sp.lat == SLOT_LAT_CATEGORICAL) {
     const int64_t need = (int64_t)d + (int64_t)d * d;
@@ -957,6 +988,14 @@ extern "C" int gh_model_create(gh_ctx* ctx, const gh_model_desc* desc, gh_model*
     sp.L0 = sp.lat == SLOT_LAT_AFFINE ? q + 2 * d * d + 2 * d : q;
     sp.cprior = q;
     sp.cT = sp.lat == SLOT_LAT_CATEGORICAL ? q + d : q;
+    sp.SW = q;
+    if (sp.lat == SLOT_LAT_SWITCHING) {
+      const int nz = sp.nz, dx = d - nz;
+      sp.cT = q + nz;
+      sp.SW = q + nz + nz * nz;
+      sp.mu0 = sp.SW + nz * (2 * dx * dx + dx);
+      sp.L0 = sp.mu0 + dx;
+    }
     for (int k = 0; k < kMaxSlots; ++k) sp.P[k] = m->dparams + (k < sp.K ? slot_off[5 + k] : 0);
   }
   *out = m;
@@ -1128,7 +1167,8 @@ static bool proposal_ok(const gh_model* m, int proposal) {
   if (proposal == GH_PROPOSAL_GAUSSIAN) return m->family == GH_FAMILY_KITAGAWA;
   if (proposal == GH_PROPOSAL_LINEAR)  // (u_t follows the step's observed values)
     return (m->family == GH_FAMILY_LGSSM && m->d + m->dy <= kMaxObs) ||
-           (m->family == GH_FAMILY_SLOTS && m->slots.lat != SLOT_LAT_CATEGORICAL && m->d + m->slots.qoff <= kMaxObs);
+           (m->family == GH_FAMILY_SLOTS && m->slots.lat != SLOT_LAT_CATEGORICAL && m->slots.lat != SLOT_LAT_SWITCHING &&
+            m->d + m->slots.qoff <= kMaxObs);
   if (proposal != GH_PROPOSAL_OPTIMAL) return false;
   return m->family == GH_FAMILY_HMM || (m->family == GH_FAMILY_LGSSM && m->lg_opt);
 }
@@ -1583,7 +1623,7 @@ static int with_model(const gh_model* m, F&& f) {
       switch (m->d) {
 #define GH_SL_CASE(DD) \
   case DD:                                                    \
-    if (m->slot_lib) f(SlotModel<DD, true>{}, m->slots);      \
+    if (m->slot_ext) f(SlotModel<DD, true>{}, m->slots);      \
     else f(SlotModel<DD>{}, m->slots);                        \
     break;
         GH_SL_CASE(1) GH_SL_CASE(2) GH_SL_CASE(3) GH_SL_CASE(4) GH_SL_CASE(5) GH_SL_CASE(6) GH_SL_CASE(7)
@@ -1615,7 +1655,7 @@ static int launch_step(gh_pf* pf, const StepObs& o, const StepArgs& a, bool init
     switch (pf->m->d) {
 #define GH_SLL_CASE(DD) \
   case DD:                                                                     \
-    if (pf->m->slot_lib) launch_step_t<SlotLinModel<DD, true>>(pf, p, o, a, init, e0, e1); \
+    if (pf->m->slot_ext) launch_step_t<SlotLinModel<DD, true>>(pf, p, o, a, init, e0, e1); \
     else launch_step_t<SlotLinModel<DD>>(pf, p, o, a, init, e0, e1);                     \
     break;
       GH_SLL_CASE(1) GH_SLL_CASE(2) GH_SLL_CASE(3) GH_SLL_CASE(4) GH_SLL_CASE(5) GH_SLL_CASE(6)
@@ -2127,7 +2167,7 @@ static const gh_obs* slot_chain(const std::vector<double>& r, gh_obs* chain) {
 // the same slot layout (a parameter change keeps every address and its form)
 static bool same_slots(const gh_model* a, const gh_model* b) {
   const SlotParams &p = a->slots, &q = b->slots;
-  if (p.lat != q.lat || p.K != q.K || (p.uoff >= 0) != (q.uoff >= 0)) return false;
+  if (p.lat != q.lat || p.K != q.K || (p.uoff >= 0) != (q.uoff >= 0) || p.nz != q.nz) return false;
   for (int k = 0; k < p.K; ++k)
     if (p.dist[k] != q.dist[k] || p.m[k] != q.m[k] || p.link[k] != q.link[k]) return false;
   return true;
@@ -3682,7 +3722,8 @@ extern "C" int gh_pf_mh_drift(gh_pf* pf, uint32_t selection, const double* sd, i
   if (!pf || !sd) return set_err(GH_E_INVAL, "gh_pf_mh_drift: null argument");
   if (n_moves < 0) return set_err(GH_E_INVAL, "gh_pf_mh_drift: n_moves < 0");
   if (pf->m->family == GH_FAMILY_HMM ||
-      (pf->m->family == GH_FAMILY_SLOTS && pf->m->slots.lat == SLOT_LAT_CATEGORICAL))
+      (pf->m->family == GH_FAMILY_SLOTS &&
+       (pf->m->slots.lat == SLOT_LAT_CATEGORICAL || pf->m->slots.lat == SLOT_LAT_SWITCHING)))
     return set_err(GH_E_INVAL, "gh_pf_mh_drift: a Gaussian drift needs a continuous latent (not a categorical one)");
   if (selection == 0 || (selection & ~latent_addresses(pf->m)) != 0)
     return set_err(GH_E_INVAL, "gh_pf_mh_drift: selection 0x%x names no latent address of this step (valid: 0x%x)",

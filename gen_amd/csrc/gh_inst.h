@@ -90,7 +90,7 @@
                                                             int*);                                               \
   X __global__ void gh::k_pin_pre<gh::SlotModel<D, L>, true>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs); \
   X __global__ void gh::k_pin_pre<gh::SlotModel<D, L>, false>(const double*, gh::SlotParams, gh::StepObs, gh::PinArgs);
-// (L: the instantiations for models with a library slot, gh_inst_slots4..7.hip)
+// (L: the extended instantiations — a library slot or the switching latent — gh_inst_slots4..7.hip)
 #define GH_SL_KERNELS(X, D) GH_SL_KERNELS_L(X, D, false)
 #define GH_SLL_KERNELS(X, D) GH_SL_KERNELS_L(X, D, true)
 #define GH_SL_UNIT0(X) \

@@ -1,4 +1,4 @@
-// gh_inst_slots6.hip — explicit instantiations of the slot family's kernels for models with a library slot (see gh_inst.h)
+// gh_inst_slots6.hip — explicit instantiations of the slot family's kernels for models with a library slot or the switching latent (see gh_inst.h)
 #include <hip/hip_runtime.h>
 #include "gh_inst.h"
 

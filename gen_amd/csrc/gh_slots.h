@@ -13,6 +13,10 @@
 //         or z_t ~ categorical(T[:, z_{t-1}])       (z_1 ~ categorical(prior); stored one-hot, d = K)
 //         or x_t ~ normal(x/2 + 25x/(1+x^2) + 8cos(1.2t), sd_x)   (d = 1;
 //            x_1 ~ normal(mu1, s1)) — examples/pmmh/model.jl:9-13
+//         or two latent addresses, a switching linear-Gaussian state:
+//            z_t ~ categorical(T[:, z_{t-1}]), x_t ~ mvnormal(A_z x_{t-1} + b_z, Q_z)
+//            (z_1 ~ categorical(prior), x_1 ~ mvnormal(mu0, P0)); stored as
+//            x (dx values) then z one-hot (nz values), d = dx + nz
 //   slots    mvnormal(H x + c, R)                         mvnormal.jl:12-16
 //            normal(h.x + c, sd) or normal(x^2/20, sd)    normal.jl:56-60
 //            normal(h.x + c, exp(g.x + s))                normal.jl:56-60 (stochastic volatility)
@@ -122,7 +126,8 @@ enum SlotLink : int {
   LINK_LOGSCALE = 5  // normal slot with a log-linear standard deviation
 };
 // (latent form 2 — affine with per-step inputs — is SLOT_LAT_AFFINE with uoff >= 0)
-enum SlotLatent : int { SLOT_LAT_AFFINE = 0, SLOT_LAT_KITAGAWA = 1, SLOT_LAT_CATEGORICAL = 3 };
+enum SlotLatent : int { SLOT_LAT_AFFINE = 0, SLOT_LAT_KITAGAWA = 1, SLOT_LAT_CATEGORICAL = 3, SLOT_LAT_SWITCHING = 4 };
+constexpr int kMaxRegimes = 8;  // switching latent: regimes
 
 struct SlotParams {
   const double* base;
@@ -131,6 +136,11 @@ struct SlotParams {
   // categorical latent (K = d classes, one-hot state): prior[K] | T[K*K], T[new*K + prev]
   const double *cprior, *cT;
   double cstQ, cst0;  // their log-normalisers (score columns)
+  // switching latent (nz regimes, state x[dx] | one-hot z[nz]): prior | T as above,
+  // then per regime A_z [dx*dx] | b_z [dx] | chol(Q_z) [dx*dx] (SW), mu0 [dx] | chol(P0) [dx*dx]
+  const double* SW;
+  int nz;
+  double cstQz[kMaxRegimes];
   KitParams kit;      // Kitagawa latent (mu1, s1, sx, inv2vx, cstx, inv2v1, cst1)
   int lat, K;
   int dist[kMaxSlots], m[kMaxSlots], link[kMaxSlots];
@@ -160,15 +170,17 @@ struct SlotParams {
     q.L0 = rebased(*this, prm, L0);
     q.cprior = rebased(*this, prm, cprior);
     q.cT = rebased(*this, prm, cT);
+    q.SW = rebased(*this, prm, SW);
 #pragma unroll
     for (int k = 0; k < kMaxSlots; ++k) q.P[k] = rebased(*this, prm, P[k]);
     return q;
   }
 };
 
-// LIB: the model has a library slot (its logpdf and sampler are out-of-line
-// calls; the instantiations without them keep call-free kernels)
-template <int D, bool LIB = false>
+// EXT: the extended instantiations, for a model with a library slot (its
+// logpdf and sampler are out-of-line calls) or the switching latent; the
+// others keep the leaner call-free kernels
+template <int D, bool EXT = false>
 struct SlotModel {
   static constexpr int kD = D;
   static constexpr int kMinWaves = D <= 3 ? 8 : (D <= 6 ? 6 : (D <= 10 ? 4 : 3));
@@ -199,6 +211,15 @@ struct SlotModel {
     }
   }
 
+  // the regime of a switching state (its one-hot tail x[dx..D))
+  __device__ static int regime(const Params& p, const double* x) {
+    const int dx = D - p.nz;
+    int z = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) z = (j >= dx && x[j] != 0.0) ? j - dx : z;
+    return z;
+  }
+
   // the class of a one-hot categorical latent
   __device__ static int onehot(const double* x) {
     int z = 0;
@@ -214,12 +235,12 @@ struct SlotModel {
     const int m = p.m[k];
     switch (p.dist[k]) {
       case SLOT_LIBRARY: {  // the library's logpdf (gh_dists.h, the reference's formulas)
-        if constexpr (LIB) {
+        if constexpr (EXT) {
           double a[3];
           lib_args(P, lib_nargs(m), x, a);
           return lib_logpdf(m, v[0], a[0], a[1], a[2]);
         } else {
-          return NAN;  // (never: the host picks the LIB instantiation for such a model)
+          return NAN;  // (never: the host picks the EXT instantiation for such a model)
         }
       }
       case SLOT_MVNORMAL: {  // LGModel::obs (dense): v = L_R^-1 (y - c)
@@ -276,6 +297,33 @@ struct SlotModel {
                                        const double* x) {
     if (p.lat == SLOT_LAT_CATEGORICAL)  // categorical.jl:10-12: log prior[z] or log T[z | z_prev]
       return gh_log(t == 1 ? p.cprior[onehot(x)] : p.cT[onehot(x) * D + onehot(xp)]);
+    if (EXT && p.lat == SLOT_LAT_SWITCHING) {  // log p(z | z_prev) + mvnormal.jl:12-16 under regime z, in that order
+      const int dx = D - p.nz, z = regime(p, x);
+      const double* blk = p.SW + z * (2 * dx * dx + dx);
+      const double lz = gh_log(t == 1 ? p.cprior[z] : p.cT[z * p.nz + regime(p, xp)]);
+      const double* L = t == 1 ? p.L0 : blk + dx * dx + dx;
+      double u[D];
+      double quad = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        if (i >= dx) break;
+        double mean;
+        if (t == 1) {
+          mean = p.mu0[i];
+        } else {
+          mean = blk[dx * dx + i];
+#pragma unroll
+          for (int k = 0; k < D; ++k)
+            if (k < dx) mean = fma(blk[i * dx + k], xp[k], mean);
+        }
+        double r = x[i] - mean;
+#pragma unroll
+        for (int k = 0; k < i; ++k) r = fma(-L[i * dx + k], u[k], r);
+        u[i] = r / L[i * dx + i];
+        quad = fma(u[i], u[i], quad);
+      }
+      return lz + ((t == 1 ? p.cst0 : p.cstQz[z]) - 0.5 * quad);
+    }
     if (p.lat == SLOT_LAT_KITAGAWA) {
       double mean = p.kit.mu1, inv2 = p.kit.inv2v1, cst = p.kit.cst1;
       if (t > 1) {
@@ -323,6 +371,36 @@ struct SlotModel {
       const int z = t == 1 ? cat_sample(p.cprior, D, 1, u) : cat_sample(p.cT + onehot(xp), D, D, u);
 #pragma unroll
       for (int j = 0; j < D; ++j) x[j] = j == z ? 1.0 : 0.0;
+      return;
+    }
+    if (EXT && p.lat == SLOT_LAT_SWITCHING) {  // the regime (inverse CDF, draw base), then x given it (normals from base + 1)
+      const int dx = D - p.nz;
+      const u32x4 w = rng_block(seed, pid, t, dr.stream, dr.base);
+      const double u = u53(w.x, w.y);
+      const int z = t == 1 ? cat_sample(p.cprior, p.nz, 1, u) : cat_sample(p.cT + regime(p, xp), p.nz, p.nz, u);
+      const double* blk = p.SW + z * (2 * dx * dx + dx);
+      const double* L = t == 1 ? p.L0 : blk + dx * dx + dx;
+      double zn[D + 1];
+      normals_n<D>(seed, pid, t, dr.stream, dr.base + 1, zn, dr.tab);
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        if (i < dx) {
+          double acc;
+          if (t == 1) {
+            acc = p.mu0[i];
+          } else {
+            acc = blk[dx * dx + i];
+#pragma unroll
+            for (int k = 0; k < D; ++k)
+              if (k < dx) acc = fma(blk[i * dx + k], xp[k], acc);
+          }
+#pragma unroll
+          for (int k = 0; k <= i; ++k) acc = fma(L[i * dx + k], zn[k], acc);
+          x[i] = acc;
+        } else {
+          x[i] = i - dx == z ? 1.0 : 0.0;
+        }
+      }
       return;
     }
     if (p.lat == SLOT_LAT_KITAGAWA) {  // the nonlinear SSM's paired normals (KitModel::znorm)
@@ -378,7 +456,7 @@ struct SlotModel {
       double lp;
       switch (p.dist[k]) {
         case SLOT_LIBRARY: {  // the library's sampler (gh_dists.h) on draws kSlotLibDraw + 256 k
-          if constexpr (LIB) {
+          if constexpr (EXT) {
             double a[3];
             lib_args(P, lib_nargs(m), x, a);
             yk[0] = lib_random(m, seed, pid, t, kSlotLibDraw + 256u * (uint32_t)k, a[0], a[1], a[2], tab);
@@ -488,12 +566,12 @@ struct SlotModel {
 // trace_translators.jl:775-802): the model's score of the new choices — the
 // latent's logpdf (affine or Kitagawa) and the present slots' — minus q's
 // logpdf of the drawn value.
-template <int D, bool LIB = false>
+template <int D, bool EXT = false>
 struct SlotLinModel {
   static constexpr int kD = D;
-  static constexpr int kMinWaves = SlotModel<D, LIB>::kMinWaves;
+  static constexpr int kMinWaves = SlotModel<D, EXT>::kMinWaves;
   using Params = SlotParams;
-  using Prior = SlotModel<D, LIB>;
+  using Prior = SlotModel<D, EXT>;
 
   __device__ static double loglik(const Params& p, const StepObs& o, const double* x) { return Prior::loglik(p, o, x); }
 

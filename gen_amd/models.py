@@ -73,6 +73,17 @@ class Model:
         """Latent rows [n, d] as the choice values of n traces (trace[addr])."""
         return col[:, 0] if col.shape[1] == 1 else col
 
+    # a step's latent addresses (one here; a switching slot model has two) and
+    # each one's value from the state row / rows
+    def latent_addresses(self, t: int) -> list:
+        return [self.latent_address(t)]
+
+    def latent_part(self, k: int, x):
+        return self.latent_value(x)
+
+    def latent_part_column(self, k: int, col):
+        return self.latent_column(col)
+
     def obs_values(self, value) -> np.ndarray:
         return np.ascontiguousarray(np.atleast_1d(np.asarray(value, dtype=np.float64)).ravel())
 
@@ -378,6 +389,12 @@ class SlotSSM(Model):
         end
 
     latent: {"form": "affine", "A", "b", "Q", "mu0", "P0"[, "inputs": True]} or
+            {"form": "switching", "prior" [nz], "T" [nz, nz], "A" [nz, dx, dx], "b" [nz, dx],
+             "Q" [nz, dx, dx], "mu0" [dx], "P0" [dx, dx][, "regime_name": "z"]}: two
+            latent addresses, z_t ~ categorical(T[:, z_{t-1}]) and
+            x_t ~ mvnormal(A[z_t] x_{t-1} + b[z_t], Q[z_t]); the state is x then z
+            one-hot (d = dx + nz), so a slot's h.x + c loads x and adds a
+            per-regime offset h[dx + z]; or
             {"form": "kitagawa", "mu1", "s1", "sd_x"} (d = 1) or
             {"form": "categorical", "prior" [K], "T" [K, K] (T[new, prev])}: z_t ~
             categorical(T[:, z_{t-1}]); the engine keeps z one-hot (d = K), so a
@@ -410,6 +427,20 @@ class SlotSSM(Model):
             self.b = f("b", (self.d,)) if "b" in latent else np.zeros(self.d)
             self.Q, self.mu0, self.P0 = f("Q", (self.d, self.d)), f("mu0", (self.d,)), f("P0", (self.d, self.d))
             self.inputs = bool(latent.get("inputs", False))
+        elif form == "switching":
+            self.inputs = False
+            self.prior = np.asarray(latent["prior"], dtype=np.float64).ravel()
+            self.nz = self.prior.size
+            self.T = np.asarray(latent["T"], dtype=np.float64).reshape(self.nz, self.nz)
+            self.A = np.asarray(latent["A"], dtype=np.float64)
+            self.dx = self.A.shape[-1]
+            self.A = self.A.reshape(self.nz, self.dx, self.dx)
+            self.b = np.asarray(latent.get("b", np.zeros((self.nz, self.dx))), dtype=np.float64).reshape(self.nz, self.dx)
+            self.Q = np.asarray(latent["Q"], dtype=np.float64).reshape(self.nz, self.dx, self.dx)
+            self.mu0 = np.asarray(latent["mu0"], dtype=np.float64).reshape(self.dx)
+            self.P0 = np.asarray(latent["P0"], dtype=np.float64).reshape(self.dx, self.dx)
+            self.regime_name = latent.get("regime_name", "z")
+            self.d = self.dx + self.nz
         elif form == "categorical":
             self.inputs = False
             self.prior = np.asarray(latent["prior"], dtype=np.float64).ravel()
@@ -420,7 +451,7 @@ class SlotSSM(Model):
             self.d = 1
             self.mu1, self.s1, self.sd_x = float(latent["mu1"]), float(latent["s1"]), float(latent["sd_x"])
         else:
-            raise ValueError(f"latent form {form!r}: 'affine', 'kitagawa' or 'categorical'")
+            raise ValueError(f"latent form {form!r}: 'affine', 'kitagawa', 'categorical' or 'switching'")
         self.form = form
         if not 1 <= len(slots) <= 4:
             raise ValueError("1..4 observed slots")
@@ -477,7 +508,7 @@ class SlotSSM(Model):
         self.dy = sum(s["m"] if s["dist"] == "mvnormal" and "lib" not in s else 1 for s in self.slots)
 
     def params(self):
-        code = {"affine": 2.0 if self.inputs else 0.0, "kitagawa": 1.0, "categorical": 3.0}[self.form]
+        code = {"affine": 2.0 if self.inputs else 0.0, "kitagawa": 1.0, "categorical": 3.0, "switching": 4.0}[self.form]
         p = [code, float(len(self.slots))]
         for s in self.slots:
             if "lib" in s:
@@ -488,6 +519,11 @@ class SlotSSM(Model):
             p += list(self.A.ravel()) + list(self.b) + list(self.Q.ravel()) + list(self.mu0) + list(self.P0.ravel())
         elif self.form == "categorical":
             p += list(self.prior) + list(self.T.ravel())
+        elif self.form == "switching":
+            p += [float(self.nz)] + list(self.prior) + list(self.T.ravel())
+            for z in range(self.nz):
+                p += list(self.A[z].ravel()) + list(self.b[z]) + list(self.Q[z].ravel())
+            p += list(self.mu0) + list(self.P0.ravel())
         else:
             p += [self.mu1, self.s1, self.sd_x]
         for s in self.slots:
@@ -556,6 +592,32 @@ class SlotSSM(Model):
         if self.form == "categorical":  # (the class: Gen's categorical returns an Int; 0-based here)
             return int(np.argmax(x))
         return super().latent_value(x)
+
+    def latent_addresses(self, t: int) -> list:
+        if self.form == "switching":
+            return [("chain", t, self.regime_name), ("chain", t, self.latent_name)]
+        return [self.latent_address(t)]
+
+    def latent_part(self, k: int, x):
+        if self.form == "switching":  # (z: 0-based regime; x: the continuous state)
+            x = np.asarray(x)
+            return int(np.argmax(x[self.dx:])) if k == 0 else (float(x[0]) if self.dx == 1 else x[:self.dx].copy())
+        return self.latent_value(x)
+
+    def latent_part_column(self, k: int, col):
+        if self.form == "switching":
+            return np.argmax(col[:, self.dx:], axis=1) if k == 0 else (col[:, 0] if self.dx == 1 else col[:, :self.dx])
+        return self.latent_column(col)
+
+    def latent_part_logpdf(self, k: int, t: int, xp, x) -> float:
+        """A switching model's z (k = 0) or x (k = 1) score at step t."""
+        z = int(np.argmax(x[self.dx:]))
+        if k == 0:
+            return float(np.log(self.prior[z] if t == 1 else self.T[z, int(np.argmax(xp[self.dx:]))]))
+        from scipy import stats
+
+        mean, cov = (self.mu0, self.P0) if t == 1 else (self.A[z] @ xp[:self.dx] + self.b[z], self.Q[z])
+        return float(stats.multivariate_normal.logpdf(x[:self.dx], mean, cov))
 
     def latent_column(self, col):
         if self.form == "categorical":
@@ -693,6 +755,13 @@ class SlotSSM(Model):
                 u = np.zeros(self.d) if inputs is None or t == 1 else np.asarray(inputs[t - 1], dtype=np.float64)
                 x = (rng.multivariate_normal(self.mu0, self.P0) if t == 1 else
                      rng.multivariate_normal(self.A @ xs[t - 2] + (self.b + u), self.Q))
+            elif self.form == "switching":  # (x then z one-hot, as the engine stores it)
+                zp = None if t == 1 else int(np.argmax(xs[t - 2, self.dx:]))
+                pz = self.prior if t == 1 else self.T[:, zp]
+                z = rng.choice(self.nz, p=pz / pz.sum())
+                xc = (rng.multivariate_normal(self.mu0, self.P0) if t == 1 else
+                      rng.multivariate_normal(self.A[z] @ xs[t - 2, :self.dx] + self.b[z], self.Q[z]))
+                x = np.concatenate([xc, np.eye(self.nz)[z]])
             elif self.form == "categorical":  # (one-hot, as the engine stores it)
                 pz = self.prior if t == 1 else self.T[:, int(np.argmax(xs[t - 2]))]
                 x = np.eye(self.d)[rng.choice(self.d, p=pz / pz.sum())]

@@ -308,8 +308,9 @@ class ParticleTraces:
     def _step_of(self, addr):
         m = self.state.model
         for t in range(1, self.state.t + 1):
-            if m.latent_address(t) == addr:
-                return t, "latent"
+            for k, la in enumerate(m.latent_addresses(t)):
+                if tuple(la) == addr:
+                    return t, ("latent", k)
             if m.obs_address(t) == addr or (hasattr(m, "names") and len(addr) == 3 and addr[:2] == ("chain", t)
                                             and addr[2] in m.names):
                 return t, "obs"
@@ -327,7 +328,7 @@ class ParticleTraces:
         self._fresh()
         if t not in self._cache:
             self._cache[t] = self.state.states(t)
-        return self.state.model.latent_column(self._cache[t])
+        return self.state.model.latent_part_column(kind[1], self._cache[t])
 
     def __getitem__(self, i):
         return _TraceView(self, int(i))
@@ -397,7 +398,8 @@ class _TraceView:
             return cm
         for t in range(1, st.t + 1):
             x = xs[t - 1]
-            cm[m.latent_address(t)] = m.latent_value(x)
+            for k, la in enumerate(m.latent_addresses(t)):
+                cm[la] = m.latent_part(k, x)
             y = st.observations.get(t)
             if isinstance(y, dict):  # a slot model: every constrained slot
                 for name, v in y.items():
@@ -439,7 +441,11 @@ class _TraceView:
                         total += _normal_lp(float(ys[i]), x[0] * m.xs[i] + x[1], m.sigma)
                 continue
             for t in range(1, st.t + 1):
-                if a == tuple(m.latent_address(t)):
+                las = [tuple(la) for la in m.latent_addresses(t)]
+                if a in las and len(las) > 1:  # one of several latent addresses: its own score on the host
+                    tr = self.trajectory()
+                    total += m.latent_part_logpdf(las.index(a), t, tr[t - 2] if t > 1 else None, tr[t - 1])
+                elif a == tuple(m.latent_address(t)):
                     total += ps[t - 1, 0, self.i]
                 elif hasattr(m, "names") and len(a) == 3 and a[:2] == ("chain", t) and a[2] in m.names:
                     # one slot of a slot model (the device column sums the step's slots): its logpdf on the host
@@ -692,7 +698,9 @@ def _latent_mask(state: ParticleFilterState, selection) -> int:
     if m.static:
         names = {("slope",): 1, ("intercept",): 2}
     else:
-        names = {tuple(m.latent_address(state.t)): 1}
+        names = {tuple(a): 1 for a in m.latent_addresses(state.t)}
+    if len(names) > 1 and not all(a in set(map(tuple, sel)) for a in names):
+        raise _lib.GenHipError(1, f"selection must name every latent address of the step together: {sorted(names)}")
     mask = 0
     for a in sel:
         if a not in names:

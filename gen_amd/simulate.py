@@ -46,8 +46,9 @@ class SimulatedTraces:
                     return "y", 1, i - 1
             raise KeyError(addr)
         for t in range(1, self.T + 1):
-            if a == tuple(m.latent_address(t)):
-                return "x", t, None
+            las = [tuple(la) for la in m.latent_addresses(t)]
+            if a in las:
+                return "x", t, (None if len(las) == 1 else ("part", las.index(a)))
             if a == tuple(m.obs_address(t)):
                 return "y", t, None
         raise KeyError(addr)
@@ -57,6 +58,8 @@ class SimulatedTraces:
         kind, t, comp = self._locate(addr)
         src = self.xs if kind == "x" else self.ys
         col = src[t - 1]
+        if isinstance(comp, tuple):  # one of several latent addresses
+            return self.model.latent_part_column(comp[1], col.T)
         if comp is not None:
             return col[comp]
         if isinstance(self.model, DiscreteHMM):
@@ -94,7 +97,12 @@ class SimulatedTrace:
             return cm
         for t in range(1, tr.T + 1):
             x, y = tr.xs[t - 1, :, i], tr.ys[t - 1, :, i]
-            cm[m.latent_address(t)] = _value(m, x)
+            las = m.latent_addresses(t)
+            if len(las) > 1:
+                for k, la in enumerate(las):
+                    cm[la] = m.latent_part(k, x)
+            else:
+                cm[m.latent_address(t)] = _value(m, x)
             cm[m.obs_address(t)] = _value(m, y)
         return cm
 

@@ -111,6 +111,12 @@ typedef enum {
          z_1 ~ categorical(prior); z_t ~ categorical(T[:, z_{t-1}]) (T[new*K + prev]);
          the state is stored one-hot (K values), so a slot's affine mean h.x + c
          is h[z] + c (per-class parameters); no drift MH, no linear proposal
+                   lat = GH_SLOT_LAT_SWITCHING (4), two latent addresses, d = dx + nz:
+         nz (2..8) prior[nz] T[nz*nz], per regime A_z[dx*dx] b_z[dx] Q_z[dx*dx], mu0[dx] P0[dx*dx]
+         z_1 ~ categorical(prior), x_1 ~ mvnormal(mu0, P0); z_t ~ categorical(T[:, z_{t-1}]),
+         x_t ~ mvnormal(A_z x_{t-1} + b_z, Q_z) with z = z_t; the state is x (dx values) then
+         z one-hot (nz values), so a slot's h.x + c loads x and adds h[dx + z];
+         no drift MH, no linear proposal, MH selections name both addresses
      slot blocks (m_k values of the slot; its value rows in simulate's output
      follow slot order, one row for a scalar slot):
        GH_SLOT_MVNORMAL, link GH_LINK_AFFINE, m <= 32: H[m*d] c[m] R[m*m]   y ~ mvnormal(H x + c, R)
@@ -139,7 +145,8 @@ typedef enum {
   GH_FAMILY_SLOTS = 5
 } gh_family;
 
-enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1, GH_SLOT_LAT_AFFINE_INPUT = 2, GH_SLOT_LAT_CATEGORICAL = 3 };
+enum { GH_SLOT_LAT_AFFINE = 0, GH_SLOT_LAT_KITAGAWA = 1, GH_SLOT_LAT_AFFINE_INPUT = 2, GH_SLOT_LAT_CATEGORICAL = 3,
+       GH_SLOT_LAT_SWITCHING = 4 };
 /* gh_obs.slot of a step's latent input u_t (latent form 2): d values, an
    argument of the step's kernel application, not a choice */
 enum { GH_SLOT_INPUT = -1 };

@@ -343,6 +343,11 @@ typedef struct {
      observation vector, parameter block (mvnormal M = L_R^-1 H | H | c | L_R;
      normal / poisson / bernoulli h | c; categorical W | c) and constants */
   int lat, K, sdist[4], sm[4], slink[4], svoff[4], syoff[4], snv, uin;  /* uin: per-step latent inputs (form 2) */
+  /* switching latent (form 4): nz regimes, state x[dx] | one-hot z[nz]; prior, T as
+     the categorical latent's; SW: per regime A_z | b_z | chol(Q_z); mu0, L0 */
+  int nz;
+  double* SW;
+  double cstQz[8];
   double* sP[4];
   double scst[4], sinv2v[4], ssd[4];
 } model_t;
@@ -354,6 +359,7 @@ static void model_free(model_t* m) {
   free(m->H); free(m->LS); free(m->Kt); free(m->FA); free(m->Fb); free(m->LSig); free(m->WA); free(m->Wb);
   free(m->LS1); free(m->Kt1); free(m->LSig1);
   for (int k = 0; k < 4; ++k) free(m->sP[k]);
+  free(m->SW);
 }
 
 /* the optimal proposal's factors for state prior covariance P: chol(S), K^T,
@@ -477,7 +483,7 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
     /* include/gen_hip.h GH_FAMILY_SLOTS (the engine's slots_build, same checks) */
     if (d < 1 || d > 16 || np < 2) return -1;
     m->lat = (int)p[0]; m->K = (int)p[1];
-    if ((double)m->lat != p[0] || m->lat < 0 || m->lat > 3 || (m->lat == 1 && d != 1) || (m->lat == 3 && d < 2))
+    if ((double)m->lat != p[0] || m->lat < 0 || m->lat > 4 || (m->lat == 1 && d != 1) || (m->lat == 3 && d < 2))
       return -1;
     m->uin = m->lat == 2;  /* affine with per-step inputs: x_t ~ mvnormal(A x + (b + u_t), Q) */
     if (m->uin) m->lat = 0;
@@ -516,6 +522,32 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
       if (chol(d, P0, m->L0)) return -2;
       m->cstQ = gauss_cst(d, m->LQ);
       m->cst0 = gauss_cst(d, m->L0);
+      i += need;
+    } else if (m->lat == 4) {  /* switching: nz prior[nz] T[nz*nz] (A_z b_z Q_z per regime) mu0 P0 */
+      if (np < i + 1) return -1;
+      int nz = (int)p[i], dx = d - nz;
+      if ((double)nz != p[i] || nz < 2 || nz > 8 || dx < 1) return -1;
+      int64_t per = 2 * (int64_t)dx * dx + dx;
+      int64_t need = 1 + nz + (int64_t)nz * nz + nz * per + dx + (int64_t)dx * dx;
+      if (np < i + need) return -1;
+      const double* pr = p + i + 1;
+      for (int64_t j = 0; j < nz + (int64_t)nz * nz; ++j)
+        if (!(pr[j] >= 0.0) || pr[j] == INFINITY) return -1;
+      m->nz = nz;
+      m->prior = malloc(sizeof(double) * nz); memcpy(m->prior, pr, sizeof(double) * nz);
+      m->T = malloc(sizeof(double) * nz * nz); memcpy(m->T, pr + nz, sizeof(double) * nz * nz);
+      m->SW = malloc(sizeof(double) * (size_t)(nz * per));
+      const double* rb = pr + nz + nz * nz;
+      for (int z = 0; z < nz; ++z, rb += per) {
+        double* blk = m->SW + z * per;
+        memcpy(blk, rb, sizeof(double) * (size_t)(dx * dx + dx));
+        if (chol(dx, rb + dx * dx + dx, blk + dx * dx + dx)) return -2;
+        m->cstQz[z] = gauss_cst(dx, blk + dx * dx + dx);
+      }
+      m->mu0 = malloc(sizeof(double) * dx); memcpy(m->mu0, rb, sizeof(double) * dx);
+      m->L0 = malloc(sizeof(double) * dx * dx);
+      if (chol(dx, rb + dx, m->L0)) return -2;
+      m->cst0 = gauss_cst(dx, m->L0);
       i += need;
     } else if (m->lat == 3) {  /* categorical latent: prior[K] T[K*K] (T[new*K + prev]), one-hot state */
       int64_t need = (int64_t)d + (int64_t)d * d;
@@ -892,8 +924,41 @@ static int slot_onehot(const double* x, int d) {
   for (int j = 0; j < d; ++j) z = x[j] != 0.0 ? j : z;
   return z;
 }
+/* the regime of a switching state (its one-hot tail, SlotModel::regime) */
+static int slot_regime(const model_t* m, const double* x) {
+  int dx = m->d - m->nz, z = 0;
+  for (int j = dx; j < m->d; ++j) z = x[j] != 0.0 ? j - dx : z;
+  return z;
+}
 static void slot_latent(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, const obs_t* o,
                         const double* xp, double* x, uint32_t stream, uint32_t base) {
+  if (m->lat == 4) {  /* the regime (inverse CDF, draw base), then x under it (normals from base + 1) */
+    uint32_t w[4];
+    rng(seed, pid, t, stream, base, w);
+    const double u = unif53(w[0], w[1]);
+    const int nz = m->nz, d = m->d, dx = d - nz;
+    const int z = t == 1 ? cat_sample(m->prior, nz, 1, u) : cat_sample(m->T + slot_regime(m, xp), nz, nz, u);
+    const double* blk = m->SW + z * (2 * dx * dx + dx);
+    const double* L = t == 1 ? m->L0 : blk + dx * dx + dx;
+    double zn[64];
+    normals_at(seed, pid, t, stream, base + 1, d, zn);
+    for (int i = 0; i < d; ++i) {
+      if (i < dx) {
+        double acc;
+        if (t == 1) {
+          acc = m->mu0[i];
+        } else {
+          acc = blk[dx * dx + i];
+          for (int k = 0; k < dx; ++k) acc = fma(blk[i * dx + k], xp[k], acc);
+        }
+        for (int k = 0; k <= i; ++k) acc = fma(L[i * dx + k], zn[k], acc);
+        x[i] = acc;
+      } else {
+        x[i] = i - dx == z ? 1.0 : 0.0;
+      }
+    }
+    return;
+  }
   if (m->lat == 3) {  /* inverse-CDF draw (categorical.jl:20-22), as the HMM family's */
     uint32_t w[4];
     rng(seed, pid, t, stream, base, w);
@@ -1244,7 +1309,7 @@ static int proposal_ok(const model_t* m, int proposal) {
   if (proposal == ORC_PROPOSAL_GAUSSIAN) return m->family == ORC_KITAGAWA && m->qa[3] > 0.0;
   if (proposal == ORC_PROPOSAL_LINEAR)
     return m->qlin && ((m->family == ORC_LGSSM && m->d + m->dy <= 32) ||
-                       (m->family == ORC_SLOTS && m->lat != 3 && m->d + m->snv + (m->uin ? m->d : 0) <= 32));
+                       (m->family == ORC_SLOTS && m->lat != 3 && m->lat != 4 && m->d + m->snv + (m->uin ? m->d : 0) <= 32));
   return proposal == ORC_PROPOSAL_OPTIMAL && (m->family == ORC_HMM || (m->family == ORC_LGSSM && m->opt));
 }
 int orc_pf_set_proposal_args(orc_pf* pf, const double* args, int n) {
@@ -1652,6 +1717,26 @@ static void model_score(const model_t* m, const obs_t* o, int t, const double* x
       quad = fma(u[i], u[i], quad);
     }
     *lat = (t == 1 ? m->cst0 : m->cstQ) - 0.5 * quad;
+  } else if (m->family == ORC_SLOTS && m->lat == 4) {  /* log p(z | z_prev) + mvnormal.jl:12-16 under z */
+    const int nz = m->nz, dx = m->d - nz, z = slot_regime(m, x);
+    const double* blk = m->SW + z * (2 * dx * dx + dx);
+    const double lz = orc_log(t == 1 ? m->prior[z] : m->T[z * nz + slot_regime(m, xp)]);
+    const double* L = t == 1 ? m->L0 : blk + dx * dx + dx;
+    double u[64], quad = 0.0;
+    for (int i = 0; i < dx; ++i) {
+      double mean;
+      if (t == 1) {
+        mean = m->mu0[i];
+      } else {
+        mean = blk[dx * dx + i];
+        for (int k = 0; k < dx; ++k) mean = fma(blk[i * dx + k], xp[k], mean);
+      }
+      double r = x[i] - mean;
+      for (int k = 0; k < i; ++k) r = fma(-L[i * dx + k], u[k], r);
+      u[i] = r / L[i * dx + i];
+      quad = fma(u[i], u[i], quad);
+    }
+    *lat = lz + ((t == 1 ? m->cst0 : m->cstQz[z]) - 0.5 * quad);
   } else if (m->family == ORC_SLOTS && m->lat == 3) {  /* categorical.jl:10-12 */
     const int z = slot_onehot(x, m->d);
     *lat = orc_log(t == 1 ? m->prior[z] : m->T[z * m->d + slot_onehot(xp, m->d)]);

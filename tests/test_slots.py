@@ -162,6 +162,35 @@ def library_obs(name, T=10, seed=6):
     return m, obs
 
 
+def slds_model(same=False):
+    """A switching linear dynamical system: two latent addresses per step,
+    z_t ~ categorical(T[:, z_{t-1}]) and x_t ~ mvnormal(A[z] x + b[z], Q[z]),
+    with a normal observation of x (plus a per-regime offset) and a Poisson
+    count whose rate depends on the regime.  same=True: both regimes share the
+    dynamics and the emission ignores z (the LG-SSM with a decoupled chain)."""
+    A = np.array([[[0.95, 0.1], [0.0, 0.9]], [[0.5, -0.3], [0.2, 0.6]]])
+    b = np.array([[0.0, 0.1], [0.5, -0.2]])
+    Q = np.array([[[0.05, 0.01], [0.01, 0.04]], [[0.2, 0.0], [0.0, 0.15]]])
+    if same:
+        A, b, Q = np.stack([A[0], A[0]]), np.stack([b[0], b[0]]), np.stack([Q[0], Q[0]])
+    lat = {"form": "switching", "prior": [0.7, 0.3], "T": [[0.9, 0.2], [0.1, 0.8]], "A": A, "b": b, "Q": Q,
+           "mu0": [0.0, 0.0], "P0": [[0.5, 0.0], [0.0, 0.5]]}
+    if same:
+        return gen.SlotSSM(lat, [{"name": "y", "dist": "mvnormal", "H": [[1.0, 0.0, 0.0, 0.0], [0.0, 1.0, 0.0, 0.0]],
+                                  "c": [0.0, 0.0], "R": [[0.3, 0.0], [0.0, 0.3]]}])
+    return gen.SlotSSM(lat, [{"name": "y", "dist": "normal", "h": [1.0, 0.5, 0.0, 1.5], "c": 0.0, "sd": 0.4},
+                             {"name": "n", "dist": "poisson", "h": [0.2, 0.0, 0.0, 1.0], "c": 0.3}])
+
+
+def slds_obs(T=12, seed=4):
+    m = slds_model()
+    _, ys = m.simulate(T, np.random.default_rng(seed))
+    obs = [dict(y) for y in ys]
+    del obs[3]["n"]
+    obs[6] = {}
+    return m, obs
+
+
 def count_obs(T=10, seed=5):
     """Observations with some slots missing at some steps (and one empty step)."""
     m = count_model()
@@ -319,6 +348,36 @@ def test_oracle_library_slots_reduce_to_the_fixed_slots():
     b = O.run_pf(lib, ys, 600, 5, thr=0.0)
     assert np.array_equal(a.state(), b.state())
     np.testing.assert_allclose(b.log_weights(), a.log_weights(), rtol=1e-13, atol=1e-12)
+
+
+def test_oracle_switching_latent_scores_equal_reference_densities():
+    """The switching latent (two latent addresses): simulate's latent column is
+    log p(z_t | z_{t-1}) + mvnormal's logpdf of x_t under regime z_t (scipy),
+    the observation column the slots' densities; with both regimes sharing
+    the dynamics and an emission that ignores z, the filter's log-ML is the
+    Kalman filter's of the LG-SSM to Monte Carlo error."""
+    from scipy import stats
+
+    m = slds_model()
+    T, n = 5, 64
+    X, Y, PS, _ = O.simulate(m, T, n, 3)
+    for t in range(T):
+        for j in range(n):
+            x = X[t, :, j]
+            xp = X[t - 1, :, j] if t > 0 else None
+            ref = m.latent_part_logpdf(0, t + 1, xp, x) + m.latent_part_logpdf(1, t + 1, xp, x)
+            assert abs(ref - PS[t, 0, j]) < 1e-11 * max(1.0, abs(ref)), (t, j, ref, PS[t, 0, j])
+            z = int(np.argmax(x[2:]))
+            assert x[2 + z] == 1.0 and x[2:].sum() == 1.0
+            ob = stats.norm.logpdf(Y[t, 0, j], x[0] + 0.5 * x[1] + 1.5 * z, 0.4) + \
+                stats.poisson.logpmf(Y[t, 1, j], np.exp(0.2 * x[0] + 0.3 + z))
+            assert abs(ob - PS[t, 1, j]) < 1e-11 * max(1.0, abs(ob))
+    same = slds_model(same=True)
+    lg = gen.LinearGaussianSSM(same.A[0], same.Q[0], np.eye(2), 0.3 * np.eye(2), same.mu0, same.P0, b=same.b[0])
+    _, ys = same.simulate(15, np.random.default_rng(7))
+    exact = lg.kalman_log_marginal([v["y"] for v in ys])
+    est = [O.run_pf(same, ys, 20000, s).log_ml_estimate() for s in (1, 2)]
+    assert all(abs(e - exact) < 0.25 for e in est), (est, exact)
 
 
 def test_slot_model_rejects_bad_descriptions():
@@ -664,6 +723,32 @@ def test_gpu_library_slots_equal_oracle_bitexact(gh_ctx, name, batched):
     X, Y, PS, TOT = O.simulate(m, 5, 513, 29)
     assert np.array_equal(tr.xs, X) and np.array_equal(tr.ys, Y)
     assert np.array_equal(tr.per_step, PS) and np.array_equal(tr.total, TOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched,rejuv", [(False, 0), (True, 0), (False, 2)])
+def test_gpu_switching_latent_bitexact(gh_ctx, batched, rejuv):
+    """A switching linear dynamical system (two latent addresses per step):
+    GPU == oracle bit for bit (states, weights, parents, score columns;
+    log-ML 1e-9), with rejuvenation moves of the whole latent in one case;
+    the traces name both addresses; simulate bit-exact."""
+    m, obs = slds_obs()
+    n = 4097
+    st = _gpu_run(m, obs, n, 23, batched, None, rejuv)
+    orc = _orc_run(m, obs, n, 23, None, rejuv)
+    _same(st, orc=orc)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    tr = gen.get_traces(st)
+    cm = dict(tr[5].get_choices())
+    z, x = cm[("chain", 3, "z")], cm[("chain", 3, "x")]
+    assert z in (0, 1) and np.asarray(x).shape == (2,)
+    assert np.array_equal(tr.column(("chain", 3, "z")), np.argmax(st.states(3)[:, 2:], axis=1))
+    sim = gen.simulate(m, (6,), num_traces=321, seed=31)
+    X, Y, PS, TOT = O.simulate(m, 6, 321, 31)
+    assert np.array_equal(sim.xs, X) and np.array_equal(sim.ys, Y)
+    assert np.array_equal(sim.per_step, PS) and np.array_equal(sim.total, TOT)
 
 
 @pytest.mark.gpu
