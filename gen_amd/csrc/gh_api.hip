@@ -787,6 +787,32 @@ static const char* slots_build(gh_model* m, const double* p, int64_t np, std::ve
       i += d + 1;
     }
   }
+  // optional: dependencies between the step's observed addresses, nd then
+  // (child k, parent j < k, coefficient g) per dependency
+  sp.dep = 0;
+  sp.doff = sp.qoff + d;
+  for (int k = 0; k < kMaxSlots; ++k)
+    for (int j = 0; j < kMaxSlots; ++j) sp.dg[k][j] = 0.0;
+  if (np > i) {
+    const int nd = (int)p[i];
+    if (p[i] != nd || nd < 0 || np < i + 1 + 3LL * nd) return "slots: dependency block: nd then (child, parent, g) per dependency";
+    auto scalar = [&](int k) { return sp.dist[k] != SLOT_MVNORMAL; };
+    auto child_ok = [&](int k) {
+      return sp.dist[k] == SLOT_POISSON || sp.dist[k] == SLOT_BERNOULLI || sp.dist[k] == SLOT_LIBRARY ||
+             (sp.dist[k] == SLOT_NORMAL && sp.link[k] != LINK_KITAGAWA);
+    };
+    for (int q = 0; q < nd; ++q) {
+      const double* e = p + i + 1 + 3 * q;
+      const int k = (int)e[0], j = (int)e[1];
+      if (e[0] != k || e[1] != j || k < 0 || k >= sp.K || j < 0 || j >= k || !std::isfinite(e[2]))
+        return "slots: a dependency names a child slot and an earlier parent slot";
+      if (!child_ok(k) || !scalar(j))
+        return "slots: dependencies: a normal (affine mean), poisson, bernoulli or library child; a scalar parent";
+      sp.dg[k][j] = e[2];
+      sp.dep |= 1 << k;
+    }
+    if (sp.dep && sp.doff + sp.K > kMaxObs) return "slots: too many observed values for the dependency terms";
+  }
   return nullptr;
 }
 
@@ -1068,6 +1094,18 @@ static int make_obs_slots(const gh_model* m, const gh_obs* in, StepObs* o) {
       v[0] = y;
     }
     o->present |= 1 << k;
+  }
+  // the dependent slots' parent terms: fma over the (constrained) parents in slot order
+  for (int k = 0; k < sp.K; ++k) {
+    if (!((sp.dep >> k) & 1) || !((o->present >> k) & 1)) continue;
+    double dk = 0.0;
+    for (int j = 0; j < k; ++j) {
+      if (sp.dg[k][j] == 0.0) continue;
+      if (!((o->present >> j) & 1))
+        return set_err(GH_E_INVAL, "slots: slot %d is constrained but slot %d, which it depends on, is not", k, j);
+      dk = std::fma(sp.dg[k][j], o->v[sp.voff[j]], dk);
+    }
+    o->v[sp.doff + k] = dk;
   }
   return GH_OK;
 }
@@ -2168,8 +2206,12 @@ static const gh_obs* slot_chain(const std::vector<double>& r, gh_obs* chain) {
 static bool same_slots(const gh_model* a, const gh_model* b) {
   const SlotParams &p = a->slots, &q = b->slots;
   if (p.lat != q.lat || p.K != q.K || (p.uoff >= 0) != (q.uoff >= 0) || p.nz != q.nz) return false;
-  for (int k = 0; k < p.K; ++k)
+  if (p.dep != q.dep) return false;
+  for (int k = 0; k < p.K; ++k) {
     if (p.dist[k] != q.dist[k] || p.m[k] != q.m[k] || p.link[k] != q.link[k]) return false;
+    for (int j = 0; j < k; ++j)
+      if ((p.dg[k][j] != 0.0) != (q.dg[k][j] != 0.0)) return false;
+  }
   return true;
 }
 

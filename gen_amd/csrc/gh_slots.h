@@ -75,8 +75,10 @@ enum : int { LIB_IDENTITY = 0, LIB_EXP = 2, LIB_LOGISTIC = 3 };
 GH_HD double lib_link(int link, double eta) {
   return link == LIB_EXP ? gh_exp(eta) : (link == LIB_LOGISTIC ? 1.0 / (1.0 + gh_exp(-eta)) : eta);
 }
-// the library's logpdf and sampler by run-time id (out of line: one call per
-// library slot, no registers taken from the other slots' code)
+// the library's logpdf and sampler by run-time id (out of line, in the
+// extended instantiations only; the sampler reads the Box–Muller tables from
+// the constant copy: an LDS table pointer handed to the call came back unusable
+// to the caller's later normal draws — see DESIGN.md §5)
 static __device__ __noinline__ double lib_logpdf(int dist, double v, double a0, double a1, double a2) {
   const double P[3] = {a0, a1, a2};
   switch (dist) {
@@ -98,7 +100,8 @@ static __device__ __noinline__ double lib_logpdf(int dist, double v, double a0, 
   }
 }
 static __device__ __noinline__ double lib_random(int dist, uint64_t seed, uint64_t pid, uint32_t t, uint32_t base, double a0,
-                                          double a1, double a2, const double* tab) {
+                                          double a1, double a2) {
+  const double* tab = gh_math_tab_dev;
   const double P[3] = {a0, a1, a2};
   const DistRng r{seed, pid, t, STREAM_SIM, base};
   double x = 0.0;
@@ -154,6 +157,12 @@ struct SlotParams {
   double inv2v[kMaxSlots];  // normal 1 / (2 sd^2)
   double sd[kMaxSlots];     // normal sd (simulate)
   // (the observed values fill StepObs::v[0..voff of the last slot + its count); a poisson slot takes 2)
+  // dependencies between the observed addresses of one step: slot k's linear
+  // predictor adds delta_k = sum_{j<k} dg[k][j] y_j over its scalar parent slots
+  // (dep: the slots with parents; filtering reads delta_k from v[doff + k], the
+  // host's fma chain over the constrained parents; simulate forms it from the draws)
+  int dep, doff;
+  double dg[kMaxSlots][kMaxSlots];
   int uoff;                 // the step's latent input u_t (affine latent with inputs) in v[uoff..], or -1
   int qoff;                 // the linear proposal's mean offset in v[qoff..] (after the input, if any)
   // the linear custom proposal (SlotLinModel): the filter's own buffer,
@@ -202,12 +211,14 @@ struct SlotModel {
     return -(diff * diff) / (2.0 * var) - 0.5 * gh_log(0x1.921fb54442d18p+2 * var);
   }
 
-  // a library slot's arguments at latent x
-  __device__ static void lib_args(const double* P, int na, const double* x, double a[3]) {
+  // a library slot's arguments at latent x (the parent term joins the first one)
+  __device__ static void lib_args(const Params& p, const double* P, int na, const double* x, int k, double dk,
+                                  double a[3]) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const double* B = P + j * (D + 2);
-      a[j] = j < na ? lib_link((int)B[0], affine(B + 1, B[D + 1], x)) : 0.0;
+      a[j] = j < na ? lib_link((int)B[0], j == 0 ? eta(p, B + 1, B[D + 1], x, k, dk) : affine(B + 1, B[D + 1], x))
+                    : 0.0;
     }
   }
 
@@ -228,16 +239,24 @@ struct SlotModel {
     return z;
   }
 
-  // the logpdf of slot k's value (o.v + voff) at latent x
+  // c + h.x, plus slot k's parent term when it has parents
+  __device__ static double eta(const Params& p, const double* h, double c, const double* x, int k, double dk) {
+    const double e = affine(h, c, x);
+    return ((p.dep >> k) & 1) ? e + dk : e;
+  }
+
+  // the logpdf of slot k's value (o.v + voff) at latent x; dk: its parent term
   __device__ static double slot_lpdf(const Params& p, const StepObs& o, int k, const double* x) {
+    return slot_lpdf_d(p, o.v + p.voff[k], k, x, ((p.dep >> k) & 1) ? o.v[p.doff + k] : 0.0);
+  }
+  __device__ static double slot_lpdf_d(const Params& p, const double* v, int k, const double* x, double dk) {
     const double* P = p.P[k];
-    const double* v = o.v + p.voff[k];
     const int m = p.m[k];
     switch (p.dist[k]) {
       case SLOT_LIBRARY: {  // the library's logpdf (gh_dists.h, the reference's formulas)
         if constexpr (EXT) {
           double a[3];
-          lib_args(P, lib_nargs(m), x, a);
+          lib_args(p, P, lib_nargs(m), x, k, dk, a);
           return lib_logpdf(m, v[0], a[0], a[1], a[2]);
         } else {
           return NAN;  // (never: the host picks the EXT instantiation for such a model)
@@ -254,17 +273,17 @@ struct SlotModel {
         return p.cst[k] - 0.5 * quad;
       }
       case SLOT_NORMAL: {
-        const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : affine(P, P[D], x);
+        const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : eta(p, P, P[D], x, k, dk);
         const double diff = v[0] - mean;
         if (p.link[k] == LINK_LOGSCALE) return normal_logscale_lpdf(diff, affine(P + D + 1, P[2 * D + 1], x));
         return -(diff * diff) * p.inv2v[k] + p.cst[k];
       }
       case SLOT_POISSON: {  // poisson.jl:10-12 with lambda = exp(h.x + c); v[1] = log Gamma(y + 1)
-        const double lam = gh_exp(affine(P, P[D], x));
+        const double lam = gh_exp(eta(p, P, P[D], x, k, dk));
         return v[0] < 0.0 ? -INFINITY : (v[0] * gh_log(lam) - lam) - v[1];
       }
       case SLOT_BERNOULLI: {  // bernoulli.jl:10-12 with prob = 1 / (1 + exp(-(h.x + c)))
-        const double prob = 1.0 / (1.0 + gh_exp(-affine(P, P[D], x)));
+        const double prob = 1.0 / (1.0 + gh_exp(-eta(p, P, P[D], x, k, dk)));
         return v[0] != 0.0 ? gh_log(prob) : gh_log(1.0 - prob);
       }
       default: {  // categorical.jl:10-12 with probs = softmax(W x + c): exp(eta - max) / sum
@@ -446,20 +465,30 @@ struct SlotModel {
   __device__ static double sim_obs(const Params& p, uint64_t seed, uint64_t pid, uint32_t t, const double* x,
                                    double* y, int64_t ys, const double* tab) {
     double total = 0.0;
-#pragma unroll
+    double ysc[kMaxSlots];  // the scalar slots' draws (the parents of later slots)
+    // (a rolled loop: the unrolled form of the extended instantiation, four
+    // copies of every slot kind around the library calls, came out with wrong
+    // draws after the first call — DESIGN.md §5)
+#pragma unroll 1
     for (int k = 0; k < kMaxSlots; ++k) {
       if (k >= p.K) break;
       const double* P = p.P[k];
       const int m = p.m[k];
       const uint32_t draw = kSimObsDraw + kSlotSimDraws * (uint32_t)k;
       double* yk = y + (int64_t)p.yoff[k] * ys;
+      double dk = 0.0;  // the parent term, as the host forms it for a step (fma over the parents in slot order)
+      if ((p.dep >> k) & 1) {
+#pragma unroll
+        for (int j = 0; j < kMaxSlots; ++j)
+          if (j < k && p.dg[k][j] != 0.0) dk = fma(p.dg[k][j], ysc[j], dk);
+      }
       double lp;
       switch (p.dist[k]) {
         case SLOT_LIBRARY: {  // the library's sampler (gh_dists.h) on draws kSlotLibDraw + 256 k
           if constexpr (EXT) {
             double a[3];
-            lib_args(P, lib_nargs(m), x, a);
-            yk[0] = lib_random(m, seed, pid, t, kSlotLibDraw + 256u * (uint32_t)k, a[0], a[1], a[2], tab);
+            lib_args(p, P, lib_nargs(m), x, k, dk, a);
+            yk[0] = lib_random(m, seed, pid, t, kSlotLibDraw + 256u * (uint32_t)k, a[0], a[1], a[2]);
             lp = lib_logpdf(m, yk[0], a[0], a[1], a[2]);
           } else {
             yk[0] = NAN;
@@ -494,7 +523,7 @@ struct SlotModel {
         case SLOT_NORMAL: {
           double z0, z1;
           normal_pair(rng_block(seed, pid, t, STREAM_SIM, draw), &z0, &z1, tab);
-          const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : affine(P, P[D], x);
+          const double mean = p.link[k] == LINK_KITAGAWA ? div20(x[0] * x[0]) : eta(p, P, P[D], x, k, dk);
           if (p.link[k] == LINK_LOGSCALE) {
             const double eta = affine(P + D + 1, P[2 * D + 1], x);
             yk[0] = mean + gh_exp(eta) * z0;
@@ -508,7 +537,7 @@ struct SlotModel {
         }
         case SLOT_POISSON: {
           const u32x4 w = rng_block(seed, pid, t, STREAM_SIM, draw);
-          const double lam = gh_exp(affine(P, P[D], x));
+          const double lam = gh_exp(eta(p, P, P[D], x, k, dk));
           const double v = poisson_chop(lam, u53(w.x, w.y));
           yk[0] = v;
           lp = (v * gh_log(lam) - lam) - gh_lgamma(v + 1.0);
@@ -516,7 +545,7 @@ struct SlotModel {
         }
         case SLOT_BERNOULLI: {  // bernoulli.jl:19: rand() < prob
           const u32x4 w = rng_block(seed, pid, t, STREAM_SIM, draw);
-          const double prob = 1.0 / (1.0 + gh_exp(-affine(P, P[D], x)));
+          const double prob = 1.0 / (1.0 + gh_exp(-eta(p, P, P[D], x, k, dk)));
           const bool b = u53(w.x, w.y) < prob;
           yk[0] = b ? 1.0 : 0.0;
           lp = b ? gh_log(prob) : gh_log(1.0 - prob);
@@ -553,6 +582,7 @@ struct SlotModel {
         }
       }
       total = total + lp;
+      ysc[k] = yk[0];
     }
     return total;
   }

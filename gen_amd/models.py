@@ -412,6 +412,10 @@ class SlotSSM(Model):
             beta_uniform — Gen's argument order), each a constant or
             {"link": "identity" | "exp" | "logistic", "h": [d], "c"}
     Observations of step t: {("chain", t, name): value} (any subset of the slots).
+    A slot may depend on earlier scalar slots of its step: "parents": {name: g}
+    adds sum g * y_name to its linear predictor (a normal slot's mean, a Poisson
+    or Bernoulli slot's h.x + c, a library slot's first argument); a step that
+    constrains such a slot constrains its parents too.
     """
 
     family = _lib.FAMILY_SLOTS
@@ -505,6 +509,19 @@ class SlotSSM(Model):
                     s["c"] = float(s.get("c", 0.0))
             self.slots.append(s)
         self.names = [s["name"] for s in self.slots]
+        self.deps = []  # (child k, parent j, g)
+        for k, s in enumerate(self.slots):
+            for name, g in dict(s.get("parents", {})).items():
+                if name not in self.names[:k]:
+                    raise ValueError(f"slot {s['name']!r}: parent {name!r} must be an earlier slot")
+                j = self.names.index(name)
+                if self.slots[j]["dist"] == "mvnormal" and "lib" not in self.slots[j]:
+                    raise ValueError("a parent slot is scalar")
+                if not ("lib" in s or s["dist"] in ("poisson", "bernoulli") or
+                        (s["dist"] == "normal" and s["link"] != "x^2/20")):
+                    raise ValueError(f"slot {s['name']!r}: a dependent slot is a normal (affine mean), poisson, "
+                                     "bernoulli or library slot")
+                self.deps.append((k, j, float(g)))
         self.dy = sum(s["m"] if s["dist"] == "mvnormal" and "lib" not in s else 1 for s in self.slots)
 
     def params(self):
@@ -540,6 +557,10 @@ class SlotSSM(Model):
                 p += list(s["W"].ravel()) + list(s["c"])
             else:
                 p += [*s["h"], s["c"]]
+        if self.deps:
+            p += [float(len(self.deps))]
+            for k, j, g in self.deps:
+                p += [float(k), float(j), g]
         return np.asarray(p, dtype=np.float64)
 
     def obs_address(self, t: int, name: str | None = None):
@@ -625,7 +646,7 @@ class SlotSSM(Model):
         return super().latent_column(col)
 
     # ---- host-side reference densities (numpy / closed forms; the tests' pins)
-    def _mean_param(self, s, x):
+    def _mean_param(self, s, x, dk: float = 0.0):
         x = np.atleast_1d(x)
         if s["dist"] == "mvnormal":
             return s["H"] @ x + s["c"]
@@ -635,16 +656,16 @@ class SlotSSM(Model):
             return e / e.sum()
         if s["link"] == "x^2/20":
             return x[0] * x[0] / 20.0
-        eta = float(s["h"] @ x + s["c"])
+        eta = float(s["h"] @ x + s["c"]) + dk
         return {"normal": eta, "poisson": np.exp(eta), "bernoulli": 1.0 / (1.0 + np.exp(-eta))}[s["dist"]]
 
     @staticmethod
-    def lib_args(s, x) -> list:
-        """A library slot's arguments at latent x."""
+    def lib_args(s, x, dk: float = 0.0) -> list:
+        """A library slot's arguments at latent x (dk: the parent term, joining the first)."""
         x = np.atleast_1d(x)
         out = []
-        for link, h, c in s["args"]:
-            eta = float(h @ x + c)
+        for i, (link, h, c) in enumerate(s["args"]):
+            eta = float(h @ x + c) + (dk if i == 0 else 0.0)
             out.append({"identity": eta, "exp": float(np.exp(eta)), "logistic": 1.0 / (1.0 + np.exp(-eta))}[link])
         return out
 
@@ -725,15 +746,27 @@ class SlotSSM(Model):
             return float(np.exp(s["g"] @ np.atleast_1d(x) + s["s"]))
         return s["sd"]
 
-    def slot_logpdf(self, k: int, y, x) -> float:
+    def parent_term(self, k: int, yvals: dict | None) -> float:
+        """Slot k's parent term, sum of g * y_parent in slot order (the engine
+        takes an fma chain; host-side references agree to rounding)."""
+        dk = 0.0
+        for kk, j, g in sorted(self.deps, key=lambda e: e[1]):
+            if kk == k and g != 0.0:
+                dk = g * float(np.asarray(yvals[self.names[j]]).ravel()[0]) + dk
+        return dk
+
+    def slot_logpdf(self, k: int, y, x, yvals: dict | None = None) -> float:
         """logpdf of slot k's value y at latent x (scipy-free closed forms of
-        the reference's distributions)."""
+        the reference's distributions); yvals: the step's other slot values
+        (a dependent slot's parents)."""
         from math import lgamma
 
         s = self.slots[k]
+        dk = self.parent_term(k, yvals) if any(kk == k for kk, _, _ in self.deps) else 0.0
         if "lib" in s:
-            return self.lib_logpdf(s["dist"], float(y), self.lib_args(s, x))
-        mp = self._mean_param(s, x)
+            a = self.lib_args(s, x, dk)
+            return self.lib_logpdf(s["dist"], float(y), a)
+        mp = self._mean_param(s, x, dk)
         if s["dist"] == "mvnormal":
             return _mvn_logpdf(np.atleast_1d(y), mp, s["R"])
         if s["dist"] == "normal":
@@ -771,11 +804,12 @@ class SlotSSM(Model):
                               rng.normal(v / 2 + 25 * v / (1 + v * v) + 8 * np.cos(1.2 * t), self.sd_x)])
             xs[t - 1] = x
             y = {}
-            for s in self.slots:
+            for k, s in enumerate(self.slots):
+                dk = self.parent_term(k, y) if any(kk == k for kk, _, _ in self.deps) else 0.0
                 if "lib" in s:
-                    y[s["name"]] = self.lib_sample(s["dist"], self.lib_args(s, x), rng)
+                    y[s["name"]] = self.lib_sample(s["dist"], self.lib_args(s, x, dk), rng)
                     continue
-                mp = self._mean_param(s, x)
+                mp = self._mean_param(s, x, dk)
                 if s["dist"] == "mvnormal":
                     y[s["name"]] = rng.multivariate_normal(mp, s["R"])
                 elif s["dist"] == "normal":

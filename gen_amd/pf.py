@@ -453,7 +453,8 @@ class _TraceView:
                     if y is not None:
                         total += m.slot_logpdf(m.names.index(a[2]), np.asarray(y).ravel() if
                                                m.slots[m.names.index(a[2])]["dist"] == "mvnormal" else
-                                               float(np.asarray(y).ravel()[0]), self.trajectory()[t - 1])
+                                               float(np.asarray(y).ravel()[0]), self.trajectory()[t - 1],
+                                               st.observations.get(t))
                 elif a == tuple(m.obs_address(t)):
                     total += ps[t - 1, 1, self.i]
         return float(total)

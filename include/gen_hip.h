@@ -137,6 +137,13 @@ typedef enum {
          link_j(h_j.x + c_j) with link_j GH_ARG_IDENTITY, GH_ARG_EXP or
          GH_ARG_LOGISTIC; y ~ dist(args...) scored by the library's logpdf
          (gh_dist_logpdf's formulas) and drawn by its sampler in simulate
+     Optional trailing block, dependencies between a step's observed addresses:
+       nd, then nd triples (child k, parent j < k, g): the child's linear
+       predictor (a normal slot's affine mean, a poisson / bernoulli slot's
+       h.x + c, a library slot's first argument) adds the fma chain of g * y_j
+       over its parents in slot order; parents are scalar slots; a step that
+       constrains a child constrains its parents (else GH_E_INVAL); simulate
+       draws the parents first.
      At most 32 observed values per step (a poisson slot counts 2).  An LGSSM
      or Kitagawa model written as slots filters bit for bit as its family does
      (those stay the fast paths); the default proposal or GH_PROPOSAL_LINEAR

@@ -348,6 +348,10 @@ typedef struct {
   int nz;
   double* SW;
   double cstQz[8];
+  /* dependencies between a step's observed addresses: slot k's linear predictor
+     adds the fma chain of sdg[k][j] y_j over its parents j < k (sdep: slots with parents) */
+  int sdep;
+  double sdg[4][4];
   double* sP[4];
   double scst[4], sinv2v[4], ssd[4];
 } model_t;
@@ -624,6 +628,21 @@ static int model_build(model_t* m, int family, int d, int dy, int k, int v, cons
         i += d + 1;
       }
     }
+    m->sdep = 0;
+    memset(m->sdg, 0, sizeof m->sdg);
+    if (np > i) {  /* the dependency block: nd, then (child, parent < child, g) */
+      int nd = (int)p[i];
+      if ((double)nd != p[i] || nd < 0 || np < i + 1 + 3 * (int64_t)nd) return -1;
+      for (int q = 0; q < nd; ++q) {
+        const double* e = p + i + 1 + 3 * q;
+        int k = (int)e[0], j = (int)e[1];
+        if ((double)k != e[0] || (double)j != e[1] || k < 0 || k >= m->K || j < 0 || j >= k || !isfinite(e[2])) return -1;
+        int child = m->sdist[k] == 3 || m->sdist[k] == 4 || m->sdist[k] == 6 || (m->sdist[k] == 2 && m->slink[k] != 1);
+        if (!child || m->sdist[j] == 1) return -1;
+        m->sdg[k][j] = e[2];
+        m->sdep |= 1 << k;
+      }
+    }
   } else if (family == ORC_REGRESSION) {
     if (dy < 1 || dy > 32 || np < 5 + (int64_t)dy) return -1;
     m->d = 2;
@@ -653,6 +672,7 @@ typedef struct {
   double g[64], vt[64], w0;
   double raw[64]; /* the observation as given (rebuilt under other parameters: orc_pf_step_params) */
   int nraw;
+  double sdk[4];  /* slot models: each dependent slot's parent term (NaN when a parent is not constrained) */
 } obs_t;
 
 static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* o) {
@@ -684,6 +704,14 @@ static void obs_build(const model_t* m, int t, const double* y, int has, obs_t* 
         v[1] = orc_lgamma(yk[0] + 1.0);
       } else {
         v[0] = yk[0];
+      }
+    }
+    for (int k = 0; k < m->K; ++k) {  /* the parent terms (make_obs_slots' fma chain) */
+      o->sdk[k] = 0.0;
+      if (!((m->sdep >> k) & 1) || !((has >> k) & 1)) continue;
+      for (int j = 0; j < k; ++j) {
+        if (m->sdg[k][j] == 0.0) continue;
+        o->sdk[k] = ((has >> j) & 1) ? fma(m->sdg[k][j], o->bt[m->svoff[j]], o->sdk[k]) : NAN;
       }
     }
     return;
@@ -858,20 +886,31 @@ static double slot_logscale_lpdf(double diff, double eta) {
 static double slot_link(int link, double eta) {
   return link == 2 ? orc_exp(eta) : (link == 3 ? 1.0 / (1.0 + orc_exp(-eta)) : eta);
 }
-static void slot_lib_args(const double* P, int na, const double* x, int d, double a[3]) {
+static double slot_eta(const model_t* m, const double* h, double c, const double* x, int k, double dk);
+static void slot_lib_args(const model_t* m, const double* P, int na, const double* x, int k, double dk, double a[3]) {
+  const int d = m->d;
   for (int j = 0; j < 3; ++j) {
     const double* B = P + j * (d + 2);
-    a[j] = j < na ? slot_link((int)B[0], slot_affine(B + 1, B[d + 1], x, d)) : 0.0;
+    a[j] = j < na ? slot_link((int)B[0], j == 0 ? slot_eta(m, B + 1, B[d + 1], x, k, dk) : slot_affine(B + 1, B[d + 1], x, d))
+                  : 0.0;
   }
 }
+/* c + h.x, plus slot k's parent term when it has parents (SlotModel::eta) */
+static double slot_eta(const model_t* m, const double* h, double c, const double* x, int k, double dk) {
+  double e = slot_affine(h, c, x, m->d);
+  return ((m->sdep >> k) & 1) ? e + dk : e;
+}
+static double slot_lpdf_d(const model_t* m, const double* v, int k, const double* x, double dk);
 static double slot_lpdf(const model_t* m, const obs_t* o, int k, const double* x) {
+  return slot_lpdf_d(m, o->bt + m->svoff[k], k, x, ((m->sdep >> k) & 1) ? o->sdk[k] : 0.0);
+}
+static double slot_lpdf_d(const model_t* m, const double* v, int k, const double* x, double dk) {
   const int d = m->d, mm = m->sm[k];
   const double* P = m->sP[k];
-  const double* v = o->bt + m->svoff[k];
   switch (m->sdist[k]) {
     case 6: {  /* the library's logpdf (od_logpdf: the reference's formulas) */
       double a[3];
-      slot_lib_args(P, slot_lib_nargs(mm), x, d, a);
+      slot_lib_args(m, P, slot_lib_nargs(mm), x, k, dk, a);
       return od_logpdf(mm, v, 1, a, 1, 0);
     }
     case 1: {  /* mvnormal(H x + c, R) through L_R^-1 (y - c) (mvnormal.jl:12-16) */
@@ -884,17 +923,17 @@ static double slot_lpdf(const model_t* m, const obs_t* o, int k, const double* x
       return m->scst[k] - 0.5 * quad;
     }
     case 2: {  /* normal.jl:56-60 */
-      double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_affine(P, P[d], x, d);
+      double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_eta(m, P, P[d], x, k, dk);
       double diff = v[0] - mean;
       if (m->slink[k] == 5) return slot_logscale_lpdf(diff, slot_affine(P + d + 1, P[2 * d + 1], x, d));
       return -(diff * diff) * m->sinv2v[k] + m->scst[k];
     }
     case 3: {  /* poisson.jl:10-12, lambda = exp(h.x + c) */
-      double lam = orc_exp(slot_affine(P, P[d], x, d));
+      double lam = orc_exp(slot_eta(m, P, P[d], x, k, dk));
       return v[0] < 0.0 ? -INFINITY : (v[0] * orc_log(lam) - lam) - v[1];
     }
     case 4: {  /* bernoulli.jl:10-12, prob = 1 / (1 + exp(-(h.x + c))) */
-      double prob = 1.0 / (1.0 + orc_exp(-slot_affine(P, P[d], x, d)));
+      double prob = 1.0 / (1.0 + orc_exp(-slot_eta(m, P, P[d], x, k, dk)));
       return v[0] != 0.0 ? orc_log(prob) : orc_log(1.0 - prob);
     }
     default: {  /* categorical.jl:10-12, probs = exp(eta - max eta) / sum (0-based value) */
@@ -1014,15 +1053,20 @@ static double slot_poisson_chop(double lam, double u) {
    the observation vector's layout */
 static void slot_sim(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, const double* x, double* y) {
   const int d = m->d;
+  double ysc[4];  /* the scalar slots' draws (parents of later slots) */
   for (int k = 0; k < m->K; ++k) {
     const int mm = m->sm[k];
+    double dk = 0.0;  /* the parent term (SlotModel::sim_obs) */
+    if ((m->sdep >> k) & 1)
+      for (int j = 0; j < k; ++j)
+        if (m->sdg[k][j] != 0.0) dk = fma(m->sdg[k][j], ysc[j], dk);
     const uint32_t draw = 32u + 32u * (uint32_t)k;
     const double* P = m->sP[k];
     double* yk = y + m->syoff[k];
     uint32_t w[4];
     if (m->sdist[k] == 6) {
       double a[3];
-      slot_lib_args(P, slot_lib_nargs(mm), x, d, a);
+      slot_lib_args(m, P, slot_lib_nargs(mm), x, k, dk, a);
       const od_rng r = {seed, pid, t, 7, SLOT_LIB_DRAW + 256u * (uint32_t)k};
       od_random(mm, &r, yk, 1, a, 1, 0);
     } else if (m->sdist[k] == 1) {
@@ -1038,15 +1082,15 @@ static void slot_sim(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, 
     } else if (m->sdist[k] == 2) {
       double z[2];
       normals_at(seed, pid, t, 7, draw, 1, z);
-      double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_affine(P, P[d], x, d);
+      double mean = m->slink[k] == 1 ? x[0] * x[0] / 20.0 : slot_eta(m, P, P[d], x, k, dk);
       double sd = m->slink[k] == 5 ? orc_exp(slot_affine(P + d + 1, P[2 * d + 1], x, d)) : m->ssd[k];
       yk[0] = mean + sd * z[0];
     } else if (m->sdist[k] == 3) {
       rng(seed, pid, t, 7, draw, w);
-      yk[0] = slot_poisson_chop(orc_exp(slot_affine(P, P[d], x, d)), unif53(w[0], w[1]));
+      yk[0] = slot_poisson_chop(orc_exp(slot_eta(m, P, P[d], x, k, dk)), unif53(w[0], w[1]));
     } else if (m->sdist[k] == 4) {
       rng(seed, pid, t, 7, draw, w);
-      double prob = 1.0 / (1.0 + orc_exp(-slot_affine(P, P[d], x, d)));
+      double prob = 1.0 / (1.0 + orc_exp(-slot_eta(m, P, P[d], x, k, dk)));
       yk[0] = unif53(w[0], w[1]) < prob ? 1.0 : 0.0;
     } else {
       rng(seed, pid, t, 7, draw, w);
@@ -1055,6 +1099,7 @@ static void slot_sim(const model_t* m, uint64_t seed, uint64_t pid, uint32_t t, 
       for (int j = 0; j < mm; ++j) e[j] = orc_exp(slot_affine(P + j * d, P[mm * d + j], x, d) - mx);
       yk[0] = (double)cat_sample(e, mm, 1, unif53(w[0], w[1]));
     }
+    ysc[k] = yk[0];
   }
 }
 

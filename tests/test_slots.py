@@ -191,6 +191,28 @@ def slds_obs(T=12, seed=4):
     return m, obs
 
 
+def dep_model(g=(0.3, -0.5, 0.1, 0.05)):
+    """Observed addresses that depend on each other within a step: a normal
+    reading, a count whose log-rate adds 0.3 x the reading, an alarm whose
+    logit adds -0.5 x the reading + 0.1 x the count, and a gamma whose log-shape
+    adds 0.05 x the count."""
+    return gen.SlotSSM(_LAT2, [
+        {"name": "a", "dist": "normal", "h": [1.0, 0.0], "c": 0.0, "sd": 0.5},
+        {"name": "n", "dist": "poisson", "h": [0.5, 0.2], "c": 0.1, "parents": {"a": g[0]}},
+        {"name": "b", "dist": "bernoulli", "h": [0.0, 1.0], "c": 0.0, "parents": {"a": g[1], "n": g[2]}},
+        {"name": "g", "dist": "gamma", "args": [_arg("exp", [0.2, 0.0], 0.1), 1.5], "parents": {"n": g[3]}}])
+
+
+def dep_obs(T=10, seed=12):
+    m = dep_model()
+    _, ys = m.simulate(T, np.random.default_rng(seed))
+    obs = [dict(y) for y in ys]
+    del obs[2]["b"]           # a child left out: fine
+    del obs[4]["g"], obs[4]["b"]
+    obs[6] = {"a": obs[6]["a"]}
+    return m, obs
+
+
 def count_obs(T=10, seed=5):
     """Observations with some slots missing at some steps (and one empty step)."""
     m = count_model()
@@ -378,6 +400,40 @@ def test_oracle_switching_latent_scores_equal_reference_densities():
     exact = lg.kalman_log_marginal([v["y"] for v in ys])
     est = [O.run_pf(same, ys, 20000, s).log_ml_estimate() for s in (1, 2)]
     assert all(abs(e - exact) < 0.25 for e in est), (est, exact)
+
+
+def test_oracle_dependent_slots_scores_equal_reference_densities():
+    """Observed addresses depending on earlier ones in the step: simulate's
+    observation column is the sum of the reference densities with each
+    child's linear predictor shifted by g x its parents' values; with every
+    coefficient 0 the model filters as the one without dependencies, bit for
+    bit; a step constraining a child without its parent is refused on the
+    host side (the oracle's weights turn NaN)."""
+    m = dep_model()
+    T, n = 5, 64
+    X, Y, PS, _ = O.simulate(m, T, n, 3)
+    for t in range(T):
+        for j in range(n):
+            x = X[t, :, j]
+            yv = {name: Y[t, k, j] for k, name in enumerate(m.names)}
+            ref = sum(m.slot_logpdf(k, Y[t, k, j], x, yv) for k in range(4))
+            assert abs(ref - PS[t, 1, j]) < 1e-10 * max(1.0, abs(ref)), (t, j, ref, PS[t, 1, j])
+    flat = dep_model(g=(0.0, 0.0, 0.0, 0.0))
+    plain = gen.SlotSSM(_LAT2, [{k: v for k, v in sl.items() if k != "parents"} for sl in
+                                [{"name": "a", "dist": "normal", "h": [1.0, 0.0], "c": 0.0, "sd": 0.5},
+                                 {"name": "n", "dist": "poisson", "h": [0.5, 0.2], "c": 0.1},
+                                 {"name": "b", "dist": "bernoulli", "h": [0.0, 1.0], "c": 0.0},
+                                 {"name": "g", "dist": "gamma", "args": [_arg("exp", [0.2, 0.0], 0.1), 1.5]}]])
+    _, obs = dep_obs()
+    a = O.run_pf(flat, obs, 500, 4)
+    b = O.run_pf(plain, obs, 500, 4)
+    assert np.array_equal(a.state(), b.state()) and np.array_equal(a.log_weights(), b.log_weights())
+    pf = O.OraclePF(m, 50, 1)
+    pf.init({"n": 2.0})  # the count without the reading it depends on
+    assert np.all(np.isnan(pf.log_weights()))
+    with pytest.raises(ValueError):
+        gen.SlotSSM(_LAT2, [{"name": "n", "dist": "poisson", "h": [0.0, 0.0], "c": 0.0, "parents": {"a": 1.0}},
+                            {"name": "a", "dist": "normal", "h": [1.0, 0.0], "c": 0.0, "sd": 0.5}])
 
 
 def test_slot_model_rejects_bad_descriptions():
@@ -749,6 +805,32 @@ def test_gpu_switching_latent_bitexact(gh_ctx, batched, rejuv):
     X, Y, PS, TOT = O.simulate(m, 6, 321, 31)
     assert np.array_equal(sim.xs, X) and np.array_equal(sim.ys, Y)
     assert np.array_equal(sim.per_step, PS) and np.array_equal(sim.total, TOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched,rejuv", [(False, 0), (True, 0), (False, 2)])
+def test_gpu_dependent_slots_bitexact(gh_ctx, batched, rejuv):
+    """Dependent observed addresses (normal -> Poisson -> Bernoulli, Poisson
+    -> gamma library slot), steps leaving children out: GPU == oracle bit for
+    bit (states, weights, parents, score columns; log-ML 1e-9), with
+    rejuvenation moves in one case (the likelihood evaluated repeatedly in one
+    launch), simulate bit-exact (a fixed-sd normal slot after a library slot,
+    over several steps); a step constraining a child without its parent is
+    refused."""
+    m, obs = dep_obs()
+    n = 4093
+    st = _gpu_run(m, obs, n, 27, batched, None, rejuv)
+    orc = _orc_run(m, obs, n, 27, None, rejuv)
+    _same(st, orc=orc)
+    tot, ps = gen.get_traces(st).scores(per_step=True)
+    otot, ops = orc.scores(per_step=True)
+    assert np.array_equal(tot, otot) and np.array_equal(ps, ops)
+    sim = gen.simulate(m, (6,), num_traces=257, seed=37)
+    X, Y, PS, TOT = O.simulate(m, 6, 257, 37)
+    assert np.array_equal(sim.xs, X) and np.array_equal(sim.ys, Y)
+    assert np.array_equal(sim.per_step, PS) and np.array_equal(sim.total, TOT)
+    with pytest.raises(gen.GenHipError):
+        gen.initialize_particle_filter(m, (1,), _obs_at(m, {"n": 2.0}, 1), 64, seed=1)
 
 
 @pytest.mark.gpu
