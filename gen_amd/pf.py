@@ -700,8 +700,8 @@ def _latent_mask(state: ParticleFilterState, selection) -> int:
         names = {("slope",): 1, ("intercept",): 2}
     else:
         names = {tuple(a): 1 for a in m.latent_addresses(state.t)}
-    if len(names) > 1 and not all(a in set(map(tuple, sel)) for a in names):
-        raise _lib.GenHipError(1, f"selection must name every latent address of the step together: {sorted(names)}")
+        if len(names) > 1 and not all(a in set(map(tuple, sel)) for a in names):  # (a switching slot model)
+            raise _lib.GenHipError(1, f"selection must name every latent address of the step together: {sorted(names)}")
     mask = 0
     for a in sel:
         if a not in names:
