@@ -34,6 +34,14 @@ def build_model(name):
         from tests.test_slots import switching_model
 
         return switching_model()
+    if name == "slds":  # two latent addresses (regime, state): the extended slot instantiations
+        from tests.test_slots import slds_model
+
+        return slds_model()
+    if name == "deps":  # dependent observed addresses incl. a library (gamma) slot
+        from tests.test_slots import dep_model
+
+        return dep_model()
     raise ValueError(name)
 
 

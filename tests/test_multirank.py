@@ -480,7 +480,7 @@ def _check_genealogy(out, model, R, n, T, seed, thr, batched, resampler="systema
     ("peer", "lg4", 2, 1e9, 3001, True), ("peer", "kit", 3, None, 4096, True), ("peer", "lg10", 2, 3001.0, 3001, False),
     ("rccl1", "lg4", 1, None, 3001, True), ("gloo", "kit", 2, 1e9, 3001, "mid"), ("peer", "lg4", 3, 1e9, 3001, "mid"),
     ("peer", "count", 3, None, 4003, True), ("gloo", "count", 2, 1e9, 3001, False), ("rccl1", "count", 1, 1e9, 3001, True),
-    ("peer", "switch", 3, 1e9, 4003, False)])
+    ("peer", "switch", 3, 1e9, 4003, False), ("peer", "slds", 2, 1e9, 3001, True), ("gloo", "deps", 2, None, 3001, False)])
 def test_gpu_multirank_genealogy(tmp_path, gh_ctx, transport, model, R, thr, n, batched):
     """The genealogy across ranks (get_traces at earlier steps, the trace score
     columns, sample_unweighted_traces; particle_filter.jl:31-34, 62-70): each
