@@ -349,9 +349,11 @@ def secondary_c4(gen, ctx, a):
 def secondary_slots(gen, ctx, a):
     """Slot-described Unfold kernels (GH_FAMILY_SLOTS) at the C2
     size: a count SSM (2-d affine latent; Poisson, normal, Bernoulli and
-    categorical addresses, every one observed each step) and the C2 model
-    written as slots, beside the hand-lowered family on the same data — the
-    generic functor's price."""
+    categorical addresses, every one observed each step), a switching linear
+    dynamical system and a model with dependent addresses and a gamma library
+    slot (both on the extended instantiations), and the C2 model written as
+    slots, beside the hand-lowered family on the same data — the generic
+    functor's price."""
     n = a.particles
     T = a.warmup + a.steps + 1
 
@@ -378,6 +380,23 @@ def secondary_slots(gen, ctx, a):
          {"name": "on", "dist": "bernoulli", "h": [1.5, 0.0], "c": -0.3},
          {"name": "kind", "dist": "categorical", "W": [[1.0, 0.0], [0.0, 1.0], [-1.0, 1.0]], "c": [0.0, 0.2, -0.1]}])
     _, cys = count.simulate(T, np.random.default_rng(5))
+    # the extended instantiations: two latent addresses (a switching linear-Gaussian
+    # state), and dependent addresses with a library (gamma) slot
+    slds = gen.SlotSSM(
+        {"form": "switching", "prior": [0.7, 0.3], "T": [[0.9, 0.2], [0.1, 0.8]],
+         "A": [[[0.95, 0.1], [0.0, 0.9]], [[0.5, -0.3], [0.2, 0.6]]], "b": [[0.0, 0.1], [0.5, -0.2]],
+         "Q": [[[0.05, 0.01], [0.01, 0.04]], [[0.2, 0.0], [0.0, 0.15]]], "mu0": [0.0, 0.0], "P0": [[0.5, 0.0], [0.0, 0.5]]},
+        [{"name": "y", "dist": "normal", "h": [1.0, 0.5, 0.0, 1.5], "c": 0.0, "sd": 0.4},
+         {"name": "n", "dist": "poisson", "h": [0.2, 0.0, 0.0, 1.0], "c": 0.3}])
+    _, sys_ = slds.simulate(T, np.random.default_rng(6))
+    deps = gen.SlotSSM(
+        {"form": "affine", "A": [[0.9, 0.05], [0.0, 0.8]], "b": [0.0, 0.1], "Q": [[0.05, 0.01], [0.01, 0.04]],
+         "mu0": [0.5, 0.0], "P0": [[0.3, 0.0], [0.0, 0.3]]},
+        [{"name": "a", "dist": "normal", "h": [1.0, 0.0], "c": 0.0, "sd": 0.5},
+         {"name": "n", "dist": "poisson", "h": [0.5, 0.2], "c": 0.1, "parents": {"a": 0.3}},
+         {"name": "g", "dist": "gamma", "args": [{"link": "exp", "h": [0.2, 0.0], "c": 0.1}, 1.5],
+          "parents": {"n": 0.05}}])
+    _, dys = deps.simulate(T, np.random.default_rng(7))
     lg = gen.LinearGaussianSSM.benchmark(a.d)
     lgs = gen.SlotSSM({"form": "affine", "A": lg.A, "b": lg.b, "Q": lg.Q, "mu0": lg.mu0, "P0": lg.P0},
                       [{"name": "y", "dist": "mvnormal", "H": lg.H, "c": lg.c, "R": lg.R}])
@@ -390,6 +409,8 @@ def secondary_slots(gen, ctx, a):
         "particles": n,
         "steps": a.steps,
         "count_ssm": timed(count, [dict(y) for y in cys], {("chain", 1, k): v for k, v in cys[0].items()}),
+        "switching_lds": timed(slds, [dict(y) for y in sys_], {("chain", 1, k): v for k, v in sys_[0].items()}),
+        "dependent_library": timed(deps, [dict(y) for y in dys], {("chain", 1, k): v for k, v in dys[0].items()}),
         "lgssm_d%d_as_slots" % a.d: sl,
         "lgssm_d%d_family" % a.d: fam,
         "slots_vs_family": fam["ms_per_step"] / sl["ms_per_step"],
